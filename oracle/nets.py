@@ -1,0 +1,409 @@
+"""Oracle: the reference acoustic models restated in PyTorch-CPU eager (test infrastructure only).
+
+Same parameter names (state_dict keys), same torch-RNG consumption at init and the same in-place
+quirks as the reference, so a model built here from a seed equals the reference model:
+
+  MLP    neural_networks.py:81-319   (mask W in place, drop(act(BN(W x + b))), LogSoftmax head)
+  LSTM   neural_networks.py:468-1112 (bidir forced off :835, per-step loop :1077-1097)
+  liGRU  neural_networks.py:1429-1599 (shared-weight bidir via cat/flip :1536-1538, :1590-1594)
+  QuantLinear quantized_modules.py:182-222 (train: clamp W in place, STE with Wq; input quantised
+              in place through .data so later users of the same tensor see it)
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import masks as M
+
+
+def _b(v):
+    return str(v).strip().lower() in ("1", "true", "yes", "y", "on", "t")
+
+
+def _lst(opts, key, f=str):
+    return [f(x) for x in opts[key].split(",")]
+
+
+class LayerNorm(nn.Module):
+    """neural_networks.py:40-51: gamma*(x-mean)/(std_unbiased+eps)+beta."""
+
+    def __init__(self, n, eps=1e-6):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(n))
+        self.beta = nn.Parameter(torch.zeros(n))
+        self.eps = eps
+
+    def forward(self, x):
+        mu = x.mean(-1, keepdim=True)
+        sd = x.std(-1, keepdim=True)
+        return self.gamma * (x - mu) / (sd + self.eps) + self.beta
+
+
+def act_fn(name, x):
+    """neural_networks.py:54-78 ('linear' is LeakyReLU(1) == identity)."""
+    if name == "relu":
+        return F.relu(x)
+    if name == "tanh":
+        return torch.tanh(x)
+    if name == "sigmoid":
+        return torch.sigmoid(x)
+    if name == "htanh":
+        return F.hardtanh(x)
+    if name == "leaky_relu":
+        return F.leaky_relu(x, 0.2)
+    if name == "elu":
+        return F.elu(x)
+    if name == "softmax":
+        return F.log_softmax(x, dim=1)
+    if name == "linear":
+        return x
+    raise ValueError(name)
+
+
+class QLinear(nn.Module):
+    """quantized_modules.py:182-222 (training branch)."""
+
+    def __init__(self, fin, fout, bits, bias, inp_bits=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.bias = nn.Parameter(torch.empty(fout)) if bias else None
+        s = 1.0 / math.sqrt(fin)
+        self.weight.data.uniform_(-s, s)
+        if self.bias is not None:
+            self.bias.data.uniform_(-s, s)
+        self.bits = bits
+        self.inp_bits = inp_bits
+
+    def forward(self, x):
+        wc, wq = M.quantize(self.weight.data, self.bits)
+        self.weight.data = wc                      # clamp persists (quantized_modules.py:79)
+        keep = self.weight.data
+        self.weight.data = wq
+        if self.inp_bits is not None:
+            x.data = M.quantize_inp(x.data, self.inp_bits)
+        y = F.linear(x, self.weight, self.bias)
+        self.weight.data = keep
+        return y
+
+
+class MLP(nn.Module):
+    def __init__(self, o, inp_dim):
+        super().__init__()
+        self.input_dim = inp_dim
+        self.lay = _lst(o, "dnn_lay", int)
+        self.dropp = _lst(o, "dnn_drop", float)
+        self.use_bn = _lst(o, "dnn_use_batchnorm", _b)
+        self.use_ln = _lst(o, "dnn_use_laynorm", _b)
+        self.ln_inp = _b(o["dnn_use_laynorm_inp"])
+        self.bn_inp = _b(o["dnn_use_batchnorm_inp"])
+        self.acts = _lst(o, "dnn_act")
+        self.hcgs_on = _b(o.get("mlp_hcgs", "False"))
+        self.quant = _b(o.get("mlp_quant", "False"))
+        self.quant_inp = _b(o.get("mlp_quant_inp", "False"))
+        self.prune = _b(o.get("mlp_prune", "False"))
+        bits = _lst(o, "param_quant", int) if "param_quant" in o else [8] * len(self.lay)
+        ibits = int(o["inp_quant"].split(",")[0]) if "inp_quant" in o else 16
+        self.prune_perc = _lst(o, "mlp_prune_perc", float) if "mlp_prune_perc" in o else []
+        blocks = _lst(o, "hcgs_block", int) if "hcgs_block" in o else []
+        drops = _lst(o, "hcgs_sparse", float) if "hcgs_sparse" in o else []
+        self.wx, self.bn, self.ln = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        if self.hcgs_on:
+            self.hcgs = nn.ModuleList()
+        if self.ln_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.bn_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.lay):
+            self.ln.append(LayerNorm(n))
+            self.bn.append(nn.BatchNorm1d(n, momentum=0.05))
+            add_bias = not (self.use_ln[i] or self.use_bn[i])
+            if self.quant:
+                lin = QLinear(cur, n, bits[i], add_bias, ibits if self.quant_inp else None)
+            else:
+                lin = nn.Linear(cur, n, bias=add_bias)
+            self.wx.append(lin)
+            if self.hcgs_on:
+                hm = nn.Module()
+                hm.mask = nn.Parameter(torch.from_numpy(M.hcgs_conn_mat(n, cur, blocks, drops)))
+                self.hcgs.append(hm)
+            s = np.sqrt(0.01 / (cur + n))                         # neural_networks.py:233-235
+            lin.weight = nn.Parameter(torch.Tensor(n, cur).uniform_(-s, s))
+            lin.bias = nn.Parameter(torch.zeros(n))
+            cur = n
+        self.out_dim = cur
+
+    def forward(self, x, drop_masks=None):
+        if self.ln_inp:
+            x = self.ln0(x)
+        if self.bn_inp:
+            x = self.bn0(x)
+        for i in range(len(self.lay)):
+            w = self.wx[i].weight
+            if self.hcgs_on:
+                w.data.mul_(self.hcgs[i].mask.data)
+            if self.prune:
+                w.data.mul_(M.prune_mask(w, self.prune_perc[i]))
+            z = self.wx[i](x)
+            if self.use_ln[i]:
+                z = self.ln[i](z)
+            if self.use_bn[i]:
+                z = self.bn[i](z)
+            z = act_fn(self.acts[i], z)
+            if self.training and self.dropp[i] > 0:
+                m = drop_masks[i] if drop_masks is not None else \
+                    torch.bernoulli(torch.full_like(z, 1 - self.dropp[i]))
+                z = z * m / (1 - self.dropp[i])
+            x = z
+        return x
+
+
+def flip_time(x):
+    """neural_networks.py:2419-2426 on dim 0."""
+    return x.flip(0)
+
+
+class _Rec(nn.Module):
+    """Shared plumbing of the two recurrent families."""
+
+    def _drop_mask(self, i, rows, H, masks):
+        p = self.dropp[i]
+        if self.training:
+            if masks is not None:
+                return masks[i]
+            return torch.bernoulli(torch.full((rows, H), 1 - p))   # NOT rescaled (:843-847)
+        return torch.tensor([1 - p])
+
+
+class liGRU(_Rec):
+    """neural_networks.py:1429-1599."""
+
+    def __init__(self, o, inp_dim):
+        super().__init__()
+        self.lay = _lst(o, "ligru_lay", int)
+        self.dropp = _lst(o, "ligru_drop", float)
+        self.use_bn = _lst(o, "ligru_use_batchnorm", _b)
+        self.use_ln = _lst(o, "ligru_use_laynorm", _b)
+        self.ln_inp = _b(o["ligru_use_laynorm_inp"])
+        self.bn_inp = _b(o["ligru_use_batchnorm_inp"])
+        self.orth = _b(o["ligru_orthinit"])
+        self.acts = _lst(o, "ligru_act")
+        self.bidir = _b(o["ligru_bidir"])
+        self.wh, self.uh, self.wz, self.uz = (nn.ModuleList() for _ in range(4))
+        self.ln, self.bn_wh, self.bn_wz = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        if self.ln_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.bn_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.lay):
+            add_bias = not (self.use_ln[i] or self.use_bn[i])
+            self.wh.append(nn.Linear(cur, n, bias=add_bias))
+            self.wz.append(nn.Linear(cur, n, bias=add_bias))
+            self.uh.append(nn.Linear(n, n, bias=False))
+            self.uz.append(nn.Linear(n, n, bias=False))
+            if self.orth:
+                nn.init.orthogonal_(self.uh[i].weight)
+                nn.init.orthogonal_(self.uz[i].weight)
+            self.bn_wh.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.bn_wz.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def forward(self, x, drop_masks=None):
+        if self.ln_inp:
+            x = self.ln0(x)
+        if self.bn_inp:
+            T, B, Fd = x.shape
+            x = self.bn0(x.reshape(T * B, Fd)).view(T, B, Fd)
+        for i, H in enumerate(self.lay):
+            if self.bidir:
+                x = torch.cat([x, flip_time(x)], 1)
+            T, B2, _ = x.shape
+            dm = self._drop_mask(i, B2, H, drop_masks)
+            wh = self.wh[i](x)
+            wz = self.wz[i](x)
+            if self.use_bn[i]:
+                wh = self.bn_wh[i](wh.reshape(T * B2, H)).view(T, B2, H)
+                wz = self.bn_wz[i](wz.reshape(T * B2, H)).view(T, B2, H)
+            h = torch.zeros(B2, H)
+            hs = []
+            for k in range(T):
+                z = torch.sigmoid(wz[k] + self.uz[i](h))
+                a = wh[k] + self.uh[i](h)
+                hc = act_fn(self.acts[i], a) * dm
+                h = z * h + (1 - z) * hc
+                if self.use_ln[i]:
+                    h = self.ln[i](h)
+                hs.append(h)
+            y = torch.stack(hs)
+            if self.bidir:
+                y = torch.cat([y[:, :B2 // 2], flip_time(y[:, B2 // 2:])], 2)
+            x = y
+        return x
+
+
+class LSTM(_Rec):
+    """neural_networks.py:468-1112 (bidir forced 0 at :835, so only uni-directional)."""
+
+    GATES = ("f", "i", "o", "c")
+
+    def __init__(self, o, inp_dim):
+        super().__init__()
+        self.lay = _lst(o, "lstm_lay", int)
+        self.dropp = _lst(o, "lstm_drop", float)
+        self.use_bn = _lst(o, "lstm_use_batchnorm", _b)
+        self.use_ln = _lst(o, "lstm_use_laynorm", _b)
+        self.ln_inp = _b(o["lstm_use_laynorm_inp"])
+        self.bn_inp = _b(o["lstm_use_batchnorm_inp"])
+        self.acts = _lst(o, "lstm_act")
+        self.orth = _b(o["lstm_orthinit"])
+        self.hcgs_on = _b(o.get("lstm_hcgs", "False"))
+        self.quant = _b(o.get("lstm_quant", "False"))
+        self.quant_inp = _b(o.get("lstm_quant_inp", "False"))
+        self.prune = _b(o.get("lstm_prune", "False"))
+        self.if_pattern = _b(o["if_pattern"]) if "if_pattern" in o else False
+        bits = _lst(o, "param_quant", int) if "param_quant" in o else [8] * len(self.lay)
+        ibits = int(o["inp_quant"].split(",")[0]) if "inp_quant" in o else 16
+        self.prune_perc = _lst(o, "lstm_prune_perc", float) if "lstm_prune_perc" in o else []
+        bx = _lst(o, "hcgsx_block", int) if self.hcgs_on else []
+        bh = _lst(o, "hcgsh_block", int) if self.hcgs_on else []
+        dx = _lst(o, "hcgsx_sparse", float) if self.hcgs_on else []
+        dh = _lst(o, "hcgsh_sparse", float) if self.hcgs_on else []
+        for g in self.GATES:
+            setattr(self, "w%sx" % g, nn.ModuleList())
+            setattr(self, "u%sh" % g, nn.ModuleList())
+        if self.hcgs_on:
+            self.hcgsx, self.hcgsh = nn.ModuleList(), nn.ModuleList()
+        self.ln = nn.ModuleList()
+        for g in self.GATES:
+            setattr(self, "bn_w%sx" % g, nn.ModuleList())
+        if self.ln_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.bn_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        self.pattern_kernels = None
+        cur = inp_dim
+        for i, n in enumerate(self.lay):
+            if not (self.use_ln[i] or self.use_bn[i]):
+                raise IndexError("reference LSTM creates W/U only with BN or LN (:681-791)")
+            for g in self.GATES:
+                if self.quant:
+                    lin = QLinear(cur, n, bits[i], False, ibits if self.quant_inp else None)
+                else:
+                    lin = nn.Linear(cur, n, bias=False)
+                getattr(self, "w%sx" % g).append(lin)
+            if self.hcgs_on:
+                hm = nn.Module()
+                hm.mask = nn.Parameter(torch.from_numpy(M.hcgs_conn_mat(n, cur, bx, dx)))
+                self.hcgsx.append(hm)
+            for g in self.GATES:
+                if self.quant:
+                    lin = QLinear(n, n, bits[i], False, ibits if self.quant_inp else None)
+                else:
+                    lin = nn.Linear(n, n, bias=False)
+                getattr(self, "u%sh" % g).append(lin)
+            if self.hcgs_on:
+                hm = nn.Module()
+                hm.mask = nn.Parameter(torch.from_numpy(M.hcgs_conn_mat(n, n, bh, dh)))
+                self.hcgsh.append(hm)
+            if self.orth:
+                for g in self.GATES:
+                    nn.init.orthogonal_(getattr(self, "u%sh" % g)[i].weight)
+            for g in self.GATES:
+                getattr(self, "bn_w%sx" % g).append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = n
+        self.out_dim = self.lay[-1]
+        self.pattern_masks = None
+
+    def _pattern_update(self):
+        """neural_networks.py:876-884 / 1202-1237: masks computed once from |W|, then ALL layers'
+        W and U multiplied by their masks on every call (called once per layer per forward)."""
+        if self.pattern_masks is None:
+            self.pattern_masks = {}
+            for g in self.GATES:
+                for nm in ("w%sx" % g, "u%sh" % g):
+                    self.pattern_masks[nm] = [
+                        torch.from_numpy(M.apply_patterns(getattr(self, nm)[i].weight.data.numpy(),
+                                                          self.pattern_kernels))
+                        for i in range(len(self.lay))]
+        for g in self.GATES:
+            for nm in ("w%sx" % g, "u%sh" % g):
+                for i in range(len(self.lay)):
+                    getattr(self, nm)[i].weight.data.mul_(self.pattern_masks[nm][i])
+
+    def forward(self, x, drop_masks=None):
+        if self.ln_inp:
+            x = self.ln0(x)
+        if self.bn_inp:
+            T, B, Fd = x.shape
+            x = self.bn0(x.reshape(T * B, Fd)).view(T, B, Fd)
+        for i, H in enumerate(self.lay):
+            T, B, _ = x.shape
+            dm = self._drop_mask(i, B, H, drop_masks)
+            W = {g: getattr(self, "w%sx" % g)[i] for g in self.GATES}
+            U = {g: getattr(self, "u%sh" % g)[i] for g in self.GATES}
+            if self.hcgs_on:
+                for g in self.GATES:
+                    W[g].weight.data.mul_(self.hcgsx[i].mask.data)
+            if self.if_pattern:
+                self._pattern_update()
+            if self.prune:
+                for g in self.GATES:
+                    W[g].weight.data.mul_(M.prune_mask(W[g].weight, self.prune_perc[i]))
+            wo = {g: W[g](x) for g in self.GATES}
+            if self.use_bn[i]:
+                for g in self.GATES:
+                    bn = getattr(self, "bn_w%sx" % g)[i]
+                    wo[g] = bn(wo[g].reshape(T * B, H)).view(T, B, H)
+            if self.hcgs_on:
+                for g in self.GATES:
+                    U[g].weight.data.mul_(self.hcgsh[i].mask.data)
+            if self.prune:
+                for g in self.GATES:
+                    U[g].weight.data.mul_(M.prune_mask(U[g].weight, self.prune_perc[i]))
+            h = torch.zeros(B, H)
+            c = h
+            hs = []
+            for k in range(T):
+                f = torch.sigmoid(wo["f"][k] + U["f"](h))
+                ig = torch.sigmoid(wo["i"][k] + U["i"](h))
+                og = torch.sigmoid(wo["o"][k] + U["o"](h))
+                c = ig * act_fn(self.acts[i], wo["c"][k] + U["c"](h)) * dm + f * c
+                h = og * act_fn(self.acts[i], c)
+                if self.use_ln[i]:
+                    h = self.ln[i](h)
+                hs.append(h)
+            x = torch.stack(hs)
+        return x
+
+
+def nll_err(logp, labels):
+    """utils.py:1935-1952 (NLLLoss mean) and utils.py:1993-2011 (argmax error rate)."""
+    lab = labels.view(-1).long()
+    return F.nll_loss(logp, lab), torch.mean((logp.max(dim=1)[1] != lab).float())
+
+
+def make_optimizer(params, o):
+    """utils.py:1833-1881."""
+    lr = float(o["arch_lr"])
+    kind = o["arch_opt"]
+    if kind == "sgd":
+        return torch.optim.SGD(params, lr=lr, momentum=float(o["opt_momentum"]),
+                               weight_decay=float(o["opt_weight_decay"]),
+                               dampening=float(o["opt_dampening"]), nesterov=_b(o["opt_nesterov"]))
+    if kind == "rmsprop":
+        return torch.optim.RMSprop(params, lr=lr, momentum=float(o["opt_momentum"]),
+                                   alpha=float(o["opt_alpha"]), eps=float(o["opt_eps"]),
+                                   centered=_b(o["opt_centered"]),
+                                   weight_decay=float(o["opt_weight_decay"]))
+    if kind == "adam":
+        return torch.optim.Adam(params, lr=lr, betas=_lst(o, "opt_betas", float),
+                                eps=float(o["opt_eps"]), weight_decay=float(o["opt_weight_decay"]),
+                                amsgrad=_b(o["opt_amsgrad"]))
+    raise ValueError(kind)

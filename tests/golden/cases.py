@@ -1,0 +1,73 @@
+"""Configurations shared by the golden generator (make_golden.py) and the parity tests.
+
+Option names and values follow the reference's cfg schema (proto/MLP.proto, proto/liGRU.proto,
+proto/LSTM.proto plus the CGS keys read at neural_networks.py:98-131, 490-529).
+"""
+import configparser
+
+_TMP = "/tmp"
+
+MLP_DEF = dict(dnn_drop="0.0", dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False",
+               dnn_use_batchnorm="True", dnn_use_laynorm="False", dnn_act="relu", to_do="train",
+               mlp_hcgs="False", hcgs_block="16,4", hcgs_sparse="50,50", out_folder=_TMP,
+               mlp_quant="False", param_quant="8", mlp_quant_inp="False", inp_quant="16",
+               mlp_prune="False", mlp_prune_perc="70", skip_regularization="True",
+               guided_hcgs="False", apply_guided_hcgs="False", arch_name="MLP_layers1",
+               use_cuda="False")
+
+
+
+def build_mlp_config(variant):
+    cfg = configparser.ConfigParser()
+    cfg["exp"] = {"use_cuda": "False", "to_do": "train", "seed": "2234"}
+    body = dict(MLP_DEF, arch_name="MLP_layers1", dnn_lay="48,32", dnn_act="relu,relu",
+                dnn_drop="0.0,0.0", dnn_use_batchnorm="True,True", dnn_use_laynorm="False,False",
+                param_quant="8,8", mlp_prune_perc="70,70",
+                arch_library="neural_networks", arch_class="MLP", arch_freeze="False",
+                arch_seq_model="False", arch_lr="0.08", arch_opt="sgd", opt_momentum="0.0",
+                opt_weight_decay="0.0", opt_dampening="0.0", opt_nesterov="False")
+    head = dict(MLP_DEF, arch_name="MLP_layers2", dnn_lay="96", dnn_act="softmax",
+                dnn_use_batchnorm="False", arch_library="neural_networks", arch_class="MLP",
+                arch_freeze="False", arch_seq_model="False", arch_lr="0.0004", arch_opt="rmsprop",
+                opt_momentum="0.0", opt_alpha="0.95", opt_eps="1e-8", opt_centered="False",
+                opt_weight_decay="0.0")
+    mono = dict(head, arch_name="MLP_layers3", dnn_lay="8")
+    if variant == "hcgs":
+        body.update(mlp_hcgs="True", hcgs_block="16,4", hcgs_sparse="50,50")
+        head.update(mlp_hcgs="True", hcgs_block="16,4", hcgs_sparse="25,50")
+    if variant == "quant":
+        for d in (body, head, mono):
+            d.update(mlp_quant="True", mlp_quant_inp="True")
+    if variant == "ln":
+        body.update(dnn_use_batchnorm="False,True", dnn_use_laynorm="True,True",
+                    dnn_use_batchnorm_inp="True", dnn_act="relu,tanh")
+    cfg["architecture1"] = body
+    cfg["architecture2"] = head
+    cfg["architecture3"] = mono
+    cfg["model"] = {"model": "out_dnn1=compute(MLP_layers1,fmllr)\n"
+                             "out_dnn2=compute(MLP_layers2,out_dnn1)\n"
+                             "out_dnn3=compute(MLP_layers3,out_dnn1)\n"
+                             "loss_mono=cost_nll(out_dnn3,lab_mono)\n"
+                             "loss_mono_w=mult_constant(loss_mono,1.0)\n"
+                             "loss_cd=cost_nll(out_dnn2,lab_cd)\n"
+                             "loss_final=sum(loss_cd,loss_mono_w)\n"
+                             "err_final=cost_err(out_dnn2,lab_cd)"}
+    return cfg
+
+
+
+LIGRU_DEF = dict(ligru_lay="16,16", ligru_drop="0.0,0.0", ligru_use_laynorm_inp="False",
+                 ligru_use_batchnorm_inp="False", ligru_use_laynorm="False,False",
+                 ligru_use_batchnorm="True,True", ligru_bidir="True", ligru_act="relu,relu",
+                 ligru_orthinit="True", use_cuda="False", to_do="train")
+LSTM_DEF = dict(lstm_lay="16,16", lstm_drop="0.0,0.0", lstm_use_laynorm_inp="False",
+                lstm_use_batchnorm_inp="False", lstm_use_laynorm="False,False",
+                lstm_use_batchnorm="True,True", lstm_bidir="False", lstm_act="tanh,tanh",
+                lstm_orthinit="True", use_cuda="False", to_do="train", lstm_hcgs="False",
+                hcgsx_block="8,2", hcgsh_block="8,2", hcgsx_sparse="50,50", hcgsh_sparse="50,50",
+                out_folder=_TMP, lstm_quant="False", param_quant="8,8", lstm_quant_inp="False",
+                inp_quant="16", lstm_prune="False", lstm_prune_perc="70,70",
+                skip_regularization="True", guided_hcgs="False", apply_guided_hcgs="False",
+                if_hsigmoid="True", arch_name="LSTM_layers")
+
+
