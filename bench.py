@@ -1,0 +1,253 @@
+"""bench.py — training throughput (acoustic frames/s) of the pkc run_nn hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "TIMIT_baselines MLP 5x1024 bf16 on 1 MI355X, dense MFMA
+path"): cfg/TIMIT_baselines/TIMIT_MLP_fmllr.cfg architecture — fMLLR 40 x 11 context = 440 inputs,
+5 x 1024 ReLU+BN+dropout 0.15 (SGD lr 0.08), heads 1928 cd + 48 mono LogSoftmax (RMSprop 4e-4),
+batch_size_train = 128 frames, loss = NLL(cd) + 1.0 NLL(mono), err = cost_err(cd).
+Synthetic "TIMIT-shaped fMLLR" chunk: ~740 utterances of 150-450 frames x 40 dims,
+prepared on the GPU (context window + chunk normalisation + frame shuffle) like a real chunk.
+
+A step = one batch of the chunk: batch gather, forward, fused LogSoftmax/NLL heads, backward,
+[RCCL all-reduce of the flat gradient buffer when N > 1], optimizer — replayed from hipGraphs.
+Multi-GPU: one process per GPU (torch.distributed.run), chunk-level data parallelism: every rank
+trains its own chunk slice at the cfg batch size (weak scaling), gradients averaged every step.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense MFMA peaks (spec)
+
+
+def c1_cfg(drop="0.15"):
+    import configparser
+    base = dict(dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False", to_do="train",
+                mlp_hcgs="False", mlp_quant="False", mlp_prune="False", guided_hcgs="False",
+                apply_guided_hcgs="False", skip_regularization="False", arch_freeze="False")
+    cfg = configparser.ConfigParser()
+    cfg["architecture1"] = dict(base, arch_name="MLP_layers1", dnn_lay="1024,1024,1024,1024,1024",
+                                dnn_drop=",".join([drop] * 5), dnn_use_batchnorm="True,True,True,True,True",
+                                dnn_use_laynorm="False,False,False,False,False",
+                                dnn_act="relu,relu,relu,relu,relu", arch_lr="0.08", arch_opt="sgd",
+                                opt_momentum="0.0", opt_weight_decay="0.0", opt_dampening="0.0",
+                                opt_nesterov="False")
+    head = dict(base, arch_name="MLP_layers2", dnn_lay="1928", dnn_drop="0.0",
+                dnn_use_batchnorm="False", dnn_use_laynorm="False", dnn_act="softmax",
+                arch_lr="0.0004", arch_opt="rmsprop", opt_momentum="0.0", opt_alpha="0.95",
+                opt_eps="1e-8", opt_centered="False", opt_weight_decay="0.0")
+    cfg["architecture2"] = head
+    cfg["architecture3"] = dict(head, arch_name="MLP_layers3", dnn_lay="48")
+    cfg["model"] = {"model": "out_dnn1=compute(MLP_layers1,fmllr)\n"
+                             "out_dnn2=compute(MLP_layers2,out_dnn1)\n"
+                             "out_dnn3=compute(MLP_layers3,out_dnn1)\n"
+                             "loss_mono=cost_nll(out_dnn3,lab_mono)\n"
+                             "loss_mono_w=mult_constant(loss_mono,1.0)\n"
+                             "loss_cd=cost_nll(out_dnn2,lab_cd)\n"
+                             "loss_final=sum(loss_cd,loss_mono_w)\n"
+                             "err_final=cost_err(out_dnn2,lab_cd)"}
+    return cfg
+
+
+DIMS = (("architecture1", 440), ("architecture2", 1024), ("architecture3", 1024))
+
+
+def synth_chunk(seed, n_utt):
+    """lengths U[150,450], 40-dim N(0,1) + per-utterance offset N(0,0.3),
+    cd labels U[0,1928), mono U[1,48]."""
+    rs = np.random.RandomState(seed)
+    fea, cd, mono = {}, {}, {}
+    for i in range(n_utt):
+        k = "spk%03d_utt%05d" % (i % 462, i)
+        T = rs.randint(150, 451)
+        fea[k] = (rs.randn(T, 40) + rs.randn(1, 40) * 0.3).astype(np.float32)
+        cd[k] = rs.randint(0, 1928, size=T).astype(np.int32)
+        mono[k] = rs.randint(1, 49, size=T).astype(np.int32)
+    return fea, cd, mono
+
+
+def build(prec, batch, rank, world, seed=2234):
+    from pkc import _lib
+    from pkc.data_io import prepare_chunk
+    from pkc.engine import Engine, parse_model
+    from pkc.neural_networks import MLP
+    cfg = c1_cfg()
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    nets, opts = {}, {}
+    for sec, inp in DIMS:
+        o = cfg[sec]
+        nets[o["arch_name"]] = MLP(o, inp).cuda().train()
+        opts[o["arch_name"]] = o
+    # chunk-level DP: rank r prepares its own chunk slice (different utterances)
+    fea, cd, mono = synth_chunk(seed + 1000 * rank, 740)
+    t0 = time.time()
+    chunk = prepare_chunk(fea, [cd, mono], ["lab_cd", "lab_mono"], 5, 5, 1000,
+                          shuffle_rng=np.random.RandomState(seed), fea_name="fmllr")
+    torch.cuda.synchronize()
+    prep_s = time.time() - t0
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), chunk.fea_cols, chunk.lab_names,
+                 batch=batch, prec=prec, seed=seed + rank, grad_scale=1.0 / world)
+    eng.bind_chunk(chunk.feats, chunk.labels, chunk.n_rows)
+    return eng, chunk, prep_s, nets
+
+
+def cpu_baseline(batch, seconds=12.0):
+    """The oracle (reference algorithm restated in PyTorch-CPU eager) on the host cores."""
+    from oracle import nets as ON
+    from oracle import run as OR
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    threads = min(threads, os.cpu_count())
+    torch.set_num_threads(threads)
+    cfg = c1_cfg()
+    torch.manual_seed(0)
+    nets, opts = {}, {}
+    for sec, inp in DIMS:
+        o = cfg[sec]
+        nets[o["arch_name"]] = ON.MLP(o, inp).train()
+        opts[o["arch_name"]] = ON.make_optimizer(nets[o["arch_name"]].parameters(), o)
+    lines = OR.parse_model(cfg["model"]["model"])
+    rs = np.random.RandomState(1)
+    inp = torch.from_numpy(np.concatenate([rs.randn(batch, 440), rs.randint(0, 48, (batch, 2))],
+                                          1).astype(np.float32))
+    seq = {k: False for k in nets}
+    fc, lc = {"fmllr": (0, 440)}, {"lab_cd": 440, "lab_mono": 441}
+    for _ in range(2):
+        OR.train_step(lines, nets, opts, seq, fc, lc, inp)
+    n, t0 = 0, time.time()
+    while time.time() - t0 < seconds:
+        OR.train_step(lines, nets, opts, seq, fc, lc, inp)
+        n += 1
+    dt = time.time() - t0
+    return {"value": round(n * batch / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "%d training steps of the C1 MLP at B=%d (oracle restatement, torch-CPU eager, "
+                      "%d threads, %.1f s)" % (n, batch, threads, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--prec", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    allreduce = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+        def allreduce(t):
+            dist.all_reduce(t)
+    from pkc import _lib
+    prec = _lib.PREC_BF16 if args.prec == "bf16" else _lib.PREC_FP32
+    eng, chunk, prep_s, nets = build(prec, args.batch, rank, world)
+
+    # per-launch device times of warm eager steps -> dominant kernel + its roofline inputs
+    for _ in range(3):
+        eng.train_step(allreduce)
+    agg = {}
+    NPROF = 5
+    for _ in range(NPROF):
+        prof = eng.profile_step()
+        for label, fn, fl, nb, ms in prof:
+            a = agg.setdefault(label, [0, 0.0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += ms / NPROF
+            a[2] += fl
+            a[3] += nb
+    for v in agg.values():
+        v[0] //= NPROF
+    eng.capture(split_optimizer=world > 1)
+    for _ in range(args.warmup):
+        eng.train_step(allreduce)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.train_step(allreduce)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = float(tt.item())
+    loss_sum, err_sum = eng.chunk_totals()
+    n_done = args.warmup + args.steps
+
+    # dominant kernel: re-measure it live with HIP events on its stream (50 launches)
+    dom = max(agg.items(), key=lambda kv: kv[1][1])
+    label, (cnt, ms_tot, fl_tot, nb_tot) = dom
+    dom_launches = [p for p in prof if p[0] == label]
+    per_launch_fl = dom_launches[0][2]
+    per_launch_nb = dom_launches[0][3]
+    avg_ms = ms_tot / cnt
+    if rank == 0:
+        is_gemm = label.startswith("gemm")
+        if is_gemm and args.prec == "fp32":
+            bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS["fp32"], "TFLOP/s"
+            achieved = per_launch_fl / (avg_ms * 1e-3) / 1e12
+        else:
+            bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
+            achieved = per_launch_nb / (avg_ms * 1e-3) / 1e9
+        frames = args.steps * args.batch * world
+        res = {
+            "metric": "acoustic frames/sec (train)",
+            "value": round(frames / dt, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.prec,
+            "data": "synthetic TIMIT-shaped fMLLR chunk (740 utts x U[150,450] frames x 40 dims, "
+                    "context +-5, GPU-prepared), random-init weights",
+            "config": {"workload": "TIMIT_baselines MLP 440-5x1024-{1928,48} (TIMIT_MLP_fmllr.cfg), "
+                                   "batch_size_train=128, dropout 0.15, SGD body + RMSprop heads",
+                       "global_batch": args.batch * world, "parallelism": "dp%d" % world,
+                       "chunk_frames_per_rank": chunk.n_rows},
+            "roofline": {"kernel": label, "bound": bound, "achieved": round(achieved, 2),
+                         "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+                         "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 3),
+                         "launches_per_step": cnt,
+                         "algorithmic_bytes_per_launch": per_launch_nb,
+                         "algorithmic_flops_per_launch": per_launch_fl},
+            "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
+                                  sorted(agg.items(), key=lambda kv: -kv[1][1])},
+            "chunk_prep_s": round(prep_s, 3),
+            "mean_loss": round(loss_sum / max(1, n_done), 4),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args.batch, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+/* pkc.h — C ABI of libpkc.so, the MI355X-native (gfx950) hot path of pytorch-kaldi-CGS run_nn().
+ *
+ * Every entry point replaces an implicit PyTorch-eager op sequence of the reference (file:line
+ * cited per function, paths relative to the reference repo).  Conventions:
+ *   - plain pointers + sizes, no torch types; all device pointers are caller-owned HBM buffers,
+ *     the library never allocates device memory on a hot call;
+ *   - `stream` is a hipStream_t passed as void*; every call is asynchronous on that stream;
+ *   - return 0 (PKC_OK) or a negative status; pkc_last_error() gives a thread-local message;
+ *   - thread-safe across streams (no global mutable state besides the error string).
+ * Layouts: row-major matrices, fp32 in HBM ("parity" precision); PKC_PREC_BF16 computes the
+ * matmuls on bf16 MFMA with fp32 accumulation ("performance" precision).
+ */
+#ifndef PKC_H_
+#define PKC_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PKC_ABI_VERSION 1
+
+enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
+enum { PKC_PREC_FP32 = 0, PKC_PREC_BF16 = 1 };
+/* neural_networks.py:54-78 act_fun */
+enum { PKC_ACT_LINEAR = 0, PKC_ACT_RELU = 1, PKC_ACT_TANH = 2, PKC_ACT_SIGMOID = 3,
+       PKC_ACT_HTANH = 4, PKC_ACT_LEAKY = 5, PKC_ACT_ELU = 6 };
+enum { PKC_NORM_NONE = 0, PKC_NORM_BN_TRAIN = 1, PKC_NORM_BN_EVAL = 2 };
+enum { PKC_OPT_SGD = 0, PKC_OPT_RMSPROP = 1, PKC_OPT_ADAM = 2 };
+
+int pkc_abi_version(void);
+const char* pkc_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Matmul (replaces the cuBLAS GEMMs behind nn.Linear / F.linear in the reference:
+ * neural_networks.py:306-317 (MLP wx), 951-954 (LSTM W), 1554-1555 (liGRU W) and their autograd
+ * backward).  Computes, for split z = 0..splits-1 over the K range [z*Kc, (z+1)*Kc):
+ *     C[z*slab_stride + m*ldc + n] = sum_k A(m,k) * B(n,k)
+ * with A(m,k) = a_kcontig ? A[m*lda+k] : A[k*lda+m] and B(n,k) = b_kcontig ? B[n*ldb+k] : B[k*ldb+n].
+ * forward  Y = X W^T      : a_kcontig=1, b_kcontig=1
+ * backward dX = dY W      : a_kcontig=1, b_kcontig=0
+ * backward dW = dY^T X    : a_kcontig=0, b_kcontig=0
+ * Split-K partial slabs are summed by the consumer kernels (dense_fwd/dense_bwd/nll) in a fixed
+ * order, so results are deterministic.  splits<=0 picks a split count for the shape.
+ * ------------------------------------------------------------------------------------------- */
+int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+             const float* A, int64_t lda, const float* B, int64_t ldb,
+             float* C, int64_t ldc, int splits, int64_t slab_stride, void* stream);
+int pkc_gemm_pick_splits(int M, int N, int K);
+
+/* ---------------------------------------------------------------------------------------------
+ * Dense layer epilogue, forward (neural_networks.py:306-317: drop(act(BN(z)))) where
+ * z = sum_{s<nslab} zslab[s] + bias.  BN in training mode uses batch statistics over the M rows
+ * (biased variance for normalisation, unbiased for running_var, momentum as nn.BatchNorm1d).
+ * Outputs: out (M x N) and, for the backward, xhat (normalised z; == z when norm NONE) and the
+ * dropout keep mask (u8; NULL when p == 0).  Dropout is inverted (x*keep/(1-p)) as nn.Dropout.
+ * When keep_in != NULL the mask is read instead of generated (parity tests).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int M, N, nslab;
+  const float* zslab; int64_t slab_stride;   /* nslab partial slabs, each M x N (ldz = N) */
+  const float* bias;                          /* N or NULL */
+  int norm;                                   /* PKC_NORM_* */
+  const float* gamma; const float* beta;      /* N */
+  float* running_mean; float* running_var;    /* N (updated in BN_TRAIN) */
+  float momentum, eps;
+  float* save_mean; float* save_invstd;       /* N (written in BN_TRAIN, read in backward) */
+  int act;                                    /* PKC_ACT_* */
+  float drop_p; uint64_t seed; const int64_t* step_ctr; int64_t stream_id;
+  const uint8_t* keep_in;                     /* optional injected dropout mask (M x N) */
+  uint8_t* keep_out;                          /* M x N, may be NULL when drop_p == 0 */
+  float* xhat;                                /* M x N (BN input normalised), may be NULL in eval */
+  float* out;                                 /* M x N */
+} pkc_dense_fwd_args;
+int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream);
+/* floats of device workspace pkc_dense_fwd / pkc_dense_bwd need (per-16-row column partials) */
+int64_t pkc_dense_work_size(int M, int N);
+
+/* Dense layer backward through dropout, activation, BN and bias (autograd of the same ops).
+ * g = sum_s gslab[s] (dL/d out).  Writes dz (M x N, dL/dz), dgamma, dbeta, dbias (N).  A bias in
+ * front of BatchNorm cancels in z - mean(z): its gradient is written as exactly 0 (the reference's
+ * autograd value is rounding noise of order 1e-9 with no effect on any output). */
+typedef struct {
+  int M, N, nslab;
+  const float* gslab; int64_t slab_stride;
+  int norm, act;
+  const float* gamma; const float* beta; const float* save_invstd;
+  const float* xhat; const uint8_t* keep; float drop_p;
+  float* dz; float* dgamma; float* dbeta; float* dbias;
+} pkc_dense_bwd_args;
+int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused LogSoftmax + NLLLoss(mean) + error rate + d(loss)/d(logits) for one output head
+ * (neural_networks.py:73-74 LogSoftmax(dim=1); utils.py:1935-1952 NLLLoss; utils.py:1993-2011
+ * cost_err; autograd backward softmax - onehot).  logits = sum_s zslab[s] + bias.
+ * labels are read as float from a strided column (the reference stores them as float columns of
+ * the chunk, core.py:94, cast with .long() at utils.py:1942).  Per-row loss/err go to row_loss /
+ * row_err; dlogits = weight/M * (softmax - onehot) (NULL in forward-only mode); logp (M x N) is
+ * the head output (NULL when not needed).  prior (N, log prior) is subtracted from logp when
+ * non-NULL (core.py:242-245 posterior normalisation).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int M, N, nslab;
+  const float* zslab; int64_t slab_stride; const float* bias;
+  const int32_t* labels; int64_t label_stride;
+  float weight;
+  float* logp; const float* log_prior;
+  float* dlogits; float* row_loss; float* row_err;
+} pkc_nll_args;
+int pkc_nll_fused(const pkc_nll_args* a, void* stream);
+
+/* Reduce per-row losses of up to 8 heads: loss_final = sum_h w_h * mean(row_loss_h),
+ * err = mean(row_err_of_err_head); writes out[0]=loss_final, out[1]=err, out[2+h]=mean loss h and
+ * accumulates acc[0]+=loss_final, acc[1]+=err (core.py:251-252 loss_sum/err_sum on device). */
+int pkc_loss_finalize(int nheads, const float* const* row_loss, const float* weights, int M,
+                      const float* row_err, float* out, float* acc, void* stream);
+
+/* Column sums over rows of sum_s slabs (bias gradient of a head: autograd of + bias). */
+int pkc_colsum(int M, int N, int nslab, const float* x, int64_t slab_stride, float* out,
+               int accumulate, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Multi-tensor optimizer step (torch.optim SGD / RMSprop / Adam as built by utils.py:1833-1881,
+ * stepped at core.py:230-232) fused with the reference's per-forward weight preparation:
+ * p <- clamp(p_new * mask, -clampv, clampv) when mask / clampv>0 are given — the in-place HCGS /
+ * pattern multiply (neural_networks.py:258, 858-861, 980-983) and the in-place QuantizeLinear
+ * clamp (quantized_modules.py:79) that the next forward would otherwise apply.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  float* p; const float* g; float* s1; float* s2; float* s3; const float* mask;
+  int64_t n;
+  int kind;            /* PKC_OPT_* */
+  float lr, wd, momentum, dampening, alpha, eps, beta1, beta2, clampv;
+  int nesterov, centered, amsgrad, step;   /* step = 1-based count for this tensor */
+} pkc_opt_tensor;
+int pkc_optim_step(const pkc_opt_tensor* tensors_dev, int ntensors, const int32_t* chunk_map_dev,
+                   int nchunks, void* stream);
+/* Host helper: size of the chunk map (pairs tensor,start) for pkc_optim_step. */
+int pkc_optim_chunks(const int64_t* sizes, int ntensors, int32_t* map_out, int cap);
+
+/* p <- clamp(p * mask) (mask may be NULL, clampv <= 0 disables the clamp). */
+int pkc_apply_mask(float* p, const float* mask, int64_t n, float clampv, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Batch assembly for non-sequential models (core.py:203-205: inp = data_set[b:b+B]):
+ * copy rows [i*B, (i+1)*B) of the chunk's feature matrix and label columns into static buffers,
+ * with i read from a device counter (so the step can be replayed from a hipGraph); the counter
+ * is incremented by the last block when `advance` is set.
+ * ------------------------------------------------------------------------------------------- */
+int pkc_batch_gather(const float* feats, int64_t ld_feats, int F, const int32_t* labels, int nlab,
+                     int B, int64_t n_batches, int64_t* step_ctr, float* x_out, int32_t* lab_out,
+                     int advance, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Chunk preparation on the GPU (data_io.py:105-145 context_window + load_chunk normalisation,
+ * data_io.py:269-270 frame shuffle as a row permutation):
+ *   cw_stats : column mean / population std (fp64) of the context-expanded chunk;
+ *   cw_apply : out[r] = (expand(raw)[perm[r]] - mean) / std as fp32, labels shifted by -lab_min.
+ * raw is N x D (length-sorted concatenated utterances); expanded row r (0 <= r < N-L-R), block b
+ * (0..L+R) holds raw[(r + 2L - b) mod N] (np.roll order, future frame first).
+ * ------------------------------------------------------------------------------------------- */
+int pkc_cw_stats(const float* raw, int64_t N, int D, int L, int R, double* mean, double* std,
+                 double* work, void* stream);
+int64_t pkc_cw_stats_work_size(int64_t N, int D, int L, int R);
+int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double* mean,
+                 const double* std, const int64_t* perm, float* out, int64_t ld_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Host-side Kaldi ark I/O (data_io.py:770-806 write_mat; 645-711 read_mat_ark binary FM/DM).
+ * ------------------------------------------------------------------------------------------- */
+int pkc_ark_write_mat(const char* path, int append, const char* key, int64_t rows, int64_t cols,
+                      const float* data);
+/* Index a binary ark of FM matrices: fills up to cap entries of (data byte offset, rows, cols)
+ * and key offsets into keys_buf; returns the number of matrices or <0. */
+int64_t pkc_ark_index(const char* path, int64_t* offsets, int64_t* rows, int64_t* cols, int64_t cap,
+                      char* keys_buf, int64_t keys_cap);
+int pkc_ark_read_rows(const char* path, int64_t offset, int64_t rows, int64_t cols, float* dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PKC_H_ */

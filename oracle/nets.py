@@ -148,6 +148,9 @@ class MLP(nn.Module):
             if self.prune:
                 w.data.mul_(M.prune_mask(w, self.prune_perc[i]))
             z = self.wx[i](x)
+            if getattr(self, "debug_z", None) is not None:
+                z.retain_grad()
+                self.debug_z.append(z)
             if self.use_ln[i]:
                 z = self.ln[i](z)
             if self.use_bn[i]:

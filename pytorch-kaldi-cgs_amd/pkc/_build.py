@@ -1,0 +1,62 @@
+"""Build libpkc.so (HIP kernels for gfx950 + the C ABI) in-tree with hipcc.
+
+No cmake / no JIT cache: objects go to pytorch-kaldi-cgs_amd/build/, the shared library to
+pytorch-kaldi-cgs_amd/pkc/libpkc.so so it travels with the repository snapshot to the GPU box.
+"""
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+TOP = os.path.dirname(PKG)
+CSRC = os.path.join(TOP, "csrc")
+BUILD = os.path.join(TOP, "build")
+LIB = os.path.join(PKG, "libpkc.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PKC_ARCH", "gfx950")
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wno-unused-result"]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _deps():
+    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(TOP, "..", "include", "*.h"))
+
+
+def _compile(src):
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(d) for d in _deps()])
+    if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+        return obj
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-x", "c++", "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed on %s:\n%s" % (src, r.stderr[-6000:]))
+    return obj
+
+
+def build(verbose=False):
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n%s" % r.stderr[-6000:])
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

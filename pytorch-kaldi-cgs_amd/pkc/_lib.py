@@ -1,0 +1,118 @@
+"""ctypes binding of libpkc.so (the C ABI declared in include/pkc.h).
+
+The product path has no CPU fallback: if libpkc.so is missing or does not load, every entry point
+raises.  Build it with ``python -c "import __graft_entry__ as g; g.build()"`` (or pkc/_build.py).
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
+
+PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
+PREC_FP32, PREC_BF16 = 0, 1
+ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
+NORM_NONE, NORM_BN_TRAIN, NORM_BN_EVAL = 0, 1, 2
+OPT = {"sgd": 0, "rmsprop": 1, "adam": 2}
+
+p_f = C.POINTER(C.c_float)
+vp = C.c_void_p
+i64 = C.c_int64
+
+
+class DenseFwdArgs(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("nslab", C.c_int),
+                ("zslab", vp), ("slab_stride", i64), ("bias", vp),
+                ("norm", C.c_int), ("gamma", vp), ("beta", vp),
+                ("running_mean", vp), ("running_var", vp), ("momentum", C.c_float), ("eps", C.c_float),
+                ("save_mean", vp), ("save_invstd", vp),
+                ("act", C.c_int), ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp),
+                ("stream_id", i64), ("keep_in", vp), ("keep_out", vp), ("xhat", vp), ("out", vp)]
+
+
+class DenseBwdArgs(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("nslab", C.c_int),
+                ("gslab", vp), ("slab_stride", i64), ("norm", C.c_int), ("act", C.c_int),
+                ("gamma", vp), ("beta", vp), ("save_invstd", vp), ("xhat", vp), ("keep", vp),
+                ("drop_p", C.c_float), ("dz", vp), ("dgamma", vp), ("dbeta", vp), ("dbias", vp)]
+
+
+class NllArgs(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("nslab", C.c_int), ("zslab", vp),
+                ("slab_stride", i64), ("bias", vp), ("labels", vp), ("label_stride", i64),
+                ("weight", C.c_float), ("logp", vp), ("log_prior", vp), ("dlogits", vp),
+                ("row_loss", vp), ("row_err", vp)]
+
+
+class OptTensor(C.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("s1", vp), ("s2", vp), ("s3", vp), ("mask", vp), ("n", i64),
+                ("kind", C.c_int), ("lr", C.c_float), ("wd", C.c_float), ("momentum", C.c_float),
+                ("dampening", C.c_float), ("alpha", C.c_float), ("eps", C.c_float),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("clampv", C.c_float),
+                ("nesterov", C.c_int), ("centered", C.c_int), ("amsgrad", C.c_int), ("step", C.c_int)]
+
+
+_SIGS = {
+    "pkc_abi_version": (C.c_int, []),
+    "pkc_last_error": (C.c_char_p, []),
+    "pkc_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64, vp, i64,
+                           vp, i64, C.c_int, i64, vp]),
+    "pkc_gemm_pick_splits": (C.c_int, [C.c_int, C.c_int, C.c_int]),
+    "pkc_dense_fwd": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp]),
+    "pkc_dense_bwd": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp]),
+    "pkc_dense_work_size": (i64, [C.c_int, C.c_int]),
+    "pkc_nll_fused": (C.c_int, [C.POINTER(NllArgs), vp]),
+    "pkc_loss_finalize": (C.c_int, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp]),
+    "pkc_colsum": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, C.c_int, vp]),
+    "pkc_optim_step": (C.c_int, [vp, C.c_int, vp, C.c_int, vp]),
+    "pkc_optim_chunks": (C.c_int, [C.POINTER(i64), C.c_int, C.POINTER(C.c_int32), C.c_int]),
+    "pkc_apply_mask": (C.c_int, [vp, vp, i64, C.c_float, vp]),
+    "pkc_batch_gather": (C.c_int, [vp, i64, C.c_int, vp, C.c_int, C.c_int, i64, vp, vp, vp, C.c_int,
+                                   vp]),
+    "pkc_cw_stats": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]),
+    "pkc_cw_stats_work_size": (i64, [i64, C.c_int, C.c_int, C.c_int]),
+    "pkc_cw_apply": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, i64, vp]),
+    "pkc_ark_write_mat": (C.c_int, [C.c_char_p, C.c_int, C.c_char_p, i64, i64, vp]),
+    "pkc_ark_index": (i64, [C.c_char_p, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), i64,
+                            C.c_char_p, i64]),
+    "pkc_ark_read_rows": (C.c_int, [C.c_char_p, i64, i64, i64, vp]),
+}
+
+_lib = None
+
+
+class PkcError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpkc.so once; raise (never fall back) if it is not there."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PkcError("libpkc.so not found at %s: build it first (__graft_entry__.build())"
+                           % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.pkc_abi_version() != 1:
+            raise PkcError("libpkc ABI mismatch")
+        _lib = L
+    return _lib
+
+
+def check(status, what=""):
+    if status != PKC_OK:
+        raise PkcError("%s failed (%d): %s" % (what, status, lib().pkc_last_error().decode()))
+    return status
+
+
+def call(name, *args):
+    return check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t):
+    """Device/host pointer of a tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())

@@ -1,0 +1,171 @@
+"""Drop-in architecture plug-ins: ``arch_library = pkc.neural_networks``, ``arch_class = MLP``.
+
+Loaded exactly like the reference's classes (utils.py:1766-1779:
+``getattr(importlib.import_module(arch_library), arch_class)(options, inp_dim)``) and exposing the
+same contract: ``.out_dim``, ``forward(x)``, ``parameters()/state_dict()/load_state_dict()``,
+``train()/eval()``, and the attributes core.run_nn reads (``prune``, ``prune_parameters()``,
+``guided_hcgs``, ``apply_guided_hcgs``, ``if_pattern``, ``skip_regularization``).
+
+Parameter names, shapes and the construction-time RNG consumption follow neural_networks.py:81-243
+so a state_dict / .pkl checkpoint moves between the reference and this package unchanged and the
+same seed gives the same initial weights and HCGS masks.
+
+The math is NOT executed here: training and forward passes run through pkc.engine (HIP kernels in
+libpkc.so), driven by pkc.core.run_nn or by ``forward()`` below.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .cgs import hcgs_mask
+
+
+def strtobool(v):
+    v = str(v).strip().lower()
+    if v in ("y", "yes", "t", "true", "on", "1"):
+        return 1
+    if v in ("n", "no", "f", "false", "off", "0"):
+        return 0
+    raise ValueError("invalid truth value %r" % v)
+
+
+def _lst(opts, key, f=str):
+    return [f(x) for x in opts[key].split(",")]
+
+
+class LayerNorm(nn.Module):
+    """Parameter holder with the reference's names (neural_networks.py:40-51)."""
+
+    def __init__(self, features, eps=1e-6):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(features))
+        self.beta = nn.Parameter(torch.zeros(features))
+        self.eps = eps
+
+
+class _Mask(nn.Module):
+    """HCGS.HCGS: a non-learnable ``mask`` Parameter of shape (out, in) (HCGS.py:24-28)."""
+
+    def __init__(self, mask):
+        super().__init__()
+        self.mask = nn.Parameter(torch.from_numpy(mask))
+
+
+class _QLinear(nn.Module):
+    """Parameter layout + init draws of QuantizeLinear (quantized_modules.py:184-205)."""
+
+    def __init__(self, fin, fout, bits, bias, inp_bits=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.Tensor(fout, fin))
+        self.bias = nn.Parameter(torch.Tensor(fout)) if bias else None
+        s = 1.0 / math.sqrt(fin)
+        self.weight.data.uniform_(-s, s)
+        if self.bias is not None:
+            self.bias.data.uniform_(-s, s)
+        self.numBits = bits
+        self.inp_quant = inp_bits
+
+
+class MLP(nn.Module):
+    """neural_networks.py:81-361 (options per proto/MLP.proto + the CGS keys)."""
+
+    seq_model = False
+
+    def __init__(self, options, inp_dim):
+        super().__init__()
+        o = options
+        self.input_dim = inp_dim
+        self.dnn_lay = _lst(o, "dnn_lay", int)
+        self.dnn_drop = _lst(o, "dnn_drop", float)
+        self.dnn_use_batchnorm = _lst(o, "dnn_use_batchnorm", strtobool)
+        self.dnn_use_laynorm = _lst(o, "dnn_use_laynorm", strtobool)
+        self.dnn_use_laynorm_inp = strtobool(o["dnn_use_laynorm_inp"])
+        self.dnn_use_batchnorm_inp = strtobool(o["dnn_use_batchnorm_inp"])
+        self.dnn_act = _lst(o, "dnn_act")
+        self.to_do = o.get("to_do", "train")
+        self.mlp_hcgs = strtobool(o.get("mlp_hcgs", "False"))
+        self.hcgs_block = _lst(o, "hcgs_block", int) if "hcgs_block" in o else []
+        self.hcgs_sparse = _lst(o, "hcgs_sparse", float) if "hcgs_sparse" in o else []
+        self.mlp_quant = strtobool(o.get("mlp_quant", "False"))
+        self.param_quant = _lst(o, "param_quant", int) if "param_quant" in o else [8]
+        self.mlp_quant_inp = strtobool(o.get("mlp_quant_inp", "False"))
+        self.inp_quant = _lst(o, "inp_quant", int) if "inp_quant" in o else [16]
+        self.prune = strtobool(o.get("mlp_prune", "False"))
+        self.prune_perc = _lst(o, "mlp_prune_perc", float) if "mlp_prune_perc" in o else [0.0]
+        self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
+        self.guided_hcgs = strtobool(o.get("guided_hcgs", "False"))
+        self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
+        self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
+        self.arch_name = o.get("arch_name", "MLP")
+        if self.guided_hcgs:
+            raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
+        if self.if_pattern:
+            self.pattern, self.pattern_mask = [], []
+
+        if self.mlp_hcgs:                    # registered first, as neural_networks.py:151-152
+            self.hcgs = nn.ModuleList()
+        self.wx, self.bn, self.ln = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        if self.dnn_use_laynorm_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.dnn_use_batchnorm_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.dnn_lay):
+            self.ln.append(LayerNorm(n))
+            self.bn.append(nn.BatchNorm1d(n, momentum=0.05))
+            add_bias = not (self.dnn_use_laynorm[i] or self.dnn_use_batchnorm[i])
+            if self.mlp_quant:
+                lin = _QLinear(cur, n, self.param_quant[i], add_bias,
+                               self.inp_quant[0] if self.mlp_quant_inp else None)
+            else:
+                lin = nn.Linear(cur, n, bias=add_bias)          # consumes the torch RNG as the ref
+            self.wx.append(lin)
+            if self.mlp_hcgs:
+                self.hcgs.append(_Mask(hcgs_mask(n, cur, self.hcgs_block, self.hcgs_sparse)))
+            s = np.sqrt(0.01 / (cur + n))                        # neural_networks.py:233-235
+            lin.weight = nn.Parameter(torch.Tensor(n, cur).uniform_(-s, s))
+            lin.bias = nn.Parameter(torch.zeros(n))
+            cur = n
+        self.out_dim = cur
+        self._engine = None
+
+    # --------------------------------------------------------------------- reference hooks
+    def prune_parameters(self):
+        raise NotImplementedError("magnitude pruning (quantized_modules.prune) is not on the "
+                                  "pkc MLP path yet")
+
+    def apply_ghcgs(self):
+        raise NotImplementedError("guided HCGS is outside the pkc hot path")
+
+    def layer_specs(self):
+        """Per-layer description consumed by pkc.engine."""
+        specs = []
+        for i, n in enumerate(self.dnn_lay):
+            specs.append(dict(out=n, act=self.dnn_act[i], bn=bool(self.dnn_use_batchnorm[i]),
+                              ln=bool(self.dnn_use_laynorm[i]), drop=self.dnn_drop[i],
+                              W=self.wx[i].weight, b=self.wx[i].bias, gamma=self.bn[i].weight,
+                              beta=self.bn[i].bias, rm=self.bn[i].running_mean,
+                              rv=self.bn[i].running_var, nbt=self.bn[i].num_batches_tracked,
+                              mask=self.hcgs[i].mask if self.mlp_hcgs else None,
+                              quant=self.param_quant[i] if self.mlp_quant else 0,
+                              inp_quant=self.inp_quant[0] if self.mlp_quant_inp else 0))
+        return specs
+
+    def check_supported(self):
+        if self.dnn_use_laynorm_inp or self.dnn_use_batchnorm_inp:
+            raise NotImplementedError("input LayerNorm/BatchNorm is not on the pkc MLP path yet")
+        if any(self.dnn_use_laynorm):
+            raise NotImplementedError("LayerNorm layers are not on the pkc MLP path yet")
+        if self.mlp_quant or self.prune or self.if_pattern:
+            raise NotImplementedError("quantised / pruned / pattern MLP layers are not on the pkc "
+                                      "MLP path yet")
+
+    def forward(self, x):
+        """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
+        ``self.training`` is False, batch statistics otherwise; no autograd)."""
+        from .engine import ModuleRunner
+        if self._engine is None or self._engine.rows != x.shape[0]:
+            self._engine = ModuleRunner(self, x.shape[0], x.shape[1])
+        return self._engine.forward(x, train=self.training)

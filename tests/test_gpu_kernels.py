@@ -1,0 +1,260 @@
+"""GPU parity of the individual HIP kernels (through the C ABI) against PyTorch-CPU references of
+the same ops (fp32 / fp64)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.fixture(scope="module")
+def L():
+    from pkc import _lib
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    _lib.lib()
+    return _lib
+
+
+GEMM_SHAPES = [(128, 1024, 1024), (128, 1928, 1024), (128, 48, 1024), (128, 1024, 440),
+               (37, 70, 45), (16, 96, 32), (64, 64, 32), (1, 5, 3), (200, 130, 260)]
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("orient", ["nt", "nn", "tn"])
+def test_gemm(L, prec, M, N, K, orient):
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    # logical C[M,N] = sum_k A(m,k) B(n,k)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
+    Ast = A if akc else A.t().contiguous()      # stored (M,K) or (K,M)
+    Bst = B if bkc else B.t().contiguous()
+    if prec == 1:
+        A = A.bfloat16().float()
+        B = B.bfloat16().float()
+    ref = (A.double() @ B.double().t()).float()
+    splits = L.lib().pkc_gemm_pick_splits(M, N, K)
+    Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+    Cd = torch.full((splits, M, N), float("nan"), device=DEV)
+    L.call("pkc_gemm", prec, akc, bkc, M, N, K, L.ptr(Ad), Ast.shape[1], L.ptr(Bd), Bst.shape[1],
+           L.ptr(Cd), N, splits, M * N, _s())
+    out = Cd.sum(0).cpu()
+    tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=tol)
+
+
+def test_gemm_unaligned_lda(L):
+    """First layer reading straight out of a (N, 442) chunk matrix: scalar-load path."""
+    M, N, K = 33, 64, 440
+    X = torch.randn(M, 442)
+    W = torch.randn(N, K)
+    ref = X[:, :K].double() @ W.double().t()
+    Xd, Wd = X.to(DEV), W.to(DEV)
+    Cd = torch.zeros(M, N, device=DEV)
+    L.call("pkc_gemm", 0, 1, 1, M, N, K, L.ptr(Xd), 442, L.ptr(Wd), K, L.ptr(Cd), N, 1, 0, _s())
+    torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-5, atol=1e-4)
+
+
+def _bn_ref(z, gamma, beta, act, keep, p):
+    zz = z.clone().requires_grad_(True)
+    gg = gamma.clone().requires_grad_(True)
+    bb = beta.clone().requires_grad_(True)
+    y = torch.nn.functional.batch_norm(zz, None, None, gg, bb, training=True, momentum=0.05, eps=1e-5)
+    a = {"relu": torch.relu, "tanh": torch.tanh, "sigmoid": torch.sigmoid, "linear": lambda t: t}[act](y)
+    if p > 0:
+        a = a * keep / (1 - p)
+    return zz, gg, bb, a
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "sigmoid", "linear"])
+@pytest.mark.parametrize("p", [0.0, 0.15])
+@pytest.mark.parametrize("M,N,S", [(128, 1024, 4), (16, 48, 1), (50, 70, 3)])
+def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
+    g = torch.Generator().manual_seed(M + N + S)
+    slabs = torch.randn(S, M, N, generator=g)
+    bias = torch.randn(N, generator=g) * 0.1
+    gamma = torch.rand(N, generator=g) + 0.5
+    beta = torch.randn(N, generator=g) * 0.1
+    keep = (torch.rand(M, N, generator=g) > p).to(torch.uint8)
+    z = slabs.sum(0) + bias
+    zz, gg, bb, a = _bn_ref(z, gamma, beta, act, keep.float(), p)
+    gout = torch.randn(2, M, N, generator=g)
+    a.backward(gout.sum(0))
+    d = {k: v.to(DEV) for k, v in dict(slabs=slabs, bias=bias, gamma=gamma, beta=beta,
+                                        keep=keep, gout=gout).items()}
+    rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+    sm, si = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+    xhat, out = torch.zeros(M, N, device=DEV), torch.zeros(M, N, device=DEV)
+    a_ = L.DenseFwdArgs(M=M, N=N, nslab=S, zslab=d["slabs"].data_ptr(), slab_stride=M * N,
+                        bias=d["bias"].data_ptr(), norm=L.NORM_BN_TRAIN, gamma=d["gamma"].data_ptr(),
+                        beta=d["beta"].data_ptr(), running_mean=rm.data_ptr(),
+                        running_var=rv.data_ptr(), momentum=0.05, eps=1e-5, save_mean=sm.data_ptr(),
+                        save_invstd=si.data_ptr(), act=L.ACT[act], drop_p=p, seed=1, step_ctr=None,
+                        stream_id=0, keep_in=d["keep"].data_ptr() if p > 0 else None,
+                        keep_out=None, xhat=xhat.data_ptr(), out=out.data_ptr())
+    work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
+    L.call("pkc_dense_fwd", C.byref(a_), L.ptr(work), _s())
+    torch.testing.assert_close(out.cpu(), a.detach(), rtol=1e-4, atol=1e-5)
+    mu = z.mean(0)
+    var = z.var(0, unbiased=True)
+    torch.testing.assert_close(rm.cpu(), 0.05 * mu, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(rv.cpu(), 0.95 + 0.05 * var, rtol=1e-4, atol=1e-6)
+    dz = torch.zeros(M, N, device=DEV)
+    dgam, dbet, dbias = (torch.zeros(N, device=DEV) for _ in range(3))
+    b_ = L.DenseBwdArgs(M=M, N=N, nslab=2, gslab=d["gout"].data_ptr(), slab_stride=M * N,
+                        norm=L.NORM_BN_TRAIN, act=L.ACT[act], gamma=d["gamma"].data_ptr(),
+                        beta=d["beta"].data_ptr(), save_invstd=si.data_ptr(), xhat=xhat.data_ptr(),
+                        keep=d["keep"].data_ptr() if p > 0 else None, drop_p=p, dz=dz.data_ptr(),
+                        dgamma=dgam.data_ptr(), dbeta=dbet.data_ptr(), dbias=dbias.data_ptr())
+    L.call("pkc_dense_bwd", C.byref(b_), L.ptr(work), _s())
+    torch.testing.assert_close(dz.cpu(), zz.grad, rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(dgam.cpu(), gg.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dbet.cpu(), bb.grad, rtol=1e-4, atol=1e-4)
+    assert (dbias.cpu() == 0).all()          # bias before BN: exact zero gradient
+    assert zz.grad.sum(0).abs().max() < 1e-4  # ... which autograd reproduces up to rounding
+
+
+def test_dense_dropout_rate_and_determinism(L):
+    M, N, p = 256, 512, 0.15
+    z = torch.randn(1, M, N, device=DEV)
+    ctr = torch.tensor([3, 0], dtype=torch.int64, device=DEV)
+    outs, keeps = [], []
+    for _ in range(2):
+        keep = torch.zeros(M, N, dtype=torch.uint8, device=DEV)
+        out = torch.zeros(M, N, device=DEV)
+        a_ = L.DenseFwdArgs(M=M, N=N, nslab=1, zslab=z.data_ptr(), slab_stride=M * N, bias=None,
+                            norm=L.NORM_NONE, act=L.ACT["linear"], drop_p=p, seed=7,
+                            step_ctr=ctr.data_ptr(), stream_id=5, keep_out=keep.data_ptr(),
+                            out=out.data_ptr())
+        L.call("pkc_dense_fwd", C.byref(a_), None, _s())
+        outs.append(out.cpu())
+        keeps.append(keep.cpu())
+    assert torch.equal(keeps[0], keeps[1])
+    rate = 1 - keeps[0].float().mean().item()
+    assert abs(rate - p) < 0.01
+    k = keeps[0].bool()
+    torch.testing.assert_close(outs[0][k], z[0].cpu()[k] / (1 - p))
+    assert (outs[0][~k] == 0).all()
+
+
+@pytest.mark.parametrize("M,N,S", [(128, 1928, 4), (128, 48, 2), (7, 100, 1)])
+def test_nll_fused(L, M, N, S):
+    g = torch.Generator().manual_seed(N)
+    slabs = torch.randn(S, M, N, generator=g) * 3
+    bias = torch.randn(N, generator=g)
+    lab = torch.randint(0, N, (M, 2), generator=g, dtype=torch.int32)
+    z = (slabs.sum(0) + bias).requires_grad_(True)
+    lp = torch.log_softmax(z, 1)
+    loss = torch.nn.functional.nll_loss(lp, lab[:, 1].long())
+    (0.7 * loss).backward()
+    err = (lp.argmax(1) != lab[:, 1].long()).float().mean()
+    d = [t.to(DEV) for t in (slabs, bias, lab)]
+    logp, dl = torch.zeros(M, N, device=DEV), torch.zeros(M, N, device=DEV)
+    rl, re_ = torch.zeros(M, device=DEV), torch.zeros(M, device=DEV)
+    a = L.NllArgs(M=M, N=N, nslab=S, zslab=d[0].data_ptr(), slab_stride=M * N, bias=d[1].data_ptr(),
+                  labels=d[2].data_ptr() + 4, label_stride=2, weight=0.7, logp=logp.data_ptr(),
+                  log_prior=None, dlogits=dl.data_ptr(), row_loss=rl.data_ptr(), row_err=re_.data_ptr())
+    L.call("pkc_nll_fused", C.byref(a), _s())
+    torch.testing.assert_close(logp.cpu(), lp.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dl.cpu(), z.grad, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(rl.mean().cpu(), loss.detach(), rtol=1e-5, atol=1e-6)
+    assert abs(re_.mean().item() - err.item()) < 1e-6
+    out, acc = torch.zeros(3, device=DEV), torch.zeros(2, device=DEV)
+    ptrs = torch.tensor([rl.data_ptr()], dtype=torch.int64, device=DEV)
+    w = torch.tensor([0.7], device=DEV)
+    L.call("pkc_loss_finalize", 1, L.ptr(ptrs), L.ptr(w), M, L.ptr(re_), L.ptr(out), L.ptr(acc), _s())
+    torch.testing.assert_close(out[0].cpu(), 0.7 * loss.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "rmsprop", "adam", "sgd_mom"])
+def test_optimizer_step_matches_torch(L, kind):
+    g = torch.Generator().manual_seed(3)
+    sizes = [1000, 5000, 3]
+    ps = [torch.randn(n, generator=g) for n in sizes]
+    masks = [None, (torch.rand(5000, generator=g) > 0.5).float(), None]
+    grads = [[torch.randn(n, generator=g) for n in sizes] for _ in range(3)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    if kind == "sgd":
+        opt = torch.optim.SGD(ref, lr=0.08)
+    elif kind == "sgd_mom":
+        opt = torch.optim.SGD(ref, lr=0.05, momentum=0.9, nesterov=True, weight_decay=1e-3)
+    elif kind == "rmsprop":
+        opt = torch.optim.RMSprop(ref, lr=4e-4, alpha=0.95, eps=1e-8)
+    else:
+        opt = torch.optim.Adam(ref, lr=1e-3, betas=(0.9, 0.98), eps=1e-8)
+    dps = [p.to(DEV) for p in ps]
+    for i, m in enumerate(masks):
+        if m is not None:
+            dps[i].mul_(m.to(DEV))
+            with torch.no_grad():
+                ref[i].mul_(m)
+    dgs = [torch.zeros(n, device=DEV) for n in sizes]
+    st = [[torch.zeros(n, device=DEV) for n in sizes] for _ in range(3)]
+    dmask = [m.to(DEV) if m is not None else None for m in masks]
+    n = len(sizes)
+    szs = (C.c_int64 * n)(*sizes)
+    nch = L.lib().pkc_optim_chunks(szs, n, None, 0)
+    cmap = (C.c_int32 * (2 * nch))()
+    L.lib().pkc_optim_chunks(szs, n, cmap, nch)
+    dmap = torch.from_numpy(np.frombuffer(cmap, dtype=np.int32).copy()).to(DEV)
+    for step in range(3):
+        arr = (L.OptTensor * n)()
+        for i in range(n):
+            t = arr[i]
+            t.p, t.g, t.s1, t.s2, t.s3 = (dps[i].data_ptr(), dgs[i].data_ptr(), st[0][i].data_ptr(),
+                                          st[1][i].data_ptr(), st[2][i].data_ptr())
+            t.mask = dmask[i].data_ptr() if dmask[i] is not None else None
+            t.n = sizes[i]
+            t.step = step + 1
+            if kind == "sgd":
+                t.kind, t.lr = 0, 0.08
+            elif kind == "sgd_mom":
+                t.kind, t.lr, t.momentum, t.nesterov, t.wd = 0, 0.05, 0.9, 1, 1e-3
+            elif kind == "rmsprop":
+                t.kind, t.lr, t.alpha, t.eps = 1, 4e-4, 0.95, 1e-8
+            else:
+                t.kind, t.lr, t.beta1, t.beta2, t.eps = 2, 1e-3, 0.9, 0.98, 1e-8
+        desc = torch.frombuffer(bytearray(C.string_at(arr, C.sizeof(arr))), dtype=torch.uint8).to(DEV)
+        for i in range(n):
+            dgs[i].copy_(grads[step][i].to(DEV))
+            ref[i].grad = grads[step][i].clone()
+        L.call("pkc_optim_step", L.ptr(desc), n, L.ptr(dmap), nch, _s())
+        opt.step()
+        with torch.no_grad():
+            for i, m in enumerate(masks):
+                if m is not None:
+                    ref[i].mul_(m)
+    for i in range(n):
+        torch.testing.assert_close(dps[i].cpu(), ref[i].detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("L_,R_", [(5, 5), (2, 1), (0, 0), (1, 3)])
+def test_context_window_chunk_prep(L, L_, R_):
+    """pkc_cw_stats/pkc_cw_apply vs the oracle's numpy float64 load_chunk (+ shuffle)."""
+    from oracle import loader as OL
+    from pkc import data_io
+    rs = np.random.RandomState(L_ * 10 + R_)
+    fea = {"u%02d" % i: (rs.randn(rs.randint(20, 90), 40) + rs.randn(1, 40)).astype(np.float32)
+           for i in range(9)}
+    cd = {k: rs.randint(2, 1928, size=len(v)).astype(np.int32) for k, v in fea.items()}
+    mono = {k: rs.randint(1, 49, size=len(v)).astype(np.int32) for k, v in fea.items()}
+    names, end, fcols, lcols, ref = OL.read_lab_fea([("fmllr", fea, L_, R_)],
+                                                    [("lab_cd", cd), ("lab_mono", mono)], False,
+                                                    rng=np.random.RandomState(2234))
+    ch = data_io.prepare_chunk(fea, [cd, mono], ["lab_cd", "lab_mono"], L_, R_, 1000,
+                               shuffle_rng=np.random.RandomState(2234), fea_name="fmllr")
+    assert ch.names == names
+    np.testing.assert_array_equal(ch.end_index, end)
+    C_ = 40 * (L_ + R_ + 1)
+    np.testing.assert_allclose(ch.feats.cpu().numpy(), ref[:, :C_].astype(np.float32), rtol=1e-6,
+                               atol=1e-6)
+    np.testing.assert_array_equal(ch.labels.cpu().numpy(), ref[:, C_:].astype(np.int32))

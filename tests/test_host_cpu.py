@@ -1,0 +1,110 @@
+"""CPU-only checks of the product's host side: the C ABI library loads and exports every symbol
+declared in include/pkc.h, host-side mask generation and module construction match the reference
+(golden vectors), and the host ark writer/reader is byte-compatible with data_io.write_mat."""
+import configparser
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT
+from cases import build_mlp_config
+
+HDR = os.path.join(ROOT, "include", "pkc.h")
+
+
+def G(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def declared_symbols():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int64_t|int|const char\*)\s+(pkc_\w+)\(", txt, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "pkc_gemm" in syms and "pkc_optim_step" in syms and len(syms) >= 18
+
+
+def test_library_exports_every_declared_symbol():
+    from pkc import _lib
+    lib = _lib.lib()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    assert lib.pkc_abi_version() == 1
+
+
+def test_gemm_split_policy():
+    from pkc import _lib
+    lib = _lib.lib()
+    for M, N, K in [(128, 1024, 1024), (128, 1928, 1024), (128, 48, 1024), (1024, 440, 128),
+                    (7, 9, 5), (128, 1024, 440)]:
+        s = lib.pkc_gemm_pick_splits(M, N, K)
+        assert 1 <= s <= 16
+        kchunk = -(-(-(-K // s)) // 32) * 32
+        assert (s - 1) * kchunk < K      # every split owns a non-empty k range
+
+
+HCGS = [((1024, 440), [128, 4], [25, 62.5], 1), ((1024, 1024), [128, 4], [25, 62.5], 2),
+        ((512, 512), [32, 2], [75, 75], 3), ((512, 440), [32, 2], [75, 75], 4),
+        ((550, 550), [64, 4], [50, 25], 5), ((550, 440), [64, 4], [50, 25], 6),
+        ((100, 70), [16, 4], [50, 50], 7), ((64, 48), [16], [50], 8),
+        ((96, 40), [32, 8, 2], [50, 50, 50], 9)]
+
+
+@pytest.mark.parametrize("i", range(len(HCGS)))
+def test_product_hcgs_mask_matches_reference(i):
+    from pkc.cgs import hcgs_mask
+    g = G("hcgs.npz")
+    (r, c), bl, dr, seed = HCGS[i]
+    m = hcgs_mask(r, c, bl, dr, rng=np.random.RandomState(seed))
+    ref = np.unpackbits(g["m%d" % i])[:r * c].reshape(r, c)
+    np.testing.assert_array_equal(m.astype(np.uint8), ref)
+
+
+@pytest.mark.parametrize("variant", ["plain", "hcgs", "quant", "ln"])
+def test_product_mlp_init_matches_reference(variant):
+    """Same seed -> same weights, masks, BN buffers and state_dict keys as the reference."""
+    from pkc.neural_networks import MLP
+    g = G("mlp_%s.npz" % variant)
+    cfg = build_mlp_config(variant)
+    torch.manual_seed(2234)
+    np.random.seed(2234)
+    for sec, inp in (("architecture1", 40), ("architecture2", 32), ("architecture3", 32)):
+        o = cfg[sec]
+        net = MLP(o, inp)
+        sd = net.state_dict()
+        ref_keys = sorted(k.split("/", 2)[2] for k in g.files if k.startswith("init/%s/" % o["arch_name"]))
+        assert sorted(sd.keys()) == ref_keys
+        for k, v in sd.items():
+            np.testing.assert_array_equal(v.numpy(), g["init/%s/%s" % (o["arch_name"], k)], err_msg=k)
+
+
+def test_ark_writer_bytes_match_reference(tmp_path):
+    from pkc import data_io
+    gi = G("post_inputs.npz")
+    counts = gi["counts"].astype(np.float32)
+    path = str(tmp_path / "post.ark")
+    for i, (k, m) in enumerate(zip(["spkA_utt1", "spkB_utt2"], [gi["m0"], gi["m1"]])):
+        data_io.write_mat_path(path, m - np.log(counts / np.sum(counts)), k, append=i > 0)
+    with open(os.path.join(GOLDEN, "post.ark"), "rb") as f:
+        ref = f.read()
+    with open(path, "rb") as f:
+        assert f.read() == ref
+
+
+def test_ark_reader_roundtrip(tmp_path):
+    from pkc import data_io
+    rs = np.random.RandomState(0)
+    mats = {"a_1": rs.randn(5, 7).astype(np.float32), "b_2": rs.randn(1, 7).astype(np.float32),
+            "c_3": rs.randn(11, 7).astype(np.float32)}
+    path = str(tmp_path / "f.ark")
+    for i, (k, m) in enumerate(mats.items()):
+        data_io.write_mat_path(path, m, k, append=i > 0)
+    got = dict(data_io.read_mat_ark_path(path))
+    assert list(got) == list(mats)
+    for k in mats:
+        np.testing.assert_array_equal(got[k], mats[k])
