@@ -1,0 +1,274 @@
+"""pkc.core.run_nn — drop-in for the reference's core.run_nn (core.py:24-362).
+
+Same signature, same return value ([data_name, data_set, data_end_index, fea_dict, lab_dict,
+arch_dict], patterns, pattern_masks) and the same side files:
+  * ``<info>``: [results] loss= err= elapsed_time_chunk= (core.py:338-345; forward: time only),
+  * one ``<info>_<arch>.pkl`` per architecture in train mode ({'model_par', 'optimizer_par'},
+    core.py:285-322),
+  * ``<info>_<out>_to_decode.ark`` posteriors in forward mode (core.py:134-145, 238-249) in the
+    byte format of data_io.write_mat, consumed unchanged by kaldi_decoding_scripts/decode_dnn.sh.
+
+The chunk lives in HBM between calls: ``data_set`` is a pkc.data_io.Chunk (the reference returns a
+CUDA tensor; run_exp only hands it back to the next call).  Everything per batch runs on the HIP
+kernels through pkc.engine; the host only parses arks and bookkeeps utterances.
+"""
+import configparser
+import importlib
+import os
+import random
+import re
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+from . import data_io as D
+from . import neural_networks as NN
+from .engine import Engine, ForwardRunner, parse_model
+from .neural_networks import strtobool
+
+
+def _cfg_item2sec(config, field, value):
+    for sec in config.sections():
+        if field in config[sec] and config[sec][field] == value:
+            return sec
+    raise KeyError("%s=%s not found in cfg" % (field, value))
+
+
+def dict_fea_lab_arch(config):
+    """utils.py:1611-1711: feature / label / architecture descriptors used by the [model]."""
+    lines = parse_model(config["model"]["model"])
+    fea_field = config["data_chunk"]["fea"]
+    lab_field = config["data_chunk"]["lab"]
+    fea_names = re.findall(r"fea_name=(.*)\n", fea_field.replace(" ", "") + "\n")
+    lab_names = re.findall(r"lab_name=(.*)\n", lab_field.replace(" ", "") + "\n")
+    fea_dict, lab_dict, arch_dict = {}, {}, {}
+    for out, op, a, b in lines:
+        for inp in (a, b):
+            if inp in fea_names and inp not in fea_dict:
+                m = re.findall("fea_name=" + inp + r"\nfea_lst=(.*)\nfea_opts=(.*)\ncw_left=(.*)\ncw_right=(.*)",
+                               fea_field)[0]
+                fea_dict[inp] = [inp] + list(m)
+            if inp in lab_names and inp not in lab_dict:
+                m = re.findall("lab_name=" + inp + r"\nlab_folder=(.*)\nlab_opts=(.*)", lab_field)[0]
+                lab_dict[inp] = [inp] + list(m)
+        if op == "compute" and a not in arch_dict:
+            sec = _cfg_item2sec(config, "arch_name", a)
+            arch_dict[a] = [sec, a, strtobool(config[sec]["arch_seq_model"])]
+    return fea_dict, lab_dict, arch_dict
+
+
+def _read_features(fea_scp, fea_opts, output_folder):
+    """Feature stream of one chunk: ``copy-feats scp:<scp> ark:- |<opts>`` as data_io.py:18.
+    Without Kaldi on the box, an scp of binary arks ("key path:offset" or "key path") is read
+    directly; with fea_opts set the Kaldi pipeline is run exactly as the reference does."""
+    if fea_opts.strip():
+        import subprocess
+        cmd = "copy-feats scp:" + fea_scp + " ark:- |" + fea_opts
+        out = subprocess.run(cmd, shell=True, capture_output=True, check=True).stdout
+        return dict(D.parse_mat_ark_bytes(out))
+    feats = {}
+    by_file = {}
+    with open(fea_scp) as f:
+        for line in f:
+            if not line.strip():
+                continue
+            key, spec = line.split(None, 1)
+            path = spec.strip().rsplit(":", 1)[0] if re.search(r":\d+$", spec.strip()) else spec.strip()
+            by_file.setdefault(path, set()).add(key)
+    for path, keys in by_file.items():
+        for k, m in D.read_mat_ark_path(path):
+            if k in keys:
+                feats[k] = m
+    return feats
+
+
+def _read_labels(lab_folder, lab_opts, output_folder):
+    """``gunzip -c ali*.gz | <lab_opts> final.mdl ark:- ark:-|`` (data_io.py:19-21); a
+    pre-converted ``<lab_folder>/<lab_opts-tag>.ark`` binary int-vector ark is read directly."""
+    tag = "pdf" if "pdf" in lab_opts else "phones"
+    pre = os.path.join(lab_folder, "ali_%s.ark" % tag)
+    if os.path.exists(pre):
+        return dict(D.read_vec_int_ark_path(pre))
+    import subprocess
+    cmd = "gunzip -c " + lab_folder + "/ali*.gz | " + lab_opts + " " + lab_folder + "/final.mdl ark:- ark:-|"
+    out = subprocess.run(cmd[:-1], shell=True, capture_output=True, check=True).stdout
+    return dict(D.parse_vec_int_ark_bytes(out))
+
+
+def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
+    """data_io.read_lab_fea (data_io.py:155-282) on the host side: parse arks, hand raw frames to
+    the GPU chunk preparation.  Appends the same six items to shared_list; item 5 is a Chunk."""
+    config = configparser.ConfigParser()
+    config.read(cfg_file)
+    to_do = config["exp"]["to_do"]
+    max_seq = {"train": int(config["batches"].get("max_seq_length_train", "-1")),
+               "valid": int(config["batches"].get("max_seq_length_valid", "-1"))}.get(to_do, -1)
+    fea_dict, lab_dict, arch_dict = dict_fea_lab_arch(config)
+    if len(fea_dict) != 1:
+        raise NotImplementedError("pkc chunk preparation handles one feature stream per model")
+    (fname, fd), = fea_dict.items()
+    fea = _read_features(fd[1], fd[2], output_folder)
+    labs, lab_names = [], []
+    if not fea_only:
+        for lname, ld in lab_dict.items():
+            labs.append(_read_labels(ld[1], ld[2], output_folder))
+            lab_names.append(lname)
+    seq = any(a[2] for a in arch_dict.values())
+    rng = np.random if (not seq and to_do != "forward") else None
+    shared_list.append(("raw", fea, labs, lab_names, int(fd[3]), int(fd[4]), max_seq, rng, fname))
+    shared_list.append(None)
+    shared_list.append(fea_dict)
+    shared_list.append(lab_dict)
+    shared_list.append(arch_dict)
+    shared_list.append(None)
+
+
+def _finish_chunk(shared_list):
+    """GPU half of the loader: context window + normalisation + shuffle (pkc_cw_*)."""
+    _, fea, labs, lab_names, L, R, max_seq, rng, fname = shared_list[0]
+    ch = D.prepare_chunk(fea, labs, lab_names, L, R, max_seq, shuffle_rng=rng, fea_name=fname)
+    fea_dict, lab_dict = shared_list[2], shared_list[3]
+    c0, c1 = ch.fea_cols[fname]
+    fea_dict[fname] = fea_dict[fname][:5] + [c0, c1, c1 - c0]
+    for i, ln in enumerate(lab_names):
+        lab_dict[ln] = lab_dict[ln][:3] + [c1 + i]
+    return [ch.names, ch, ch.end_index, fea_dict, lab_dict, shared_list[4]]
+
+
+def model_init(config, arch_dict, fea_dims, to_do):
+    """utils.model_init (utils.py:1749-1830) restricted to pkc architectures."""
+    nns = {}
+    out_dims = dict(fea_dims)
+    for out, op, a, b in parse_model(config["model"]["model"]):
+        if op != "compute":
+            continue
+        sec = arch_dict[a][0]
+        o = config[sec]
+        lib = o.get("arch_library", "pkc.neural_networks")
+        cls_name = o["arch_class"]
+        mod = importlib.import_module(lib) if lib.startswith("pkc") else NN
+        cls = getattr(mod, cls_name, None) or getattr(NN, cls_name)
+        config.set(sec, "use_cuda", config["exp"].get("use_cuda", "True"))
+        config.set(sec, "to_do", to_do)
+        net = cls(config[sec], out_dims[b])
+        net.cuda()
+        if to_do == "train" and not strtobool(o.get("arch_freeze", "False")):
+            net.train()
+        else:
+            net.eval()
+        nns[a] = net
+        out_dims[out] = net.out_dim
+    return nns
+
+
+def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, cfg_file,
+           processed_first, next_config_file, if_prune=False, patterns=None, pattern_masks=None,
+           if_apply_ghcgs=False, if_pattern_search=False):
+    patterns = {} if patterns is None else patterns
+    pattern_masks = {} if pattern_masks is None else pattern_masks
+    if not os.path.exists(cfg_file):
+        sys.stderr.write("ERROR: The config file %s does not exist!\n" % cfg_file)
+        sys.exit(0)
+    config = configparser.ConfigParser()
+    config.read(cfg_file)
+    seed = int(config["exp"]["seed"])
+    torch.manual_seed(seed)
+    random.seed(seed)
+    np.random.seed(seed)
+    output_folder = config["exp"]["out_folder"]
+    to_do = config["exp"]["to_do"]
+    info_file = config["exp"]["out_info"]
+    is_production = strtobool(config["exp"].get("production", "False"))
+    forward_outs = config["forward"]["forward_out"].split(",")
+    forward_norm = list(map(strtobool, config["forward"]["normalize_posteriors"].split(",")))
+    forward_counts = config["forward"]["normalize_with_counts_from"].split(",")
+    require_dec = list(map(strtobool, config["forward"]["require_decoding"].split(",")))
+    batch_size = {"train": int(config["batches"]["batch_size_train"]),
+                  "valid": int(config["batches"]["batch_size_valid"])}.get(to_do, 1)
+
+    if processed_first:
+        shared = []
+        read_lab_fea(cfg_file, is_production, shared, output_folder)
+        data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict = _finish_chunk(shared)
+    shared_next = []
+    th = threading.Thread(target=read_lab_fea, args=(next_config_file, is_production, shared_next,
+                                                     output_folder))
+    th.start()
+
+    fea_dims = {k: v[-1] for k, v in fea_dict.items()}
+    nns = model_init(config, arch_dict, fea_dims, to_do)
+    for net_name in nns:
+        pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
+        if pt != "none":
+            ck = torch.load(pt, map_location="cuda", weights_only=True)
+            nns[net_name].load_state_dict(ck["model_par"])
+    if any(arch_dict[a][2] for a in arch_dict):
+        raise NotImplementedError("sequence models go through pkc.core.run_nn_seq (round 2)")
+    lines = parse_model(config["model"]["model"])
+    arch_opts = {a: config[arch_dict[a][0]] for a in nns}
+    chunk = data_set
+    fea_cols = {k: (v[5], v[6]) for k, v in fea_dict.items()}
+    lab_names = sorted(lab_dict, key=lambda k: lab_dict[k][3])
+
+    start = time.time()
+    loss_tot = err_tot = 0.0
+    if to_do in ("train", "valid"):
+        eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=seed,
+                     train=(to_do == "train"))
+        for net_name in nns:
+            pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
+            if pt != "none" and to_do == "train":
+                ck = torch.load(pt, map_location="cpu", weights_only=True)
+                eng.load_optimizer_state_dict(net_name, ck["optimizer_par"])
+                eng.set_lr(net_name, float(config[arch_dict[net_name][0]]["arch_lr"]))
+        eng.bind_chunk(chunk.feats, chunk.labels, chunk.n_rows)
+        n_batches = chunk.n_rows // batch_size
+        if to_do == "train":
+            eng.capture()
+            for i in range(n_batches):
+                eng.train_step()
+        else:
+            for i in range(n_batches):
+                eng.eval_step()
+        loss_sum, err_sum = eng.chunk_totals()
+        loss_tot, err_tot = loss_sum / max(1, n_batches), err_sum / max(1, n_batches)
+        if to_do == "train":
+            eng.sync_state()
+    else:
+        runner = ForwardRunner(nns, lines, fea_cols, forward_outs)
+        post_files = {}
+        for oi, out in enumerate(forward_outs):
+            suffix = "_to_decode.ark" if require_dec[oi] else ".ark"
+            post_files[out] = info_file.replace(".info", "_" + out + suffix)
+            open(post_files[out], "wb").close()
+        priors = {}
+        for oi, out in enumerate(forward_outs):
+            if forward_norm[oi]:
+                counts = D.load_counts(forward_counts[oi])
+                priors[out] = np.log(counts / np.sum(counts)).astype(np.float32)
+        beg = 0
+        for i, end in enumerate(chunk.end_index):
+            outs = runner.forward(chunk.feats, int(beg), int(end), priors)
+            for out in forward_outs:
+                D.write_mat_path(post_files[out], outs[out], chunk.names[i], append=True)
+            beg = end
+    torch.cuda.synchronize()
+    elapsed = time.time() - start
+
+    if to_do == "train":
+        for net_name, net in nns.items():
+            ck = {"model_par": net.state_dict(), "optimizer_par": eng.optimizer_state_dict(net_name)}
+            torch.save(ck, info_file.replace(".info", "_" + arch_dict[net_name][0] + ".pkl"))
+    with open(info_file, "w") as f:
+        f.write("[results]\n")
+        if to_do != "forward":
+            f.write("loss=%s\n" % np.float32(loss_tot))
+            f.write("err=%s\n" % np.float32(err_tot))
+        f.write("elapsed_time_chunk=%f\n" % elapsed)
+
+    th.join()
+    nxt = _finish_chunk(shared_next)
+    return nxt, patterns, pattern_masks

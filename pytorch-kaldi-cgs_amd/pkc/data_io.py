@@ -42,10 +42,37 @@ def read_mat_ark_path(path):
         yield keys[i].decode("latin1"), out
 
 
+def parse_mat_ark_bytes(buf):
+    """Binary FM/DM ark held in memory (e.g. a Kaldi pipe's stdout) -> [(key, float32 matrix)]."""
+    out, pos = [], 0
+    while pos < len(buf):
+        sp = buf.index(b" ", pos)
+        key = buf[pos:sp].decode("latin1").strip()
+        pos = sp + 1
+        if buf[pos:pos + 2] != b"\0B":
+            raise ValueError("only binary matrices are supported")
+        hdr = buf[pos + 2:pos + 5]
+        dt = {b"FM ": np.float32, b"DM ": np.float64}.get(hdr)
+        if dt is None:
+            raise ValueError("compressed / unknown matrix type %r" % hdr)
+        rows = struct.unpack("<i", buf[pos + 6:pos + 10])[0]
+        cols = struct.unpack("<i", buf[pos + 11:pos + 15])[0]
+        pos += 15
+        n = rows * cols * np.dtype(dt).itemsize
+        out.append((key, np.frombuffer(buf[pos:pos + n], dtype=dt).reshape(rows, cols)
+                    .astype(np.float32)))
+        pos += n
+    return out
+
+
 def read_vec_int_ark_path(path):
     """Binary int32-vector ark (alignments after ali-to-pdf) -> generator (data_io.py:412-455)."""
     with open(path, "rb") as f:
         buf = f.read()
+    return parse_vec_int_ark_bytes(buf)
+
+
+def parse_vec_int_ark_bytes(buf):
     pos = 0
     while pos < len(buf):
         sp = buf.index(b" ", pos)

@@ -579,53 +579,102 @@ def _b(v):
 
 
 class ModuleRunner:
-    """Forward of one MLP module on the pkc kernels (used by MLP.forward for stand-alone calls)."""
+    """Forward of one MLP module on the pkc kernels for any row count <= max_rows (MLP.forward for
+    stand-alone calls, and the per-utterance forward of run_nn's forward mode)."""
 
-    def __init__(self, net, rows, inp_dim):
+    def __init__(self, net, max_rows, inp_dim):
         net.check_supported()
-        self.net, self.rows, self.dev = net, rows, next(net.parameters()).device
+        self.net, self.rows, self.dev = net, max_rows, next(net.parameters()).device
         self.specs = net.layer_specs()
         self.bufs = []
         K = inp_dim
         for sp in self.specs:
             N = sp["out"]
-            sf = L.lib().pkc_gemm_pick_splits(rows, N, K)
-            self.bufs.append(dict(sf=sf, z=_f32(sf * rows * N, self.dev), K=K, N=N,
-                                  xhat=_f32(rows * N, self.dev), sm=_f32(N, self.dev),
-                                  si=_f32(N, self.dev),
-                                  work=_f32(L.lib().pkc_dense_work_size(rows, N), self.dev)))
+            sf = L.lib().pkc_gemm_pick_splits(max_rows, N, K)
+            self.bufs.append(dict(sf=sf, z=_f32(sf * max_rows * N, self.dev), K=K, N=N,
+                                  xhat=_f32(max_rows * N, self.dev), sm=_f32(N, self.dev),
+                                  si=_f32(N, self.dev), out=_f32(max_rows * N, self.dev),
+                                  work=_f32(L.lib().pkc_dense_work_size(max_rows, N), self.dev)))
             K = N
-
-    def forward(self, x, train=False):
-        x = x.contiguous().float()
-        s = Engine._stream()
-        M = self.rows
-        cur, ld = x, x.shape[1]
-        for sp, b in zip(self.specs, self.bufs):
-            N, K = b["N"], b["K"]
+        for sp in self.specs:
             if sp["mask"] is not None:
                 call("pkc_apply_mask", ptr(sp["W"]), ptr(sp["mask"]), sp["W"].numel(),
-                     C.c_float(0.0), s)
-            call("pkc_gemm", L.PREC_FP32, 1, 1, M, N, K, ptr(cur), ld, ptr(sp["W"]), K, ptr(b["z"]),
-                 N, b["sf"], M * N, s)
-            out = torch.empty(M, N, dtype=torch.float32, device=self.dev)
+                     C.c_float(0.0), Engine._stream())
+
+    def run(self, x_ptr, ld, M, train=False, log_prior=None):
+        """x_ptr: device address of an (M, ld) fp32 matrix; returns the (M, N) output view."""
+        assert M <= self.rows
+        s = Engine._stream()
+        cur, cld = x_ptr, ld
+        for sp, b in zip(self.specs, self.bufs):
+            N, K = b["N"], b["K"]
+            sf = L.lib().pkc_gemm_pick_splits(M, N, K)
+            call("pkc_gemm", L.PREC_FP32, 1, 1, M, N, K, C.c_void_p(cur), cld, ptr(sp["W"]), K,
+                 ptr(b["z"]), N, sf, M * N, s)
             if sp["act"] == "softmax":
-                a = L.NllArgs(M=M, N=N, nslab=b["sf"], zslab=b["z"].data_ptr(), slab_stride=M * N,
+                a = L.NllArgs(M=M, N=N, nslab=sf, zslab=b["z"].data_ptr(), slab_stride=M * N,
                               bias=sp["b"].data_ptr(), labels=None, label_stride=0, weight=0.0,
-                              logp=out.data_ptr(), log_prior=None, dlogits=None, row_loss=None,
-                              row_err=None)
-                self._k("nll_fused N=%d" % lay.N, 0, 4.0 * M * lay.N * (lay.sf + 2), "pkc_nll_fused",
-                        C.byref(a), s)
+                              logp=b["out"].data_ptr(),
+                              log_prior=log_prior.data_ptr() if log_prior is not None else None,
+                              dlogits=None, row_loss=None, row_err=None)
+                call("pkc_nll_fused", C.byref(a), s)
             else:
                 a = L.DenseFwdArgs(
-                    M=M, N=N, nslab=b["sf"], zslab=b["z"].data_ptr(), slab_stride=M * N,
+                    M=M, N=N, nslab=sf, zslab=b["z"].data_ptr(), slab_stride=M * N,
                     bias=sp["b"].data_ptr(),
                     norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if sp["bn"] else L.NORM_NONE,
                     gamma=sp["gamma"].data_ptr(), beta=sp["beta"].data_ptr(),
                     running_mean=sp["rm"].data_ptr(), running_var=sp["rv"].data_ptr(), momentum=0.05,
                     eps=1e-5, save_mean=b["sm"].data_ptr(), save_invstd=b["si"].data_ptr(),
                     act=L.ACT[sp["act"]], drop_p=0.0, seed=0, step_ctr=None, stream_id=0,
-                    keep_in=None, keep_out=None, xhat=b["xhat"].data_ptr(), out=out.data_ptr())
+                    keep_in=None, keep_out=None, xhat=b["xhat"].data_ptr(), out=b["out"].data_ptr())
                 call("pkc_dense_fwd", C.byref(a), ptr(b["work"]), s)
-            cur, ld = out, N
-        return cur
+            cur, cld = b["out"].data_ptr(), N
+        return self.bufs[-1]["out"][:M * self.bufs[-1]["N"]].view(M, -1)
+
+    def forward(self, x, train=False):
+        x = x.contiguous().float()
+        return self.run(x.data_ptr(), x.shape[1], x.shape[0], train).clone()
+
+
+class ForwardRunner:
+    """run_nn forward mode (core.py:134-145, 234-249): one utterance per batch, BatchNorm with
+    running statistics, no dropout, posteriors normalised by the log class prior."""
+
+    def __init__(self, nets, lines, fea_cols, forward_outs, max_rows=4096):
+        self.lines, self.fea_cols, self.outs = lines, fea_cols, forward_outs
+        self.nets = nets
+        self.max_rows = max_rows
+        self.runners = {}
+        dims = {k: c1 - c0 for k, (c0, c1) in fea_cols.items()}
+        for out, op, a, b in lines:
+            if op == "compute":
+                self.runners[a] = ModuleRunner(nets[a], max_rows, dims[b])
+                dims[out] = nets[a].out_dim
+        self.priors_dev = {}
+
+    def forward(self, feats, beg, end, priors):
+        M = end - beg
+        if M > self.max_rows:
+            raise ValueError("utterance of %d frames exceeds the forward buffer" % M)
+        produced, res = {}, {}
+        for out, op, a, b in self.lines:
+            if op != "compute":
+                continue
+            if b in self.fea_cols:
+                c0, _ = self.fea_cols[b]
+                xp, ld = feats.data_ptr() + 4 * (beg * feats.stride(0) + c0), feats.stride(0)
+            else:
+                xp, ld = produced[b].data_ptr(), produced[b].shape[1]
+            lp = None
+            if out in self.outs and out in priors:
+                if out not in self.priors_dev:
+                    self.priors_dev[out] = torch.from_numpy(priors[out]).to(feats.device)
+                lp = self.priors_dev[out]
+            y = self.runners[a].run(xp, ld, M, train=False, log_prior=lp)
+            produced[out] = y
+            if out in self.outs:
+                res[out] = y.cpu().numpy()
+            if all(o in res for o in self.outs):
+                break
+        return res

@@ -166,6 +166,6 @@ class MLP(nn.Module):
         """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
         ``self.training`` is False, batch statistics otherwise; no autograd)."""
         from .engine import ModuleRunner
-        if self._engine is None or self._engine.rows != x.shape[0]:
+        if self._engine is None or self._engine.rows < x.shape[0]:
             self._engine = ModuleRunner(self, x.shape[0], x.shape[1])
         return self._engine.forward(x, train=self.training)

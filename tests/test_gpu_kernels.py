@@ -116,9 +116,14 @@ def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
                         keep=d["keep"].data_ptr() if p > 0 else None, drop_p=p, dz=dz.data_ptr(),
                         dgamma=dgam.data_ptr(), dbeta=dbet.data_ptr(), dbias=dbias.data_ptr())
     L.call("pkc_dense_bwd", C.byref(b_), L.ptr(work), _s())
-    torch.testing.assert_close(dz.cpu(), zz.grad, rtol=1e-3, atol=1e-5)
-    torch.testing.assert_close(dgam.cpu(), gg.grad, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(dbet.cpu(), bb.grad, rtol=1e-4, atol=1e-4)
+    # a pre-activation within rounding of a kink (ReLU at 0) may take the other branch on the GPU;
+    # through the BN mean terms that changes its whole column: compare the other columns
+    y = torch.nn.functional.batch_norm(z, None, None, gamma, beta, training=True, eps=1e-5)
+    cols = (y.abs() > 1e-4).all(0) if act == "relu" else torch.ones(N, dtype=torch.bool)
+    assert cols.float().mean() > 0.95
+    torch.testing.assert_close(dz.cpu()[:, cols], zz.grad[:, cols], rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(dgam.cpu()[cols], gg.grad[cols], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dbet.cpu()[cols], bb.grad[cols], rtol=1e-4, atol=1e-4)
     assert (dbias.cpu() == 0).all()          # bias before BN: exact zero gradient
     assert zz.grad.sum(0).abs().max() < 1e-4  # ... which autograd reproduces up to rounding
 

@@ -150,15 +150,17 @@ def test_engine_c1_full_size_vs_oracle():
         np.testing.assert_allclose(err, outs["err_final"].item())
     # Parameters after 3 steps: a pre-activation within rounding of 0 can take the other ReLU
     # branch on the GPU than on the CPU (an fp32 ordering effect the reference shows between its
-    # own CPU and GPU runs too); that flips one element's gradient and spreads through dX.  So the
-    # state is compared in relative Frobenius norm, the posteriors above element-wise.
+    # own CPU and GPU runs too); through BatchNorm's 1/std that one element moves a whole column of
+    # dz and spreads through dX.  Measured on the oracle alone: a 1e-6 relative perturbation of the
+    # input moves wx.0.weight by 3.2e-3 (relative Frobenius) after these 3 steps.  So the state is
+    # compared in relative Frobenius norm at 2e-2, the posteriors above element-wise at 1e-4.
     for a in nets:
         for k, v in nets[a].state_dict().items():
             if k.endswith("num_batches_tracked"):
                 continue
             ref = onets[a].state_dict()[k].double()
             diff = (v.cpu().double() - ref).norm().item()
-            assert diff <= 1e-4 * ref.norm().item() + 1e-9, "%s %s rel frob err %.3g" % (
+            assert diff <= 2e-2 * ref.norm().item() + 1e-7, "%s %s rel frob err %.3g" % (
                 a, k, diff / max(ref.norm().item(), 1e-30))
 
 
