@@ -71,6 +71,8 @@ typedef struct {
   uint8_t* keep_out;                          /* M x N, may be NULL when drop_p == 0 */
   float* xhat;                                /* M x N (BN input normalised), may be NULL in eval */
   float* out;                                 /* M x N */
+  int64_t count_n;   /* rows BatchNorm1d sees for the unbiased running_var (0 -> M); a shared-
+                        weight bidirectional layer normalises 2x duplicated rows (2*M) */
 } pkc_dense_fwd_args;
 int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream);
 /* floats of device workspace pkc_dense_fwd / pkc_dense_bwd need (per-16-row column partials) */
@@ -165,6 +167,40 @@ int pkc_cw_stats(const float* raw, int64_t N, int D, int L, int R, double* mean,
 int64_t pkc_cw_stats_work_size(int64_t N, int D, int L, int R);
 int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double* mean,
                  const double* std, const int64_t* perm, float* out, int64_t ld_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Recurrent layers: the per-time-step loops of liGRU (neural_networks.py:1573-1584) and LSTM
+ * (neural_networks.py:1077-1097).  wpre holds the gate pre-activations W x (+BN) for the T*B input
+ * rows, gate-major (G, T, B, H): liGRU gates (z, h), LSTM gates (f, i, o, c).  Bidirectional
+ * layers (liGRU's shared-weight cat/flip convention, :1536-1538) run 2B rows per step; rows >= B
+ * read time T-1-t and write the second half of the (T, B, 2H) output y.  Forward saves
+ * hs (T+1, B2, H) [hs[0] = 0], cs (LSTM, T+1, B2, H) and gate activations (G, T, B2, H) for BPTT.
+ * Dropout: bernoulli(1-p) mask per (row, unit), shared by all steps and NOT rescaled; (1-p) at eval.
+ * pkc_rnn_bwd: dy = dL/dy (layer output layout); writes dgates (G, T, B2, H) = dL/d pre-activation
+ * per direction and dpre (G, T, B, H) = the same folded over directions (input of the BN / W
+ * backward); work = 4*B2*H floats.
+ * ------------------------------------------------------------------------------------------- */
+enum { PKC_CELL_LIGRU = 0, PKC_CELL_LSTM = 1 };
+typedef struct {
+  int cell, T, B, H, bidir, act, train;
+  const float* wpre;
+  const float* U[4];
+  float drop_p; uint64_t seed; const int64_t* step_ctr; int64_t stream_id;
+  const float* drop_mask_in;   /* optional injected (B2, H) mask */
+  float* drop_mask;            /* (B2, H) mask in use */
+  float* hs; float* cs; float* gates; float* y;
+  const float* dy; int dy_nslab; int64_t dy_slab_stride;   /* dL/dy as split-K partial slabs */
+  float* dgates; float* work;
+} pkc_rnn_args;
+/* Sequence batch assembly (core.py:183-214): sentence k of the batch starts at chunk row beg[k],
+ * has len[k] frames and is placed at time offset left[k] (python random.randint(0, max_len-len),
+ * drawn on the host in the reference's order); the rest of the (max_len, B, F) input is zero and
+ * the labels of padded frames are 0 (they count in the loss, as in the reference). */
+int pkc_seq_gather(const float* feats, int64_t ld_feats, int F, const int32_t* labels, int nlab,
+                   const int64_t* beg, const int32_t* len, const int32_t* left, int B, int max_len,
+                   float* x_out, int32_t* lab_out, void* stream);
+int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream);
+int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Host-side Kaldi ark I/O (data_io.py:770-806 write_mat; 645-711 read_mat_ark binary FM/DM).

@@ -83,4 +83,18 @@ __device__ __forceinline__ float act_bwd(int act, float y, float a) {
   }
 }
 
+// derivative expressed through the post-activation value a = act(y) (all act_fun choices are
+// monotone, so the branch is recoverable from a)
+__device__ __forceinline__ float act_bwd_out(int act, float a) {
+  switch (act) {
+    case PKC_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case PKC_ACT_TANH: return 1.f - a * a;
+    case PKC_ACT_SIGMOID: return a * (1.f - a);
+    case PKC_ACT_HTANH: return (a > -1.f && a < 1.f) ? 1.f : 0.f;
+    case PKC_ACT_LEAKY: return a > 0.f ? 1.f : 0.2f;
+    case PKC_ACT_ELU: return a > 0.f ? 1.f : a + 1.f;
+    default: return 1.f;
+  }
+}
+
 }  // namespace pkc

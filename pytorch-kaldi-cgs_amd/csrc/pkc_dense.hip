@@ -106,7 +106,8 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
         const float is = 1.f / sqrtf(var + a.eps);
         a.save_mean[c] = mu;
         a.save_invstd[c] = is;
-        const float unb = a.M > 1 ? var * (float)a.M / (float)(a.M - 1) : var;
+        const float cn = (float)(a.count_n > 0 ? a.count_n : a.M);
+        const float unb = cn > 1.f ? var * cn / (cn - 1.f) : var;
         a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
         a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
       }

@@ -149,3 +149,33 @@ extern "C" int pkc_batch_gather(const float* feats, int64_t ld_feats, int F, con
   PKC_LAUNCH_CHECK("pkc_batch_gather");
   return PKC_OK;
 }
+
+namespace pkc {
+__global__ __launch_bounds__(256) void seq_gather_kernel(const float* feats, int64_t ld, int F,
+                                                         const int32_t* labels, int nlab,
+                                                         const int64_t* beg, const int32_t* len,
+                                                         const int32_t* left, int B, int max_len,
+                                                         float* x_out, int32_t* lab_out) {
+  const int t = blockIdx.x, k = blockIdx.y;      // output row (t, k) of the (max_len, B, F) batch
+  const int l0 = left[k], n = len[k];
+  const bool in = t >= l0 && t < l0 + n;
+  const int64_t src = beg[k] + (t - l0);
+  float* dst = x_out + ((int64_t)t * B + k) * F;
+  for (int c = threadIdx.x; c < F; c += 256) dst[c] = in ? feats[src * ld + c] : 0.f;
+  if (threadIdx.x < nlab)
+    lab_out[((int64_t)t * B + k) * nlab + threadIdx.x] = in ? labels[src * nlab + threadIdx.x] : 0;
+}
+}  // namespace pkc
+
+extern "C" int pkc_seq_gather(const float* feats, int64_t ld_feats, int F, const int32_t* labels,
+                              int nlab, const int64_t* beg, const int32_t* len, const int32_t* left,
+                              int B, int max_len, float* x_out, int32_t* lab_out, void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(feats && beg && len && left && x_out && B > 0 && max_len > 0 && nlab <= 256 &&
+                    (nlab == 0 || (labels && lab_out)),
+                "pkc_seq_gather: bad arguments");
+  hipLaunchKernelGGL(seq_gather_kernel, dim3(max_len, B), dim3(256), 0, S(stream), feats, ld_feats, F,
+                     labels, nlab, beg, len, left, B, max_len, x_out, lab_out);
+  PKC_LAUNCH_CHECK("pkc_seq_gather");
+  return PKC_OK;
+}

@@ -27,7 +27,8 @@ class DenseFwdArgs(C.Structure):
                 ("running_mean", vp), ("running_var", vp), ("momentum", C.c_float), ("eps", C.c_float),
                 ("save_mean", vp), ("save_invstd", vp),
                 ("act", C.c_int), ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp),
-                ("stream_id", i64), ("keep_in", vp), ("keep_out", vp), ("xhat", vp), ("out", vp)]
+                ("stream_id", i64), ("keep_in", vp), ("keep_out", vp), ("xhat", vp), ("out", vp),
+                ("count_n", i64)]
 
 
 class DenseBwdArgs(C.Structure):
@@ -52,7 +53,23 @@ class OptTensor(C.Structure):
                 ("nesterov", C.c_int), ("centered", C.c_int), ("amsgrad", C.c_int), ("step", C.c_int)]
 
 
+CELL_LIGRU, CELL_LSTM = 0, 1
+
+
+class RnnArgs(C.Structure):
+    _fields_ = [("cell", C.c_int), ("T", C.c_int), ("B", C.c_int), ("H", C.c_int), ("bidir", C.c_int),
+                ("act", C.c_int), ("train", C.c_int), ("wpre", vp), ("U", vp * 4),
+                ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp), ("stream_id", i64),
+                ("drop_mask_in", vp), ("drop_mask", vp), ("hs", vp), ("cs", vp), ("gates", vp),
+                ("y", vp), ("dy", vp), ("dy_nslab", C.c_int), ("dy_slab_stride", i64),
+                ("dgates", vp), ("work", vp)]
+
+
 _SIGS = {
+    "pkc_rnn_fwd": (C.c_int, [C.POINTER(RnnArgs), vp]),
+    "pkc_rnn_bwd": (C.c_int, [C.POINTER(RnnArgs), vp, vp]),
+    "pkc_seq_gather": (C.c_int, [vp, i64, C.c_int, vp, C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp,
+                                 vp]),
     "pkc_abi_version": (C.c_int, []),
     "pkc_last_error": (C.c_char_p, []),
     "pkc_gemm": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64, vp, i64,

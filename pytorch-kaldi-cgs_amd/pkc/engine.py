@@ -1,21 +1,25 @@
-"""pkc.engine — executes the cfg [model] graph of feed-forward (non-sequential) architectures on
-the HIP kernels of libpkc.so.
+"""pkc.engine — executes the cfg [model] graph on the HIP kernels of libpkc.so.
 
-What it replaces: core.run_nn's per-batch body (core.py:203-232) — utils.forward_model's
-interpreter (utils.py:1884-2050) over MLP archs (neural_networks.py:245-319), the LogSoftmax +
-NLLLoss + cost_err heads, autograd backward and the per-architecture optimizer steps.
+What it replaces: core.run_nn's per-batch body (core.py:180-232) — utils.forward_model's
+interpreter (utils.py:1884-2050) over MLP / liGRU / LSTM archs (neural_networks.py:245-319,
+823-1112, 1523-1599), the LogSoftmax + NLLLoss + cost_err heads, autograd backward and the
+per-architecture optimizer steps.
 
 Design (MI355X-first):
-  * every tensor of a step lives in preallocated HBM buffers; a step is a fixed sequence of
-    ~30 kernel launches on one stream (no host sync: loss/err accumulate on the device), which
-    is captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed per batch;
-  * the batch is gathered from the HBM-resident chunk by a device-side batch counter, so graph
-    replays walk the chunk without host involvement;
-  * matmuls: pkc_gemm (MFMA, split-K slabs); BN/act/dropout fused in pkc_dense_fwd/_bwd;
-    LogSoftmax+NLL+err+dlogits fused in pkc_nll_fused; all optimizers in one pkc_optim_step
-    that also re-applies HCGS masks (the reference's in-place W.mul_(mask)).
+  * every tensor of a step lives in preallocated HBM buffers sized for the largest batch; kernels
+    take the runtime row count (T*B for sequence batches);
+  * non-sequential models: a step is a fixed sequence of ~35 launches on one stream (no host sync:
+    loss/err accumulate on the device), captured once into a hipGraph and replayed per batch; the
+    batch is gathered from the HBM-resident chunk by a device-side batch counter;
+  * sequence models: the padded (T, B, F) batch is assembled on the GPU (pkc_seq_gather) from
+    host-drawn padding offsets; each recurrent layer = gate matmuls over all T*B rows (MFMA) +
+    BN + the per-step time loop (pkc_rnn_fwd / pkc_rnn_bwd, one launch per step);
+  * matmuls: pkc_gemm (MFMA, split-K slabs summed by the consumers); BN/act/dropout fused in
+    pkc_dense_fwd/_bwd; LogSoftmax+NLL+err+dlogits fused in pkc_nll_fused; every optimizer of
+    every architecture in one pkc_optim_step that also re-applies HCGS masks.
 """
 import ctypes as C
+import random
 import re
 import zlib
 
@@ -26,6 +30,7 @@ from . import _lib as L
 from ._lib import call, ptr
 
 _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
+MAX_SPLITS = 8
 
 
 def parse_model(text):
@@ -34,11 +39,20 @@ def parse_model(text):
 
 
 def _f32(n, dev):
-    return torch.zeros(int(n), dtype=torch.float32, device=dev)
+    return torch.zeros(int(max(1, n)), dtype=torch.float32, device=dev)
+
+
+def _b(v):
+    return str(v).strip().lower() in ("1", "true", "yes", "y", "on", "t")
+
+
+def _splits(M, N, K, cap):
+    return max(1, min(cap, L.lib().pkc_gemm_pick_splits(M, N, K)))
 
 
 class Layer:
     """One dense layer of an MLP architecture inside the graph."""
+    rec = False
 
     def __init__(self, arch, idx, spec, K):
         self.arch, self.idx, self.K = arch, idx, K
@@ -51,9 +65,9 @@ class Layer:
         self.W, self.b = spec["W"], spec["b"]
         self.gamma, self.beta, self.rm, self.rv = spec["gamma"], spec["beta"], spec["rm"], spec["rv"]
         self.mask = spec["mask"]
-        self.src = None          # ("fea", c0, c1) or ("layer", Layer)
-        self.consumers = []      # layers reading this output
-        self.label_col = None    # head: label column index in the batch label buffer
+        self.src = None          # ("fea", c0, c1) or ("node", producer)
+        self.consumers = []
+        self.label_col = None
         self.nbt0 = int(spec["nbt"].item()) if spec.get("nbt") is not None else 0
         self.loss_weight = 0.0
         self.name = "%s.%d" % (arch, idx)
@@ -67,42 +81,96 @@ class Layer:
         if self.act not in L.ACT and not self.head:
             raise NotImplementedError("%s: activation %s" % (self.name, self.act))
 
+    def params(self):
+        out = [(self.W, "dW", self.mask), (self.b, "db", None)]
+        if self.bn:
+            out += [(self.gamma, "dgamma", None), (self.beta, "dbeta", None)]
+        return out
+
+
+class RecNode:
+    """A whole liGRU / LSTM architecture (all its layers) as one graph node."""
+    rec = True
+    head = False
+
+    def __init__(self, arch, net, K):
+        self.arch, self.net, self.K = arch, net, K
+        self.name = arch
+        self.cell = L.CELL_LSTM if net.cell == "lstm" else L.CELL_LIGRU
+        self.G = 4 if self.cell == L.CELL_LSTM else 2
+        self.layers = net.layer_specs()
+        self.N = net.out_dim
+        self.src = None
+        self.consumers = []
+        self.loss_weight = 0.0
+        self.label_col = None
+        for sp in self.layers:
+            if sp["act"] not in L.ACT:
+                raise NotImplementedError("%s: activation %s" % (arch, sp["act"]))
+            sp["nbt0"] = [int(bn.num_batches_tracked.item()) for bn in sp["bnm"]]
+
+    def params(self):
+        out = []
+        for li, sp in enumerate(self.layers):
+            for g in range(self.G):
+                out.append((sp["W"][g], ("dW", li, g), sp["Wmask"]))
+                if sp["b"][g] is not None:
+                    out.append((sp["b"][g], ("db", li, g), None))
+            for g in range(self.G):
+                out.append((sp["U"][g], ("dU", li, g), sp["Umask"]))
+            if sp["bn"]:
+                for g in range(self.G):
+                    out.append((sp["bnm"][g].weight, ("dgamma", li, g), None))
+                    out.append((sp["bnm"][g].bias, ("dbeta", li, g), None))
+        return out
+
 
 class Engine:
-    """Training / validation / forward executor of a non-sequential [model] graph.
+    """Training / validation executor of a [model] graph.
 
-    nets      : {arch_name: pkc.neural_networks.MLP} (parameters already on the device)
+    nets      : {arch_name: pkc.neural_networks module} (parameters already on the device)
     arch_opts : {arch_name: configparser section} (optimizer + arch_freeze keys)
     lines     : parsed [model] lines
     fea_cols  : {fea_name: (c0, c1)} column range of each feature stream in the chunk matrix
     lab_names : ordered label names (label buffer column order)
+    batch     : frames per batch (non-sequential) or sentences per batch (sequential)
+    max_len   : sequential models: the longest padded batch (frames) the buffers must hold
     """
 
     def __init__(self, nets, arch_opts, lines, fea_cols, lab_names, batch, prec=L.PREC_FP32,
-                 device="cuda", seed=0, train=True, drop_keep_in=None, grad_scale=1.0):
+                 device="cuda", seed=0, train=True, drop_keep_in=None, grad_scale=1.0, max_len=None,
+                 rnn_drop_in=None):
         self.dev = torch.device(device)
         self.nets, self.arch_opts, self.lines = nets, arch_opts, lines
-        self.M = int(batch)
+        self.B = int(batch)
         self.prec = prec
         self.train = train
         self.seed = int(seed)
-        self.grad_scale = float(grad_scale)   # 1/world_size under data parallelism
+        self.grad_scale = float(grad_scale)    # 1/world_size under data parallelism
         self.prof = None                       # profile mode: list of per-launch events
         self.F = max(c1 for _, c1 in fea_cols.values())
         self.fea_cols = fea_cols
         self.lab_names = list(lab_names)
         self.nlab = len(self.lab_names)
+        self.seq = any(getattr(n, "seq_model", False) for n in nets.values())
+        if self.seq and not max_len:
+            raise ValueError("sequence models need max_len")
+        self.max_len = int(max_len) if self.seq else 1
+        self.Mmax = self.B * self.max_len
+        self.M = self.Mmax                     # runtime rows of the current batch
+        self.T = self.max_len
+        self.drop_keep_in = drop_keep_in or {}
+        self.rnn_drop_in = rnn_drop_in or {}
         self._build_graph()
         self._alloc()
         self._build_optim()
         self.graph = None
         self.graph_opt = None
         self.steps_done = 0
-        self.drop_keep_in = drop_keep_in or {}
 
     # ------------------------------------------------------------------ graph construction
     def _build_graph(self):
-        self.layers, produced = [], {}
+        self.nodes, produced = [], {}
         for out, op, a, b in self.lines:
             if op != "compute":
                 continue
@@ -112,23 +180,30 @@ class Engine:
                 src = ("fea",) + tuple(self.fea_cols[b])
                 K = src[2] - src[1]
             elif b in produced:
-                src = ("layer", produced[b])
+                src = ("node", produced[b])
                 K = produced[b].N
             else:
                 raise ValueError("input %s of %s is neither a feature nor a produced output" % (b, a))
+            if getattr(net, "seq_model", False):
+                if src[0] != "fea":
+                    raise NotImplementedError("%s: a recurrent arch must read a feature stream" % a)
+                node = RecNode(a, net, K)
+                node.src = src
+                self.nodes.append(node)
+                produced[out] = node
+                continue
             prev = src
             for i, spec in enumerate(net.layer_specs()):
                 lay = Layer(a, i, spec, K)
                 lay.src = prev
-                if prev[0] == "layer":
+                if prev[0] == "node":
                     prev[1].consumers.append(lay)
-                self.layers.append(lay)
-                prev = ("layer", lay)
+                self.nodes.append(lay)
+                prev = ("node", lay)
                 K = lay.N
                 if lay.head and i != len(net.dnn_lay) - 1:
                     raise NotImplementedError("softmax only as the last layer of an MLP")
             produced[out] = prev[1]
-        # loss expression (core.py uses loss_final / err_final)
         scal, self.err_layer = {}, None
         for out, op, a, b in self.lines:
             if op == "cost_nll":
@@ -159,68 +234,65 @@ class Engine:
                 continue
             else:
                 raise NotImplementedError("[model] operation %s is not on the pkc path" % op)
-        self.heads = [l for l in self.layers if l.head]
+        self.produced = produced
+        self.heads = [l for l in self.nodes if l.head]
         if self.train and "loss_final" not in scal:
             raise ValueError("[model] has no loss_final")
         for lay, w in scal.get("loss_final", {}).items():
             lay.loss_weight = w
         if self.err_layer is None and self.heads:
             self.err_layer = self.heads[0]
-        for lay in self.layers:
+        for lay in self.nodes:
             if lay.head and lay.label_col is None:
                 lay.label_col = -1
+        self.layers = [n for n in self.nodes if not n.rec]     # dense layers (compat)
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
-        M, dev = self.M, self.dev
+        M, dev = self.Mmax, self.dev
+        self.cap = MAX_SPLITS if self.seq else None
         self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)      # batch counter + done word
         self.x = _f32(M * self.F, dev)
         self.labs = torch.zeros(M * max(1, self.nlab), dtype=torch.int32, device=dev)
-        for lay in self.layers:
-            N, K = lay.N, lay.K
-            lay.sf = L.lib().pkc_gemm_pick_splits(M, N, K)
-            lay.zslab = _f32(lay.sf * M * N, dev)
-            lay.out = _f32(M * N, dev)
-            lay.xhat = None if lay.head else _f32(M * N, dev)
-            lay.keep = torch.zeros(M * N, dtype=torch.uint8, device=dev) if lay.drop > 0 else None
-            lay.save_mean = _f32(N, dev)
-            lay.save_invstd = _f32(N, dev)
-            lay.dz = _f32(M * N, dev)
-            lay.work = _f32(L.lib().pkc_dense_work_size(M, N), dev)
-            if lay.head:
-                lay.row_loss = _f32(M, dev)
-                lay.row_err = _f32(M, dev)
-        for lay in self.layers:
-            off = 0
-            lay.cons_off = []
-            for c in lay.consumers:
-                s = L.lib().pkc_gemm_pick_splits(M, lay.N, c.N)
-                c.sx = s
-                lay.cons_off.append(off)
-                off += s
-            lay.sb = off
-            lay.gslab = _f32(max(1, off) * M * lay.N, dev) if off else None
+        for n in self.nodes:
+            if n.rec:
+                self._alloc_rec(n)
+                continue
+            N, K = n.N, n.K
+            n.scap = self.cap or _splits(M, N, K, MAX_SPLITS)
+            n.zslab = _f32(n.scap * M * N, dev)
+            n.out = _f32(M * N, dev)
+            n.xhat = None if n.head else _f32(M * N, dev)
+            n.keep = torch.zeros(M * N, dtype=torch.uint8, device=dev) if n.drop > 0 else None
+            n.save_mean = _f32(N, dev)
+            n.save_invstd = _f32(N, dev)
+            n.dz = _f32(M * N, dev)
+            n.work = _f32(L.lib().pkc_dense_work_size(M, N), dev)
+            if n.head:
+                n.row_loss = _f32(M, dev)
+                n.row_err = _f32(M, dev)
+        for n in self.nodes:
+            cap = 0
+            for c in n.consumers:
+                c.sxcap = self.cap or _splits(M, n.N, c.N, MAX_SPLITS)
+                cap += c.sxcap
+            n.gslab = _f32(cap * M * n.N, dev) if cap else None
         self.needs_grad = {}
-        for lay in reversed(self.layers):
-            self.needs_grad[lay] = (lay.head and lay.loss_weight != 0.0) or any(
-                self.needs_grad[c] for c in lay.consumers)
+        for n in reversed(self.nodes):
+            self.needs_grad[n] = (n.head and n.loss_weight != 0.0) or any(
+                self.needs_grad[c] for c in n.consumers)
         # all gradients in ONE flat buffer (a single RCCL all-reduce under data parallelism)
-        total = 0
-        for lay in self.layers:
-            total += lay.W.numel() + lay.b.numel() + (2 * lay.gamma.numel() if lay.bn else 0)
-        self.gflat = _f32(total, dev)
+        plist = [(n, p, key, m) for n in self.nodes for (p, key, m) in n.params()]
+        self.gflat = _f32(sum(p.numel() for _, p, _, _ in plist), dev)
         off = 0
-
-        def take(like):
-            nonlocal off
-            t = self.gflat[off:off + like.numel()].view_as(like)
-            off += like.numel()
-            return t
-        for lay in self.layers:
-            lay.dW, lay.db = take(lay.W), take(lay.b)
-            lay.dgamma = take(lay.gamma) if lay.bn else None
-            lay.dbeta = take(lay.beta) if lay.bn else None
-        # loss finalize descriptors
+        self.grads = {}
+        for n, p, key, m in plist:
+            g = self.gflat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+            if isinstance(key, tuple):
+                n.lbuf[key[1]][key[0]][key[2]] = g
+            else:
+                setattr(n, key, g)
         self.loss_heads = [l for l in self.heads if l.label_col >= 0]
         if self.loss_heads:
             if self.err_layer not in self.loss_heads:
@@ -231,22 +303,50 @@ class Engine:
             self.loss_ptrs = torch.from_numpy(ptrs.view(np.int64)).to(dev)
             self.loss_w = torch.tensor([l.loss_weight for l in self.loss_heads], dtype=torch.float32,
                                        device=dev)
+        if self.seq:
+            self.seq_meta = torch.zeros(4 * self.B, dtype=torch.int64, device=dev)
+
+    def _alloc_rec(self, n):
+        M, dev, B, T = self.Mmax, self.dev, self.B, self.max_len
+        G = n.G
+        n.lbuf = []
+        K = n.K
+        for sp in n.layers:
+            H = sp["H"]
+            B2 = 2 * B if sp["bidir"] else B
+            D = 2 * H if sp["bidir"] else H
+            lb = dict(K=K, H=H, B2=B2, D=D,
+                      zslab=_f32(MAX_SPLITS * M * H, dev), wpre=_f32(G * M * H, dev),
+                      xhat=_f32(G * M * H, dev), sm=_f32(G * H, dev), si=_f32(G * H, dev),
+                      work=_f32(L.lib().pkc_dense_work_size(M, H), dev),
+                      hs=_f32((T + 1) * B2 * H, dev),
+                      cs=_f32((T + 1) * B2 * H, dev) if n.cell == L.CELL_LSTM else None,
+                      gates=_f32(G * T * B2 * H, dev), y=_f32(M * D, dev),
+                      drop=_f32(B2 * H, dev), dgates=_f32(G * T * B2 * H, dev),
+                      dpre=_f32(G * M * H, dev), dz=_f32(G * M * H, dev),
+                      rwork=_f32(4 * B2 * H, dev),
+                      dx=_f32(G * MAX_SPLITS * M * K, dev),
+                      dW=[None] * G, db=[None] * G, dU=[None] * G, dgamma=[None] * G,
+                      dbeta=[None] * G)
+            n.lbuf.append(lb)
+            K = D
+        n.out = n.lbuf[-1]["y"]
 
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
-        self.opt_entries = []   # (arch, param tensor, grad, state dict)
-        for lay in self.layers:
-            if not self.needs_grad[lay]:
+        self.opt_entries = []
+        for n in self.nodes:
+            if not self.needs_grad[n]:
                 continue
-            o = self.arch_opts[lay.arch]
-            from .neural_networks import strtobool
-            if strtobool(o.get("arch_freeze", "False")):
+            o = self.arch_opts[n.arch]
+            if _b(o.get("arch_freeze", "False")):
                 continue
-            plist = [(lay.W, lay.dW, lay.mask), (lay.b, lay.db, None)]
-            if lay.bn:
-                plist += [(lay.gamma, lay.dgamma, None), (lay.beta, lay.dbeta, None)]
-            for p, g, m in plist:
-                self.opt_entries.append(dict(arch=lay.arch, p=p, g=g, mask=m, o=o,
+            for p, key, m in n.params():
+                if isinstance(key, tuple):
+                    g = n.lbuf[key[1]][key[0]][key[2]]
+                else:
+                    g = getattr(n, key)
+                self.opt_entries.append(dict(arch=n.arch, p=p, g=g, mask=m, o=o,
                                              s1=torch.zeros_like(p), s2=None, s3=None, step=0))
         for e in self.opt_entries:
             kind = e["o"]["arch_opt"]
@@ -273,10 +373,10 @@ class Engine:
             self.opt_desc = torch.zeros(n * C.sizeof(L.OptTensor), dtype=torch.uint8, device=self.dev)
             self._upload_opt_desc(step_inc=1)
         # the reference multiplies the masks in before the first forward; do it once here
-        for lay in self.layers:
-            if lay.mask is not None:
-                call("pkc_apply_mask", ptr(lay.W), ptr(lay.mask), lay.W.numel(), C.c_float(0.0),
-                     self._stream())
+        for n_ in self.nodes:
+            for p, key, m in n_.params():
+                if m is not None:
+                    call("pkc_apply_mask", ptr(p), ptr(m), p.numel(), C.c_float(0.0), self._stream())
 
     def _upload_opt_desc(self, step_inc):
         n = len(self.opt_entries)
@@ -317,17 +417,39 @@ class Engine:
             self._upload_opt_desc(step_inc=1)
 
     # ------------------------------------------------------------------ chunk binding
-    def bind_chunk(self, feats, labels, n_rows):
-        """feats: (N, F) fp32 device tensor (row stride >= F); labels: (N, nlab) int32 device."""
+    def bind_chunk(self, feats, labels, n_rows, end_index=None):
+        """feats: (N, F) fp32 device tensor (row stride >= F); labels: (N, nlab) int32 device;
+        end_index: cumulative utterance ends (sequence models)."""
         assert feats.dtype == torch.float32 and labels.dtype == torch.int32
         assert feats.shape[1] >= self.F and labels.shape[1] == self.nlab
         self.chunk_feats, self.chunk_labels = feats, labels
-        self.n_batches = int(n_rows) // self.M
+        if self.seq:
+            self.end_index = np.asarray(end_index, dtype=np.int64)
+            self.n_batches = len(self.end_index) // self.B         # core.py:157-159
+            self.snt = 0
+        else:
+            self.n_batches = int(n_rows) // self.B                  # core.py:161-162
         self.ctr.zero_()
         if self.loss_heads:
             self.loss_acc.zero_()
 
-    # ------------------------------------------------------------------ kernels of one step
+    def next_seq_batch(self, rng=None):
+        """core.py:183-200: the next B sentences, padded to the longest with a random number of
+        leading zeros (python random.randint, drawn in the reference's order)."""
+        rng = rng or random
+        e = self.end_index
+        i0 = self.snt
+        ends = e[i0:i0 + self.B]
+        begs = np.concatenate([[e[i0 - 1] if i0 > 0 else 0], ends[:-1]])
+        lens = ends - begs
+        T = int(lens.max())
+        if T > self.max_len:
+            raise ValueError("batch of %d frames exceeds max_len %d" % (T, self.max_len))
+        lefts = np.array([rng.randint(0, T - int(l)) for l in lens], dtype=np.int64)
+        self.snt += self.B
+        return begs.astype(np.int64), lens.astype(np.int64), lefts, T
+
+    # ------------------------------------------------------------------ launch helpers
     @staticmethod
     def _stream():
         return C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -344,94 +466,240 @@ class Engine:
         else:
             call(fn, *args)
 
-    def _src(self, lay):
-        if lay.src[0] == "fea":
-            return self.x.data_ptr() + 4 * lay.src[1], self.F
-        return lay.src[1].out.data_ptr(), lay.src[1].N
+    def _src(self, n):
+        if n.src[0] == "fea":
+            return self.x.data_ptr() + 4 * n.src[1], self.F
+        return n.src[1].out.data_ptr(), n.src[1].N
 
-    def _forward_kernels(self, s, train):
+    # ------------------------------------------------------------------ forward
+    def _gather(self, s, batch=None):
+        if not self.seq:
+            M = self.M
+            self._k("batch_gather", 0, 8.0 * M * self.F, "pkc_batch_gather", ptr(self.chunk_feats),
+                    self.chunk_feats.stride(0), self.F, ptr(self.chunk_labels), self.nlab, self.B,
+                    self.n_batches, ptr(self.ctr), ptr(self.x), ptr(self.labs), 1, s)
+            return
+        begs, lens, lefts, T = batch
+        # [B x int64 begin rows][B x int32 lengths][B x int32 left pads]
+        host = np.zeros(4 * self.B, dtype=np.int64)
+        host[:self.B] = begs
+        h32 = host[self.B:].view(np.int32)
+        h32[:self.B] = lens
+        h32[self.B:2 * self.B] = lefts
+        self.seq_meta.copy_(torch.from_numpy(host), non_blocking=False)
+        mp = self.seq_meta.data_ptr()
+        self._k("seq_gather", 0, 8.0 * T * self.B * self.F, "pkc_seq_gather", ptr(self.chunk_feats),
+                self.chunk_feats.stride(0), self.F, ptr(self.chunk_labels), self.nlab,
+                C.c_void_p(mp), C.c_void_p(mp + 8 * self.B), C.c_void_p(mp + 8 * self.B + 4 * self.B),
+                self.B, T, ptr(self.x), ptr(self.labs), s)
+
+    def _dense_fwd(self, n, s, train):
         M = self.M
-        self._k("batch_gather", 0, 8.0 * M * self.F, "pkc_batch_gather", ptr(self.chunk_feats),
-                self.chunk_feats.stride(0), self.F, ptr(self.chunk_labels), self.nlab, M,
-                self.n_batches, ptr(self.ctr), ptr(self.x), ptr(self.labs), 1, s)
-        for lay in self.layers:
-            a_ptr, lda = self._src(lay)
-            self._k("gemm_fwd %dx%dx%d" % (M, lay.N, lay.K), 2.0 * M * lay.N * lay.K,
-                    4.0 * (M * lay.K + lay.N * lay.K + lay.sf * M * lay.N), "pkc_gemm", self.prec,
-                    1, 1, M, lay.N, lay.K, C.c_void_p(a_ptr), lda, ptr(lay.W), lay.K, ptr(lay.zslab),
-                    lay.N, lay.sf, M * lay.N, s)
-            if lay.head:
-                has_lab = lay.label_col >= 0
-                a = L.NllArgs(M=M, N=lay.N, nslab=lay.sf, zslab=lay.zslab.data_ptr(),
-                              slab_stride=M * lay.N, bias=lay.b.data_ptr(),
-                              labels=(self.labs.data_ptr() + 4 * lay.label_col) if has_lab else None,
-                              label_stride=self.nlab, weight=lay.loss_weight * self.grad_scale,
-                              logp=lay.out.data_ptr(),
-                              log_prior=None,
-                              dlogits=lay.dz.data_ptr() if (train and has_lab) else None,
-                              row_loss=lay.row_loss.data_ptr(), row_err=lay.row_err.data_ptr())
-                self._k("nll_fused N=%d" % lay.N, 0, 4.0 * M * lay.N * (lay.sf + 2), "pkc_nll_fused",
-                        C.byref(a), s)
-            else:
-                keep_in = self.drop_keep_in.get(lay.name)
+        a_ptr, lda = self._src(n)
+        sf = _splits(M, n.N, n.K, n.scap)
+        n.sf = sf
+        self._k("gemm_fwd %dx%dx%d" % (M, n.N, n.K), 2.0 * M * n.N * n.K,
+                4.0 * (M * n.K + n.N * n.K + sf * M * n.N), "pkc_gemm", self.prec,
+                1, 1, M, n.N, n.K, C.c_void_p(a_ptr), lda, ptr(n.W), n.K, ptr(n.zslab),
+                n.N, sf, M * n.N, s)
+        if n.head:
+            has_lab = n.label_col >= 0
+            a = L.NllArgs(M=M, N=n.N, nslab=sf, zslab=n.zslab.data_ptr(), slab_stride=M * n.N,
+                          bias=n.b.data_ptr(),
+                          labels=(self.labs.data_ptr() + 4 * n.label_col) if has_lab else None,
+                          label_stride=self.nlab, weight=n.loss_weight * self.grad_scale,
+                          logp=n.out.data_ptr(), log_prior=None,
+                          dlogits=n.dz.data_ptr() if (train and has_lab) else None,
+                          row_loss=n.row_loss.data_ptr(), row_err=n.row_err.data_ptr())
+            self._k("nll_fused N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_nll_fused",
+                    C.byref(a), s)
+            return
+        keep_in = self.drop_keep_in.get(n.name)
+        a = L.DenseFwdArgs(
+            M=M, N=n.N, nslab=sf, zslab=n.zslab.data_ptr(), slab_stride=M * n.N,
+            bias=n.b.data_ptr(),
+            norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if n.bn else L.NORM_NONE,
+            gamma=n.gamma.data_ptr(), beta=n.beta.data_ptr(),
+            running_mean=n.rm.data_ptr(), running_var=n.rv.data_ptr(),
+            momentum=0.05, eps=1e-5, save_mean=n.save_mean.data_ptr(),
+            save_invstd=n.save_invstd.data_ptr(), act=L.ACT[n.act],
+            drop_p=n.drop if train else 0.0, seed=self.seed,
+            step_ctr=self.ctr.data_ptr(), stream_id=zlib.crc32(n.name.encode()),
+            keep_in=keep_in.data_ptr() if keep_in is not None else None,
+            keep_out=n.keep.data_ptr() if (n.keep is not None and train) else None,
+            xhat=n.xhat.data_ptr(), out=n.out.data_ptr(), count_n=0)
+        self._k("dense_fwd N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_dense_fwd",
+                C.byref(a), ptr(n.work), s)
+
+    def _rnn_args(self, n, li, train, T):
+        sp, lb = n.layers[li], n.lbuf[li]
+        H = lb["H"]
+        a = L.RnnArgs()
+        a.cell, a.T, a.B, a.H, a.bidir = n.cell, T, self.B, H, int(sp["bidir"])
+        a.act, a.train = L.ACT[sp["act"]], int(train)
+        a.wpre = lb["wpre"].data_ptr()
+        for g in range(n.G):
+            a.U[g] = sp["U"][g].data_ptr()
+        a.drop_p = float(sp["drop"])
+        a.seed = self.seed
+        a.step_ctr = self.ctr.data_ptr()
+        a.stream_id = zlib.crc32(("%s.%d" % (n.arch, li)).encode())
+        din = self.rnn_drop_in.get((n.arch, li))
+        a.drop_mask_in = din.data_ptr() if din is not None else None
+        a.drop_mask = lb["drop"].data_ptr()
+        a.hs = lb["hs"].data_ptr()
+        a.cs = lb["cs"].data_ptr() if lb["cs"] is not None else None
+        a.gates = lb["gates"].data_ptr()
+        a.y = lb["y"].data_ptr()
+        a.dgates = lb["dgates"].data_ptr()
+        a.work = lb["rwork"].data_ptr()
+        return a
+
+    def _rec_fwd(self, n, s, train):
+        M, T = self.M, self.T
+        x_ptr, ldx = self._src(n)
+        for li, (sp, lb) in enumerate(zip(n.layers, n.lbuf)):
+            H, K = lb["H"], lb["K"]
+            for g in range(n.G):
+                sf = _splits(M, H, K, MAX_SPLITS)
+                self._k("rnn_gemm_W %dx%dx%d" % (M, H, K), 2.0 * M * H * K,
+                        4.0 * (M * K + H * K + sf * M * H), "pkc_gemm", self.prec, 1, 1, M, H, K,
+                        C.c_void_p(x_ptr), ldx, ptr(sp["W"][g]), K, ptr(lb["zslab"]), H, sf, M * H, s)
+                bn = sp["bnm"][g]
                 a = L.DenseFwdArgs(
-                    M=M, N=lay.N, nslab=lay.sf, zslab=lay.zslab.data_ptr(), slab_stride=M * lay.N,
-                    bias=lay.b.data_ptr(),
-                    norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if lay.bn else L.NORM_NONE,
-                    gamma=lay.gamma.data_ptr(), beta=lay.beta.data_ptr(),
-                    running_mean=lay.rm.data_ptr(), running_var=lay.rv.data_ptr(),
-                    momentum=0.05, eps=1e-5, save_mean=lay.save_mean.data_ptr(),
-                    save_invstd=lay.save_invstd.data_ptr(), act=L.ACT[lay.act],
-                    drop_p=lay.drop if train else 0.0, seed=self.seed,
-                    step_ctr=self.ctr.data_ptr(), stream_id=zlib.crc32(lay.name.encode()),
-                    keep_in=keep_in.data_ptr() if keep_in is not None else None,
-                    keep_out=lay.keep.data_ptr() if (lay.keep is not None and train) else None,
-                    xhat=lay.xhat.data_ptr(), out=lay.out.data_ptr())
-                self._k("dense_fwd N=%d" % lay.N, 0, 4.0 * M * lay.N * (lay.sf + 2), "pkc_dense_fwd",
-                        C.byref(a), ptr(lay.work), s)
+                    M=M, N=H, nslab=sf, zslab=lb["zslab"].data_ptr(), slab_stride=M * H,
+                    bias=sp["b"][g].data_ptr() if sp["b"][g] is not None else None,
+                    norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if sp["bn"] else L.NORM_NONE,
+                    gamma=bn.weight.data_ptr(), beta=bn.bias.data_ptr(),
+                    running_mean=bn.running_mean.data_ptr(), running_var=bn.running_var.data_ptr(),
+                    momentum=0.05, eps=1e-5, save_mean=lb["sm"].data_ptr() + 4 * g * H,
+                    save_invstd=lb["si"].data_ptr() + 4 * g * H, act=L.ACT["linear"], drop_p=0.0,
+                    seed=0, step_ctr=None, stream_id=0, keep_in=None, keep_out=None,
+                    xhat=lb["xhat"].data_ptr() + 4 * g * M * H,
+                    out=lb["wpre"].data_ptr() + 4 * g * M * H,
+                    count_n=M * (2 if sp["bidir"] else 1))
+                self._k("rnn_bn_fwd H=%d" % H, 0, 4.0 * M * H * (sf + 2), "pkc_dense_fwd",
+                        C.byref(a), ptr(lb["work"]), s)
+            ra = self._rnn_args(n, li, train, T)
+            self._k("rnn_fwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
+                    4.0 * T * n.G * H * H, "pkc_rnn_fwd", C.byref(ra), s)
+            x_ptr, ldx = lb["y"].data_ptr(), lb["D"]
+
+    def _forward_kernels(self, s, train, batch=None):
+        self._gather(s, batch)
+        for n in self.nodes:
+            if n.rec:
+                self._rec_fwd(n, s, train)
+            else:
+                self._dense_fwd(n, s, train)
         if self.loss_heads:
-            err_out = self.err_layer.row_err
-            self._k("loss_finalize", 0, 4.0 * M * (len(self.loss_heads) + 1), "pkc_loss_finalize",
-                    len(self.loss_heads), ptr(self.loss_ptrs), ptr(self.loss_w), M, ptr(err_out),
-                    ptr(self.loss_out), ptr(self.loss_acc), s)
+            self._k("loss_finalize", 0, 4.0 * self.M * (len(self.loss_heads) + 1),
+                    "pkc_loss_finalize", len(self.loss_heads), ptr(self.loss_ptrs), ptr(self.loss_w),
+                    self.M, ptr(self.err_layer.row_err), ptr(self.loss_out), ptr(self.loss_acc), s)
+
+    # ------------------------------------------------------------------ backward
+    def _grad_slabs(self, n):
+        """(pointer, nslab) of dL/d(out of n) as the consumers' dX slabs, with their offsets."""
+        M = self.M
+        off = 0
+        n.cons_off = []
+        for c in n.consumers:
+            c.sx = _splits(M, c.K, c.N, c.sxcap)
+            n.cons_off.append(off)
+            off += c.sx
+        return off
+
+    def _dense_bwd(self, n, s):
+        M = self.M
+        if n.head:
+            self._k("colsum N=%d" % n.N, 0, 4.0 * M * n.N, "pkc_colsum", M, n.N, 1, ptr(n.dz), 0,
+                    ptr(n.db), 0, s)
+        else:
+            a = L.DenseBwdArgs(M=M, N=n.N, nslab=n.sb, gslab=n.gslab.data_ptr(),
+                               slab_stride=M * n.N,
+                               norm=L.NORM_BN_TRAIN if n.bn else L.NORM_NONE,
+                               act=L.ACT[n.act], gamma=n.gamma.data_ptr(),
+                               beta=n.beta.data_ptr(), save_invstd=n.save_invstd.data_ptr(),
+                               xhat=n.xhat.data_ptr(),
+                               keep=n.keep.data_ptr() if n.keep is not None else None,
+                               drop_p=n.drop, dz=n.dz.data_ptr(),
+                               dgamma=n.dgamma.data_ptr() if n.bn else None,
+                               dbeta=n.dbeta.data_ptr() if n.bn else None,
+                               dbias=n.db.data_ptr())
+            self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (n.sb + 3), "pkc_dense_bwd",
+                    C.byref(a), ptr(n.work), s)
+        a_ptr, lda = self._src(n)
+        self._k("gemm_dW %dx%dx%d" % (n.N, n.K, M), 2.0 * M * n.N * n.K,
+                4.0 * (M * n.N + M * n.K + n.N * n.K), "pkc_gemm", self.prec, 0, 0,
+                n.N, n.K, M, ptr(n.dz), n.N, C.c_void_p(a_ptr), lda, ptr(n.dW), n.K, 1, 0, s)
+        if n.src[0] == "node" and self.needs_grad[n.src[1]]:
+            P = n.src[1]
+            off = P.cons_off[P.consumers.index(n)]
+            self._k("gemm_dX %dx%dx%d" % (M, n.K, n.N), 2.0 * M * n.N * n.K,
+                    4.0 * (M * n.N + n.N * n.K + n.sx * M * n.K), "pkc_gemm",
+                    self.prec, 1, 0, M, n.K, n.N, ptr(n.dz), n.N, ptr(n.W), n.K,
+                    C.c_void_p(P.gslab.data_ptr() + 4 * off * M * P.N), n.K, n.sx, M * n.K, s)
+
+    def _rec_bwd(self, n, s, want_dx0=False):
+        M, T = self.M, self.T
+        dy_ptr, dy_ns = n.gslab.data_ptr(), n.sb
+        dy_stride = M * n.N
+        for li in reversed(range(len(n.layers))):
+            sp, lb = n.layers[li], n.lbuf[li]
+            H, K = lb["H"], lb["K"]
+            ra = self._rnn_args(n, li, True, T)
+            ra.dy, ra.dy_nslab, ra.dy_slab_stride = dy_ptr, dy_ns, dy_stride
+            self._k("rnn_bwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
+                    4.0 * T * n.G * H * H, "pkc_rnn_bwd", C.byref(ra), ptr(lb["dpre"]), s)
+            if li > 0:
+                x_ptr, ldx = n.lbuf[li - 1]["y"].data_ptr(), n.lbuf[li - 1]["D"]
+            else:
+                x_ptr, ldx = self._src(n)
+            nx = 0
+            for g in range(n.G):
+                bn = sp["bnm"][g]
+                a = L.DenseBwdArgs(M=M, N=H, nslab=1, gslab=lb["dpre"].data_ptr() + 4 * g * M * H,
+                                   slab_stride=0, norm=L.NORM_BN_TRAIN if sp["bn"] else L.NORM_NONE,
+                                   act=L.ACT["linear"], gamma=bn.weight.data_ptr(),
+                                   beta=bn.bias.data_ptr(),
+                                   save_invstd=lb["si"].data_ptr() + 4 * g * H,
+                                   xhat=lb["xhat"].data_ptr() + 4 * g * M * H, keep=None, drop_p=0.0,
+                                   dz=lb["dz"].data_ptr() + 4 * g * M * H,
+                                   dgamma=lb["dgamma"][g].data_ptr() if sp["bn"] else None,
+                                   dbeta=lb["dbeta"][g].data_ptr() if sp["bn"] else None,
+                                   dbias=lb["db"][g].data_ptr() if lb["db"][g] is not None else None)
+                self._k("rnn_bn_bwd H=%d" % H, 0, 4.0 * M * H * 4, "pkc_dense_bwd", C.byref(a),
+                        ptr(lb["work"]), s)
+                dz = C.c_void_p(lb["dz"].data_ptr() + 4 * g * M * H)
+                self._k("rnn_gemm_dW %dx%dx%d" % (H, K, M), 2.0 * M * H * K,
+                        4.0 * (M * H + M * K + H * K), "pkc_gemm", self.prec, 0, 0, H, K, M, dz, H,
+                        C.c_void_p(x_ptr), ldx, ptr(lb["dW"][g]), K, 1, 0, s)
+                # dU = sum_t dgates[t]^T h_{t-1}: K = T*B2 rows of hs[0:T]
+                R2 = T * lb["B2"]
+                self._k("rnn_gemm_dU %dx%dx%d" % (H, H, R2), 2.0 * R2 * H * H,
+                        4.0 * (2 * R2 * H + H * H), "pkc_gemm", self.prec, 0, 0, H, H, R2,
+                        C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,
+                        ptr(lb["hs"]), H, ptr(lb["dU"][g]), H, 1, 0, s)
+                if li > 0 or want_dx0:
+                    sx = _splits(M, K, H, MAX_SPLITS)
+                    self._k("rnn_gemm_dX %dx%dx%d" % (M, K, H), 2.0 * M * H * K,
+                            4.0 * (M * H + H * K + sx * M * K), "pkc_gemm", self.prec, 1, 0, M, K, H,
+                            dz, H, ptr(sp["W"][g]), K,
+                            C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
+                    nx += sx
+            dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
 
     def _backward_kernels(self, s):
-        M = self.M
-        for lay in reversed(self.layers):
-            if not self.needs_grad[lay]:
+        for n in self.nodes:
+            if n.gslab is not None:
+                n.sb = self._grad_slabs(n)
+        for n in reversed(self.nodes):
+            if not self.needs_grad[n]:
                 continue
-            if lay.head:
-                self._k("colsum N=%d" % lay.N, 0, 4.0 * M * lay.N, "pkc_colsum", M, lay.N, 1,
-                        ptr(lay.dz), 0, ptr(lay.db), 0, s)
+            if n.rec:
+                self._rec_bwd(n, s)
             else:
-                a = L.DenseBwdArgs(M=M, N=lay.N, nslab=lay.sb, gslab=lay.gslab.data_ptr(),
-                                   slab_stride=M * lay.N,
-                                   norm=L.NORM_BN_TRAIN if lay.bn else L.NORM_NONE,
-                                   act=L.ACT[lay.act], gamma=lay.gamma.data_ptr(),
-                                   beta=lay.beta.data_ptr(), save_invstd=lay.save_invstd.data_ptr(),
-                                   xhat=lay.xhat.data_ptr(),
-                                   keep=lay.keep.data_ptr() if lay.keep is not None else None,
-                                   drop_p=lay.drop, dz=lay.dz.data_ptr(),
-                                   dgamma=lay.dgamma.data_ptr() if lay.bn else None,
-                                   dbeta=lay.dbeta.data_ptr() if lay.bn else None,
-                                   dbias=lay.db.data_ptr())
-                self._k("dense_bwd N=%d" % lay.N, 0, 4.0 * M * lay.N * (lay.sb + 3), "pkc_dense_bwd",
-                        C.byref(a), ptr(lay.work), s)
-            a_ptr, lda = self._src(lay)
-            # dW = dz^T X
-            self._k("gemm_dW %dx%dx%d" % (lay.N, lay.K, M), 2.0 * M * lay.N * lay.K,
-                    4.0 * (M * lay.N + M * lay.K + lay.N * lay.K), "pkc_gemm", self.prec, 0, 0,
-                    lay.N, lay.K, M, ptr(lay.dz), lay.N, C.c_void_p(a_ptr), lda, ptr(lay.dW), lay.K,
-                    1, 0, s)
-            if lay.src[0] == "layer" and self.needs_grad[lay.src[1]]:
-                P = lay.src[1]
-                off = P.cons_off[P.consumers.index(lay)]
-                # dX slabs = dz W into the producer's gradient slabs
-                self._k("gemm_dX %dx%dx%d" % (M, lay.K, lay.N), 2.0 * M * lay.N * lay.K,
-                        4.0 * (M * lay.N + lay.N * lay.K + lay.sx * M * lay.K), "pkc_gemm",
-                        self.prec, 1, 0, M, lay.K, lay.N, ptr(lay.dz), lay.N, ptr(lay.W), lay.K,
-                        C.c_void_p(P.gslab.data_ptr() + 4 * off * M * P.N), lay.K, lay.sx,
-                        M * lay.K, s)
+                self._dense_bwd(n, s)
 
     def _optim_kernels(self, s):
         if self.opt_entries:
@@ -439,31 +707,53 @@ class Engine:
             self._k("optim_step", 0, 4.0 * nparam * 5, "pkc_optim_step", ptr(self.opt_desc),
                     len(self.opt_entries), ptr(self.opt_map), self.opt_nchunks, s)
 
-    def _train_step_kernels(self, allreduce=None):
+    def _train_step_kernels(self, allreduce=None, batch=None):
         s = self._stream()
-        self._forward_kernels(s, True)
+        self._forward_kernels(s, True, batch)
         self._backward_kernels(s)
         if allreduce is not None:
             allreduce(self.gflat)
         self._optim_kernels(s)
 
     # ------------------------------------------------------------------ public API
-    def train_step(self, allreduce=None):
-        """One batch: forward, backward, [allreduce(flat grads)], optimizer (core.py:216-232)."""
-        if self.graph is not None:
+    def _set_rows(self, batch):
+        if self.seq:
+            self.T = batch[3]
+            self.M = self.T * self.B
+        else:
+            self.M = self.B
+
+    def train_step(self, allreduce=None, batch=None):
+        """One batch: forward, backward, [allreduce(flat grads)], optimizer (core.py:216-232).
+        Sequence models: batch = next_seq_batch() (drawn here when None)."""
+        if self.seq:
+            batch = batch or self.next_seq_batch()
+            self._set_rows(batch)
+            self._train_step_kernels(allreduce, batch)
+            self.ctr.add_(1)           # step counter of the dropout RNG streams
+        elif self.graph is not None:
             self.graph.replay()
             if self.graph_opt is not None:
                 if allreduce is not None:
                     allreduce(self.gflat)
                 self.graph_opt.replay()
         else:
+            self._set_rows(None)
             self._train_step_kernels(allreduce)
         self._after_step()
+
+    def eval_step(self, batch=None):
+        """Validation batch: forward with running BN statistics, loss/err accumulated."""
+        if self.seq:
+            batch = batch or self.next_seq_batch()
+        self._set_rows(batch)
+        self._forward_kernels(self._stream(), False, batch)
 
     def profile_step(self):
         """Run one eager training step with events around every launch; returns
         [(label, fn, flops, bytes, ms)] (device time per launch)."""
         self.prof = []
+        self._set_rows(None)
         self._train_step_kernels()
         torch.cuda.synchronize()
         out = [(l, f, fl, nb, e0.elapsed_time(e1)) for (l, f, fl, nb, e0, e1) in self.prof]
@@ -479,11 +769,12 @@ class Engine:
             self._upload_opt_desc(step_inc=1)
 
     def capture(self, split_optimizer=False):
-        """Capture the training step into hipGraph(s) (needs step-independent optimizer
-        descriptors: RMSprop / momentum-free SGD).  split_optimizer=True captures forward+backward
-        and the optimizer separately so a gradient all-reduce can run in between."""
-        if not self.static_opt:
+        """Capture the training step into hipGraph(s) (non-sequential models with step-independent
+        optimizer descriptors: RMSprop / momentum-free SGD).  split_optimizer=True captures
+        forward+backward and the optimizer separately so a gradient all-reduce fits in between."""
+        if not self.static_opt or self.seq:
             return False
+        self._set_rows(None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
@@ -503,10 +794,6 @@ class Engine:
         self.graph = g
         return True
 
-    def eval_step(self):
-        """Validation batch: forward with running BN statistics, loss/err accumulated."""
-        self._forward_kernels(self._stream(), False)
-
     def loss_values(self):
         """(loss_final, err) of the last step (forces a sync)."""
         v = self.loss_out.cpu()
@@ -517,12 +804,22 @@ class Engine:
         v = self.loss_acc.cpu()
         return float(v[0]), float(v[1])
 
+    def head_output(self, out_name):
+        """(M, N) view of a head / layer output of the current batch."""
+        n = self.produced[out_name]
+        return n.out[:self.M * n.N].view(self.M, n.N)
+
     def sync_state(self):
         """Reflect the step count into BN num_batches_tracked (nn.BatchNorm1d increments it on
         every training forward; the kernels update running stats but not this counter)."""
-        for lay in self.layers:
-            if lay.bn:
-                lay.spec["nbt"].fill_(lay.nbt0 + self.steps_done)
+        for n in self.nodes:
+            if n.rec:
+                for sp in n.layers:
+                    if sp["bn"]:
+                        for g, bn in enumerate(sp["bnm"]):
+                            bn.num_batches_tracked.fill_(sp["nbt0"][g] + self.steps_done)
+            elif n.bn:
+                n.spec["nbt"].fill_(n.nbt0 + self.steps_done)
 
     def optimizer_state_dict(self, arch):
         """torch.optim-compatible state_dict of one architecture's optimizer (core.py:317-322)."""
@@ -574,10 +871,6 @@ class Engine:
         self._upload_opt_desc(step_inc=1)
 
 
-def _b(v):
-    return str(v).strip().lower() in ("1", "true", "yes", "y", "on", "t")
-
-
 class ModuleRunner:
     """Forward of one MLP module on the pkc kernels for any row count <= max_rows (MLP.forward for
     stand-alone calls, and the per-utterance forward of run_nn's forward mode)."""
@@ -590,8 +883,7 @@ class ModuleRunner:
         K = inp_dim
         for sp in self.specs:
             N = sp["out"]
-            sf = L.lib().pkc_gemm_pick_splits(max_rows, N, K)
-            self.bufs.append(dict(sf=sf, z=_f32(sf * max_rows * N, self.dev), K=K, N=N,
+            self.bufs.append(dict(z=_f32(MAX_SPLITS * max_rows * N, self.dev), K=K, N=N,
                                   xhat=_f32(max_rows * N, self.dev), sm=_f32(N, self.dev),
                                   si=_f32(N, self.dev), out=_f32(max_rows * N, self.dev),
                                   work=_f32(L.lib().pkc_dense_work_size(max_rows, N), self.dev)))
@@ -608,7 +900,7 @@ class ModuleRunner:
         cur, cld = x_ptr, ld
         for sp, b in zip(self.specs, self.bufs):
             N, K = b["N"], b["K"]
-            sf = L.lib().pkc_gemm_pick_splits(M, N, K)
+            sf = _splits(M, N, K, MAX_SPLITS)
             call("pkc_gemm", L.PREC_FP32, 1, 1, M, N, K, C.c_void_p(cur), cld, ptr(sp["W"]), K,
                  ptr(b["z"]), N, sf, M * N, s)
             if sp["act"] == "softmax":
@@ -627,7 +919,8 @@ class ModuleRunner:
                     running_mean=sp["rm"].data_ptr(), running_var=sp["rv"].data_ptr(), momentum=0.05,
                     eps=1e-5, save_mean=b["sm"].data_ptr(), save_invstd=b["si"].data_ptr(),
                     act=L.ACT[sp["act"]], drop_p=0.0, seed=0, step_ctr=None, stream_id=0,
-                    keep_in=None, keep_out=None, xhat=b["xhat"].data_ptr(), out=b["out"].data_ptr())
+                    keep_in=None, keep_out=None, xhat=b["xhat"].data_ptr(), out=b["out"].data_ptr(),
+                    count_n=0)
                 call("pkc_dense_fwd", C.byref(a), ptr(b["work"]), s)
             cur, cld = b["out"].data_ptr(), N
         return self.bufs[-1]["out"][:M * self.bufs[-1]["N"]].view(M, -1)
@@ -638,8 +931,8 @@ class ModuleRunner:
 
 
 class ForwardRunner:
-    """run_nn forward mode (core.py:134-145, 234-249): one utterance per batch, BatchNorm with
-    running statistics, no dropout, posteriors normalised by the log class prior."""
+    """run_nn forward mode (core.py:134-145, 234-249) for feed-forward models: one utterance per
+    batch, BatchNorm with running statistics, no dropout, posteriors normalised by the log prior."""
 
     def __init__(self, nets, lines, fea_cols, forward_outs, max_rows=4096):
         self.lines, self.fea_cols, self.outs = lines, fea_cols, forward_outs

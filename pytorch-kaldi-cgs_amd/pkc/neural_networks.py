@@ -169,3 +169,189 @@ class MLP(nn.Module):
         if self._engine is None or self._engine.rows < x.shape[0]:
             self._engine = ModuleRunner(self, x.shape[0], x.shape[1])
         return self._engine.forward(x, train=self.training)
+
+
+class liGRU(nn.Module):
+    """neural_networks.py:1429-1599 (options per proto/liGRU.proto).  Parameters: wh, wz (input
+    Linear), uh, uz (recurrent Linear, no bias), bn_wh, bn_wz, ln; same names and init draws."""
+
+    seq_model = True
+    cell = "ligru"
+    GATES = ("z", "h")
+
+    def __init__(self, options, inp_dim):
+        super().__init__()
+        o = options
+        self.input_dim = inp_dim
+        self.ligru_lay = _lst(o, "ligru_lay", int)
+        self.ligru_drop = _lst(o, "ligru_drop", float)
+        self.ligru_use_batchnorm = _lst(o, "ligru_use_batchnorm", strtobool)
+        self.ligru_use_laynorm = _lst(o, "ligru_use_laynorm", strtobool)
+        self.ligru_use_laynorm_inp = strtobool(o["ligru_use_laynorm_inp"])
+        self.ligru_use_batchnorm_inp = strtobool(o["ligru_use_batchnorm_inp"])
+        self.ligru_orthinit = strtobool(o["ligru_orthinit"])
+        self.ligru_act = _lst(o, "ligru_act")
+        self.bidir = strtobool(o["ligru_bidir"])
+        self.to_do = o.get("to_do", "train")
+        self.prune = False
+        self.guided_hcgs = False
+        self.apply_guided_hcgs = False
+        self.if_pattern = False
+        self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
+        self.wh, self.uh = nn.ModuleList(), nn.ModuleList()
+        self.wz, self.uz = nn.ModuleList(), nn.ModuleList()
+        self.ln, self.bn_wh, self.bn_wz = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        if self.ligru_use_laynorm_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.ligru_use_batchnorm_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.ligru_lay):
+            add_bias = not (self.ligru_use_laynorm[i] or self.ligru_use_batchnorm[i])
+            self.wh.append(nn.Linear(cur, n, bias=add_bias))
+            self.wz.append(nn.Linear(cur, n, bias=add_bias))
+            self.uh.append(nn.Linear(n, n, bias=False))
+            self.uz.append(nn.Linear(n, n, bias=False))
+            if self.ligru_orthinit:
+                nn.init.orthogonal_(self.uh[i].weight)
+                nn.init.orthogonal_(self.uz[i].weight)
+            self.bn_wh.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.bn_wz.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def prune_parameters(self):
+        raise NotImplementedError("the reference liGRU has no prune hook")
+
+    def check_supported(self):
+        if self.ligru_use_laynorm_inp or self.ligru_use_batchnorm_inp or any(self.ligru_use_laynorm):
+            raise NotImplementedError("LayerNorm / input normalisation in liGRU is not on the pkc path yet")
+
+    def layer_specs(self):
+        specs = []
+        for i, n in enumerate(self.ligru_lay):
+            specs.append(dict(H=n, act=self.ligru_act[i], bn=bool(self.ligru_use_batchnorm[i]),
+                              drop=self.ligru_drop[i], bidir=bool(self.bidir),
+                              W=[self.wz[i].weight, self.wh[i].weight],
+                              b=[self.wz[i].bias, self.wh[i].bias],
+                              U=[self.uz[i].weight, self.uh[i].weight],
+                              bnm=[self.bn_wz[i], self.bn_wh[i]], Wmask=None, Umask=None))
+        return specs
+
+
+class LSTM(nn.Module):
+    """neural_networks.py:468-1237.  The reference forces bidir off inside forward (:835), so a
+    bidirectional cfg crashes there on layer 2; pkc runs bidirectional LSTMs with the liGRU
+    shared-weight convention (BASELINE C4) and uni-directional ones exactly as the reference."""
+
+    seq_model = True
+    cell = "lstm"
+    GATES = ("f", "i", "o", "c")
+
+    def __init__(self, options, inp_dim):
+        super().__init__()
+        o = options
+        self.input_dim = inp_dim
+        self.lstm_lay = _lst(o, "lstm_lay", int)
+        self.lstm_drop = _lst(o, "lstm_drop", float)
+        self.lstm_use_batchnorm = _lst(o, "lstm_use_batchnorm", strtobool)
+        self.lstm_use_laynorm = _lst(o, "lstm_use_laynorm", strtobool)
+        self.lstm_use_laynorm_inp = strtobool(o["lstm_use_laynorm_inp"])
+        self.lstm_use_batchnorm_inp = strtobool(o["lstm_use_batchnorm_inp"])
+        self.lstm_act = _lst(o, "lstm_act")
+        self.lstm_orthinit = strtobool(o["lstm_orthinit"])
+        self.bidir = strtobool(o["lstm_bidir"])
+        self.to_do = o.get("to_do", "train")
+        self.lstm_hcgs = strtobool(o.get("lstm_hcgs", "False"))
+        self.hcgsx_block = _lst(o, "hcgsx_block", int) if "hcgsx_block" in o else []
+        self.hcgsh_block = _lst(o, "hcgsh_block", int) if "hcgsh_block" in o else []
+        self.hcgsx_sparse = _lst(o, "hcgsx_sparse", float) if "hcgsx_sparse" in o else []
+        self.hcgsh_sparse = _lst(o, "hcgsh_sparse", float) if "hcgsh_sparse" in o else []
+        self.lstm_quant = strtobool(o.get("lstm_quant", "False"))
+        self.param_quant = _lst(o, "param_quant", int) if "param_quant" in o else [8] * len(self.lstm_lay)
+        self.lstm_quant_inp = strtobool(o.get("lstm_quant_inp", "False"))
+        self.inp_quant = _lst(o, "inp_quant", int) if "inp_quant" in o else [16]
+        self.prune = strtobool(o.get("lstm_prune", "False"))
+        self.prune_perc = _lst(o, "lstm_prune_perc", float) if "lstm_prune_perc" in o else [0.0]
+        self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
+        self.guided_hcgs = strtobool(o.get("guided_hcgs", "False"))
+        self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
+        self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
+        self.arch_name = o.get("arch_name", "LSTM")
+        if self.guided_hcgs:
+            raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
+        if self.lstm_hcgs:                      # registered first, as neural_networks.py:548-550
+            self.hcgsx, self.hcgsh = nn.ModuleList(), nn.ModuleList()
+        if self.if_pattern:
+            self.pattern = {k: [] for k in ("pattern_w%sx" % g for g in self.GATES)}
+            self.pattern.update({k: [] for k in ("pattern_u%sh" % g for g in self.GATES)})
+            self.pattern_mask = {}
+        for g in self.GATES:
+            setattr(self, "w%sx" % g, nn.ModuleList())
+            setattr(self, "u%sh" % g, nn.ModuleList())
+        # registration order above = the reference's wfx, ufh, wix, uih, wox, uoh, wcx, uch
+        # (neural_networks.py:606-616), so parameters() / optimizer indices line up
+        self.ln = nn.ModuleList()
+        for g in self.GATES:
+            setattr(self, "bn_w%sx" % g, nn.ModuleList())
+        if self.lstm_use_laynorm_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.lstm_use_batchnorm_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.lstm_lay):
+            if not (self.lstm_use_laynorm[i] or self.lstm_use_batchnorm[i]):
+                raise IndexError("the reference LSTM creates its W/U layers only with BN or LN "
+                                 "(neural_networks.py:681-791)")
+            for g in self.GATES:
+                if self.lstm_quant:
+                    lin = _QLinear(cur, n, self.param_quant[i], False,
+                                   self.inp_quant[0] if self.lstm_quant_inp else None)
+                else:
+                    lin = nn.Linear(cur, n, bias=False)
+                getattr(self, "w%sx" % g).append(lin)
+            if self.lstm_hcgs:
+                self.hcgsx.append(_Mask(hcgs_mask(n, cur, self.hcgsx_block, self.hcgsx_sparse)))
+            for g in self.GATES:
+                if self.lstm_quant:
+                    lin = _QLinear(n, n, self.param_quant[i], False,
+                                   self.inp_quant[0] if self.lstm_quant_inp else None)
+                else:
+                    lin = nn.Linear(n, n, bias=False)
+                getattr(self, "u%sh" % g).append(lin)
+            if self.lstm_hcgs:
+                self.hcgsh.append(_Mask(hcgs_mask(n, n, self.hcgsh_block, self.hcgsh_sparse)))
+            if self.lstm_orthinit:
+                for g in self.GATES:
+                    nn.init.orthogonal_(getattr(self, "u%sh" % g)[i].weight)
+            for g in self.GATES:
+                getattr(self, "bn_w%sx" % g).append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def prune_parameters(self):
+        raise NotImplementedError("LSTM magnitude pruning is not on the pkc path yet")
+
+    def apply_ghcgs(self):
+        raise NotImplementedError("guided HCGS is outside the pkc hot path")
+
+    def check_supported(self):
+        if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp or any(self.lstm_use_laynorm):
+            raise NotImplementedError("LayerNorm / input normalisation in LSTM is not on the pkc path yet")
+        if self.lstm_quant or self.prune or self.if_pattern:
+            raise NotImplementedError("quantised / pruned / pattern LSTM is not on the pkc path yet")
+
+    def layer_specs(self):
+        specs = []
+        for i, n in enumerate(self.lstm_lay):
+            specs.append(dict(H=n, act=self.lstm_act[i], bn=bool(self.lstm_use_batchnorm[i]),
+                              drop=self.lstm_drop[i], bidir=bool(self.bidir),
+                              W=[getattr(self, "w%sx" % g)[i].weight for g in self.GATES],
+                              b=[None] * 4,
+                              U=[getattr(self, "u%sh" % g)[i].weight for g in self.GATES],
+                              bnm=[getattr(self, "bn_w%sx" % g)[i] for g in self.GATES],
+                              Wmask=self.hcgsx[i].mask if self.lstm_hcgs else None,
+                              Umask=self.hcgsh[i].mask if self.lstm_hcgs else None))
+        return specs

@@ -83,6 +83,27 @@ def test_product_mlp_init_matches_reference(variant):
             np.testing.assert_array_equal(v.numpy(), g["init/%s/%s" % (o["arch_name"], k)], err_msg=k)
 
 
+@pytest.mark.parametrize("tag,cls,kind,F,seed", [
+    ("ligru_bidir", "liGRU", "ligru", 20, 21), ("lstm", "LSTM", "lstm", 20, 23),
+    ("lstm_hcgs_quant", "LSTM", "lstm_hq", 24, 24)])
+def test_product_recurrent_init_matches_reference(tag, cls, kind, F, seed):
+    import pkc.neural_networks as NN
+    from cases import LIGRU_DEF, LSTM_DEF
+    opts = {"ligru": LIGRU_DEF, "lstm": LSTM_DEF,
+            "lstm_hq": dict(LSTM_DEF, lstm_hcgs="True", lstm_quant="True", lstm_quant_inp="True")}[kind]
+    cp = configparser.ConfigParser()
+    cp["s"] = {k: str(v) for k, v in opts.items()}
+    g = G("rnn.npz")
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    net = getattr(NN, cls)(cp["s"], F)
+    sd = net.state_dict()
+    ref_keys = sorted(k[len(tag) + 6:] for k in g.files if k.startswith(tag + "/init/"))
+    assert sorted(sd) == ref_keys
+    for k, v in sd.items():
+        np.testing.assert_array_equal(v.numpy(), g[tag + "/init/" + k], err_msg=k)
+
+
 def test_ark_writer_bytes_match_reference(tmp_path):
     from pkc import data_io
     gi = G("post_inputs.npz")
