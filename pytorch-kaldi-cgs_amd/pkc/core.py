@@ -205,8 +205,7 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         if pt != "none":
             ck = torch.load(pt, map_location="cuda", weights_only=True)
             nns[net_name].load_state_dict(ck["model_par"])
-    if any(arch_dict[a][2] for a in arch_dict):
-        raise NotImplementedError("sequence models go through pkc.core.run_nn_seq (round 2)")
+    seq_model = any(arch_dict[a][2] for a in arch_dict)
     lines = parse_model(config["model"]["model"])
     arch_opts = {a: config[arch_dict[a][0]] for a in nns}
     chunk = data_set
@@ -215,7 +214,43 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
 
     start = time.time()
     loss_tot = err_tot = 0.0
-    if to_do in ("train", "valid"):
+    lens = np.diff(np.concatenate([[0], np.asarray(chunk.end_index)]))
+    if seq_model:
+        eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=seed,
+                     train=(to_do == "train"), max_len=int(lens.max()))
+        for net_name in nns:
+            pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
+            if pt != "none" and to_do == "train":
+                ck = torch.load(pt, map_location="cpu", weights_only=True)
+                eng.load_optimizer_state_dict(net_name, ck["optimizer_par"])
+                eng.set_lr(net_name, float(config[arch_dict[net_name][0]]["arch_lr"]))
+        eng.bind_chunk(chunk.feats, chunk.labels, chunk.n_rows, end_index=chunk.end_index)
+        post_files, priors = {}, {}
+        if to_do == "forward":
+            for oi, out in enumerate(forward_outs):
+                suffix = "_to_decode.ark" if require_dec[oi] else ".ark"
+                post_files[out] = info_file.replace(".info", "_" + out + suffix)
+                open(post_files[out], "wb").close()
+                if forward_norm[oi]:
+                    counts = D.load_counts(forward_counts[oi])
+                    priors[out] = np.log(counts / np.sum(counts)).astype(np.float32)
+        for i in range(eng.n_batches):
+            if to_do == "train":
+                eng.train_step()       # python random draws the padding offsets (core.py:193)
+            else:
+                eng.eval_step()
+            if to_do == "forward":
+                for out in forward_outs:
+                    post = eng.head_output(out).cpu().numpy()
+                    if out in priors:                       # core.py:242-245, host side as there
+                        post = post - priors[out]
+                    D.write_mat_path(post_files[out], post, chunk.names[i], append=True)
+        if to_do != "forward":
+            loss_sum, err_sum = eng.chunk_totals()
+            loss_tot, err_tot = loss_sum / max(1, eng.n_batches), err_sum / max(1, eng.n_batches)
+        if to_do == "train":
+            eng.sync_state()
+    elif to_do in ("train", "valid"):
         eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=seed,
                      train=(to_do == "train"))
         for net_name in nns:

@@ -67,6 +67,56 @@ def chunk_cfg(d, name, to_do, scp, ali, pretrain="none", counts=None):
     return path
 
 
+def make_seq(path):
+    """Turn a chunk cfg into a liGRU (2 x 32, bidirectional) body cfg."""
+    cfg = configparser.ConfigParser()
+    cfg.read(path)
+    a1 = cfg["architecture1"]
+    keep = {k: a1[k] for k in ("arch_name", "arch_pretrain_file", "arch_freeze", "arch_opt",
+                               "opt_momentum", "opt_alpha", "opt_eps", "opt_centered",
+                               "opt_weight_decay")}
+    cfg["architecture1"] = dict(keep, arch_library="pkc.neural_networks", arch_class="liGRU",
+                                arch_seq_model="True", arch_lr="0.0016", ligru_lay="32,32",
+                                ligru_drop="0.2,0.2", ligru_use_laynorm_inp="False",
+                                ligru_use_batchnorm_inp="False", ligru_use_laynorm="False,False",
+                                ligru_use_batchnorm="True,True", ligru_bidir="True",
+                                ligru_act="relu,relu", ligru_orthinit="True", arch_opt="rmsprop")
+    cfg["batches"]["batch_size_train"] = "4"
+    cfg["batches"]["batch_size_valid"] = "4"
+    with open(path, "w") as f:
+        cfg.write(f)
+    return path
+
+
+def test_run_nn_ligru_train_forward(tmp_path):
+    from pkc.core import run_nn
+    d = str(tmp_path)
+    scp0, ali0 = write_data(d, 0)
+    counts = os.path.join(d, "counts")
+    with open(counts, "w") as f:
+        f.write("[ " + " ".join(str(i + 3) for i in range(64)) + " ]\n")
+    c_tr = make_seq(chunk_cfg(d, "train_ck0", "train", scp0, ali0))
+    c_va = make_seq(chunk_cfg(d, "valid", "valid", scp0, ali0))
+    data, _, _ = run_nn(None, None, None, None, None, None, c_tr, True, c_va)
+    info = configparser.ConfigParser()
+    info.read(os.path.join(d, "train_ck0.info"))
+    assert 0 < float(info["results"]["loss"]) < 20
+    c_fw = make_seq(chunk_cfg(d, "forward", "forward", scp0, ali0, counts=counts))
+    cfg = configparser.ConfigParser()
+    cfg.read(c_fw)
+    for i in (1, 2, 3):
+        cfg["architecture%d" % i]["arch_pretrain_file"] = os.path.join(d, "train_ck0_architecture%d.pkl" % i)
+    with open(c_fw, "w") as f:
+        cfg.write(f)
+    run_nn(None, None, None, None, None, None, c_fw, True, c_fw)
+    with open(os.path.join(d, "forward_out_dnn2_to_decode.ark"), "rb") as f:
+        mats = OL.parse_mat_ark(f.read())
+    assert len(mats) == 24
+    c = np.arange(3, 67, dtype=np.float64)
+    for k, m in mats:
+        np.testing.assert_allclose(np.exp(m + np.log(c / c.sum())).sum(1), 1.0, rtol=1e-4)
+
+
 def test_run_nn_train_valid_forward(tmp_path):
     from pkc.core import run_nn
     d = str(tmp_path)

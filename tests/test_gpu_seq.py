@@ -1,0 +1,111 @@
+"""Sequence-model training through the pkc engine vs the oracle: liGRU (bidirectional, BN, ReLU,
+recurrent dropout) and LSTM bodies with LogSoftmax cd/mono heads, padded batches with the
+reference's random left padding (core.py:183-200), three optimizer steps."""
+import configparser
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from cases import LIGRU_DEF, LSTM_DEF
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def make_cfg(body):
+    cfg = configparser.ConfigParser()
+    opt = dict(arch_opt="rmsprop", arch_lr="0.0016", opt_momentum="0.0", opt_alpha="0.95",
+               opt_eps="1e-8", opt_centered="False", opt_weight_decay="0.0", arch_freeze="False")
+    if body == "ligru":
+        cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2", **opt)
+    else:
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", **opt)
+    head = dict(dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False", to_do="train",
+                arch_name="head", dnn_lay="64", dnn_drop="0.0", dnn_use_batchnorm="False",
+                dnn_use_laynorm="False", dnn_act="softmax", **opt)
+    cfg["a2"] = head
+    cfg["a3"] = dict(head, arch_name="mono", dnn_lay="8", arch_lr="0.0004")
+    cfg["model"] = {"model": "o1=compute(rnn,fea)\no2=compute(head,o1)\no3=compute(mono,o1)\n"
+                             "lm=cost_nll(o3,lab_mono)\nlmw=mult_constant(lm,1.0)\n"
+                             "lc=cost_nll(o2,lab_cd)\nloss_final=sum(lc,lmw)\n"
+                             "err_final=cost_err(o2,lab_cd)"}
+    return cfg
+
+
+@pytest.mark.parametrize("body", ["ligru", "lstm"])
+def test_seq_engine_vs_oracle(body):
+    import pkc.neural_networks as NN
+    from oracle import nets as ON
+    from oracle import run as OR
+    from pkc.engine import Engine, parse_model
+    cfg = make_cfg(body)
+    F, B = 20, 4
+    secs = (("a1", F), ("a2", None), ("a3", None))
+    nets, onets, opts = {}, {}, {}
+    for sec, inp in secs:
+        o = cfg[sec]
+        if inp is None:
+            inp = nets["rnn"].out_dim
+        torch.manual_seed(3)
+        np.random.seed(3)
+        cls = {"ligru": "liGRU", "lstm": "LSTM"}[body] if sec == "a1" else "MLP"
+        nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
+        onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
+        onets[o["arch_name"]].load_state_dict(nets[o["arch_name"]].state_dict())
+        opts[o["arch_name"]] = o
+    for k in nets:
+        nets[k].to(DEV).train()
+        onets[k].train()
+    rs = np.random.RandomState(0)
+    lens = np.sort(rs.randint(5, 13, size=12))
+    end = np.cumsum(lens)
+    X = rs.randn(end[-1], F).astype(np.float32)
+    lab = np.stack([rs.randint(0, 64, end[-1]), rs.randint(0, 8, end[-1])], 1).astype(np.int32)
+    H = nets["rnn"].layer_specs()
+    bid = 2 if H[0]["bidir"] else 1
+    masks = {(("rnn", li)): torch.from_numpy((rs.rand(bid * B, sp["H"]) > 0.2).astype(np.float32))
+             for li, sp in enumerate(H)}
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fea": (0, F)}, ["lab_cd", "lab_mono"],
+                 batch=B, max_len=16, seed=1, rnn_drop_in={k: v.to(DEV) for k, v in masks.items()})
+    eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), end[-1], end_index=end)
+    oopt = {k: ON.make_optimizer(onets[k].parameters(), opts[k]) for k in onets}
+    lines = OR.parse_model(cfg["model"]["model"])
+    rng_e, rng_o = random.Random(7), random.Random(7)
+    snt = 0
+    for step in range(3):
+        batch = eng.next_seq_batch(rng_e)
+        begs, blens, lefts, T = batch
+        # oracle batch assembly exactly as core.py:183-200
+        inp = torch.zeros(T, B, F + 2)
+        for k in range(B):
+            n = int(lens[snt])
+            left = rng_o.randint(0, T - n)
+            b0 = int(end[snt] - n)
+            inp[left:left + n, k, :F] = torch.from_numpy(X[b0:b0 + n])
+            inp[left:left + n, k, F:] = torch.from_numpy(lab[b0:b0 + n].astype(np.float32))
+            assert left == lefts[k]
+            snt += 1
+        body_net = onets["rnn"]
+        f = body_net.forward
+        body_net.forward = lambda x, _f=f: _f(x, drop_masks=[masks[("rnn", i)] for i in range(len(H))])
+        outs = OR.train_step(lines, onets, oopt, {"rnn": True, "head": False, "mono": False},
+                             {"fea": (0, F)}, {"lab_cd": F, "lab_mono": F + 1}, inp, T, B)
+        body_net.forward = f
+        eng.train_step(batch=batch)
+        loss, err = eng.loss_values()
+        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-4)
+        np.testing.assert_allclose(err, outs["err_final"].item(), atol=1e-6)
+        post = eng.head_output("o2").cpu()
+        ref = outs["o2"].detach()
+        rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
+        assert rel < 1e-4, "step %d posterior rel err %.3g" % (step, rel)
+    for k in nets:
+        for name, v in nets[k].state_dict().items():
+            if name.endswith("num_batches_tracked"):
+                continue
+            ref = onets[k].state_dict()[name].double()
+            d = (v.cpu().double() - ref).norm().item()
+            assert d <= 1e-3 * ref.norm().item() + 1e-7, "%s %s %.3g" % (k, name, d)
