@@ -135,6 +135,7 @@ typedef struct {
   int kind;            /* PKC_OPT_* */
   float lr, wd, momentum, dampening, alpha, eps, beta1, beta2, clampv;
   int nesterov, centered, amsgrad, step;   /* step = 1-based count for this tensor */
+  float* qout; int qbits;   /* QuantizeLinear: also write the fake-quantised weight (qbits > 0) */
 } pkc_opt_tensor;
 int pkc_optim_step(const pkc_opt_tensor* tensors_dev, int ntensors, const int32_t* chunk_map_dev,
                    int nchunks, void* stream);
@@ -191,7 +192,21 @@ typedef struct {
   float* hs; float* cs; float* gates; float* y;
   const float* dy; int dy_nslab; int64_t dy_slab_stride;   /* dL/dy as split-K partial slabs */
   float* dgates; float* work;
+  /* QuantizeLinear U layers with input quantisation (quantized_modules.py:99-119): h_{t-1} is
+   * re-quantised once per gate (q1..q4, per-tensor max-abs) before each U product; U[] then points
+   * at the fake-quantised weights.  hq (T+1, B2, H) receives q4(h_{t-1}) — the value the reference
+   * keeps as hiddens[t-1] and as the saved input of the U backward. qbits = 0: off. */
+  int qbits; float* hq;
 } pkc_rnn_args;
+int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
+/* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that
+ * `reps` successive QuantizeLinear calls apply to one tensor; work >= 136 floats. */
+int pkc_fakequant_input(const float* x, float* out, int64_t n, int bits, int reps, float* work,
+                        void* stream);
+/* Pattern mask (sparsity.py:1112-1146) of W (rows x cols, multiples of ph x pw) for P <= 32
+ * patterns (P x ph x pw, {0,1}); ties select every maximal pattern (mask values can exceed 1). */
+int pkc_pattern_mask(const float* W, int rows, int cols, const float* patterns, int P, int ph,
+                     int pw, float* mask, void* stream);
 /* Sequence batch assembly (core.py:183-214): sentence k of the batch starts at chunk row beg[k],
  * has len[k] frames and is placed at time offset left[k] (python random.randint(0, max_len-len),
  * drawn on the host in the reference's order); the rest of the (max_len, B, F) input is zero and

@@ -69,6 +69,11 @@ __global__ __launch_bounds__(OPT_T) void optim_kernel(const pkc_opt_tensor* ts, 
     if (t.mask) p *= t.mask[i];
     if (t.clampv > 0.f) p = fminf(fmaxf(p, -t.clampv), t.clampv);
     t.p[i] = p;
+    if (t.qbits > 0) {   // Quantize(balanced=False) of the clamped weight (quantized_modules.py:91-96)
+      const float sc = ldexpf(1.f, t.qbits - 1);
+      const float sg = p > 0.f ? 1.f : (p < 0.f ? -1.f : 0.f);
+      t.qout[i] = ceilf(fabsf(p) * sc) / sc * sg;
+    }
   }
 }
 

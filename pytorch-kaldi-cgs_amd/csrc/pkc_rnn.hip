@@ -57,16 +57,56 @@ __device__ __forceinline__ float drop_val(const pkc_rnn_args& a, int r, int j, i
   return a.drop_mask[(int64_t)r * a.H + j];
 }
 
+// Dynamic input quantisation of h_{t-1} (quantized_modules.py:99-119), applied in place by each of
+// the four recurrent QuantizeLinear calls of a step (neural_networks.py:1086-1091): gate g reads
+// q_{g+1} = Q(q_g) with its own per-tensor max-abs var_{g+1}.
+__device__ __forceinline__ float qin(float x, float var, float scale) {
+  if (var == 0.f) return x;
+  const float s = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+  return ceilf(fabsf(x / var) * scale) / scale * var * s;
+}
+
+template <int G>
+__device__ void h_quant_vars(const float* hprev, int64_t n, float scale, float* vars) {
+  // vars[g] = max(|max q_g|, |min q_g|) over all of h_{t-1}, q_0 = h (block-redundant reduction)
+  __shared__ float rmx[RT], rmn[RT];
+  for (int g = 0; g < G; ++g) {
+    float mx = -INFINITY, mn = INFINITY;
+    for (int64_t e = threadIdx.x; e < n; e += RT) {
+      float v = hprev[e];
+      for (int p = 0; p < g; ++p) v = qin(v, vars[p], scale);
+      mx = fmaxf(mx, v);
+      mn = fminf(mn, v);
+    }
+    rmx[threadIdx.x] = mx;
+    rmn[threadIdx.x] = mn;
+    __syncthreads();
+    for (int o = RT / 2; o > 0; o >>= 1) {
+      if (threadIdx.x < o) {
+        rmx[threadIdx.x] = fmaxf(rmx[threadIdx.x], rmx[threadIdx.x + o]);
+        rmn[threadIdx.x] = fminf(rmn[threadIdx.x], rmn[threadIdx.x + o]);
+      }
+      __syncthreads();
+    }
+    const float a = fabsf(rmx[0]), b = fabsf(rmn[0]);
+    vars[g] = a > b ? a : b;
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------- forward step
-template <int G, int CELL>
+template <int G, int CELL, bool QH>
 __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
-  __shared__ float hsm[RR][KC + 1];
+  __shared__ float hsm[QH ? G : 1][RR][KC + 1];
   __shared__ float usm[G][RU][KC + 1];
   const RnnIdx ix = mkidx(a);
   const int j = blockIdx.x * RU + threadIdx.x % RU;
   const int r = blockIdx.y * RR + threadIdx.x / RU;
   const int H = a.H;
   const float* hprev = a.hs + (int64_t)t * ix.B2 * H;     // hs[t] = h_{t-1}
+  float vars[4] = {0.f, 0.f, 0.f, 0.f};
+  const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
+  if (QH) h_quant_vars<G>(hprev, (int64_t)ix.B2 * H, qscale, vars);
   float acc[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) acc[g] = 0.f;
@@ -75,7 +115,16 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
     for (int e = threadIdx.x; e < RR * KC; e += RT) {
       const int rr = e / KC, kk = e % KC;
       const int R = blockIdx.y * RR + rr, K = k0 + kk;
-      hsm[rr][kk] = (R < ix.B2 && K < H) ? hprev[(int64_t)R * H + K] : 0.f;
+      float v = (R < ix.B2 && K < H) ? hprev[(int64_t)R * H + K] : 0.f;
+      if (QH) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          v = qin(v, vars[g], qscale);
+          hsm[g][rr][kk] = v;
+        }
+      } else {
+        hsm[0][rr][kk] = v;
+      }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -88,12 +137,20 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
     const int rl = threadIdx.x / RU, jl = threadIdx.x % RU;
 #pragma unroll 8
     for (int kk = 0; kk < KC; ++kk) {
-      const float hv = hsm[rl][kk];
 #pragma unroll
-      for (int g = 0; g < G; ++g) acc[g] = fmaf(usm[g][jl][kk], hv, acc[g]);
+      for (int g = 0; g < G; ++g) acc[g] = fmaf(usm[g][jl][kk], hsm[QH ? g : 0][rl][kk], acc[g]);
     }
   }
   if (r >= ix.B2 || j >= H) return;
+  if (QH) {
+    // the hidden state the reference keeps for step t-1 (hiddens[t-1], and the saved input of the
+    // U backward) is the 4x re-quantised tensor; the last step's h is never quantised
+    float v = hprev[(int64_t)r * H + j];
+#pragma unroll
+    for (int g = 0; g < G; ++g) v = qin(v, vars[g], qscale);
+    a.hq[(int64_t)t * ix.B2 * H + (int64_t)r * H + j] = v;
+    if (t > 0) a.y[ix.out(t - 1, r, j)] = v;
+  }
   const int64_t TBH = (int64_t)a.T * a.B * H;   // gate stride of the (G, T, B, H) pre-activations
   const int64_t TB2H = (int64_t)a.T * ix.B2 * H; // gate stride of the saved activations
   const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
@@ -287,7 +344,10 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   }
   dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
   for (int t = 0; t < a->T; ++t) {
-    hipLaunchKernelGGL((rnn_fwd_step<G, CELL>), grid, dim3(RT), 0, s, *a, t);
+    if (a->qbits > 0)
+      hipLaunchKernelGGL((rnn_fwd_step<G, CELL, true>), grid, dim3(RT), 0, s, *a, t);
+    else
+      hipLaunchKernelGGL((rnn_fwd_step<G, CELL, false>), grid, dim3(RT), 0, s, *a, t);
   }
   PKC_LAUNCH_CHECK("pkc_rnn_fwd step");
   return PKC_OK;
@@ -316,6 +376,8 @@ static int check(const pkc_rnn_args* a, bool bwd) {
   for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U[g], "pkc_rnn: null U[%d]", g);
   PKC_CHECK_ARG(!a->train || a->drop_p <= 0.f || a->drop_mask, "pkc_rnn: dropout needs drop_mask");
   if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work, "pkc_rnn_bwd: null buffer");
+  PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir && (a->bidir ? 2 * a->B : a->B) <= RR),
+                "pkc_rnn: quantised h needs hq, a uni-directional layer and <= %d rows", RR);
   return PKC_OK;
 }
 

@@ -50,7 +50,8 @@ class OptTensor(C.Structure):
                 ("kind", C.c_int), ("lr", C.c_float), ("wd", C.c_float), ("momentum", C.c_float),
                 ("dampening", C.c_float), ("alpha", C.c_float), ("eps", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("clampv", C.c_float),
-                ("nesterov", C.c_int), ("centered", C.c_int), ("amsgrad", C.c_int), ("step", C.c_int)]
+                ("nesterov", C.c_int), ("centered", C.c_int), ("amsgrad", C.c_int), ("step", C.c_int),
+                ("qout", vp), ("qbits", C.c_int)]
 
 
 CELL_LIGRU, CELL_LSTM = 0, 1
@@ -62,10 +63,13 @@ class RnnArgs(C.Structure):
                 ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp), ("stream_id", i64),
                 ("drop_mask_in", vp), ("drop_mask", vp), ("hs", vp), ("cs", vp), ("gates", vp),
                 ("y", vp), ("dy", vp), ("dy_nslab", C.c_int), ("dy_slab_stride", i64),
-                ("dgates", vp), ("work", vp)]
+                ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp)]
 
 
 _SIGS = {
+    "pkc_fakequant_weight": (C.c_int, [vp, vp, i64, C.c_int, vp]),
+    "pkc_fakequant_input": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, vp, vp]),
+    "pkc_pattern_mask": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp]),
     "pkc_rnn_fwd": (C.c_int, [C.POINTER(RnnArgs), vp]),
     "pkc_rnn_bwd": (C.c_int, [C.POINTER(RnnArgs), vp, vp]),
     "pkc_seq_gather": (C.c_int, [vp, i64, C.c_int, vp, C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp,

@@ -75,17 +75,21 @@ class Layer:
             raise NotImplementedError("%s: BatchNorm before LogSoftmax is not on the pkc path" % self.name)
         if spec["ln"]:
             raise NotImplementedError("%s: LayerNorm is not on the pkc path yet" % self.name)
-        if spec["quant"] or spec["inp_quant"]:
-            raise NotImplementedError("%s: QuantizeLinear MLP layers are not on the pkc path yet"
-                                      % self.name)
         if self.act not in L.ACT and not self.head:
             raise NotImplementedError("%s: activation %s" % (self.name, self.act))
+        self.qbits = int(spec["quant"] or 0)      # QuantizeLinear weight bits (0: nn.Linear)
+        self.ibits = int(spec["inp_quant"] or 0)  # QuantizeLinear input bits (0: off)
+        self.reads = 1 if self.ibits else 0       # in-place input quantisations this layer applies
+        self.Wq = None
 
     def params(self):
         out = [(self.W, "dW", self.mask), (self.b, "db", None)]
         if self.bn:
             out += [(self.gamma, "dgamma", None), (self.beta, "dbeta", None)]
         return out
+
+    def quant_of(self, p):
+        return (self.Wq, self.qbits) if (p is self.W and self.qbits) else (None, 0)
 
 
 class RecNode:
@@ -108,21 +112,44 @@ class RecNode:
             if sp["act"] not in L.ACT:
                 raise NotImplementedError("%s: activation %s" % (arch, sp["act"]))
             sp["nbt0"] = [int(bn.num_batches_tracked.item()) for bn in sp["bnm"]]
+            sp.setdefault("qbits", 0)
+            sp.setdefault("ibits", 0)
+            if sp["ibits"] and sp["bidir"]:
+                raise NotImplementedError("%s: input quantisation of a bidirectional layer" % arch)
+        # in-place quantisations of the node's input (gate linears of layer 0)
+        self.ibits = self.layers[0]["ibits"]
+        self.reads = self.G if self.ibits else 0
+        self.qw = {}            # id(param) -> fake-quantised copy
+        self.emask = {}         # id(param) -> effective (HCGS x pattern) mask
 
     def params(self):
         out = []
         for li, sp in enumerate(self.layers):
             for g in range(self.G):
-                out.append((sp["W"][g], ("dW", li, g), sp["Wmask"]))
+                W = sp["W"][g]
+                out.append((W, ("dW", li, g), self.emask.get(id(W), sp["Wmask"])))
                 if sp["b"][g] is not None:
                     out.append((sp["b"][g], ("db", li, g), None))
             for g in range(self.G):
-                out.append((sp["U"][g], ("dU", li, g), sp["Umask"]))
+                U = sp["U"][g]
+                out.append((U, ("dU", li, g), self.emask.get(id(U), sp["Umask"])))
             if sp["bn"]:
                 for g in range(self.G):
                     out.append((sp["bnm"][g].weight, ("dgamma", li, g), None))
                     out.append((sp["bnm"][g].bias, ("dbeta", li, g), None))
         return out
+
+    def quant_of(self, p):
+        q = self.qw.get(id(p))
+        if q is None:
+            return None, 0
+        return q
+
+    def wq(self, li, kind, g):
+        """The weight a GEMM / the time loop multiplies with (fake-quantised when quantised)."""
+        p = self.layers[li][kind][g]
+        q = self.qw.get(id(p))
+        return q[0] if q is not None else p
 
 
 class Engine:
@@ -163,6 +190,7 @@ class Engine:
         self.rnn_drop_in = rnn_drop_in or {}
         self._build_graph()
         self._alloc()
+        self._build_masks()
         self._build_optim()
         self.graph = None
         self.graph_opt = None
@@ -246,8 +274,33 @@ class Engine:
             if lay.head and lay.label_col is None:
                 lay.label_col = -1
         self.layers = [n for n in self.nodes if not n.rec]     # dense layers (compat)
+        self._build_quant()
 
-    # ------------------------------------------------------------------ buffers
+    def _build_quant(self):
+        """Input fake-quantisation chains (quantized_modules.py:99-119, applied through `.data` at
+        :211-212): each quantising consumer of a tensor re-quantises its CURRENT value in place, so
+        the consumers of one tensor see versions q1, q2, ... in model order, a non-quantising
+        consumer sees the version current when it runs, and every weight gradient taken against
+        that tensor uses the final version (autograd saved the same tensor object)."""
+        self.qsrc = {}
+        for n in self.nodes:
+            key = ("fea", n.src[1], n.src[2]) if n.src[0] == "fea" else id(n.src[1])
+            ent = self.qsrc.setdefault(key, dict(bits=0, Q=0, src=n.src))
+            n.qkey, n.qv0 = key, ent["Q"]
+            if n.reads:
+                if ent["bits"] not in (0, n.ibits):
+                    raise NotImplementedError("%s: two input-quantisation widths on one tensor" % n.name)
+                ent["bits"] = n.ibits
+                ent["Q"] += n.reads
+        for key, ent in self.qsrc.items():
+            if not ent["Q"] or ent["src"][0] != "node":
+                continue
+            P = ent["src"][1]
+            # a quantised-in-place activation output changes the saved result only where autograd
+            # differentiates through it (tanh/sigmoid/elu with no dropout in between)
+            if not P.rec and P.act not in ("relu", "linear", "leaky_relu") and P.drop == 0.0:
+                raise NotImplementedError("%s: %s output quantised in place by a consumer" %
+                                          (P.name, P.act))
     def _alloc(self):
         M, dev = self.Mmax, self.dev
         self.cap = MAX_SPLITS if self.seq else None
@@ -268,9 +321,24 @@ class Engine:
             n.save_invstd = _f32(N, dev)
             n.dz = _f32(M * N, dev)
             n.work = _f32(L.lib().pkc_dense_work_size(M, N), dev)
+            if n.qbits:
+                n.Wq = torch.zeros_like(n.W)
             if n.head:
                 n.row_loss = _f32(M, dev)
                 n.row_err = _f32(M, dev)
+        for key, ent in self.qsrc.items():
+            if not ent["Q"]:
+                continue
+            src = ent["src"]
+            if src[0] == "fea":
+                if src[1] != 0 or src[2] != self.F:
+                    raise NotImplementedError("input quantisation of one of several feature streams")
+                width = self.F
+            else:
+                width = src[1].N
+            ent["width"] = width
+            ent["buf"] = _f32(ent["Q"] * M * width, dev)
+            ent["work"] = _f32(256, dev)
         for n in self.nodes:
             cap = 0
             for c in n.consumers:
@@ -328,9 +396,50 @@ class Engine:
                       dx=_f32(G * MAX_SPLITS * M * K, dev),
                       dW=[None] * G, db=[None] * G, dU=[None] * G, dgamma=[None] * G,
                       dbeta=[None] * G)
+            if sp["ibits"]:
+                lb["hq"] = _f32((T + 1) * B2 * H, dev)      # q4(h_{t-1}) per step
+                if n.lbuf:                                   # layers >= 1: q1..qG of y_{l-1}
+                    lb["xq"] = _f32(G * M * K, dev)
+                    lb["qwork"] = _f32(256, dev)
+            if sp["qbits"]:
+                for g in range(G):
+                    for p in (sp["W"][g], sp["U"][g]):
+                        n.qw[id(p)] = (torch.zeros_like(p), sp["qbits"])
             n.lbuf.append(lb)
             K = D
         n.out = n.lbuf[-1]["y"]
+
+    def _build_masks(self):
+        """Pattern masks (neural_networks.py:876-884, sparsity.py:1112-1146): computed once, at the
+        first forward, from |W| of every layer's gate weights — W_0 already multiplied by its HCGS
+        mask, the other layers' W and every U raw — and then multiplied into W / U once per layer
+        call (L times per forward; the masks are {0,1} except on tied tiles).  Folded here with the
+        HCGS masks into one effective mask per parameter that the optimizer epilogue applies."""
+        for n in self.nodes:
+            if not n.rec or not any(sp.get("pattern") for sp in n.layers):
+                continue
+            pk = n.net.pattern_kernels
+            P, ph, pw = pk.shape
+            pat = torch.from_numpy(np.ascontiguousarray(pk, dtype=np.float32)).to(self.dev)
+            nl = len(n.layers)
+            s = self._stream()
+            for li, sp in enumerate(n.layers):
+                for kind, hmask in (("W", sp["Wmask"]), ("U", sp["Umask"])):
+                    for g in range(n.G):
+                        p = sp[kind][g]
+                        src = p
+                        if kind == "W" and li == 0 and hmask is not None:
+                            src = p * hmask
+                        src = src.contiguous()
+                        rows, cols = p.shape
+                        if rows % ph or cols % pw:
+                            raise NotImplementedError("%s: %dx%d weight not tiled by %dx%d patterns"
+                                                      % (n.name, rows, cols, ph, pw))
+                        pm = torch.empty_like(p)
+                        call("pkc_pattern_mask", ptr(src), rows, cols, ptr(pat), P, ph, pw, ptr(pm), s)
+                        if nl > 1:
+                            pm = pm.pow(nl)
+                        n.emask[id(p)] = pm * hmask if hmask is not None else pm
 
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
@@ -346,7 +455,8 @@ class Engine:
                     g = n.lbuf[key[1]][key[0]][key[2]]
                 else:
                     g = getattr(n, key)
-                self.opt_entries.append(dict(arch=n.arch, p=p, g=g, mask=m, o=o,
+                q, qb = n.quant_of(p)
+                self.opt_entries.append(dict(arch=n.arch, p=p, g=g, mask=m, o=o, q=q, qbits=qb,
                                              s1=torch.zeros_like(p), s2=None, s3=None, step=0))
         for e in self.opt_entries:
             kind = e["o"]["arch_opt"]
@@ -372,11 +482,16 @@ class Engine:
             self.opt_map = torch.from_numpy(np.frombuffer(cmap, dtype=np.int32).copy()).to(self.dev)
             self.opt_desc = torch.zeros(n * C.sizeof(L.OptTensor), dtype=torch.uint8, device=self.dev)
             self._upload_opt_desc(step_inc=1)
-        # the reference multiplies the masks in before the first forward; do it once here
+        # the reference multiplies the masks in (and QuantizeLinear clamps W to [-1, 1]) before
+        # the first forward; do it once here, then fake-quantise the copy the GEMMs multiply with
+        s = self._stream()
         for n_ in self.nodes:
             for p, key, m in n_.params():
-                if m is not None:
-                    call("pkc_apply_mask", ptr(p), ptr(m), p.numel(), C.c_float(0.0), self._stream())
+                q, qb = n_.quant_of(p)
+                if m is not None or qb:
+                    call("pkc_apply_mask", ptr(p), ptr(m), p.numel(), C.c_float(1.0 if qb else 0.0), s)
+                if qb:
+                    call("pkc_fakequant_weight", ptr(p), ptr(q), p.numel(), qb, s)
 
     def _upload_opt_desc(self, step_inc):
         n = len(self.opt_entries)
@@ -404,7 +519,9 @@ class Engine:
                 t.amsgrad = _b(o["opt_amsgrad"])
             t.nesterov = _b(o.get("opt_nesterov", "False"))
             t.centered = _b(o.get("opt_centered", "False"))
-            t.clampv = 0.0
+            t.clampv = 1.0 if e["qbits"] else 0.0
+            t.qout = e["q"].data_ptr() if e["qbits"] else None
+            t.qbits = e["qbits"]
             t.step = e["step"] + step_inc
         host = torch.frombuffer(bytearray(C.string_at(arr, C.sizeof(arr))), dtype=torch.uint8)
         self.opt_desc.copy_(host)
@@ -471,6 +588,30 @@ class Engine:
             return self.x.data_ptr() + 4 * n.src[1], self.F
         return n.src[1].out.data_ptr(), n.src[1].N
 
+    def _version(self, n, v):
+        """(pointer, ld) of version v of n's input tensor (0: as produced, k: after k in-place
+        input quantisations)."""
+        if v == 0:
+            return self._src(n)
+        ent = self.qsrc[n.qkey]
+        w = ent["width"]
+        return ent["buf"].data_ptr() + 4 * (v - 1) * self.M * w, w
+
+    def _final_version(self, n):
+        """The value autograd saw for n's input at backward time (dW operand)."""
+        return self._version(n, self.qsrc[n.qkey]["Q"])
+
+    def _quant_chain(self, n, s):
+        """Materialise q1..qQ of n's input once, at its first quantising consumer."""
+        if not n.reads or n.qv0 != 0:
+            return
+        ent = self.qsrc[n.qkey]
+        x_ptr, _ = self._src(n)
+        nel = self.M * ent["width"]
+        self._k("fakequant_input x%d" % ent["Q"], 0, 4.0 * nel * (ent["Q"] + 2),
+                "pkc_fakequant_input", C.c_void_p(x_ptr), ptr(ent["buf"]), nel, ent["bits"],
+                ent["Q"], ptr(ent["work"]), s)
+
     # ------------------------------------------------------------------ forward
     def _gather(self, s, batch=None):
         if not self.seq:
@@ -495,12 +636,14 @@ class Engine:
 
     def _dense_fwd(self, n, s, train):
         M = self.M
-        a_ptr, lda = self._src(n)
+        self._quant_chain(n, s)
+        a_ptr, lda = self._version(n, n.qv0 + n.reads)
         sf = _splits(M, n.N, n.K, n.scap)
         n.sf = sf
+        W = n.Wq if n.qbits else n.W
         self._k("gemm_fwd %dx%dx%d" % (M, n.N, n.K), 2.0 * M * n.N * n.K,
                 4.0 * (M * n.K + n.N * n.K + sf * M * n.N), "pkc_gemm", self.prec,
-                1, 1, M, n.N, n.K, C.c_void_p(a_ptr), lda, ptr(n.W), n.K, ptr(n.zslab),
+                1, 1, M, n.N, n.K, C.c_void_p(a_ptr), lda, ptr(W), n.K, ptr(n.zslab),
                 n.N, sf, M * n.N, s)
         if n.head:
             has_lab = n.label_col >= 0
@@ -539,7 +682,9 @@ class Engine:
         a.act, a.train = L.ACT[sp["act"]], int(train)
         a.wpre = lb["wpre"].data_ptr()
         for g in range(n.G):
-            a.U[g] = sp["U"][g].data_ptr()
+            a.U[g] = n.wq(li, "U", g).data_ptr()
+        if sp["ibits"]:
+            a.qbits, a.hq = sp["ibits"], lb["hq"].data_ptr()
         a.drop_p = float(sp["drop"])
         a.seed = self.seed
         a.step_ctr = self.ctr.data_ptr()
@@ -555,16 +700,40 @@ class Engine:
         a.work = lb["rwork"].data_ptr()
         return a
 
+    def _rec_inputs(self, n, li):
+        """[(ptr, ld)] per gate of layer li's GEMM input, and the dW operand (final version)."""
+        M, G = self.M, n.G
+        sp, lb = n.layers[li], n.lbuf[li]
+        if li == 0:
+            vs = [self._version(n, n.qv0 + (g + 1 if n.reads else 0)) for g in range(G)]
+            fin = self._final_version(n) if self.qsrc[n.qkey]["Q"] else self._src(n)
+            return vs, fin
+        prev = n.lbuf[li - 1]
+        if not sp["ibits"]:
+            v = (prev["y"].data_ptr(), prev["D"])
+            return [v] * G, v
+        K = lb["K"]
+        vs = [(lb["xq"].data_ptr() + 4 * g * M * K, K) for g in range(G)]
+        return vs, vs[-1]
+
     def _rec_fwd(self, n, s, train):
         M, T = self.M, self.T
-        x_ptr, ldx = self._src(n)
+        self._quant_chain(n, s)
         for li, (sp, lb) in enumerate(zip(n.layers, n.lbuf)):
             H, K = lb["H"], lb["K"]
+            if li > 0 and sp["ibits"]:
+                prev = n.lbuf[li - 1]
+                self._k("fakequant_input x%d" % n.G, 0, 4.0 * M * K * (n.G + 2),
+                        "pkc_fakequant_input", ptr(prev["y"]), ptr(lb["xq"]), M * K, sp["ibits"],
+                        n.G, ptr(lb["qwork"]), s)
+            xin, _ = self._rec_inputs(n, li)
             for g in range(n.G):
+                x_ptr, ldx = xin[g]
                 sf = _splits(M, H, K, MAX_SPLITS)
                 self._k("rnn_gemm_W %dx%dx%d" % (M, H, K), 2.0 * M * H * K,
                         4.0 * (M * K + H * K + sf * M * H), "pkc_gemm", self.prec, 1, 1, M, H, K,
-                        C.c_void_p(x_ptr), ldx, ptr(sp["W"][g]), K, ptr(lb["zslab"]), H, sf, M * H, s)
+                        C.c_void_p(x_ptr), ldx, ptr(n.wq(li, "W", g)), K, ptr(lb["zslab"]), H, sf,
+                        M * H, s)
                 bn = sp["bnm"][g]
                 a = L.DenseFwdArgs(
                     M=M, N=H, nslab=sf, zslab=lb["zslab"].data_ptr(), slab_stride=M * H,
@@ -583,7 +752,6 @@ class Engine:
             ra = self._rnn_args(n, li, train, T)
             self._k("rnn_fwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_fwd", C.byref(ra), s)
-            x_ptr, ldx = lb["y"].data_ptr(), lb["D"]
 
     def _forward_kernels(self, s, train, batch=None):
         self._gather(s, batch)
@@ -628,7 +796,7 @@ class Engine:
                                dbias=n.db.data_ptr())
             self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (n.sb + 3), "pkc_dense_bwd",
                     C.byref(a), ptr(n.work), s)
-        a_ptr, lda = self._src(n)
+        a_ptr, lda = self._final_version(n) if self.qsrc[n.qkey]["Q"] else self._src(n)
         self._k("gemm_dW %dx%dx%d" % (n.N, n.K, M), 2.0 * M * n.N * n.K,
                 4.0 * (M * n.N + M * n.K + n.N * n.K), "pkc_gemm", self.prec, 0, 0,
                 n.N, n.K, M, ptr(n.dz), n.N, C.c_void_p(a_ptr), lda, ptr(n.dW), n.K, 1, 0, s)
@@ -637,7 +805,7 @@ class Engine:
             off = P.cons_off[P.consumers.index(n)]
             self._k("gemm_dX %dx%dx%d" % (M, n.K, n.N), 2.0 * M * n.N * n.K,
                     4.0 * (M * n.N + n.N * n.K + n.sx * M * n.K), "pkc_gemm",
-                    self.prec, 1, 0, M, n.K, n.N, ptr(n.dz), n.N, ptr(n.W), n.K,
+                    self.prec, 1, 0, M, n.K, n.N, ptr(n.dz), n.N, ptr(n.Wq if n.qbits else n.W), n.K,
                     C.c_void_p(P.gslab.data_ptr() + 4 * off * M * P.N), n.K, n.sx, M * n.K, s)
 
     def _rec_bwd(self, n, s, want_dx0=False):
@@ -651,10 +819,8 @@ class Engine:
             ra.dy, ra.dy_nslab, ra.dy_slab_stride = dy_ptr, dy_ns, dy_stride
             self._k("rnn_bwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_bwd", C.byref(ra), ptr(lb["dpre"]), s)
-            if li > 0:
-                x_ptr, ldx = n.lbuf[li - 1]["y"].data_ptr(), n.lbuf[li - 1]["D"]
-            else:
-                x_ptr, ldx = self._src(n)
+            _, (x_ptr, ldx) = self._rec_inputs(n, li)
+            hsrc = lb["hq"] if sp["ibits"] else lb["hs"]
             nx = 0
             for g in range(n.G):
                 bn = sp["bnm"][g]
@@ -679,12 +845,12 @@ class Engine:
                 self._k("rnn_gemm_dU %dx%dx%d" % (H, H, R2), 2.0 * R2 * H * H,
                         4.0 * (2 * R2 * H + H * H), "pkc_gemm", self.prec, 0, 0, H, H, R2,
                         C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,
-                        ptr(lb["hs"]), H, ptr(lb["dU"][g]), H, 1, 0, s)
+                        ptr(hsrc), H, ptr(lb["dU"][g]), H, 1, 0, s)
                 if li > 0 or want_dx0:
                     sx = _splits(M, K, H, MAX_SPLITS)
                     self._k("rnn_gemm_dX %dx%dx%d" % (M, K, H), 2.0 * M * H * K,
                             4.0 * (M * H + H * K + sx * M * K), "pkc_gemm", self.prec, 1, 0, M, K, H,
-                            dz, H, ptr(sp["W"][g]), K,
+                            dz, H, ptr(n.wq(li, "W", g)), K,
                             C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
                     nx += sx
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
@@ -883,25 +1049,51 @@ class ModuleRunner:
         K = inp_dim
         for sp in self.specs:
             N = sp["out"]
-            self.bufs.append(dict(z=_f32(MAX_SPLITS * max_rows * N, self.dev), K=K, N=N,
-                                  xhat=_f32(max_rows * N, self.dev), sm=_f32(N, self.dev),
-                                  si=_f32(N, self.dev), out=_f32(max_rows * N, self.dev),
-                                  work=_f32(L.lib().pkc_dense_work_size(max_rows, N), self.dev)))
+            b = dict(z=_f32(MAX_SPLITS * max_rows * N, self.dev), K=K, N=N,
+                     xhat=_f32(max_rows * N, self.dev), sm=_f32(N, self.dev),
+                     si=_f32(N, self.dev), out=_f32(max_rows * N, self.dev),
+                     work=_f32(L.lib().pkc_dense_work_size(max_rows, N), self.dev))
+            if sp["quant"]:
+                b["Wq"] = torch.zeros_like(sp["W"])
+            if sp["inp_quant"]:
+                b["xq"] = _f32(max_rows * K, self.dev)
+                b["qwork"] = _f32(256, self.dev)
+            self.bufs.append(b)
             K = N
-        for sp in self.specs:
-            if sp["mask"] is not None:
+        self.refresh()
+
+    def refresh(self):
+        """Re-apply HCGS masks / the QuantizeLinear clamp and re-quantise (after weights change)."""
+        s = Engine._stream()
+        for sp, b in zip(self.specs, self.bufs):
+            qb = int(sp["quant"] or 0)
+            if sp["mask"] is not None or qb:
                 call("pkc_apply_mask", ptr(sp["W"]), ptr(sp["mask"]), sp["W"].numel(),
-                     C.c_float(0.0), Engine._stream())
+                     C.c_float(1.0 if qb else 0.0), s)
+            if qb:
+                call("pkc_fakequant_weight", ptr(sp["W"]), ptr(b["Wq"]), sp["W"].numel(), qb, s)
 
     def run(self, x_ptr, ld, M, train=False, log_prior=None):
-        """x_ptr: device address of an (M, ld) fp32 matrix; returns the (M, N) output view."""
+        """x_ptr: device address of an (M, ld) fp32 matrix; returns the (M, N) output view.
+        With input quantisation on the first layer, self.input_version holds the address of the
+        quantised input (the value the reference leaves in the caller's tensor)."""
         assert M <= self.rows
         s = Engine._stream()
         cur, cld = x_ptr, ld
-        for sp, b in zip(self.specs, self.bufs):
+        self.input_version = None
+        for li, (sp, b) in enumerate(zip(self.specs, self.bufs)):
             N, K = b["N"], b["K"]
+            if sp["inp_quant"]:
+                if cld != K:
+                    raise NotImplementedError("input quantisation of a strided feature stream")
+                call("pkc_fakequant_input", C.c_void_p(cur), ptr(b["xq"]), M * K,
+                     int(sp["inp_quant"]), 1, ptr(b["qwork"]), s)
+                cur = b["xq"].data_ptr()
+                if li == 0:
+                    self.input_version = cur
+            W = b["Wq"] if sp["quant"] else sp["W"]
             sf = _splits(M, N, K, MAX_SPLITS)
-            call("pkc_gemm", L.PREC_FP32, 1, 1, M, N, K, C.c_void_p(cur), cld, ptr(sp["W"]), K,
+            call("pkc_gemm", L.PREC_FP32, 1, 1, M, N, K, C.c_void_p(cur), cld, ptr(W), K,
                  ptr(b["z"]), N, sf, M * N, s)
             if sp["act"] == "softmax":
                 a = L.NllArgs(M=M, N=N, nslab=sf, zslab=b["z"].data_ptr(), slab_stride=M * N,
@@ -950,11 +1142,13 @@ class ForwardRunner:
         M = end - beg
         if M > self.max_rows:
             raise ValueError("utterance of %d frames exceeds the forward buffer" % M)
-        produced, res = {}, {}
+        produced, res, cur = {}, {}, {}
         for out, op, a, b in self.lines:
             if op != "compute":
                 continue
-            if b in self.fea_cols:
+            if b in cur:                       # the version an earlier consumer quantised in place
+                xp, ld = cur[b]
+            elif b in self.fea_cols:
                 c0, _ = self.fea_cols[b]
                 xp, ld = feats.data_ptr() + 4 * (beg * feats.stride(0) + c0), feats.stride(0)
             else:
@@ -965,6 +1159,8 @@ class ForwardRunner:
                     self.priors_dev[out] = torch.from_numpy(priors[out]).to(feats.device)
                 lp = self.priors_dev[out]
             y = self.runners[a].run(xp, ld, M, train=False, log_prior=lp)
+            if self.runners[a].input_version is not None:
+                cur[b] = (self.runners[a].input_version, ld)
             produced[out] = y
             if out in self.outs:
                 res[out] = y.cpu().numpy()

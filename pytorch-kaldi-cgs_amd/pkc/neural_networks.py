@@ -150,7 +150,7 @@ class MLP(nn.Module):
                               rv=self.bn[i].running_var, nbt=self.bn[i].num_batches_tracked,
                               mask=self.hcgs[i].mask if self.mlp_hcgs else None,
                               quant=self.param_quant[i] if self.mlp_quant else 0,
-                              inp_quant=self.inp_quant[0] if self.mlp_quant_inp else 0))
+                              inp_quant=self.inp_quant[0] if (self.mlp_quant and self.mlp_quant_inp) else 0))
         return specs
 
     def check_supported(self):
@@ -158,9 +158,8 @@ class MLP(nn.Module):
             raise NotImplementedError("input LayerNorm/BatchNorm is not on the pkc MLP path yet")
         if any(self.dnn_use_laynorm):
             raise NotImplementedError("LayerNorm layers are not on the pkc MLP path yet")
-        if self.mlp_quant or self.prune or self.if_pattern:
-            raise NotImplementedError("quantised / pruned / pattern MLP layers are not on the pkc "
-                                      "MLP path yet")
+        if self.prune or self.if_pattern:
+            raise NotImplementedError("pruned / pattern MLP layers are not on the pkc MLP path yet")
 
     def forward(self, x):
         """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
@@ -278,6 +277,8 @@ class LSTM(nn.Module):
         self.guided_hcgs = strtobool(o.get("guided_hcgs", "False"))
         self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
         self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
+        self.pattern_shape = _lst(o, "pattern_shape", int) if "pattern_shape" in o else [8, 8]
+        self.pattern_from_file = o.get("pattern_file", None)
         self.arch_name = o.get("arch_name", "LSTM")
         if self.guided_hcgs:
             raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
@@ -340,8 +341,27 @@ class LSTM(nn.Module):
     def check_supported(self):
         if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp or any(self.lstm_use_laynorm):
             raise NotImplementedError("LayerNorm / input normalisation in LSTM is not on the pkc path yet")
-        if self.lstm_quant or self.prune or self.if_pattern:
-            raise NotImplementedError("quantised / pruned / pattern LSTM is not on the pkc path yet")
+        if self.prune:
+            raise NotImplementedError("LSTM magnitude pruning is not on the pkc path yet")
+        if self.if_pattern and self.pattern_kernels is None:
+            raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option or "
+                                      "patterns injected by run_nn)")
+
+    @property
+    def pattern_kernels(self):
+        """(P, ph, pw) pattern set: run_nn-injected, or loaded from the ``pattern_file`` option
+        (e.g. pattern_file/b08b08_k04_n16_pattern.npy, shape (P*ph, pw))."""
+        k = getattr(self, "_pattern_kernels", None)
+        if k is None and getattr(self, "pattern_from_file", None):
+            arr = np.load(self.pattern_from_file, allow_pickle=False).astype(np.float32)
+            ph, pw = self.pattern_shape
+            k = arr.reshape(-1, ph, pw)
+            self._pattern_kernels = k
+        return k
+
+    @pattern_kernels.setter
+    def pattern_kernels(self, v):
+        self._pattern_kernels = None if v is None else np.asarray(v, dtype=np.float32)
 
     def layer_specs(self):
         specs = []
@@ -353,5 +373,8 @@ class LSTM(nn.Module):
                               U=[getattr(self, "u%sh" % g)[i].weight for g in self.GATES],
                               bnm=[getattr(self, "bn_w%sx" % g)[i] for g in self.GATES],
                               Wmask=self.hcgsx[i].mask if self.lstm_hcgs else None,
-                              Umask=self.hcgsh[i].mask if self.lstm_hcgs else None))
+                              Umask=self.hcgsh[i].mask if self.lstm_hcgs else None,
+                              qbits=self.param_quant[i] if self.lstm_quant else 0,
+                              ibits=self.inp_quant[0] if (self.lstm_quant and self.lstm_quant_inp) else 0,
+                              pattern=bool(self.if_pattern)))
         return specs

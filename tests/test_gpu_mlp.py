@@ -34,7 +34,17 @@ def build_nets(cfg, dims, seed=2234, cls=None):
     return nets, opts
 
 
-@pytest.mark.parametrize("variant", ["plain", "hcgs"])
+def out_version(eng, lay, M):
+    """The value the reference's output tensor holds after the whole forward: consumers with input
+    quantisation rewrite it in place (quantized_modules.py:211-212)."""
+    ent = eng.qsrc.get(id(lay))
+    if ent and ent["Q"]:
+        n = M * lay.N
+        return ent["buf"][(ent["Q"] - 1) * n:ent["Q"] * n]
+    return lay.out[:M * lay.N]
+
+
+@pytest.mark.parametrize("variant", ["plain", "hcgs", "quant"])
 def test_engine_matches_reference_golden_steps(variant):
     from pkc.engine import Engine, parse_model
     g = G("mlp_%s.npz" % variant)
@@ -57,8 +67,11 @@ def test_engine_matches_reference_golden_steps(variant):
         np.testing.assert_allclose(err, g["step%d/err" % s][0])
         np.testing.assert_allclose(head.out.view(16, -1).cpu().numpy(), g["step%d/out_dnn2" % s],
                                    rtol=1e-4, atol=1e-5)
-        np.testing.assert_allclose(body.out.view(16, -1).cpu().numpy(), g["step%d/out_dnn1" % s],
-                                   rtol=1e-4, atol=1e-5)
+        # 16-bit input quantisation snaps to a grid of max|x| / 2^15: a last-bit difference in
+        # the fp32 sum in front of it can move one element across a ceil boundary (one quantum)
+        q_atol = 2.0 * float(np.abs(g["step%d/out_dnn1" % s]).max()) / 2 ** 15 if variant == "quant" else 0
+        np.testing.assert_allclose(out_version(eng, body, 16).view(16, -1).cpu().numpy(),
+                                   g["step%d/out_dnn1" % s], rtol=1e-4, atol=max(1e-5, q_atol))
     eng.sync_state()
     for n, net in nets.items():
         for k, v in net.state_dict().items():
@@ -69,11 +82,12 @@ def test_engine_matches_reference_golden_steps(variant):
                 # re-masks them; pkc stores W*mask right away (numerically identical forward)
                 m = net.state_dict()["hcgs.%s.mask" % k.split(".")[1]].cpu().numpy()
                 ref = ref * m
-            np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-6, err_msg="%s %s" % (n, k))
+            np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5 if variant == "quant" else 1e-6,
+                                       err_msg="%s %s" % (n, k))
     sq = eng.optimizer_state_dict("MLP_layers2")["state"]
     for pi, st in sq.items():
         np.testing.assert_allclose(st["square_avg"].numpy(), g["opt/MLP_layers2/%d" % pi],
-                                   rtol=1e-4, atol=1e-12)
+                                   rtol=2e-3 if variant == "quant" else 1e-4, atol=1e-12)
 
 
 def c1_config(drop="0.0"):

@@ -49,8 +49,13 @@ def dx0(eng, node):
     return lb["dx"][:node.G * sx * M * K].view(node.G * sx, M, K).sum(0)
 
 
+PATTERN = dict(if_pattern="True", pattern_mode="pattern", pattern_shape="8,8", pattern_nnz="4,4",
+               pattern_num="16,16")
 CASES = [("ligru_bidir", "liGRU", LIGRU_DEF, 7, 3, 20, 21),
-         ("lstm", "LSTM", LSTM_DEF, 7, 3, 20, 23)]
+         ("lstm", "LSTM", LSTM_DEF, 7, 3, 20, 23),
+         ("lstm_hcgs_quant", "LSTM", dict(LSTM_DEF, lstm_hcgs="True", lstm_quant="True",
+                                          lstm_quant_inp="True"), 7, 3, 24, 24),
+         ("lstm_pattern", "LSTM", dict(LSTM_DEF, **PATTERN), 5, 2, 24, 25)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
@@ -61,6 +66,9 @@ def test_recurrent_layer_matches_reference(case):
     torch.manual_seed(seed)
     np.random.seed(seed)
     net = getattr(NN, cls)(section(opts), F)
+    if tag == "lstm_pattern":
+        net.pattern_kernels = np.load(os.path.join(GOLDEN, "quant.npz"),
+                                      allow_pickle=False)["pattern_set"].reshape(16, 8, 8)
     # init parity is pinned bit-exactly on the build host (test_host_cpu); the box's LAPACK
     # rounds the orthogonal init's QR differently in the last bit, so start from the golden init
     sd = {}
@@ -91,8 +99,12 @@ def test_recurrent_layer_matches_reference(case):
                 grads["bn_w%sx.%d.bias" % (gate, li)] = lb["dbeta"][gi]
     for k, v in grads.items():
         ref = g[tag + "/grad/" + k]
-        np.testing.assert_allclose(v.cpu().numpy(), ref, rtol=1e-3, atol=1e-5, err_msg=k)
+        # with 16-bit input quantisation an fp32 last-bit difference can flip one element of a
+        # quantised operand by one grid step (max|x| / 2^15); allow that much in the gradient sums
+        atol = 1e-4 if "quant" in tag else 1e-5
+        np.testing.assert_allclose(v.cpu().numpy(), ref, rtol=1e-3, atol=atol, err_msg=k)
     for k, v in net.state_dict().items():
-        if "running" in k:
+        if "running" in k or k.endswith(".weight") and k[0] in "wu":
+            # BN statistics, and W / U after the forward's in-place masking + clamping
             np.testing.assert_allclose(v.cpu().numpy(), g[tag + "/post/" + k], rtol=1e-4, atol=1e-6,
                                        err_msg=k)
