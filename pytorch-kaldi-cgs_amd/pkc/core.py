@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import data_io as D
+from . import dist as DP
 from . import neural_networks as NN
 from .engine import Engine, ForwardRunner, parse_model
 from .neural_networks import strtobool
@@ -215,16 +216,27 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
     start = time.time()
     loss_tot = err_tot = 0.0
     lens = np.diff(np.concatenate([[0], np.asarray(chunk.end_index)]))
-    if seq_model:
-        eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=seed,
-                     train=(to_do == "train"), max_len=int(lens.max()))
+    # chunk-level data parallelism (pkc.dist): every rank trains on its share of the chunk, one
+    # gradient all-reduce per step; forward mode runs on rank 0 only (one posterior ark per chunk)
+    rank, ws = DP.world()
+    ws_eff = 1 if to_do == "forward" else ws
+    allreduce = DP.GradAllReduce() if (ws_eff > 1 and to_do == "train") else None
+    eseed = seed + 7919 * rank          # per-rank dropout streams
+    if to_do == "forward" and rank != 0:
+        pass
+    elif seq_model:
+        eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
+                     train=(to_do == "train"), max_len=int(lens.max()), grad_scale=1.0 / ws_eff)
         for net_name in nns:
             pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
             if pt != "none" and to_do == "train":
                 ck = torch.load(pt, map_location="cpu", weights_only=True)
                 eng.load_optimizer_state_dict(net_name, ck["optimizer_par"])
                 eng.set_lr(net_name, float(config[arch_dict[net_name][0]]["arch_lr"]))
-        eng.bind_chunk(chunk.feats, chunk.labels, chunk.n_rows, end_index=chunk.end_index)
+        eng.bind_chunk(chunk.feats, chunk.labels, chunk.n_rows, end_index=chunk.end_index,
+                       sentences=DP.shard_sentences(chunk.end_index, rank, ws_eff))
+        if ws_eff > 1:
+            eng.n_batches = DP.agree_min(eng.n_batches, device=eng.dev)
         post_files, priors = {}, {}
         if to_do == "forward":
             for oi, out in enumerate(forward_outs):
@@ -236,7 +248,7 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
                     priors[out] = np.log(counts / np.sum(counts)).astype(np.float32)
         for i in range(eng.n_batches):
             if to_do == "train":
-                eng.train_step()       # python random draws the padding offsets (core.py:193)
+                eng.train_step(allreduce)   # python random draws the padding offsets (core.py:193)
             else:
                 eng.eval_step()
             if to_do == "forward":
@@ -246,30 +258,34 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
                         post = post - priors[out]
                     D.write_mat_path(post_files[out], post, chunk.names[i], append=True)
         if to_do != "forward":
-            loss_sum, err_sum = eng.chunk_totals()
-            loss_tot, err_tot = loss_sum / max(1, eng.n_batches), err_sum / max(1, eng.n_batches)
+            loss_sum, err_sum = DP.sum_scalars(eng.chunk_totals(), device=eng.dev)
+            nb = max(1, eng.n_batches * ws_eff)
+            loss_tot, err_tot = loss_sum / nb, err_sum / nb
         if to_do == "train":
             eng.sync_state()
     elif to_do in ("train", "valid"):
-        eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=seed,
-                     train=(to_do == "train"))
+        eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
+                     train=(to_do == "train"), grad_scale=1.0 / ws_eff)
         for net_name in nns:
             pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
             if pt != "none" and to_do == "train":
                 ck = torch.load(pt, map_location="cpu", weights_only=True)
                 eng.load_optimizer_state_dict(net_name, ck["optimizer_par"])
                 eng.set_lr(net_name, float(config[arch_dict[net_name][0]]["arch_lr"]))
-        eng.bind_chunk(chunk.feats, chunk.labels, chunk.n_rows)
-        n_batches = chunk.n_rows // batch_size
+        r0, r1 = DP.shard_rows(chunk.n_rows, rank, ws_eff)
+        eng.bind_chunk(chunk.feats[r0:r1], chunk.labels[r0:r1], r1 - r0)
+        n_batches = DP.agree_min((r1 - r0) // batch_size, device=eng.dev)
+        eng.n_batches = n_batches
         if to_do == "train":
-            eng.capture()
+            eng.capture(split_optimizer=allreduce is not None)
             for i in range(n_batches):
-                eng.train_step()
+                eng.train_step(allreduce)
         else:
             for i in range(n_batches):
                 eng.eval_step()
-        loss_sum, err_sum = eng.chunk_totals()
-        loss_tot, err_tot = loss_sum / max(1, n_batches), err_sum / max(1, n_batches)
+        loss_sum, err_sum = DP.sum_scalars(eng.chunk_totals(), device=eng.dev)
+        nb = max(1, n_batches * ws_eff)
+        loss_tot, err_tot = loss_sum / nb, err_sum / nb
         if to_do == "train":
             eng.sync_state()
     else:
@@ -293,16 +309,20 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
     torch.cuda.synchronize()
     elapsed = time.time() - start
 
-    if to_do == "train":
-        for net_name, net in nns.items():
-            ck = {"model_par": net.state_dict(), "optimizer_par": eng.optimizer_state_dict(net_name)}
-            torch.save(ck, info_file.replace(".info", "_" + arch_dict[net_name][0] + ".pkl"))
-    with open(info_file, "w") as f:
-        f.write("[results]\n")
-        if to_do != "forward":
-            f.write("loss=%s\n" % np.float32(loss_tot))
-            f.write("err=%s\n" % np.float32(err_tot))
-        f.write("elapsed_time_chunk=%f\n" % elapsed)
+    if to_do == "train" and ws_eff > 1:
+        DP.average_buffers(list(nns.values()))
+    if rank == 0:
+        if to_do == "train":
+            for net_name, net in nns.items():
+                ck = {"model_par": net.state_dict(),
+                      "optimizer_par": eng.optimizer_state_dict(net_name)}
+                torch.save(ck, info_file.replace(".info", "_" + arch_dict[net_name][0] + ".pkl"))
+        with open(info_file, "w") as f:
+            f.write("[results]\n")
+            if to_do != "forward":
+                f.write("loss=%s\n" % np.float32(loss_tot))
+                f.write("err=%s\n" % np.float32(err_tot))
+            f.write("elapsed_time_chunk=%f\n" % elapsed)
 
     th.join()
     nxt = _finish_chunk(shared_next)

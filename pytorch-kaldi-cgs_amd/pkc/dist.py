@@ -1,0 +1,134 @@
+"""pkc.dist — chunk-level data parallelism for run_nn.
+
+One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE,
+MASTER_ADDR/PORT).  Every rank builds the same model from the same seeds (HCGS / pattern masks and
+init are drawn from the cfg seed, core.py:41-44), loads the same chunk and trains on a disjoint
+share of it:
+
+  * frame models (MLP): the shuffled frame matrix is cut into R contiguous row ranges;
+  * sequence models: the length-sorted sentences are dealt round-robin (rank r takes sentences
+    r, r+R, ...), so every rank sees the same length profile and similar padded batch shapes;
+  * every rank runs the same number of steps: the minimum over ranks (the reference drops the
+    remainder of a chunk the same way, core.py:157-162).
+
+Exchange per optimizer step: ONE all-reduce (SUM) of the flat fp32 gradient buffer the engine
+keeps (Engine.gflat, 26.7 MB for C1/C2), over RCCL ("nccl" backend = RCCL on ROCm, xGMI links).
+The engine pre-scales the loss gradient by 1/R, so the summed gradient is the gradient of the
+mean of the ranks' batch losses — each rank's loss being the reference's own per-batch loss.
+No other collective is on the data path.  Per chunk: the loss / err totals are summed for the
+.info file, and the BatchNorm running statistics (updated locally from each rank's batches) are
+averaged so the saved model is one replica.
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def world():
+    """(rank, world_size) of the current process group (0, 1 when not distributed)."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def init_from_env(backend=None):
+    """Initialise the default process group from torchrun's environment (no-op for one process).
+    backend: "nccl" (RCCL) when a GPU is visible, else "gloo"."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1 or (dist.is_available() and dist.is_initialized()):
+        return world()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend)
+    return world()
+
+
+def shard_rows(n_rows, rank, ws):
+    """[r0, r1) rows of a frame chunk owned by `rank` (contiguous, equal sizes, remainder dropped)."""
+    per = n_rows // ws
+    return rank * per, (rank + 1) * per
+
+
+def shard_sentences(end_index, rank, ws):
+    """Sentences of a length-sorted chunk owned by `rank`: (begin rows, lengths) int64 arrays of
+    sentences rank, rank+ws, ... (end_index: cumulative sentence ends, data_io.py:81-83)."""
+    e = np.asarray(end_index, dtype=np.int64)
+    b = np.concatenate([[0], e[:-1]])
+    sel = np.arange(rank, len(e), ws)
+    return b[sel], (e - b)[sel]
+
+
+def agree_min(n, device=None):
+    """The minimum of an integer over all ranks (steps every rank can run)."""
+    rank, ws = world()
+    if ws == 1:
+        return int(n)
+    t = torch.tensor([int(n)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def sum_scalars(vals, device=None):
+    """Element-wise sum of a list of floats over ranks."""
+    rank, ws = world()
+    if ws == 1:
+        return [float(v) for v in vals]
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return [float(v) for v in t.cpu()]
+
+
+class GradAllReduce:
+    """Callable handed to Engine.train_step(allreduce=...): sums the flat gradient buffer over all
+    ranks in one collective (the engine already scaled the loss gradient by 1/R)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.calls = 0
+
+    def __call__(self, gflat):
+        dist.all_reduce(gflat, group=self.group)
+        self.calls += 1
+
+
+def average_buffers(modules, device=None):
+    """Average BatchNorm running_mean / running_var over ranks (one all-reduce per chunk)."""
+    rank, ws = world()
+    if ws == 1:
+        return
+    bufs = [b for m in modules for n, b in m.named_buffers()
+            if n.endswith("running_mean") or n.endswith("running_var")]
+    if not bufs:
+        return
+    flat = torch.cat([b.detach().reshape(-1).to(device or b.device) for b in bufs])
+    dist.all_reduce(flat)
+    flat /= ws
+    off = 0
+    for b in bufs:
+        n = b.numel()
+        b.copy_(flat[off:off + n].view_as(b).to(b.device))
+        off += n
+
+
+def check_replicas(modules, device=None):
+    """True when every rank holds bit-identical parameters (one max/min all-reduce of a checksum);
+    run once after init: the masks and weights come from identical seeds on every rank."""
+    rank, ws = world()
+    if ws == 1:
+        return True
+    acc = torch.zeros(2, dtype=torch.float64, device=device)
+    for m in modules:
+        for p in m.parameters():
+            v = p.detach().double().reshape(-1).to(acc.device)
+            idx = torch.arange(1, v.numel() + 1, dtype=torch.float64, device=acc.device)
+            acc[0] += (v * idx).sum()
+            acc[1] += v.abs().sum()
+    hi, lo = acc.clone(), acc.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo))

@@ -534,15 +534,20 @@ class Engine:
             self._upload_opt_desc(step_inc=1)
 
     # ------------------------------------------------------------------ chunk binding
-    def bind_chunk(self, feats, labels, n_rows, end_index=None):
+    def bind_chunk(self, feats, labels, n_rows, end_index=None, sentences=None):
         """feats: (N, F) fp32 device tensor (row stride >= F); labels: (N, nlab) int32 device;
-        end_index: cumulative utterance ends (sequence models)."""
+        end_index: cumulative utterance ends (sequence models); sentences: optional (begin rows,
+        lengths) subset of them (a data-parallel rank's share, pkc.dist.shard_sentences)."""
         assert feats.dtype == torch.float32 and labels.dtype == torch.int32
         assert feats.shape[1] >= self.F and labels.shape[1] == self.nlab
         self.chunk_feats, self.chunk_labels = feats, labels
         if self.seq:
-            self.end_index = np.asarray(end_index, dtype=np.int64)
-            self.n_batches = len(self.end_index) // self.B         # core.py:157-159
+            if sentences is None:
+                e = np.asarray(end_index, dtype=np.int64)
+                sentences = (np.concatenate([[0], e[:-1]]), e - np.concatenate([[0], e[:-1]]))
+            self.sent_beg = np.asarray(sentences[0], dtype=np.int64)
+            self.sent_len = np.asarray(sentences[1], dtype=np.int64)
+            self.n_batches = len(self.sent_beg) // self.B           # core.py:157-159
             self.snt = 0
         else:
             self.n_batches = int(n_rows) // self.B                  # core.py:161-162
@@ -554,11 +559,9 @@ class Engine:
         """core.py:183-200: the next B sentences, padded to the longest with a random number of
         leading zeros (python random.randint, drawn in the reference's order)."""
         rng = rng or random
-        e = self.end_index
         i0 = self.snt
-        ends = e[i0:i0 + self.B]
-        begs = np.concatenate([[e[i0 - 1] if i0 > 0 else 0], ends[:-1]])
-        lens = ends - begs
+        begs = self.sent_beg[i0:i0 + self.B]
+        lens = self.sent_len[i0:i0 + self.B]
         T = int(lens.max())
         if T > self.max_len:
             raise ValueError("batch of %d frames exceeds max_len %d" % (T, self.max_len))
