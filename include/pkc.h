@@ -21,7 +21,9 @@ extern "C" {
 #define PKC_ABI_VERSION 1
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
-enum { PKC_PREC_FP32 = 0, PKC_PREC_BF16 = 1 };
+/* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
+ * BF16IN: operands stored as bf16 in HBM (A and B point at bf16 arrays), fp32 accumulation */
+enum { PKC_PREC_FP32 = 0, PKC_PREC_BF16 = 1, PKC_PREC_BF16IN = 2 };
 /* neural_networks.py:54-78 act_fun */
 enum { PKC_ACT_LINEAR = 0, PKC_ACT_RELU = 1, PKC_ACT_TANH = 2, PKC_ACT_SIGMOID = 3,
        PKC_ACT_HTANH = 4, PKC_ACT_LEAKY = 5, PKC_ACT_ELU = 6 };
@@ -44,9 +46,25 @@ const char* pkc_last_error(void);
  * order, so results are deterministic.  splits<=0 picks a split count for the shape.
  * ------------------------------------------------------------------------------------------- */
 int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
-             const float* A, int64_t lda, const float* B, int64_t ldb,
+             const void* A, int64_t lda, const void* B, int64_t ldb,
              float* C, int64_t ldc, int splits, int64_t slab_stride, void* stream);
 int pkc_gemm_pick_splits(int M, int N, int K);
+/* Up to 8 independent operations in one launch — the launch boundary (~1.5-1.9 us on MI355X)
+ * dominates a 128-row batch's matmuls, so a layer's dW and dX, two heads' logits, or the heads'
+ * dW/dX together with their bias gradients and the loss reduction share one kernel.
+ *   PKC_OP_GEMM  : exactly pkc_gemm(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
+ *                  splits, slab_stride)
+ *   PKC_OP_COLSUM: C[n] = sum_m A[m*N + n]  (M rows, N columns, fp32)
+ *   PKC_OP_LOSS  : pkc_loss_finalize(nheads = M, row_loss = A, weights = B, rows = N,
+ *                  row_err = X1, out = C, acc = X2, advance_ctr = X3) */
+enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2 };
+typedef struct {
+  int a_kcontig, b_kcontig, M, N, K, splits;
+  const void* A; int64_t lda; const void* B; int64_t ldb;
+  float* C; int64_t ldc; int64_t slab_stride;
+  int kind; const void* X1; void* X2; void* X3;
+} pkc_gemm_problem;
+int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Dense layer epilogue, forward (neural_networks.py:306-317: drop(act(BN(z)))) where
@@ -109,6 +127,7 @@ typedef struct {
   float weight;
   float* logp; const float* log_prior;
   float* dlogits; float* row_loss; float* row_err;
+  void* dlogits_bf16;  /* optional bf16 copy of dlogits (operand of the fused row backward) */
 } pkc_nll_args;
 int pkc_nll_fused(const pkc_nll_args* a, void* stream);
 
@@ -116,7 +135,10 @@ int pkc_nll_fused(const pkc_nll_args* a, void* stream);
  * err = mean(row_err_of_err_head); writes out[0]=loss_final, out[1]=err, out[2+h]=mean loss h and
  * accumulates acc[0]+=loss_final, acc[1]+=err (core.py:251-252 loss_sum/err_sum on device). */
 int pkc_loss_finalize(int nheads, const float* const* row_loss, const float* weights, int M,
-                      const float* row_err, float* out, float* acc, void* stream);
+                      const float* row_err, float* out, float* acc, int64_t* advance_ctr,
+                      void* stream);   /* advance_ctr (optional): += 1 after the reduction */
+/* Several heads' pkc_nll_fused in one launch (n <= 4). */
+int pkc_nll_fused_multi(const pkc_nll_args* args, int n, void* stream);
 
 /* Column sums over rows of sum_s slabs (bias gradient of a head: autograd of + bias). */
 int pkc_colsum(int M, int N, int nslab, const float* x, int64_t slab_stride, float* out,
@@ -129,13 +151,14 @@ int pkc_colsum(int M, int N, int nslab, const float* x, int64_t slab_stride, flo
  * pattern multiply (neural_networks.py:258, 858-861, 980-983) and the in-place QuantizeLinear
  * clamp (quantized_modules.py:79) that the next forward would otherwise apply.
  * ------------------------------------------------------------------------------------------- */
-typedef struct {
+typedef struct pkc_opt_tensor_s {
   float* p; const float* g; float* s1; float* s2; float* s3; const float* mask;
   int64_t n;
   int kind;            /* PKC_OPT_* */
   float lr, wd, momentum, dampening, alpha, eps, beta1, beta2, clampv;
   int nesterov, centered, amsgrad, step;   /* step = 1-based count for this tensor */
   float* qout; int qbits;   /* QuantizeLinear: also write the fake-quantised weight (qbits > 0) */
+  void* bout;               /* optional bf16 copy of the updated parameter (MFMA operand) */
 } pkc_opt_tensor;
 int pkc_optim_step(const pkc_opt_tensor* tensors_dev, int ntensors, const int32_t* chunk_map_dev,
                    int nchunks, void* stream);
@@ -149,11 +172,15 @@ int pkc_apply_mask(float* p, const float* mask, int64_t n, float clampv, void* s
  * Batch assembly for non-sequential models (core.py:203-205: inp = data_set[b:b+B]):
  * copy rows [i*B, (i+1)*B) of the chunk's feature matrix and label columns into static buffers,
  * with i read from a device counter (so the step can be replayed from a hipGraph); the counter
- * is incremented by the last block when `advance` is set.
+ * is incremented by the last block when `advance` is set (otherwise by the step's loss
+ * reduction, pkc_loss_finalize's advance_ctr).
  * ------------------------------------------------------------------------------------------- */
 int pkc_batch_gather(const float* feats, int64_t ld_feats, int F, const int32_t* labels, int nlab,
                      int B, int64_t n_batches, int64_t* step_ctr, float* x_out, int32_t* lab_out,
-                     int advance, void* stream);
+                     int advance, void* x_bf16, void* stream);   /* x_bf16: optional bf16 copy */
+
+/* dst (bf16) = src (fp32), n elements (bf16 operand copies for the MFMA matmuls) */
+int pkc_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Chunk preparation on the GPU (data_io.py:105-145 context_window + load_chunk normalisation,

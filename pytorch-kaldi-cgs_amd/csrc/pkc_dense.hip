@@ -228,24 +228,304 @@ __global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args 
   }
 }
 
+template <int NS>
 __global__ __launch_bounds__(ET) void colsum_kernel(int M, int N, int nslab, const float* x,
                                                     int64_t slab, float* out, int accumulate) {
-  // one workgroup per 64 columns, 4 row-threads striding over all rows (bias grad of a head)
+  // one workgroup per 64 columns; 4 row-threads x 8 rows x NS slabs of loads in flight per step
+  // (clamped, unconditional loads: see the small-batch section below)
   __shared__ float red[ET];
   const int c = blockIdx.x * EC + threadIdx.x % EC;
   const int t = threadIdx.x / EC;
-  float s0 = 0.f, s1 = 0.f;
-  if (c < N) {
-    int r = t;
-    for (; r + ER < M; r += 2 * ER) {
-      s0 += slab_sum(x + (int64_t)r * N + c, slab, nslab);
-      s1 += slab_sum(x + (int64_t)(r + ER) * N + c, slab, nslab);
+  const int cc = min(c, N - 1);
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.f;
+  for (int r0 = 0; r0 < M; r0 += 8 * ER) {
+    float v[8][NS];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + t + ER * u, M - 1);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        const int sq = q < nslab ? q : nslab - 1;
+        v[u][q] = x[(int64_t)sq * slab + (int64_t)r * N + cc];
+      }
     }
-    if (r < M) s0 += slab_sum(x + (int64_t)r * N + c, slab, nslab);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float z = v[u][0];
+#pragma unroll
+      for (int q = 1; q < NS; ++q) z += (q < nslab) ? v[u][q] : 0.f;
+      acc[u] += (r0 + t + ER * u < M) ? z : 0.f;
+    }
   }
-  const float s = colsum4(s0 + s1, red);
+  const float s = colsum4(((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])),
+                          red);
   if (c < N && t == 0) out[c] = accumulate ? out[c] + s : s;
 }
+
+// ------------------------------------------------------------- small-batch fused forms (M <= 512)
+// A workgroup owns 16 columns x ALL rows of the batch, so the BatchNorm column statistics are a
+// workgroup reduction (wave shuffles + 4-entry LDS merge) and the layer epilogue is ONE launch
+// with every load issued up front: split-K slabs are summed in registers (NS = power-of-two bound
+// on the slab count, loads clamped to the last slab instead of branched, so none is serialised).
+constexpr int FG = 4, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4sel(bool k, float4 v) {
+  return k ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float f4get(const float4& v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ void f4set(float4& v, int j, float x) {
+  if (j == 0) v.x = x; else if (j == 1) v.y = x; else if (j == 2) v.z = x; else v.w = x;
+}
+
+// column-sum of a float4 (4 columns) over the 64 row-groups of the workgroup; all threads get it
+__device__ __forceinline__ float4 colsum_rows(float4 v, float4* red) {
+#pragma unroll
+  for (int o = FG; o < 64; o <<= 1) {
+    v.x += __shfl_xor(v.x, o, 64);
+    v.y += __shfl_xor(v.y, o, 64);
+    v.z += __shfl_xor(v.z, o, 64);
+    v.w += __shfl_xor(v.w, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c4 = threadIdx.x % FG;
+  __syncthreads();
+  if (lane < FG) red[wave * FG + lane] = v;
+  __syncthreads();
+  return f4add(f4add(red[c4], red[FG + c4]), f4add(red[2 * FG + c4], red[3 * FG + c4]));
+}
+
+template <int NS, int RI>
+__device__ __forceinline__ void load_slabs(const float* __restrict__ base, int64_t stride, int ns,
+                                           int rg, int M, int64_t N, int c, bool cok, float4* z) {
+  float4 v[RI][NS];
+#pragma unroll
+  for (int i = 0; i < RI; ++i) {
+    const int row = rg + RG * i;
+    const bool ok = cok && row < M;
+    const float* p = base + (ok ? (int64_t)row * N + c : 0);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const int sq = q < ns ? q : ns - 1;
+      v[i][q] = *reinterpret_cast<const float4*>(p + (int64_t)sq * stride);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RI; ++i) {
+    float4 acc = v[i][0];
+#pragma unroll
+    for (int q = 1; q < NS; ++q) acc = f4add(acc, f4sel(q < ns, v[i][q]));
+    const int row = rg + RG * i;
+    z[i] = f4sel(cok && row < M, acc);
+  }
+}
+
+template <int NS, int RI>
+__global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args a) {
+  __shared__ float4 red[4 * FG];
+  const int c4 = threadIdx.x % FG, rg = threadIdx.x / FG;
+  const int c = blockIdx.x * FC + c4 * 4;
+  const bool cok = c < a.N;
+  const int64_t N = a.N;
+  const int M = a.M;
+  float4 z[RI];
+  load_slabs<NS, RI>(a.zslab, a.slab_stride, a.nslab, rg, M, N, c, cok, z);
+  const float4 b = (cok && a.bias) ? *reinterpret_cast<const float4*>(a.bias + c)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RI; ++i) z[i] = f4sel(cok && rg + RG * i < M, f4add(z[i], b));
+  float4 mean = make_float4(0.f, 0.f, 0.f, 0.f), invstd = make_float4(1.f, 1.f, 1.f, 1.f);
+  float4 gam = make_float4(1.f, 1.f, 1.f, 1.f), bet = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.norm == PKC_NORM_BN_TRAIN) {
+    float4 sum = z[0];
+#pragma unroll
+    for (int i = 1; i < RI; ++i) sum = f4add(sum, z[i]);
+    sum = colsum_rows(sum, red);
+    const float inv = 1.f / (float)M;
+    mean = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
+    float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < RI; ++i) {
+      if (rg + RG * i < M) {
+        const float dx = z[i].x - mean.x, dy = z[i].y - mean.y, dz = z[i].z - mean.z,
+                    dw = z[i].w - mean.w;
+        m2 = f4add(m2, make_float4(dx * dx, dy * dy, dz * dz, dw * dw));
+      }
+    }
+    m2 = colsum_rows(m2, red);
+    const float4 var = make_float4(m2.x * inv, m2.y * inv, m2.z * inv, m2.w * inv);
+    invstd = make_float4(1.f / sqrtf(var.x + a.eps), 1.f / sqrtf(var.y + a.eps),
+                         1.f / sqrtf(var.z + a.eps), 1.f / sqrtf(var.w + a.eps));
+    if (cok) {
+      gam = *reinterpret_cast<const float4*>(a.gamma + c);
+      bet = *reinterpret_cast<const float4*>(a.beta + c);
+      if (rg == 0) {
+        *reinterpret_cast<float4*>(a.save_mean + c) = mean;
+        *reinterpret_cast<float4*>(a.save_invstd + c) = invstd;
+        const float cn = (float)(a.count_n > 0 ? a.count_n : M);
+        float4 rm = *reinterpret_cast<const float4*>(a.running_mean + c);
+        float4 rv = *reinterpret_cast<const float4*>(a.running_var + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float vj = f4get(var, j);
+          const float unb = cn > 1.f ? vj * cn / (cn - 1.f) : vj;
+          f4set(rm, j, (1.f - a.momentum) * f4get(rm, j) + a.momentum * f4get(mean, j));
+          f4set(rv, j, (1.f - a.momentum) * f4get(rv, j) + a.momentum * unb);
+        }
+        *reinterpret_cast<float4*>(a.running_mean + c) = rm;
+        *reinterpret_cast<float4*>(a.running_var + c) = rv;
+      }
+    }
+  } else if (a.norm == PKC_NORM_BN_EVAL && cok) {
+    mean = *reinterpret_cast<const float4*>(a.running_mean + c);
+    const float4 rv = *reinterpret_cast<const float4*>(a.running_var + c);
+    invstd = make_float4(1.f / sqrtf(rv.x + a.eps), 1.f / sqrtf(rv.y + a.eps),
+                         1.f / sqrtf(rv.z + a.eps), 1.f / sqrtf(rv.w + a.eps));
+    gam = *reinterpret_cast<const float4*>(a.gamma + c);
+    bet = *reinterpret_cast<const float4*>(a.beta + c);
+  }
+  if (!cok) return;
+  const bool drop = a.drop_p > 0.f;
+  const float scale = drop ? 1.f / (1.f - a.drop_p) : 1.f;
+  const uint32_t thr = drop ? (uint32_t)((double)(1.f - a.drop_p) * 4294967296.0) : 0u;
+  const int64_t step = a.step_ctr ? *a.step_ctr : 0;
+#pragma unroll
+  for (int i = 0; i < RI; ++i) {
+    const int row = rg + RG * i;
+    if (row >= M) break;
+    const int64_t idx = (int64_t)row * N + c;
+    float4 xh, o;
+    uint32_t kw = 0;
+    uchar4 kin = make_uchar4(1, 1, 1, 1);
+    if (drop && a.keep_in) kin = *reinterpret_cast<const uchar4*>(a.keep_in + idx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float zj = f4get(z[i], j);
+      const float x = (a.norm == PKC_NORM_NONE) ? zj : (zj - f4get(mean, j)) * f4get(invstd, j);
+      const float y = (a.norm == PKC_NORM_NONE) ? zj : x * f4get(gam, j) + f4get(bet, j);
+      float v = act_fwd(a.act, y);
+      if (drop) {
+        uint32_t k;
+        if (a.keep_in) k = j == 0 ? kin.x : (j == 1 ? kin.y : (j == 2 ? kin.z : kin.w));
+        else k = hash3(a.seed, (uint64_t)a.stream_id, (uint64_t)step * (uint64_t)(M * N) + idx + j) < thr;
+        kw |= (k ? 1u : 0u) << (8 * j);
+        v = k ? v * scale : 0.f;
+      }
+      f4set(xh, j, x);
+      f4set(o, j, v);
+    }
+    if (drop && a.keep_out) *reinterpret_cast<uint32_t*>(a.keep_out + idx) = kw;
+    if (a.xhat) *reinterpret_cast<float4*>(a.xhat + idx) = xh;
+    *reinterpret_cast<float4*>(a.out + idx) = o;
+  }
+}
+
+template <int NS, int RI>
+__global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args a) {
+  __shared__ float4 red[4 * FG];
+  const int c4 = threadIdx.x % FG, rg = threadIdx.x / FG;
+  const int c = blockIdx.x * FC + c4 * 4;
+  const bool cok = c < a.N;
+  const int64_t N = a.N;
+  const int M = a.M;
+  float4 g[RI], xh[RI];
+  uint32_t kp[RI];
+  load_slabs<NS, RI>(a.gslab, a.slab_stride, a.nslab, rg, M, N, c, cok, g);
+  const bool drop = a.drop_p > 0.f;
+#pragma unroll
+  for (int i = 0; i < RI; ++i) {
+    const int row = rg + RG * i;
+    const bool ok = cok && row < M;
+    const int64_t idx = ok ? (int64_t)row * N + c : 0;
+    xh[i] = *reinterpret_cast<const float4*>(a.xhat + idx);
+    kp[i] = drop ? *reinterpret_cast<const uint32_t*>(a.keep + idx) : 0xffffffffu;
+  }
+  const bool bn = a.norm == PKC_NORM_BN_TRAIN;
+  const float4 gam = (cok && bn) ? *reinterpret_cast<const float4*>(a.gamma + c)
+                                 : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 bet = (cok && bn) ? *reinterpret_cast<const float4*>(a.beta + c)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float scale = drop ? 1.f / (1.f - a.drop_p) : 1.f;
+  float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdyx = sdy;
+  float4 dy[RI];
+#pragma unroll
+  for (int i = 0; i < RI; ++i) {
+    const bool ok = cok && rg + RG * i < M;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = f4get(g[i], j);
+      if (drop) gj = ((kp[i] >> (8 * j)) & 0xffu) ? gj * scale : 0.f;
+      const float x = f4get(xh[i], j);
+      const float y = bn ? x * f4get(gam, j) + f4get(bet, j) : x;
+      const float d = ok ? gj * act_bwd(a.act, y, act_fwd(a.act, y)) : 0.f;
+      f4set(dy[i], j, d);
+    }
+    sdy = f4add(sdy, dy[i]);
+    sdyx = f4add(sdyx, make_float4(dy[i].x * xh[i].x, dy[i].y * xh[i].y, dy[i].z * xh[i].z,
+                                   dy[i].w * xh[i].w));
+  }
+  sdy = colsum_rows(sdy, red);
+  sdyx = colsum_rows(sdyx, red);
+  if (!cok) return;
+  if (rg == 0) {
+    if (bn) {
+      if (a.dgamma) *reinterpret_cast<float4*>(a.dgamma + c) = sdyx;
+      if (a.dbeta) *reinterpret_cast<float4*>(a.dbeta + c) = sdy;
+      // a bias in front of BatchNorm cancels in (z - mean): its gradient is exactly zero
+      if (a.dbias) *reinterpret_cast<float4*>(a.dbias + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (a.dbias) {
+      *reinterpret_cast<float4*>(a.dbias + c) = sdy;
+    }
+  }
+  float4 k = make_float4(1.f, 1.f, 1.f, 1.f), mdy = make_float4(0.f, 0.f, 0.f, 0.f), mdyx = mdy;
+  if (bn) {
+    const float4 is = *reinterpret_cast<const float4*>(a.save_invstd + c);
+    const float inv = 1.f / (float)M;
+    k = make_float4(gam.x * is.x, gam.y * is.y, gam.z * is.z, gam.w * is.w);
+    mdy = make_float4(sdy.x * inv, sdy.y * inv, sdy.z * inv, sdy.w * inv);
+    mdyx = make_float4(sdyx.x * inv, sdyx.y * inv, sdyx.z * inv, sdyx.w * inv);
+  }
+#pragma unroll
+  for (int i = 0; i < RI; ++i) {
+    const int row = rg + RG * i;
+    if (row >= M) break;
+    float4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = f4get(dy[i], j);
+      f4set(o, j, bn ? f4get(k, j) * (d - f4get(mdy, j) - f4get(xh[i], j) * f4get(mdyx, j)) : d);
+    }
+    *reinterpret_cast<float4*>(a.dz + (int64_t)row * N + c) = o;
+  }
+}
+
+static bool small_ok(int M, int N, int nslab, const void* p0, const void* p1, int64_t stride) {
+  return M <= 2 * RG && N % 4 == 0 && nslab <= 8 && ((uintptr_t)p0 % 16 == 0) &&
+         ((uintptr_t)p1 % 16 == 0) && (nslab == 1 || stride % 4 == 0);
+}
+
+#define PKC_SMALL_LAUNCH(KERN, args, M, nslab, stream)                                          \
+  do {                                                                                         \
+    dim3 grid_((args).N / FC + ((args).N % FC ? 1 : 0));                                       \
+    const int ri_ = (M) <= RG ? 1 : 2;                                                         \
+    const int ns_ = (nslab) <= 1 ? 1 : ((nslab) <= 2 ? 2 : ((nslab) <= 4 ? 4 : 8));            \
+    if (ri_ == 1) {                                                                            \
+      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 1>), grid_, dim3(FT), 0, stream, args);       \
+      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 1>), grid_, dim3(FT), 0, stream, args);  \
+      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 1>), grid_, dim3(FT), 0, stream, args);  \
+      else hipLaunchKernelGGL((KERN<8, 1>), grid_, dim3(FT), 0, stream, args);                \
+    } else {                                                                                   \
+      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 2>), grid_, dim3(FT), 0, stream, args);       \
+      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 2>), grid_, dim3(FT), 0, stream, args);  \
+      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 2>), grid_, dim3(FT), 0, stream, args);  \
+      else hipLaunchKernelGGL((KERN<8, 2>), grid_, dim3(FT), 0, stream, args);                \
+    }                                                                                          \
+  } while (0)
 
 }  // namespace pkc
 
@@ -267,6 +547,17 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   PKC_CHECK_ARG(a->drop_p >= 0.f && a->drop_p < 1.f, "pkc_dense_fwd: drop_p out of range");
   PKC_CHECK_ARG(a->nslab == 1 || a->slab_stride >= (int64_t)a->M * a->N,
                 "pkc_dense_fwd: slab_stride too small");
+  if (small_ok(a->M, a->N, a->nslab, a->zslab, a->out, a->slab_stride) &&
+      (uintptr_t)a->xhat % 16 == 0 && (!a->bias || (uintptr_t)a->bias % 16 == 0) &&
+      (a->norm == PKC_NORM_NONE || ((uintptr_t)a->gamma % 16 == 0 && (uintptr_t)a->beta % 16 == 0 &&
+                                    (uintptr_t)a->running_mean % 16 == 0 &&
+                                    (uintptr_t)a->running_var % 16 == 0)) &&
+      (a->norm != PKC_NORM_BN_TRAIN ||
+       ((uintptr_t)a->save_mean % 16 == 0 && (uintptr_t)a->save_invstd % 16 == 0))) {
+    PKC_SMALL_LAUNCH(dense_fwd_small_kernel, *a, a->M, a->nslab, S(stream));
+    PKC_LAUNCH_CHECK("pkc_dense_fwd small");
+    return PKC_OK;
+  }
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   if (a->norm == PKC_NORM_BN_TRAIN) {
     hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
@@ -285,6 +576,16 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
                 "pkc_dense_bwd: BN needs gamma/beta/save_invstd");
   PKC_CHECK_ARG(a->norm != PKC_NORM_BN_EVAL, "pkc_dense_bwd: backward through eval BN unsupported");
   PKC_CHECK_ARG(a->drop_p == 0.f || a->keep, "pkc_dense_bwd: dropout needs the keep mask");
+  if (small_ok(a->M, a->N, a->nslab, a->gslab, a->dz, a->slab_stride) &&
+      (uintptr_t)a->xhat % 16 == 0 && (!a->dbias || (uintptr_t)a->dbias % 16 == 0) &&
+      (a->norm == PKC_NORM_NONE ||
+       ((uintptr_t)a->gamma % 16 == 0 && (uintptr_t)a->beta % 16 == 0 &&
+        (uintptr_t)a->save_invstd % 16 == 0 && (!a->dgamma || (uintptr_t)a->dgamma % 16 == 0) &&
+        (!a->dbeta || (uintptr_t)a->dbeta % 16 == 0)))) {
+    PKC_SMALL_LAUNCH(dense_bwd_small_kernel, *a, a->M, a->nslab, S(stream));
+    PKC_LAUNCH_CHECK("pkc_dense_bwd small");
+    return PKC_OK;
+  }
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd stats");
@@ -297,8 +598,17 @@ extern "C" int pkc_colsum(int M, int N, int nslab, const float* x, int64_t slab_
                           int accumulate, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(M > 0 && N > 0 && nslab >= 1 && x && out, "pkc_colsum: bad arguments");
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + EC - 1) / EC), dim3(ET), 0, S(stream), M, N, nslab, x,
-                     slab_stride, out, accumulate);
+  PKC_CHECK_ARG(nslab <= 16, "pkc_colsum: at most 16 slabs");
+  const dim3 grid((N + EC - 1) / EC);
+  if (nslab == 1)
+    hipLaunchKernelGGL(colsum_kernel<1>, grid, dim3(ET), 0, S(stream), M, N, nslab, x, slab_stride, out,
+                       accumulate);
+  else if (nslab <= 4)
+    hipLaunchKernelGGL(colsum_kernel<4>, grid, dim3(ET), 0, S(stream), M, N, nslab, x, slab_stride, out,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(colsum_kernel<16>, grid, dim3(ET), 0, S(stream), M, N, nslab, x, slab_stride,
+                       out, accumulate);
   PKC_LAUNCH_CHECK("pkc_colsum");
   return PKC_OK;
 }

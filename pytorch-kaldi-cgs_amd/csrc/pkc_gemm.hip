@@ -11,8 +11,11 @@
 //              lane reads 16 contiguous floats of its row with ds_read_b128).
 //   PREC_BF16: v_mfma_f32_32x32x16_bf16 with fp32 accumulation, 2 MFMA per k-tile; operands are
 //              rounded to bf16 when staged into LDS.
+//   PREC_BF16IN: the same MFMA with operands already stored as bf16 in HBM (the bf16 copies of
+//              weights / activations / gradients the step keeps): half the bytes per workgroup,
+//              one 16-byte load per thread per operand per k-tile.
 // Split-K over blockIdx.z writes deterministic partial slabs (summed by the consumer kernels).
-#include "pkc_common.h"
+#include "pkc_ops.h"
 
 namespace pkc {
 
@@ -38,7 +41,10 @@ struct Lds<PKC_PREC_BF16> {
   __bf16 b[BN * LD];
 };
 
-// Register staging of one 64x32 operand tile (8 floats per thread).
+// Register staging of one 64x32 operand tile (8 floats per thread).  Loads are issued
+// unconditionally from clamped (always valid) addresses and out-of-range values are zeroed by a
+// select afterwards: a load guarded by a runtime condition makes hipcc branch around it and drain
+// the whole vmcnt queue, which would serialise the prefetch ring.
 template <bool KC, bool VEC>
 struct Stage {
   float v[8];
@@ -49,31 +55,31 @@ struct Stage {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int idx = t + NT * i;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (KC) {
-          const int r = idx >> 3, k = (idx & 7) * 4;
-          if (r0 + r < rmax && k0 + k < kend)
-            x = *reinterpret_cast<const float4*>(P + (int64_t)(r0 + r) * ld + k0 + k);
-        } else {
-          const int k = idx >> 4, r = (idx & 15) * 4;
-          if (k0 + k < kend && r0 + r < rmax)
-            x = *reinterpret_cast<const float4*>(P + (int64_t)(k0 + k) * ld + r0 + r);
-        }
-        v[4 * i + 0] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+        int r, k;
+        if (KC) { r = idx >> 3; k = (idx & 7) * 4; }
+        else { k = idx >> 4; r = (idx & 15) * 4; }
+        const bool ok = (r0 + r < rmax) && (k0 + k < kend);
+        const int rr = min(r0 + r, rmax - (KC ? 1 : 4));
+        const int kk = min(k0 + k, kend - (KC ? 4 : 1));
+        const float4 x = KC ? *reinterpret_cast<const float4*>(P + (int64_t)rr * ld + kk)
+                            : *reinterpret_cast<const float4*>(P + (int64_t)kk * ld + rr);
+        v[4 * i + 0] = ok ? x.x : 0.f;
+        v[4 * i + 1] = ok ? x.y : 0.f;
+        v[4 * i + 2] = ok ? x.z : 0.f;
+        v[4 * i + 3] = ok ? x.w : 0.f;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int idx = t + NT * i;
-        float x = 0.f;
-        if (KC) {
-          const int r = idx >> 5, k = idx & 31;
-          if (r0 + r < rmax && k0 + k < kend) x = P[(int64_t)(r0 + r) * ld + k0 + k];
-        } else {
-          const int k = idx >> 6, r = idx & 63;
-          if (k0 + k < kend && r0 + r < rmax) x = P[(int64_t)(k0 + k) * ld + r0 + r];
-        }
-        v[i] = x;
+        int r, k;
+        if (KC) { r = idx >> 5; k = idx & 31; }
+        else { k = idx >> 6; r = idx & 63; }
+        const bool ok = (r0 + r < rmax) && (k0 + k < kend);
+        const int rr = min(r0 + r, rmax - 1);
+        const int kk = min(k0 + k, kend - 1);
+        const float x = KC ? P[(int64_t)rr * ld + kk] : P[(int64_t)kk * ld + rr];
+        v[i] = ok ? x : 0.f;
       }
     }
   }
@@ -110,15 +116,110 @@ struct Stage {
   }
 };
 
-template <int PREC, bool AKC, bool BKC, bool VEC>
-__global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const float* __restrict__ A,
-                                                  int64_t lda, const float* __restrict__ B,
-                                                  int64_t ldb, float* __restrict__ C, int64_t ldc,
-                                                  int kchunk, int64_t slab_stride) {
-  __shared__ Lds<PREC> sm;
+__device__ __forceinline__ bf16x8 ld8h(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ bf16x8 zero8h() {
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  return z;
+}
+
+// Register staging of one 64x32 bf16 operand tile: one 16-byte load per thread (VEC) or eight
+// 2-byte loads; clamped addresses + zeroing selects as in Stage.
+template <bool KC, bool VEC>
+struct StageH {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const __bf16* __restrict__ P, int64_t ld, int r0, int rmax,
+                                       int k0, int kend) {
+    const int t = threadIdx.x;
+    int r, k;
+    if (KC) { r = t >> 2; k = (t & 3) * 8; }
+    else { k = t >> 3; r = (t & 7) * 8; }
+    if (VEC) {
+      const bool ok = (r0 + r < rmax) && (k0 + k < kend);
+      const int rr = min(r0 + r, rmax - (KC ? 1 : 8));
+      const int kk = min(k0 + k, kend - (KC ? 8 : 1));
+      const bf16x8 x = KC ? ld8h(P + (int64_t)rr * ld + kk) : ld8h(P + (int64_t)kk * ld + rr);
+      v = ok ? x : zero8h();
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rj = KC ? r : r + j, kj = KC ? k + j : k;
+        const bool ok = (r0 + rj < rmax) && (k0 + kj < kend);
+        const int rr = min(r0 + rj, rmax - 1), kk = min(k0 + kj, kend - 1);
+        const __bf16 x = KC ? P[(int64_t)rr * ld + kk] : P[(int64_t)kk * ld + rr];
+        v[j] = ok ? x : (__bf16)0.f;
+      }
+    }
+  }
+  template <typename T, int LD>
+  __device__ __forceinline__ void store(T* __restrict__ s) const {
+    const int t = threadIdx.x;
+    if (KC) {
+      const int r = t >> 2, k = (t & 3) * 8;
+      *reinterpret_cast<bf16x8*>(&s[r * LD + k]) = v;
+    } else {
+      const int k = t >> 3, r = (t & 7) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[(r + j) * LD + k] = v[j];
+    }
+  }
+};
+
+template <bool BIN, bool KC, bool VEC>
+struct StageSel {
+  using T = Stage<KC, VEC>;
+  using E = float;
+};
+template <bool KC, bool VEC>
+struct StageSel<true, KC, VEC> {
+  using T = StageH<KC, VEC>;
+  using E = __bf16;
+};
+
+template <int PREC>
+__device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, int r, int h,
+                                          f32x16& acc) {
   constexpr int LD = Lds<PREC>::LD;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int kbeg = blockIdx.z * kchunk;
+  if constexpr (PREC == PKC_PREC_FP32) {
+    const float4* pa = reinterpret_cast<const float4*>(&sm.a[(wm * 32 + r) * LD + 16 * h]);
+    const float4* pb = reinterpret_cast<const float4*>(&sm.b[(wn * 32 + r) * LD + 16 * h]);
+    float av[16], bv[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 x = pa[q], y = pb[q];
+      av[4 * q] = x.x; av[4 * q + 1] = x.y; av[4 * q + 2] = x.z; av[4 * q + 3] = x.w;
+      bv[4 * q] = y.x; bv[4 * q + 1] = y.y; bv[4 * q + 2] = y.z; bv[4 * q + 3] = y.w;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 av = *reinterpret_cast<const bf16x8*>(&sm.a[(wm * 32 + r) * LD + 16 * t + 8 * h]);
+      bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sm.b[(wn * 32 + r) * LD + 16 * t + 8 * h]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+    }
+  }
+}
+
+// DEPTH k-tiles are in flight in registers at any time: with M = 128-row batches a workgroup's
+// k-range is only a few tiles long, so the whole range is requested up front instead of one
+// HBM/L2 round trip per tile.
+template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN>
+__device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz, int M, int N, int K,
+                                          const void* __restrict__ Av, int64_t lda,
+                                          const void* __restrict__ Bv, int64_t ldb,
+                                          float* __restrict__ C, int64_t ldc, int kchunk,
+                                          int64_t slab_stride) {
+  using SA = typename StageSel<BIN, AKC, VEC>::T;
+  using SB = typename StageSel<BIN, BKC, VEC>::T;
+  const auto* A = reinterpret_cast<const typename StageSel<BIN, AKC, VEC>::E*>(Av);
+  const auto* B = reinterpret_cast<const typename StageSel<BIN, BKC, VEC>::E*>(Bv);
+  constexpr int LD = Lds<PREC>::LD;
+  const int n0 = bx * BN, m0 = by * BM;
+  const int kbeg = bz * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -128,46 +229,32 @@ __global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const flo
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 
-  Stage<AKC, VEC> sa;
-  Stage<BKC, VEC> sb;
-  if (kbeg < kend) {
-    sa.load(A, lda, m0, M, kbeg, kend);
-    sb.load(B, ldb, n0, N, kbeg, kend);
-  }
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    sa.template store<typename Lds<PREC>::T, LD>(sm.a);
-    sb.template store<typename Lds<PREC>::T, LD>(sm.b);
-    __syncthreads();
-    if (k0 + BK < kend) {  // prefetch the next k-tile into registers while computing this one
-      sa.load(A, lda, m0, M, k0 + BK, kend);
-      sb.load(B, ldb, n0, N, k0 + BK, kend);
+  SA sa[DEPTH];
+  SB sb[DEPTH];
+  if (kbeg < kend) {   // uniform: an empty trailing split writes zeros
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      sa[d].load(A, lda, m0, M, kbeg + d * BK, kend);
+      sb[d].load(B, ldb, n0, N, kbeg + d * BK, kend);
     }
-    if constexpr (PREC == PKC_PREC_FP32) {
-      const float4* pa = reinterpret_cast<const float4*>(&sm.a[(wm * 32 + r) * LD + 16 * h]);
-      const float4* pb = reinterpret_cast<const float4*>(&sm.b[(wn * 32 + r) * LD + 16 * h]);
-      float av[16], bv[16];
+    // whole rounds of DEPTH k-tiles; tiles past kend load clamped addresses and contribute zeros
+    for (int kt = kbeg; kt < kend; kt += DEPTH * BK) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 x = pa[q], y = pb[q];
-        av[4 * q] = x.x; av[4 * q + 1] = x.y; av[4 * q + 2] = x.z; av[4 * q + 3] = x.w;
-        bv[4 * q] = y.x; bv[4 * q + 1] = y.y; bv[4 * q + 2] = y.z; bv[4 * q + 3] = y.w;
-      }
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc, 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        bf16x8 av = *reinterpret_cast<const bf16x8*>(&sm.a[(wm * 32 + r) * LD + 16 * t + 8 * h]);
-        bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sm.b[(wn * 32 + r) * LD + 16 * t + 8 * h]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+      for (int d = 0; d < DEPTH; ++d) {
+        __syncthreads();
+        sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
+        sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+        __syncthreads();
+        const int kn = kt + (d + DEPTH) * BK;
+        sa[d].load(A, lda, m0, M, kn, kend);
+        sb[d].load(B, ldb, n0, N, kn, kend);
+        mfma_tile<PREC>(sm, wm, wn, r, h, acc);
       }
     }
   }
   // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-  float* Cz = C + (int64_t)blockIdx.z * slab_stride;
   const int col = n0 + wn * 32 + r;
+  float* Cz = C + (int64_t)bz * slab_stride;
   if (col < N) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -177,24 +264,87 @@ __global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const flo
   }
 }
 
-template <int PREC, bool AKC, bool BKC, bool VEC>
-static int launch(int M, int N, int K, const float* A, int64_t lda, const float* B, int64_t ldb,
+template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN>
+__global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const void* __restrict__ A,
+                                                  int64_t lda, const void* __restrict__ B,
+                                                  int64_t ldb, float* __restrict__ C, int64_t ldc,
+                                                  int kchunk, int64_t slab_stride) {
+  __shared__ Lds<PREC> sm;
+  gemm_body<PREC, AKC, BKC, VEC, DEPTH, BIN>(sm, blockIdx.x, blockIdx.y, blockIdx.z, M, N, K, A, lda,
+                                             B, ldb, C, ldc, kchunk, slab_stride);
+}
+
+// Several independent matmuls in ONE launch (e.g. a layer's dW and dX, both heads' logits):
+// workgroup ranges are assigned to problems in order; each workgroup dispatches on its problem's
+// operand orientation.  One launch boundary instead of one per matmul.
+constexpr int GMAX = 8;
+struct GroupProb {
+  int kind;              // PKC_OP_GEMM / PKC_OP_COLSUM / PKC_OP_LOSS
+  int code;              // a_kcontig*4 + b_kcontig*2 + vec
+  int M, N, K, kchunk, tn, tmn, wg0;
+  const void* A; int64_t lda; const void* B; int64_t ldb; float* C; int64_t ldc; int64_t slab;
+  const void* X1; void* X2; void* X3;
+};
+struct GroupArgs {
+  GroupProb p[GMAX];
+  int n;
+};
+
+template <int PREC, bool BIN>
+__global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
+  __shared__ Lds<PREC> sm;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < GMAX; ++j)
+    if (j < g.n && (int)blockIdx.x >= g.p[j].wg0) i = j;
+  const GroupProb& p = g.p[i];
+  const int local = blockIdx.x - p.wg0;
+  if (p.kind == PKC_OP_COLSUM) {
+    colsum_body(p.M, p.N, reinterpret_cast<const float*>(p.A), p.C, local * 64);
+    return;
+  }
+  if (p.kind == PKC_OP_LOSS) {
+    loss_finalize_body(p.M, reinterpret_cast<const float* const*>(p.A),
+                       reinterpret_cast<const float*>(p.B), p.N, reinterpret_cast<const float*>(p.X1),
+                       p.C, reinterpret_cast<float*>(p.X2), reinterpret_cast<int64_t*>(p.X3));
+    return;
+  }
+  const int bz = local / p.tmn, rem = local % p.tmn;
+  const int by = rem / p.tn, bx = rem % p.tn;
+#define PKC_GB(AK, BK_, V)                                                                      \
+  gemm_body<PREC, AK, BK_, V, 4, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
+                                      p.ldc, p.kchunk, p.slab)
+  switch (p.code) {
+    case 7: PKC_GB(true, true, true); break;
+    case 6: PKC_GB(true, true, false); break;
+    case 5: PKC_GB(true, false, true); break;
+    case 4: PKC_GB(true, false, false); break;
+    case 1: PKC_GB(false, false, true); break;
+    case 0: PKC_GB(false, false, false); break;
+    case 3: PKC_GB(false, true, true); break;
+    default: PKC_GB(false, true, false); break;
+  }
+#undef PKC_GB
+}
+
+template <int PREC, bool AKC, bool BKC, bool VEC, bool BIN>
+static int launch(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb,
                   float* C, int64_t ldc, int splits, int64_t slab, hipStream_t s) {
   int kchunk = (K + splits - 1) / splits;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((gemm_kernel<PREC, AKC, BKC, VEC>), grid, dim3(NT), 0, s, M, N, K, A, lda, B,
-                     ldb, C, ldc, kchunk, slab);
+  hipLaunchKernelGGL((gemm_kernel<PREC, AKC, BKC, VEC, 4, BIN>), grid, dim3(NT), 0, s, M, N, K, A,
+                     lda, B, ldb, C, ldc, kchunk, slab);
   PKC_LAUNCH_CHECK("pkc_gemm");
   return PKC_OK;
 }
 
-template <int PREC>
-static int dispatch(int akc, int bkc, bool vec, int M, int N, int K, const float* A, int64_t lda,
-                    const float* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
+template <int PREC, bool BIN>
+static int dispatch(int akc, int bkc, bool vec, int M, int N, int K, const void* A, int64_t lda,
+                    const void* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
                     hipStream_t s) {
 #define PKC_G(AK, BK_, V) \
-  return launch<PREC, AK, BK_, V>(M, N, K, A, lda, B, ldb, C, ldc, splits, slab, s)
+  return launch<PREC, AK, BK_, V, BIN>(M, N, K, A, lda, B, ldb, C, ldc, splits, slab, s)
   if (akc && bkc) { if (vec) PKC_G(true, true, true); PKC_G(true, true, false); }
   if (akc && !bkc) { if (vec) PKC_G(true, false, true); PKC_G(true, false, false); }
   if (!akc && !bkc) { if (vec) PKC_G(false, false, true); PKC_G(false, false, false); }
@@ -221,23 +371,105 @@ extern "C" int pkc_gemm_pick_splits(int M, int N, int K) {
 }
 
 extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
-                        const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                        const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                         int64_t ldc, int splits, int64_t slab_stride, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "pkc_gemm: negative shape");
-  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16, "pkc_gemm: bad precision %d", prec);
+  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN,
+                "pkc_gemm: bad precision %d", prec);
   if (M == 0 || N == 0) return PKC_OK;
   PKC_CHECK_ARG(A && B && C, "pkc_gemm: null operand");
   PKC_CHECK_ARG(ldc >= N, "pkc_gemm: ldc < N");
   if (splits <= 0) splits = pkc_gemm_pick_splits(M, N, K);
   PKC_CHECK_ARG(splits == 1 || slab_stride >= (int64_t)M * ldc, "pkc_gemm: slab_stride too small");
-  // float4 path: 16-byte aligned bases, leading dims and contiguous extents multiple of 4
-  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 &&
-                   ldb % 4 == 0 && (a_kcontig ? K % 4 == 0 : M % 4 == 0) &&
-                   (b_kcontig ? K % 4 == 0 : N % 4 == 0);
+  // 16-byte path: aligned bases, leading dims and contiguous extents multiple of 16 bytes
+  const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
+  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
+                   ldb % e == 0 && (a_kcontig ? K % e == 0 : M % e == 0) &&
+                   (b_kcontig ? K % e == 0 : N % e == 0);
   if (prec == PKC_PREC_FP32)
-    return dispatch<PKC_PREC_FP32>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C, ldc,
-                                   splits, slab_stride, S(stream));
-  return dispatch<PKC_PREC_BF16>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C, ldc,
-                                 splits, slab_stride, S(stream));
+    return dispatch<PKC_PREC_FP32, false>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C,
+                                          ldc, splits, slab_stride, S(stream));
+  if (prec == PKC_PREC_BF16IN)
+    return dispatch<PKC_PREC_BF16, true>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C,
+                                         ldc, splits, slab_stride, S(stream));
+  return dispatch<PKC_PREC_BF16, false>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C, ldc,
+                                        splits, slab_stride, S(stream));
+}
+
+extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(probs && n >= 1 && n <= GMAX, "pkc_gemm_grouped: 1..%d problems", GMAX);
+  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN,
+                "pkc_gemm_grouped: bad precision %d", prec);
+  GroupArgs g;
+  memset(&g, 0, sizeof(g));
+  int wg = 0, k = 0;
+  const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
+  for (int i = 0; i < n; ++i) {
+    const pkc_gemm_problem& q = probs[i];
+    if (q.kind == PKC_OP_COLSUM || q.kind == PKC_OP_LOSS) {
+      PKC_CHECK_ARG(q.M > 0 && q.N > 0 && q.A && q.C, "pkc_gemm_grouped: op %d arguments", i);
+      PKC_CHECK_ARG(q.kind != PKC_OP_LOSS || (q.M <= 8 && q.B && q.X1),
+                    "pkc_gemm_grouped: loss op %d arguments", i);
+      GroupProb& p = g.p[k++];
+      memset(&p, 0, sizeof(p));
+      p.kind = q.kind;
+      p.M = q.M; p.N = q.N; p.A = q.A; p.B = q.B; p.C = q.C; p.X1 = q.X1; p.X2 = q.X2; p.X3 = q.X3;
+      p.wg0 = wg;
+      wg += q.kind == PKC_OP_COLSUM ? (q.N + 63) / 64 : 1;
+      continue;
+    }
+    PKC_CHECK_ARG(q.kind == PKC_OP_GEMM, "pkc_gemm_grouped: problem %d kind %d", i, q.kind);
+    PKC_CHECK_ARG(q.M >= 0 && q.N >= 0 && q.K >= 0 && q.ldc >= q.N, "pkc_gemm_grouped: problem %d shape", i);
+    if (q.M == 0 || q.N == 0) continue;
+    PKC_CHECK_ARG(q.A && q.B && q.C, "pkc_gemm_grouped: problem %d null operand", i);
+    int splits = q.splits <= 0 ? pkc_gemm_pick_splits(q.M, q.N, q.K) : q.splits;
+    PKC_CHECK_ARG(splits == 1 || q.slab_stride >= (int64_t)q.M * q.ldc,
+                  "pkc_gemm_grouped: problem %d slab_stride too small", i);
+    int kchunk = (q.K + splits - 1) / splits;
+    kchunk = ((kchunk + BK - 1) / BK) * BK;
+    const bool vec = ((uintptr_t)q.A % 16 == 0) && ((uintptr_t)q.B % 16 == 0) && q.lda % e == 0 &&
+                     q.ldb % e == 0 && (q.a_kcontig ? q.K % e == 0 : q.M % e == 0) &&
+                     (q.b_kcontig ? q.K % e == 0 : q.N % e == 0);
+    GroupProb& p = g.p[k++];
+    p.kind = PKC_OP_GEMM;
+    p.code = (q.a_kcontig ? 4 : 0) + (q.b_kcontig ? 2 : 0) + (vec ? 1 : 0);
+    p.M = q.M; p.N = q.N; p.K = q.K; p.kchunk = kchunk;
+    p.tn = (q.N + BN - 1) / BN;
+    p.tmn = p.tn * ((q.M + BM - 1) / BM);
+    p.wg0 = wg;
+    p.A = q.A; p.lda = q.lda; p.B = q.B; p.ldb = q.ldb; p.C = q.C; p.ldc = q.ldc; p.slab = q.slab_stride;
+    wg += p.tmn * splits;
+  }
+  g.n = k;
+  if (k == 0) return PKC_OK;
+  if (prec == PKC_PREC_FP32)
+    hipLaunchKernelGGL((gemm_grouped_kernel<PKC_PREC_FP32, false>), dim3(wg), dim3(NT), 0, S(stream), g);
+  else if (prec == PKC_PREC_BF16IN)
+    hipLaunchKernelGGL((gemm_grouped_kernel<PKC_PREC_BF16, true>), dim3(wg), dim3(NT), 0, S(stream), g);
+  else
+    hipLaunchKernelGGL((gemm_grouped_kernel<PKC_PREC_BF16, false>), dim3(wg), dim3(NT), 0, S(stream), g);
+  PKC_LAUNCH_CHECK("pkc_gemm_grouped");
+  return PKC_OK;
+}
+
+namespace pkc {
+__global__ void cast_bf16_kernel(const float* src, __bf16* dst, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (__bf16)src[i];
+}
+}  // namespace pkc
+
+extern "C" int pkc_cast_bf16(const float* src, void* dst, int64_t n, void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(src && dst && n >= 0, "pkc_cast_bf16: bad arguments");
+  if (n == 0) return PKC_OK;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, S(stream), src,
+                     reinterpret_cast<__bf16*>(dst), n);
+  PKC_LAUNCH_CHECK("pkc_cast_bf16");
+  return PKC_OK;
 }

@@ -73,12 +73,17 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(const float* feats, i
                                                            const int32_t* labels, int nlab, int B,
                                                            int64_t n_batches, int64_t* ctr,
                                                            float* x_out, int32_t* lab_out,
-                                                           int advance, unsigned* done) {
+                                                           int advance, unsigned* done,
+                                                           __bf16* xb) {
   const int64_t i = *ctr % n_batches;
   const int64_t row0 = i * B;
   const int r = blockIdx.x;
   const float* src = feats + (row0 + r) * ld;
-  for (int c = threadIdx.x; c < F; c += 256) x_out[(int64_t)r * F + c] = src[c];
+  for (int c = threadIdx.x; c < F; c += 256) {
+    const float v = src[c];
+    x_out[(int64_t)r * F + c] = v;
+    if (xb) xb[(int64_t)r * F + c] = (__bf16)v;
+  }
   if (threadIdx.x < nlab) lab_out[r * nlab + threadIdx.x] = labels[(row0 + r) * nlab + threadIdx.x];
   if (advance) {
     __syncthreads();
@@ -137,7 +142,7 @@ extern "C" int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, co
 
 extern "C" int pkc_batch_gather(const float* feats, int64_t ld_feats, int F, const int32_t* labels,
                                 int nlab, int B, int64_t n_batches, int64_t* step_ctr, float* x_out,
-                                int32_t* lab_out, int advance, void* stream) {
+                                int32_t* lab_out, int advance, void* x_bf16, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(feats && labels && step_ctr && x_out && lab_out && B > 0 && n_batches > 0 &&
                     nlab >= 0 && nlab <= 256,
@@ -145,7 +150,8 @@ extern "C" int pkc_batch_gather(const float* feats, int64_t ld_feats, int F, con
   // the completion counter lives right after the step counter (caller allocates 2 int64)
   unsigned* done = reinterpret_cast<unsigned*>(step_ctr + 1);
   hipLaunchKernelGGL(batch_gather_kernel, dim3(B), dim3(256), 0, S(stream), feats, ld_feats, F, labels,
-                     nlab, B, n_batches, step_ctr, x_out, lab_out, advance, done);
+                     nlab, B, n_batches, step_ctr, x_out, lab_out, advance, done,
+                     reinterpret_cast<__bf16*>(x_bf16));
   PKC_LAUNCH_CHECK("pkc_batch_gather");
   return PKC_OK;
 }

@@ -4,7 +4,7 @@
 // (utils.py:1811-1812, 1935-1952), cost_err argmax (utils.py:1993-2011) and their autograd backward
 // (d logits = w/M * (softmax - onehot)) with one row-parallel pass: one wave per frame row, the
 // split-K slabs of the head matmul summed in fixed order.
-#include "pkc_common.h"
+#include "pkc_ops.h"
 
 namespace pkc {
 
@@ -82,7 +82,9 @@ __global__ __launch_bounds__(64 * LW) void nll_kernel(pkc_nll_args a) {
     if (j == y) lp_y = lp;
     if (a.dlogits) {
       const float p = expf(lp);
-      a.dlogits[(int64_t)r * N + j] = gscale * (j == y ? p - 1.f : p);
+      const float d = gscale * (j == y ? p - 1.f : p);
+      a.dlogits[(int64_t)r * N + j] = d;
+      if (a.dlogits_bf16) reinterpret_cast<__bf16*>(a.dlogits_bf16)[(int64_t)r * N + j] = (__bf16)d;
     }
     zrow[j] = a.log_prior ? lp - a.log_prior[j] : lp;
   }
@@ -93,38 +95,142 @@ __global__ __launch_bounds__(64 * LW) void nll_kernel(pkc_nll_args a) {
   }
 }
 
+// Register-resident form for heads up to 8 values per thread (N <= 2048 with 4 waves per row,
+// N <= 512 with one): the row's logits are summed from the slabs ONCE, kept in registers through
+// max / sum-exp / outputs, and every slab load is issued up front (clamped, not branched).
+struct NllShared {
+  float m[LW], s[LW];
+  int a[LW];
+};
+
+template <int WPR, int NS>
+__device__ __forceinline__ void nll_reg_body(const pkc_nll_args& a, int block, NllShared& sh) {
+  constexpr int RPB = LW / WPR;
+  constexpr int T = 64 * WPR;
+  constexpr int NPT = 8;
+  float* sh_m = sh.m;
+  float* sh_s = sh.s;
+  int* sh_a = sh.a;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rl = wave / WPR;
+  const int tr = threadIdx.x - rl * T;
+  const int r = block * RPB + rl;
+  const bool rok = r < a.M;
+  const int64_t N = a.N;
+  const int rr = rok ? r : a.M - 1;
+  const float* zb = a.zslab + (int64_t)rr * N;
+  float v[NPT][NS];
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    const int j = min(tr + T * q, a.N - 1);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int st = t < a.nslab ? t : a.nslab - 1;
+      v[q][t] = zb[(int64_t)st * a.slab_stride + j];
+    }
+  }
+  float z[NPT];
+  float mx = -INFINITY;
+  int arg = 0x7fffffff;
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    const int j = tr + T * q;
+    float acc = v[q][0];
+#pragma unroll
+    for (int t = 1; t < NS; ++t) acc += (t < a.nslab) ? v[q][t] : 0.f;
+    if (a.bias) acc += a.bias[min(j, a.N - 1)];
+    z[q] = acc;
+    if (j < a.N && acc > mx) { mx = acc; arg = j; }   // ascending j: first max per thread
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
+  if (WPR > 1) {
+    if (lane == 0) { sh_m[wave] = mx; sh_a[wave] = arg; }
+    __syncthreads();
+    for (int w = rl * WPR; w < rl * WPR + WPR; ++w) {
+      const float om = sh_m[w];
+      const int oa = sh_a[w];
+      if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int q = 0; q < NPT; ++q)
+    if (tr + T * q < a.N) se += expf(z[q] - mx);
+  se = warp_sum(se);
+  if (WPR > 1) {
+    if (lane == 0) sh_s[wave] = se;
+    __syncthreads();
+    se = 0.f;
+    for (int w = rl * WPR; w < rl * WPR + WPR; ++w) se += sh_s[w];
+  }
+  if (!rok) return;
+  const float lse = mx + logf(se);
+  const int y = a.labels ? a.labels[(int64_t)r * a.label_stride] : -1;
+  const float gscale = a.weight / (float)a.M;
+  float* lrow = a.logp + (int64_t)r * N;
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    const int j = tr + T * q;
+    if (j >= a.N) break;
+    const float lp = z[q] - lse;
+    if (a.dlogits) {
+      const float p = expf(lp);
+      const float d = gscale * (j == y ? p - 1.f : p);
+      a.dlogits[(int64_t)r * N + j] = d;
+      if (a.dlogits_bf16) reinterpret_cast<__bf16*>(a.dlogits_bf16)[(int64_t)r * N + j] = (__bf16)d;
+    }
+    lrow[j] = a.log_prior ? lp - a.log_prior[j] : lp;
+    if (j == y) {   // exactly one thread of the row owns the label column
+      if (a.row_loss) a.row_loss[r] = -lp;
+      if (a.row_err) a.row_err[r] = (arg != y) ? 1.f : 0.f;
+    }
+  }
+}
+
+template <int WPR, int NS>
+__global__ __launch_bounds__(64 * LW) void nll_reg_kernel(pkc_nll_args a) {
+  __shared__ NllShared sh;
+  nll_reg_body<WPR, NS>(a, blockIdx.x, sh);
+}
+
+// several heads' LogSoftmax/NLL in one launch (workgroup ranges per head)
+constexpr int NLL_MAX = 4;
+struct NllMulti {
+  pkc_nll_args a[NLL_MAX];
+  int wg0[NLL_MAX];
+  int code[NLL_MAX];   // 4 * (wide) + log2(NS)
+  int n;
+};
+
+__global__ __launch_bounds__(64 * LW) void nll_multi_kernel(NllMulti g) {
+  __shared__ NllShared sh;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < NLL_MAX; ++j)
+    if (j < g.n && (int)blockIdx.x >= g.wg0[j]) i = j;
+  const int b = blockIdx.x - g.wg0[i];
+  switch (g.code[i]) {
+    case 0: nll_reg_body<1, 1>(g.a[i], b, sh); break;
+    case 1: nll_reg_body<1, 2>(g.a[i], b, sh); break;
+    case 2: nll_reg_body<1, 4>(g.a[i], b, sh); break;
+    case 3: nll_reg_body<1, 8>(g.a[i], b, sh); break;
+    case 4: nll_reg_body<4, 1>(g.a[i], b, sh); break;
+    case 5: nll_reg_body<4, 2>(g.a[i], b, sh); break;
+    case 6: nll_reg_body<4, 4>(g.a[i], b, sh); break;
+    default: nll_reg_body<4, 8>(g.a[i], b, sh); break;
+  }
+}
+
 __global__ __launch_bounds__(256) void loss_finalize_kernel(int nheads, const float* const* rl,
                                                             const float* w, int M,
                                                             const float* rerr, float* out,
-                                                            float* acc) {
-  __shared__ float red[256];
-  float total = 0.f;
-  for (int h = 0; h <= nheads; ++h) {
-    const float* src = h < nheads ? rl[h] : rerr;
-    float s = 0.f;
-    for (int i = threadIdx.x; i < M; i += 256) s += src[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    const float mean = red[0] / (float)M;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      if (h < nheads) {
-        out[2 + h] = mean;
-        total += w[h] * mean;
-      } else {
-        out[0] = total;
-        out[1] = mean;
-        if (acc) {
-          acc[0] += total;
-          acc[1] += mean;
-        }
-      }
-    }
-  }
+                                                            float* acc, int64_t* advance) {
+  loss_finalize_body(nheads, rl, w, M, rerr, out, acc, advance);
 }
 
 }  // namespace pkc
@@ -134,21 +240,76 @@ extern "C" int pkc_nll_fused(const pkc_nll_args* a, void* stream) {
   PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab >= 1 && a->zslab && a->logp,
                 "pkc_nll_fused: bad arguments");
   PKC_CHECK_ARG(a->labels || !a->dlogits, "pkc_nll_fused: dlogits needs labels");
-  if (a->N >= 512)
+  const int ns = a->nslab <= 1 ? 1 : (a->nslab <= 2 ? 2 : (a->nslab <= 4 ? 4 : 8));
+  const bool wide = a->N >= 512;
+  if (a->nslab <= 8 && a->N <= (wide ? 2048 : 512)) {
+    const dim3 grid(wide ? a->M : (a->M + LW - 1) / LW), blk(64 * LW);
+#define PKC_NLL(W)                                                                    \
+    switch (ns) {                                                                     \
+      case 1: hipLaunchKernelGGL((nll_reg_kernel<W, 1>), grid, blk, 0, S(stream), *a); break; \
+      case 2: hipLaunchKernelGGL((nll_reg_kernel<W, 2>), grid, blk, 0, S(stream), *a); break; \
+      case 4: hipLaunchKernelGGL((nll_reg_kernel<W, 4>), grid, blk, 0, S(stream), *a); break; \
+      default: hipLaunchKernelGGL((nll_reg_kernel<W, 8>), grid, blk, 0, S(stream), *a); break; \
+    }
+    if (wide) { PKC_NLL(4) } else { PKC_NLL(1) }
+#undef PKC_NLL
+  } else if (wide) {
     hipLaunchKernelGGL(nll_kernel<4>, dim3(a->M), dim3(64 * LW), 0, S(stream), *a);
-  else
+  } else {
     hipLaunchKernelGGL(nll_kernel<1>, dim3((a->M + LW - 1) / LW), dim3(64 * LW), 0, S(stream), *a);
+  }
   PKC_LAUNCH_CHECK("pkc_nll_fused");
   return PKC_OK;
 }
 
+static bool nll_reg_code(const pkc_nll_args* a, int* code, int* nwg) {
+  using namespace pkc;
+  const int ns = a->nslab <= 1 ? 0 : (a->nslab <= 2 ? 1 : (a->nslab <= 4 ? 2 : 3));
+  const bool wide = a->N >= 512;
+  if (a->nslab > 8 || a->N > (wide ? 2048 : 512)) return false;
+  *code = (wide ? 4 : 0) + ns;
+  *nwg = wide ? a->M : (a->M + LW - 1) / LW;
+  return true;
+}
+
+extern "C" int pkc_nll_fused_multi(const pkc_nll_args* args, int n, void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(args && n >= 1 && n <= NLL_MAX, "pkc_nll_fused_multi: 1..%d heads", NLL_MAX);
+  NllMulti g;
+  memset(&g, 0, sizeof(g));
+  int wg = 0;
+  for (int i = 0; i < n; ++i) {
+    const pkc_nll_args* a = &args[i];
+    PKC_CHECK_ARG(a->M > 0 && a->N > 0 && a->nslab >= 1 && a->zslab && a->logp,
+                  "pkc_nll_fused_multi: head %d bad arguments", i);
+    PKC_CHECK_ARG(a->labels || !a->dlogits, "pkc_nll_fused_multi: dlogits needs labels");
+    int code, nwg;
+    if (!nll_reg_code(a, &code, &nwg)) {   // a head outside the register-resident form
+      for (int j = 0; j < n; ++j) {
+        const int rc = pkc_nll_fused(&args[j], stream);
+        if (rc != PKC_OK) return rc;
+      }
+      return PKC_OK;
+    }
+    g.a[i] = *a;
+    g.code[i] = code;
+    g.wg0[i] = wg;
+    wg += nwg;
+  }
+  g.n = n;
+  hipLaunchKernelGGL(nll_multi_kernel, dim3(wg), dim3(64 * LW), 0, S(stream), g);
+  PKC_LAUNCH_CHECK("pkc_nll_fused_multi");
+  return PKC_OK;
+}
+
 extern "C" int pkc_loss_finalize(int nheads, const float* const* row_loss, const float* weights,
-                                 int M, const float* row_err, float* out, float* acc, void* stream) {
+                                 int M, const float* row_err, float* out, float* acc,
+                                 int64_t* advance_ctr, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(nheads >= 1 && nheads <= 8 && row_loss && weights && row_err && out && M > 0,
                 "pkc_loss_finalize: bad arguments");
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, S(stream), nheads, row_loss,
-                     weights, M, row_err, out, acc);
+                     weights, M, row_err, out, acc, advance_ctr);
   PKC_LAUNCH_CHECK("pkc_loss_finalize");
   return PKC_OK;
 }

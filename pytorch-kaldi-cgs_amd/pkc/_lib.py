@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
-PREC_FP32, PREC_BF16 = 0, 1
+PREC_FP32, PREC_BF16, PREC_BF16IN = 0, 1, 2
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
 NORM_NONE, NORM_BN_TRAIN, NORM_BN_EVAL = 0, 1, 2
 OPT = {"sgd": 0, "rmsprop": 1, "adam": 2}
@@ -42,7 +42,7 @@ class NllArgs(C.Structure):
     _fields_ = [("M", C.c_int), ("N", C.c_int), ("nslab", C.c_int), ("zslab", vp),
                 ("slab_stride", i64), ("bias", vp), ("labels", vp), ("label_stride", i64),
                 ("weight", C.c_float), ("logp", vp), ("log_prior", vp), ("dlogits", vp),
-                ("row_loss", vp), ("row_err", vp)]
+                ("row_loss", vp), ("row_err", vp), ("dlogits_bf16", vp)]
 
 
 class OptTensor(C.Structure):
@@ -51,7 +51,7 @@ class OptTensor(C.Structure):
                 ("dampening", C.c_float), ("alpha", C.c_float), ("eps", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("clampv", C.c_float),
                 ("nesterov", C.c_int), ("centered", C.c_int), ("amsgrad", C.c_int), ("step", C.c_int),
-                ("qout", vp), ("qbits", C.c_int)]
+                ("qout", vp), ("qbits", C.c_int), ("bout", vp)]
 
 
 CELL_LIGRU, CELL_LSTM = 0, 1
@@ -66,7 +66,18 @@ class RnnArgs(C.Structure):
                 ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp)]
 
 
+class GemmProblem(C.Structure):
+    _fields_ = [("a_kcontig", C.c_int), ("b_kcontig", C.c_int), ("M", C.c_int), ("N", C.c_int),
+                ("K", C.c_int), ("splits", C.c_int), ("A", vp), ("lda", i64), ("B", vp),
+                ("ldb", i64), ("C", vp), ("ldc", i64), ("slab_stride", i64), ("kind", C.c_int),
+                ("X1", vp), ("X2", vp), ("X3", vp)]
+
+
+OP_GEMM, OP_COLSUM, OP_LOSS = 0, 1, 2
+
+
 _SIGS = {
+    "pkc_gemm_grouped": (C.c_int, [C.c_int, vp, C.c_int, vp]),
     "pkc_fakequant_weight": (C.c_int, [vp, vp, i64, C.c_int, vp]),
     "pkc_fakequant_input": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, vp, vp]),
     "pkc_pattern_mask": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp]),
@@ -83,13 +94,15 @@ _SIGS = {
     "pkc_dense_bwd": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp]),
     "pkc_dense_work_size": (i64, [C.c_int, C.c_int]),
     "pkc_nll_fused": (C.c_int, [C.POINTER(NllArgs), vp]),
-    "pkc_loss_finalize": (C.c_int, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp]),
+    "pkc_loss_finalize": (C.c_int, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp]),
+    "pkc_nll_fused_multi": (C.c_int, [vp, C.c_int, vp]),
     "pkc_colsum": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, C.c_int, vp]),
     "pkc_optim_step": (C.c_int, [vp, C.c_int, vp, C.c_int, vp]),
     "pkc_optim_chunks": (C.c_int, [C.POINTER(i64), C.c_int, C.POINTER(C.c_int32), C.c_int]),
     "pkc_apply_mask": (C.c_int, [vp, vp, i64, C.c_float, vp]),
     "pkc_batch_gather": (C.c_int, [vp, i64, C.c_int, vp, C.c_int, C.c_int, i64, vp, vp, vp, C.c_int,
-                                   vp]),
+                                   vp, vp]),
+    "pkc_cast_bf16": (C.c_int, [vp, vp, i64, vp]),
     "pkc_cw_stats": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]),
     "pkc_cw_stats_work_size": (i64, [i64, C.c_int, C.c_int, C.c_int]),
     "pkc_cw_apply": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, i64, vp]),

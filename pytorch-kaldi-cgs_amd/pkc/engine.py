@@ -474,12 +474,7 @@ class Engine:
             for e in self.opt_entries)
         n = len(self.opt_entries)
         if n:
-            sizes = (C.c_int64 * n)(*[e["p"].numel() for e in self.opt_entries])
-            nch = L.lib().pkc_optim_chunks(sizes, n, None, 0)
-            cmap = (C.c_int32 * (2 * nch))()
-            L.lib().pkc_optim_chunks(sizes, n, cmap, nch)
-            self.opt_nchunks = nch
-            self.opt_map = torch.from_numpy(np.frombuffer(cmap, dtype=np.int32).copy()).to(self.dev)
+            self.opt_nchunks, self.opt_map = self._chunk_map(range(n))
             self.opt_desc = torch.zeros(n * C.sizeof(L.OptTensor), dtype=torch.uint8, device=self.dev)
             self._upload_opt_desc(step_inc=1)
         # the reference multiplies the masks in (and QuantizeLinear clamps W to [-1, 1]) before
@@ -492,6 +487,20 @@ class Engine:
                     call("pkc_apply_mask", ptr(p), ptr(m), p.numel(), C.c_float(1.0 if qb else 0.0), s)
                 if qb:
                     call("pkc_fakequant_weight", ptr(p), ptr(q), p.numel(), qb, s)
+
+    def _chunk_map(self, idx):
+        """(n_chunks, device map) of pkc_optim_step work items over the entries idx (tensor ids
+        index the full descriptor array)."""
+        idx = list(idx)
+        if not idx:
+            return 0, None
+        sizes = (C.c_int64 * len(idx))(*[self.opt_entries[i]["p"].numel() for i in idx])
+        nch = L.lib().pkc_optim_chunks(sizes, len(idx), None, 0)
+        cmap = (C.c_int32 * (2 * nch))()
+        L.lib().pkc_optim_chunks(sizes, len(idx), cmap, nch)
+        m = np.frombuffer(cmap, dtype=np.int32).copy().reshape(-1, 2)
+        m[:, 0] = np.asarray(idx, dtype=np.int32)[m[:, 0]]
+        return nch, torch.from_numpy(m.reshape(-1)).to(self.dev)
 
     def _upload_opt_desc(self, step_inc):
         n = len(self.opt_entries)
@@ -621,7 +630,8 @@ class Engine:
             M = self.M
             self._k("batch_gather", 0, 8.0 * M * self.F, "pkc_batch_gather", ptr(self.chunk_feats),
                     self.chunk_feats.stride(0), self.F, ptr(self.chunk_labels), self.nlab, self.B,
-                    self.n_batches, ptr(self.ctr), ptr(self.x), ptr(self.labs), 1, s)
+                    self.n_batches, ptr(self.ctr), ptr(self.x), ptr(self.labs),
+                    0 if self.loss_heads else 1, ptr(getattr(self, "x_bf16", None)), s)
             return
         begs, lens, lefts, T = batch
         # [B x int64 begin rows][B x int32 lengths][B x int32 left pads]
@@ -637,17 +647,43 @@ class Engine:
                 C.c_void_p(mp), C.c_void_p(mp + 8 * self.B), C.c_void_p(mp + 8 * self.B + 4 * self.B),
                 self.B, T, ptr(self.x), ptr(self.labs), s)
 
-    def _dense_fwd(self, n, s, train):
+    def _fwd_problem(self, n):
+        """(label, flops, bytes, GemmProblem) of a dense layer's forward matmul Z = X W^T."""
         M = self.M
-        self._quant_chain(n, s)
         a_ptr, lda = self._version(n, n.qv0 + n.reads)
         sf = _splits(M, n.N, n.K, n.scap)
         n.sf = sf
         W = n.Wq if n.qbits else n.W
-        self._k("gemm_fwd %dx%dx%d" % (M, n.N, n.K), 2.0 * M * n.N * n.K,
-                4.0 * (M * n.K + n.N * n.K + sf * M * n.N), "pkc_gemm", self.prec,
-                1, 1, M, n.N, n.K, C.c_void_p(a_ptr), lda, ptr(W), n.K, ptr(n.zslab),
-                n.N, sf, M * n.N, s)
+        pr = L.GemmProblem(a_kcontig=1, b_kcontig=1, M=M, N=n.N, K=n.K, splits=sf, A=a_ptr, lda=lda,
+                           B=W.data_ptr(), ldb=n.K, C=n.zslab.data_ptr(), ldc=n.N,
+                           slab_stride=M * n.N)
+        return ("fwd %dx%dx%d" % (M, n.N, n.K), 2.0 * M * n.N * n.K,
+                4.0 * (M * n.K + n.N * n.K + sf * M * n.N), pr)
+
+    def _gemms(self, probs, s):
+        """Launch matmul problems: one pkc_gemm, or pkc_gemm_grouped for several (<= 8 each)."""
+        for i in range(0, len(probs), 8):
+            part = probs[i:i + 8]
+            if len(part) == 1 and part[0][3].kind == L.OP_GEMM:
+                lab, fl, nb, p = part[0]
+                self._k("gemm_" + lab, fl, nb, "pkc_gemm", self.prec, p.a_kcontig, p.b_kcontig,
+                        p.M, p.N, p.K, C.c_void_p(p.A), p.lda, C.c_void_p(p.B), p.ldb,
+                        C.c_void_p(p.C), p.ldc, p.splits, p.slab_stride, s)
+            else:
+                arr = (L.GemmProblem * len(part))(*[q[3] for q in part])
+                self._k("gemm_group[" + ", ".join(q[0] for q in part) + "]",
+                        sum(q[1] for q in part), sum(q[2] for q in part), "pkc_gemm_grouped",
+                        self.prec, arr, len(part), s)
+
+    def _dense_fwd(self, n, s, train):
+        self._quant_chain(n, s)
+        self._gemms([self._fwd_problem(n)], s)
+        self._fwd_epilogue(n, s, train)
+
+    def _fwd_epilogue(self, n, s, train, out=None):
+        """The layer's epilogue launch (BN/act/dropout, or a head's LogSoftmax/NLL); with `out`
+        the head's NllArgs are only filled in (for a grouped launch)."""
+        M, sf = self.M, n.sf
         if n.head:
             has_lab = n.label_col >= 0
             a = L.NllArgs(M=M, N=n.N, nslab=sf, zslab=n.zslab.data_ptr(), slab_stride=M * n.N,
@@ -657,6 +693,9 @@ class Engine:
                           logp=n.out.data_ptr(), log_prior=None,
                           dlogits=n.dz.data_ptr() if (train and has_lab) else None,
                           row_loss=n.row_loss.data_ptr(), row_err=n.row_err.data_ptr())
+            if out is not None:
+                C.memmove(C.byref(out), C.byref(a), C.sizeof(a))
+                return
             self._k("nll_fused N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_nll_fused",
                     C.byref(a), s)
             return
@@ -756,60 +795,120 @@ class Engine:
             self._k("rnn_fwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_fwd", C.byref(ra), s)
 
-    def _forward_kernels(self, s, train, batch=None):
+    def _forward_kernels(self, s, train, batch=None, defer_loss=False):
         self._gather(s, batch)
-        for n in self.nodes:
+        nodes, i = self.nodes, 0
+        while i < len(nodes):
+            n = nodes[i]
             if n.rec:
                 self._rec_fwd(n, s, train)
+                i += 1
+                continue
+            # output heads reading the same tensor (cd + mono senones) share one matmul launch
+            grp = [n]
+            while (n.head and i + len(grp) < len(nodes) and not nodes[i + len(grp)].rec
+                   and nodes[i + len(grp)].head and nodes[i + len(grp)].src == n.src):
+                grp.append(nodes[i + len(grp)])
+            for g in grp:
+                self._quant_chain(g, s)
+            self._gemms([self._fwd_problem(g) for g in grp], s)
+            if len(grp) > 1:
+                self._nll_multi(grp, s, train)
             else:
-                self._dense_fwd(n, s, train)
-        if self.loss_heads:
+                self._fwd_epilogue(n, s, train)
+            i += len(grp)
+        if self.loss_heads and not defer_loss:
             self._k("loss_finalize", 0, 4.0 * self.M * (len(self.loss_heads) + 1),
                     "pkc_loss_finalize", len(self.loss_heads), ptr(self.loss_ptrs), ptr(self.loss_w),
-                    self.M, ptr(self.err_layer.row_err), ptr(self.loss_out), ptr(self.loss_acc), s)
+                    self.M, ptr(self.err_layer.row_err), ptr(self.loss_out), ptr(self.loss_acc),
+                    None if self.seq else ptr(self.ctr), s)
+
+    def _loss_op(self):
+        """The loss reduction (and batch-counter advance) as an operation of the first backward
+        launch: it only needs the forward's per-row losses."""
+        p = L.GemmProblem(kind=L.OP_LOSS, M=len(self.loss_heads), N=self.M,
+                          A=self.loss_ptrs.data_ptr(), B=self.loss_w.data_ptr(),
+                          C=self.loss_out.data_ptr(), X1=self.err_layer.row_err.data_ptr(),
+                          X2=self.loss_acc.data_ptr(), X3=None if self.seq else self.ctr.data_ptr())
+        return ("loss", 0.0, 4.0 * self.M * (len(self.loss_heads) + 1), p)
+
+    def _nll_multi(self, heads, s, train):
+        """LogSoftmax/NLL of several heads in one launch."""
+        args = (L.NllArgs * len(heads))()
+        for i, n in enumerate(heads):
+            self._fwd_epilogue(n, s, train, out=args[i])
+        self._k("nll_multi[%s]" % ",".join(str(n.N) for n in heads), 0,
+                sum(4.0 * self.M * n.N * (n.sf + 2) for n in heads), "pkc_nll_fused_multi", args,
+                len(heads), s)
 
     # ------------------------------------------------------------------ backward
     def _grad_slabs(self, n):
-        """(pointer, nslab) of dL/d(out of n) as the consumers' dX slabs, with their offsets."""
+        """(pointer, nslab) of dL/d(out of n) as the consumers' dX slabs, with their offsets.  The
+        consumers share a budget of MAX_SPLITS slabs (the fused small-batch BN backward sums at
+        most that many in registers); the widest consumer gives up splits first."""
         M = self.M
+        want = [_splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
+        while sum(want) > MAX_SPLITS and max(want) > 1:
+            want[want.index(max(want))] -= 1
         off = 0
         n.cons_off = []
-        for c in n.consumers:
-            c.sx = _splits(M, c.K, c.N, c.sxcap)
+        for c, w in zip(n.consumers, want):
+            c.sx = w
             n.cons_off.append(off)
             off += c.sx
         return off
 
-    def _dense_bwd(self, n, s):
+    def _dense_bwd_pre(self, n, s):
+        """dL/dz of a dense layer: the fused dropout / activation / BatchNorm backward over the
+        consumers' dX slabs (a head's dlogits came from the forward; its bias gradient is an
+        operation of the grouped backward launch, _bwd_problems)."""
         M = self.M
         if n.head:
-            self._k("colsum N=%d" % n.N, 0, 4.0 * M * n.N, "pkc_colsum", M, n.N, 1, ptr(n.dz), 0,
-                    ptr(n.db), 0, s)
-        else:
-            a = L.DenseBwdArgs(M=M, N=n.N, nslab=n.sb, gslab=n.gslab.data_ptr(),
-                               slab_stride=M * n.N,
-                               norm=L.NORM_BN_TRAIN if n.bn else L.NORM_NONE,
-                               act=L.ACT[n.act], gamma=n.gamma.data_ptr(),
-                               beta=n.beta.data_ptr(), save_invstd=n.save_invstd.data_ptr(),
-                               xhat=n.xhat.data_ptr(),
-                               keep=n.keep.data_ptr() if n.keep is not None else None,
-                               drop_p=n.drop, dz=n.dz.data_ptr(),
-                               dgamma=n.dgamma.data_ptr() if n.bn else None,
-                               dbeta=n.dbeta.data_ptr() if n.bn else None,
-                               dbias=n.db.data_ptr())
-            self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (n.sb + 3), "pkc_dense_bwd",
-                    C.byref(a), ptr(n.work), s)
+            return
+        a = L.DenseBwdArgs(M=M, N=n.N, nslab=n.sb, gslab=n.gslab.data_ptr(),
+                           slab_stride=M * n.N,
+                           norm=L.NORM_BN_TRAIN if n.bn else L.NORM_NONE,
+                           act=L.ACT[n.act], gamma=n.gamma.data_ptr(),
+                           beta=n.beta.data_ptr(), save_invstd=n.save_invstd.data_ptr(),
+                           xhat=n.xhat.data_ptr(),
+                           keep=n.keep.data_ptr() if n.keep is not None else None,
+                           drop_p=n.drop, dz=n.dz.data_ptr(),
+                           dgamma=n.dgamma.data_ptr() if n.bn else None,
+                           dbeta=n.dbeta.data_ptr() if n.bn else None,
+                           dbias=n.db.data_ptr())
+        self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (n.sb + 3), "pkc_dense_bwd",
+                C.byref(a), ptr(n.work), s)
+
+    def _bwd_problems(self, n):
+        """dW = dz^T X (into the flat gradient buffer) and, when the producer needs it,
+        dX = dz W (into the producer's gradient slabs)."""
+        M = self.M
         a_ptr, lda = self._final_version(n) if self.qsrc[n.qkey]["Q"] else self._src(n)
-        self._k("gemm_dW %dx%dx%d" % (n.N, n.K, M), 2.0 * M * n.N * n.K,
-                4.0 * (M * n.N + M * n.K + n.N * n.K), "pkc_gemm", self.prec, 0, 0,
-                n.N, n.K, M, ptr(n.dz), n.N, C.c_void_p(a_ptr), lda, ptr(n.dW), n.K, 1, 0, s)
+        out = []
+        if n.head:
+            out.append(("db %d" % n.N, 0.0, 4.0 * M * n.N,
+                        L.GemmProblem(kind=L.OP_COLSUM, M=M, N=n.N, A=n.dz.data_ptr(),
+                                      C=n.db.data_ptr())))
+        out += [("dW %dx%dx%d" % (n.N, n.K, M), 2.0 * M * n.N * n.K,
+                4.0 * (M * n.N + M * n.K + n.N * n.K),
+                L.GemmProblem(a_kcontig=0, b_kcontig=0, M=n.N, N=n.K, K=M, splits=1,
+                              A=n.dz.data_ptr(), lda=n.N, B=a_ptr, ldb=lda, C=n.dW.data_ptr(),
+                              ldc=n.K, slab_stride=0))]
         if n.src[0] == "node" and self.needs_grad[n.src[1]]:
             P = n.src[1]
             off = P.cons_off[P.consumers.index(n)]
-            self._k("gemm_dX %dx%dx%d" % (M, n.K, n.N), 2.0 * M * n.N * n.K,
-                    4.0 * (M * n.N + n.N * n.K + n.sx * M * n.K), "pkc_gemm",
-                    self.prec, 1, 0, M, n.K, n.N, ptr(n.dz), n.N, ptr(n.Wq if n.qbits else n.W), n.K,
-                    C.c_void_p(P.gslab.data_ptr() + 4 * off * M * P.N), n.K, n.sx, M * n.K, s)
+            W = n.Wq if n.qbits else n.W
+            out.append(("dX %dx%dx%d" % (M, n.K, n.N), 2.0 * M * n.N * n.K,
+                        4.0 * (M * n.N + n.N * n.K + n.sx * M * n.K),
+                        L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=n.K, K=n.N, splits=n.sx,
+                                      A=n.dz.data_ptr(), lda=n.N, B=W.data_ptr(), ldb=n.K,
+                                      C=P.gslab.data_ptr() + 4 * off * M * P.N, ldc=n.K,
+                                      slab_stride=M * n.K)))
+        return out
+
+    def _dense_bwd(self, n, s):
+        self._dense_bwd_pre(n, s)
+        self._gemms(self._bwd_problems(n), s)
 
     def _rec_bwd(self, n, s, want_dx0=False):
         M, T = self.M, self.T
@@ -858,28 +957,41 @@ class Engine:
                     nx += sx
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
 
-    def _backward_kernels(self, s):
+    def _backward_kernels(self, s, loss_op=None):
+        """Reverse pass.  The matmuls of a layer (dW, dX) are queued and launched together with
+        those of the layers after it that are still pending, right before the first kernel that
+        needs one of their results (the producer's BatchNorm backward reads the dX slabs)."""
         for n in self.nodes:
             if n.gslab is not None:
                 n.sb = self._grad_slabs(n)
+        pend = [loss_op] if loss_op is not None else []
         for n in reversed(self.nodes):
             if not self.needs_grad[n]:
                 continue
             if n.rec:
+                self._gemms(pend, s)
+                pend = []
                 self._rec_bwd(n, s)
-            else:
-                self._dense_bwd(n, s)
+                continue
+            if not n.head:
+                self._gemms(pend, s)
+                pend = []
+            self._dense_bwd_pre(n, s)
+            pend += self._bwd_problems(n)
+        self._gemms(pend, s)
 
     def _optim_kernels(self, s):
-        if self.opt_entries:
-            nparam = sum(e["p"].numel() for e in self.opt_entries)
-            self._k("optim_step", 0, 4.0 * nparam * 5, "pkc_optim_step", ptr(self.opt_desc),
-                    len(self.opt_entries), ptr(self.opt_map), self.opt_nchunks, s)
+        if not self.opt_entries:
+            return
+        nparam = sum(e["p"].numel() for e in self.opt_entries)
+        self._k("optim_step", 0, 4.0 * nparam * 5, "pkc_optim_step", ptr(self.opt_desc),
+                len(self.opt_entries), ptr(self.opt_map), self.opt_nchunks, s)
 
     def _train_step_kernels(self, allreduce=None, batch=None):
         s = self._stream()
-        self._forward_kernels(s, True, batch)
-        self._backward_kernels(s)
+        defer = bool(self.loss_heads)
+        self._forward_kernels(s, True, batch, defer_loss=defer)
+        self._backward_kernels(s, self._loss_op() if defer else None)
         if allreduce is not None:
             allreduce(self.gflat)
         self._optim_kernels(s)
@@ -949,8 +1061,9 @@ class Engine:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
             st = self._stream()
-            self._forward_kernels(st, True)
-            self._backward_kernels(st)
+            defer = bool(self.loss_heads)
+            self._forward_kernels(st, True, defer_loss=defer)
+            self._backward_kernels(st, self._loss_op() if defer else None)
             if not split_optimizer:
                 self._optim_kernels(st)
         self.graph_opt = None

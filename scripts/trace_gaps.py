@@ -1,0 +1,40 @@
+"""Per-step kernel timeline from a rocprofv3 kernel trace: duration of each kernel and the gap
+before it, averaged over the steps of the timed (graph-replayed) region."""
+import csv
+import re
+import sys
+from collections import defaultdict
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+first = sys.argv[2] if len(sys.argv) > 2 else "batch_gather"
+starts = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
+steps = [rows[a:b] for a, b in zip(starts[-21:-1], starts[-20:])]  # last 20 complete steps
+agg = defaultdict(lambda: [0.0, 0.0, 0])
+order = []
+tot = []
+for st in steps:
+    t0 = int(st[0]["Start_Timestamp"])
+    t1 = int(st[-1]["End_Timestamp"])
+    tot.append((t1 - t0) / 1e3)
+    prev_end = None
+    for i, r in enumerate(st):
+        name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")[:60]
+        key = "%02d %s g%sx%sx%s" % (i, name, r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev_end) / 1e3 if prev_end else 0.0
+        prev_end = e
+        a = agg[key]
+        a[0] += (e - s) / 1e3
+        a[1] += gap
+        a[2] += 1
+        if key not in order:
+            order.append(key)
+n = len(steps)
+sd = sg = 0
+for k in order:
+    d, g, c = agg[k]
+    sd += d / c
+    sg += g / c
+    print("%-90s dur %7.2f  gap %6.2f" % (k, d / c, g / c))
+print("steps %d  mean step %.1f us  sum dur %.1f  sum gap %.1f" % (n, sum(tot) / n, sd, sg))

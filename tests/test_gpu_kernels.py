@@ -27,7 +27,7 @@ GEMM_SHAPES = [(128, 1024, 1024), (128, 1928, 1024), (128, 48, 1024), (128, 1024
                (37, 70, 45), (16, 96, 32), (64, 64, 32), (1, 5, 3), (200, 130, 260)]
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("orient", ["nt", "nn", "tn"])
 def test_gemm(L, prec, M, N, K, orient):
@@ -38,18 +38,52 @@ def test_gemm(L, prec, M, N, K, orient):
     akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
     Ast = A if akc else A.t().contiguous()      # stored (M,K) or (K,M)
     Bst = B if bkc else B.t().contiguous()
-    if prec == 1:
+    if prec >= 1:
         A = A.bfloat16().float()
         B = B.bfloat16().float()
     ref = (A.double() @ B.double().t()).float()
     splits = L.lib().pkc_gemm_pick_splits(M, N, K)
     Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+    if prec == 2:                                  # operands stored as bf16 in HBM
+        Ad, Bd = Ad.bfloat16().contiguous(), Bd.bfloat16().contiguous()
     Cd = torch.full((splits, M, N), float("nan"), device=DEV)
     L.call("pkc_gemm", prec, akc, bkc, M, N, K, L.ptr(Ad), Ast.shape[1], L.ptr(Bd), Bst.shape[1],
            L.ptr(Cd), N, splits, M * N, _s())
     out = Cd.sum(0).cpu()
     tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=tol)
+
+
+@pytest.mark.parametrize("prec", [0, 2])
+def test_gemm_grouped(L, prec):
+    """Several matmuls of different orientation / shape / split count in one launch."""
+    g = torch.Generator().manual_seed(11)
+    specs = [("nt", 128, 1928, 1024, 5), ("nt", 128, 48, 1024, 8), ("tn", 1024, 440, 128, 1),
+             ("nn", 128, 1024, 1024, 8), ("nn", 37, 70, 45, 1), ("tn", 16, 96, 32, 1)]
+    probs, keep, refs = [], [], []
+    for orient, M, N, K, sp in specs:
+        A = torch.randn(M, K, generator=g)
+        B = torch.randn(N, K, generator=g)
+        akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
+        Ast = A if akc else A.t().contiguous()
+        Bst = B if bkc else B.t().contiguous()
+        if prec:
+            A, B = A.bfloat16().float(), B.bfloat16().float()
+        refs.append((A.double() @ B.double().t()).float())
+        Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+        if prec == 2:
+            Ad, Bd = Ad.bfloat16().contiguous(), Bd.bfloat16().contiguous()
+        Cd = torch.full((sp, M, N), float("nan"), device=DEV)
+        keep += [Ad, Bd, Cd]
+        probs.append(L.GemmProblem(a_kcontig=akc, b_kcontig=bkc, M=M, N=N, K=K, splits=sp,
+                                   A=Ad.data_ptr(), lda=Ast.shape[1], B=Bd.data_ptr(),
+                                   ldb=Bst.shape[1], C=Cd.data_ptr(), ldc=N, slab_stride=M * N))
+    arr = (L.GemmProblem * len(probs))(*probs)
+    L.call("pkc_gemm_grouped", prec, arr, len(probs), _s())
+    torch.cuda.synchronize()
+    for (orient, M, N, K, sp), ref, Cd in zip(specs, refs, keep[2::3]):
+        tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
+        torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=tol)
 
 
 def test_gemm_unaligned_lda(L):
@@ -77,7 +111,7 @@ def _bn_ref(z, gamma, beta, act, keep, p):
 
 @pytest.mark.parametrize("act", ["relu", "tanh", "sigmoid", "linear"])
 @pytest.mark.parametrize("p", [0.0, 0.15])
-@pytest.mark.parametrize("M,N,S", [(128, 1024, 4), (16, 48, 1), (50, 70, 3)])
+@pytest.mark.parametrize("M,N,S", [(128, 1024, 4), (16, 48, 1), (50, 70, 3), (100, 1028, 7), (300, 64, 2)])
 def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
     g = torch.Generator().manual_seed(M + N + S)
     slabs = torch.randn(S, M, N, generator=g)
@@ -151,6 +185,37 @@ def test_dense_dropout_rate_and_determinism(L):
     assert (outs[0][~k] == 0).all()
 
 
+def test_nll_fused_multi_equals_single(L):
+    """Both heads' LogSoftmax/NLL in one launch == one launch per head."""
+    M = 128
+    outs = []
+    heads = [(1928, 5), (48, 8)]
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.randn(S, M, N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV),
+             torch.randint(0, N, (M,), generator=g, dtype=torch.int32).to(DEV)) for N, S in heads]
+    for multi in (False, True):
+        args = (L.NllArgs * 2)()
+        bufs = []
+        for i, ((N, S), (z, b, lab)) in enumerate(zip(heads, data)):
+            lp, dl, rl, re_ = (torch.zeros(M, N, device=DEV), torch.zeros(M, N, device=DEV),
+                               torch.zeros(M, device=DEV), torch.zeros(M, device=DEV))
+            bufs.append((lp, dl, rl, re_))
+            args[i] = L.NllArgs(M=M, N=N, nslab=S, zslab=z.data_ptr(), slab_stride=M * N,
+                                bias=b.data_ptr(), labels=lab.data_ptr(), label_stride=1, weight=0.5,
+                                logp=lp.data_ptr(), dlogits=dl.data_ptr(), row_loss=rl.data_ptr(),
+                                row_err=re_.data_ptr())
+        if multi:
+            L.call("pkc_nll_fused_multi", args, 2, _s())
+        else:
+            for i in range(2):
+                L.call("pkc_nll_fused", C.byref(args[i]), _s())
+        torch.cuda.synchronize()
+        outs.append([[t.cpu() for t in bb] for bb in bufs])
+    for a, b in zip(outs[0], outs[1]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("M,N,S", [(128, 1928, 4), (128, 48, 2), (7, 100, 1)])
 def test_nll_fused(L, M, N, S):
     g = torch.Generator().manual_seed(N)
@@ -176,8 +241,22 @@ def test_nll_fused(L, M, N, S):
     out, acc = torch.zeros(3, device=DEV), torch.zeros(2, device=DEV)
     ptrs = torch.tensor([rl.data_ptr()], dtype=torch.int64, device=DEV)
     w = torch.tensor([0.7], device=DEV)
-    L.call("pkc_loss_finalize", 1, L.ptr(ptrs), L.ptr(w), M, L.ptr(re_), L.ptr(out), L.ptr(acc), _s())
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    L.call("pkc_loss_finalize", 1, L.ptr(ptrs), L.ptr(w), M, L.ptr(re_), L.ptr(out), L.ptr(acc),
+           L.ptr(ctr), _s())
     torch.testing.assert_close(out[0].cpu(), 0.7 * loss.detach(), rtol=1e-5, atol=1e-6)
+    assert int(ctr.item()) == 1
+    # the same reduction as an operation of a grouped launch, beside a column sum
+    out2, acc2 = torch.zeros_like(out), torch.zeros_like(acc)
+    cs = torch.zeros(N, device=DEV)
+    ops = (L.GemmProblem * 2)(
+        L.GemmProblem(kind=L.OP_LOSS, M=1, N=M, A=ptrs.data_ptr(), B=w.data_ptr(),
+                      C=out2.data_ptr(), X1=re_.data_ptr(), X2=acc2.data_ptr(), X3=ctr.data_ptr()),
+        L.GemmProblem(kind=L.OP_COLSUM, M=M, N=N, A=dl.data_ptr(), C=cs.data_ptr()))
+    L.call("pkc_gemm_grouped", 0, ops, 2, _s())
+    torch.testing.assert_close(out2.cpu(), out.cpu())
+    torch.testing.assert_close(cs.cpu(), dl.sum(0).cpu(), rtol=1e-5, atol=1e-6)
+    assert int(ctr.item()) == 2
 
 
 @pytest.mark.parametrize("kind", ["sgd", "rmsprop", "adam", "sgd_mom"])
