@@ -56,8 +56,10 @@ int pkc_gemm_pick_splits(int M, int N, int K);
  *                  splits, slab_stride)
  *   PKC_OP_COLSUM: C[n] = sum_m A[m*N + n]  (M rows, N columns, fp32)
  *   PKC_OP_LOSS  : pkc_loss_finalize(nheads = M, row_loss = A, weights = B, rows = N,
- *                  row_err = X1, out = C, acc = X2, advance_ctr = X3) */
-enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2 };
+ *                  row_err = X1, out = C, acc = X2, advance_ctr = X3)
+ *   PKC_OP_OPTIM : pkc_optim_step(tensors_dev = A, chunk_map_dev = B, nchunks = M) — the update of
+ *                  a layer whose gradients are complete rides in a later launch of the backward */
+enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2, PKC_OP_OPTIM = 3 };
 typedef struct {
   int a_kcontig, b_kcontig, M, N, K, splits;
   const void* A; int64_t lda; const void* B; int64_t ldb;

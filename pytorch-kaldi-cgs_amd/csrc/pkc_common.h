@@ -58,6 +58,22 @@ __device__ __forceinline__ uint32_t hash3(uint64_t seed, uint64_t stream, uint64
   return (uint32_t)(z >> 32);
 }
 
+// Dropout mask bits: a 32-bit murmur3 finaliser of the element's flat index, keyed by a
+// per-(seed, layer, step) 32-bit key (hash_seed: one 64-bit mix per thread, not per element).
+// The reference draws torch.bernoulli; any independent uniform stream is equivalent.
+__device__ __forceinline__ uint32_t hash_seed(uint64_t seed, uint64_t stream, uint64_t step) {
+  return (uint32_t)(hash3(seed, stream, step * 0x2545F4914F6CDD1Dull + 0x5bd1e995ull) >> 0);
+}
+__device__ __forceinline__ uint32_t hash_drop(uint32_t key, uint32_t idx) {
+  uint32_t h = idx * 0x9E3779B1u ^ key;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
 // Activations (reference neural_networks.py:54-78).  'linear' is LeakyReLU(1) == identity.
 __device__ __forceinline__ float act_fwd(int act, float y) {
   switch (act) {

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
     if (drop) {
       uint8_t k;
       if (a.keep_in) k = a.keep_in[idx];
-      else k = hash3(a.seed, (uint64_t)a.stream_id, (uint64_t)step * (uint64_t)(a.M * N) + idx) < thr;
+      else k = hash_drop(hash_seed(a.seed, (uint64_t)a.stream_id, (uint64_t)step), (uint32_t)idx) < thr;
       if (a.keep_out) a.keep_out[idx] = k;
       o = k ? o * scale : 0.f;
     }
@@ -271,6 +271,7 @@ __global__ __launch_bounds__(ET) void colsum_kernel(int M, int N, int nslab, con
 // on the slab count, loads clamped to the last slab instead of branched, so none is serialised).
 constexpr int FG = 4, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
 
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
@@ -333,10 +334,20 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
   const bool cok = c < a.N;
   const int64_t N = a.N;
   const int M = a.M;
+  // every per-column parameter is requested up front, from a valid address even when absent
+  // (selected away afterwards): no load waits behind the reductions or behind a branch
+  const int cc = min(c, a.N - 4);
+  const float* dummy = a.zslab;
+  const bool hb = a.bias != nullptr, bnp = a.norm != PKC_NORM_NONE;
+  const float4 b0 = ld4(hb ? a.bias + cc : dummy);
+  const float4 g0 = ld4(bnp ? a.gamma + cc : dummy);
+  const float4 be0 = ld4(bnp ? a.beta + cc : dummy);
+  const float4 rm0 = ld4(bnp ? a.running_mean + cc : dummy);
+  const float4 rv0 = ld4(bnp ? a.running_var + cc : dummy);
+  const int64_t step0 = *(a.step_ctr ? a.step_ctr : reinterpret_cast<const int64_t*>(dummy));
   float4 z[RI];
   load_slabs<NS, RI>(a.zslab, a.slab_stride, a.nslab, rg, M, N, c, cok, z);
-  const float4 b = (cok && a.bias) ? *reinterpret_cast<const float4*>(a.bias + c)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 b = hb ? b0 : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int i = 0; i < RI; ++i) z[i] = f4sel(cok && rg + RG * i < M, f4add(z[i], b));
   float4 mean = make_float4(0.f, 0.f, 0.f, 0.f), invstd = make_float4(1.f, 1.f, 1.f, 1.f);
@@ -362,14 +373,14 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
     invstd = make_float4(1.f / sqrtf(var.x + a.eps), 1.f / sqrtf(var.y + a.eps),
                          1.f / sqrtf(var.z + a.eps), 1.f / sqrtf(var.w + a.eps));
     if (cok) {
-      gam = *reinterpret_cast<const float4*>(a.gamma + c);
-      bet = *reinterpret_cast<const float4*>(a.beta + c);
+      gam = g0;
+      bet = be0;
       if (rg == 0) {
         *reinterpret_cast<float4*>(a.save_mean + c) = mean;
         *reinterpret_cast<float4*>(a.save_invstd + c) = invstd;
         const float cn = (float)(a.count_n > 0 ? a.count_n : M);
-        float4 rm = *reinterpret_cast<const float4*>(a.running_mean + c);
-        float4 rv = *reinterpret_cast<const float4*>(a.running_var + c);
+        float4 rm = rm0;
+        float4 rv = rv0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float vj = f4get(var, j);
@@ -382,18 +393,19 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
       }
     }
   } else if (a.norm == PKC_NORM_BN_EVAL && cok) {
-    mean = *reinterpret_cast<const float4*>(a.running_mean + c);
-    const float4 rv = *reinterpret_cast<const float4*>(a.running_var + c);
+    mean = rm0;
+    const float4 rv = rv0;
     invstd = make_float4(1.f / sqrtf(rv.x + a.eps), 1.f / sqrtf(rv.y + a.eps),
                          1.f / sqrtf(rv.z + a.eps), 1.f / sqrtf(rv.w + a.eps));
-    gam = *reinterpret_cast<const float4*>(a.gamma + c);
-    bet = *reinterpret_cast<const float4*>(a.beta + c);
+    gam = g0;
+    bet = be0;
   }
   if (!cok) return;
   const bool drop = a.drop_p > 0.f;
   const float scale = drop ? 1.f / (1.f - a.drop_p) : 1.f;
   const uint32_t thr = drop ? (uint32_t)((double)(1.f - a.drop_p) * 4294967296.0) : 0u;
-  const int64_t step = a.step_ctr ? *a.step_ctr : 0;
+  const int64_t step = a.step_ctr ? step0 : 0;
+  const uint32_t seed32 = hash_seed(a.seed, (uint64_t)a.stream_id, (uint64_t)step);
 #pragma unroll
   for (int i = 0; i < RI; ++i) {
     const int row = rg + RG * i;
@@ -412,7 +424,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
       if (drop) {
         uint32_t k;
         if (a.keep_in) k = j == 0 ? kin.x : (j == 1 ? kin.y : (j == 2 ? kin.z : kin.w));
-        else k = hash3(a.seed, (uint64_t)a.stream_id, (uint64_t)step * (uint64_t)(M * N) + idx + j) < thr;
+        else k = hash_drop(seed32, (uint32_t)(idx + j)) < thr;
         kw |= (k ? 1u : 0u) << (8 * j);
         v = k ? v * scale : 0.f;
       }
@@ -433,23 +445,29 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
   const bool cok = c < a.N;
   const int64_t N = a.N;
   const int M = a.M;
+  // parameters first, from valid addresses, selected afterwards (see the forward kernel)
+  const int cc = min(c, a.N - 4);
+  const bool bn = a.norm == PKC_NORM_BN_TRAIN;
+  const float* dummy = a.xhat;
+  const float4 g0 = ld4(bn ? a.gamma + cc : dummy);
+  const float4 be0 = ld4(bn ? a.beta + cc : dummy);
+  const float4 is0 = ld4(bn ? a.save_invstd + cc : dummy);
   float4 g[RI], xh[RI];
   uint32_t kp[RI];
   load_slabs<NS, RI>(a.gslab, a.slab_stride, a.nslab, rg, M, N, c, cok, g);
   const bool drop = a.drop_p > 0.f;
+  const uint8_t* kb = drop ? a.keep : reinterpret_cast<const uint8_t*>(a.xhat);
 #pragma unroll
   for (int i = 0; i < RI; ++i) {
     const int row = rg + RG * i;
     const bool ok = cok && row < M;
     const int64_t idx = ok ? (int64_t)row * N + c : 0;
     xh[i] = *reinterpret_cast<const float4*>(a.xhat + idx);
-    kp[i] = drop ? *reinterpret_cast<const uint32_t*>(a.keep + idx) : 0xffffffffu;
+    const uint32_t kv = *reinterpret_cast<const uint32_t*>(kb + idx);
+    kp[i] = drop ? kv : 0xffffffffu;
   }
-  const bool bn = a.norm == PKC_NORM_BN_TRAIN;
-  const float4 gam = (cok && bn) ? *reinterpret_cast<const float4*>(a.gamma + c)
-                                 : make_float4(1.f, 1.f, 1.f, 1.f);
-  const float4 bet = (cok && bn) ? *reinterpret_cast<const float4*>(a.beta + c)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 gam = bn ? g0 : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 bet = bn ? be0 : make_float4(0.f, 0.f, 0.f, 0.f);
   const float scale = drop ? 1.f / (1.f - a.drop_p) : 1.f;
   float4 sdy = make_float4(0.f, 0.f, 0.f, 0.f), sdyx = sdy;
   float4 dy[RI];
@@ -484,7 +502,7 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
   }
   float4 k = make_float4(1.f, 1.f, 1.f, 1.f), mdy = make_float4(0.f, 0.f, 0.f, 0.f), mdyx = mdy;
   if (bn) {
-    const float4 is = *reinterpret_cast<const float4*>(a.save_invstd + c);
+    const float4 is = is0;
     const float inv = 1.f / (float)M;
     k = make_float4(gam.x * is.x, gam.y * is.y, gam.z * is.z, gam.w * is.w);
     mdy = make_float4(sdy.x * inv, sdy.y * inv, sdy.z * inv, sdy.w * inv);

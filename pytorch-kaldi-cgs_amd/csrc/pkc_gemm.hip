@@ -16,6 +16,7 @@
 //              one 16-byte load per thread per operand per k-tile.
 // Split-K over blockIdx.z writes deterministic partial slabs (summed by the consumer kernels).
 #include "pkc_ops.h"
+#include "pkc_optim.h"
 
 namespace pkc {
 
@@ -303,6 +304,11 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
     colsum_body(p.M, p.N, reinterpret_cast<const float*>(p.A), p.C, local * 64);
     return;
   }
+  if (p.kind == PKC_OP_OPTIM) {
+    optim_wg(reinterpret_cast<const pkc_opt_tensor*>(p.A), reinterpret_cast<const int32_t*>(p.B),
+             local);
+    return;
+  }
   if (p.kind == PKC_OP_LOSS) {
     loss_finalize_body(p.M, reinterpret_cast<const float* const*>(p.A),
                        reinterpret_cast<const float*>(p.B), p.N, reinterpret_cast<const float*>(p.X1),
@@ -408,6 +414,16 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   for (int i = 0; i < n; ++i) {
     const pkc_gemm_problem& q = probs[i];
+    if (q.kind == PKC_OP_OPTIM) {
+      PKC_CHECK_ARG(q.M > 0 && q.A && q.B, "pkc_gemm_grouped: optimizer op %d arguments", i);
+      GroupProb& p = g.p[k++];
+      memset(&p, 0, sizeof(p));
+      p.kind = q.kind;
+      p.A = q.A; p.B = q.B;
+      p.wg0 = wg;
+      wg += q.M;
+      continue;
+    }
     if (q.kind == PKC_OP_COLSUM || q.kind == PKC_OP_LOSS) {
       PKC_CHECK_ARG(q.M > 0 && q.N > 0 && q.A && q.C, "pkc_gemm_grouped: op %d arguments", i);
       PKC_CHECK_ARG(q.kind != PKC_OP_LOSS || (q.M <= 8 && q.B && q.X1),

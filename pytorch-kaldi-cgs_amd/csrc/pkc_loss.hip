@@ -119,6 +119,9 @@ __device__ __forceinline__ void nll_reg_body(const pkc_nll_args& a, int block, N
   const int64_t N = a.N;
   const int rr = rok ? r : a.M - 1;
   const float* zb = a.zslab + (int64_t)rr * N;
+  // the row's label is requested with the logits (never after the reductions)
+  const int y_ = *(a.labels ? a.labels + (int64_t)rr * a.label_stride
+                            : reinterpret_cast<const int32_t*>(a.zslab));
   float v[NPT][NS];
 #pragma unroll
   for (int q = 0; q < NPT; ++q) {
@@ -170,7 +173,7 @@ __device__ __forceinline__ void nll_reg_body(const pkc_nll_args& a, int block, N
   }
   if (!rok) return;
   const float lse = mx + logf(se);
-  const int y = a.labels ? a.labels[(int64_t)r * a.label_stride] : -1;
+  const int y = a.labels ? y_ : -1;
   const float gscale = a.weight / (float)a.M;
   float* lrow = a.logp + (int64_t)r * N;
 #pragma unroll

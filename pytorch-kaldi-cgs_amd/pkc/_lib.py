@@ -73,7 +73,7 @@ class GemmProblem(C.Structure):
                 ("X1", vp), ("X2", vp), ("X3", vp)]
 
 
-OP_GEMM, OP_COLSUM, OP_LOSS = 0, 1, 2
+OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM = 0, 1, 2, 3
 
 
 _SIGS = {

@@ -457,7 +457,8 @@ class Engine:
                     g = getattr(n, key)
                 q, qb = n.quant_of(p)
                 self.opt_entries.append(dict(arch=n.arch, p=p, g=g, mask=m, o=o, q=q, qbits=qb,
-                                             s1=torch.zeros_like(p), s2=None, s3=None, step=0))
+                                             s1=torch.zeros_like(p), s2=None, s3=None, step=0,
+                                             node=n))
         for e in self.opt_entries:
             kind = e["o"]["arch_opt"]
             if kind == "rmsprop" and (float(e["o"]["opt_momentum"]) > 0):
@@ -473,8 +474,14 @@ class Engine:
             (e["o"]["arch_opt"] == "sgd" and float(e["o"]["opt_momentum"]) == 0.0)
             for e in self.opt_entries)
         n = len(self.opt_entries)
+        self.node_opt = {}
         if n:
             self.opt_nchunks, self.opt_map = self._chunk_map(range(n))
+            # per-layer work lists: the layer's update can run as soon as its gradients are done
+            for nd in self.nodes:
+                idx = [i for i, e in enumerate(self.opt_entries) if e["node"] is nd]
+                if idx:
+                    self.node_opt[nd] = self._chunk_map(idx) + (idx,)
             self.opt_desc = torch.zeros(n * C.sizeof(L.OptTensor), dtype=torch.uint8, device=self.dev)
             self._upload_opt_desc(step_inc=1)
         # the reference multiplies the masks in (and QuantizeLinear clamps W to [-1, 1]) before
@@ -957,31 +964,56 @@ class Engine:
                     nx += sx
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
 
-    def _backward_kernels(self, s, loss_op=None):
+    def _opt_op(self, n):
+        """The optimizer update of node n's parameters as an operation of a grouped launch."""
+        if n not in self.node_opt:
+            return []
+        nch, cmap, idx = self.node_opt[n]
+        nparam = sum(self.opt_entries[i]["p"].numel() for i in idx)
+        return [("opt %s" % n.name, 0.0, 20.0 * nparam,
+                 L.GemmProblem(kind=L.OP_OPTIM, M=nch, A=self.opt_desc.data_ptr(),
+                               B=cmap.data_ptr()))]
+
+    def _backward_kernels(self, s, loss_op=None, spread_opt=False):
         """Reverse pass.  The matmuls of a layer (dW, dX) are queued and launched together with
         those of the layers after it that are still pending, right before the first kernel that
-        needs one of their results (the producer's BatchNorm backward reads the dX slabs)."""
+        needs one of their results (the producer's BatchNorm backward reads the dX slabs).
+        spread_opt: each layer's optimizer update joins the launch AFTER the one holding its dW
+        and dX (dX still reads the old weights), so the bandwidth-bound update overlaps the
+        latency-bound matmuls instead of running as its own launch at the end."""
         for n in self.nodes:
             if n.gslab is not None:
                 n.sb = self._grad_slabs(n)
         pend = [loss_op] if loss_op is not None else []
+        carry, carry_next = [], []
+
+        def flush():
+            nonlocal pend, carry, carry_next
+            if pend or carry:
+                self._gemms(pend + carry, s)
+            pend, carry, carry_next = [], carry_next, []
+
         for n in reversed(self.nodes):
             if not self.needs_grad[n]:
                 continue
             if n.rec:
-                self._gemms(pend, s)
-                pend = []
+                flush()
                 self._rec_bwd(n, s)
                 continue
             if not n.head:
-                self._gemms(pend, s)
-                pend = []
+                flush()
             self._dense_bwd_pre(n, s)
             pend += self._bwd_problems(n)
-        self._gemms(pend, s)
+            if spread_opt:
+                carry_next += self._opt_op(n)
+        flush()
+        self.spread_tail = carry        # updates still to run (the last layers')
 
-    def _optim_kernels(self, s):
+    def _optim_kernels(self, s, spread_opt=False):
         if not self.opt_entries:
+            return
+        if spread_opt:
+            self._gemms(self.spread_tail, s)
             return
         nparam = sum(e["p"].numel() for e in self.opt_entries)
         self._k("optim_step", 0, 4.0 * nparam * 5, "pkc_optim_step", ptr(self.opt_desc),
@@ -990,11 +1022,12 @@ class Engine:
     def _train_step_kernels(self, allreduce=None, batch=None):
         s = self._stream()
         defer = bool(self.loss_heads)
+        spread = not self.seq and allreduce is None
         self._forward_kernels(s, True, batch, defer_loss=defer)
-        self._backward_kernels(s, self._loss_op() if defer else None)
+        self._backward_kernels(s, self._loss_op() if defer else None, spread_opt=spread)
         if allreduce is not None:
             allreduce(self.gflat)
-        self._optim_kernels(s)
+        self._optim_kernels(s, spread_opt=spread)
 
     # ------------------------------------------------------------------ public API
     def _set_rows(self, batch):
@@ -1063,9 +1096,10 @@ class Engine:
             st = self._stream()
             defer = bool(self.loss_heads)
             self._forward_kernels(st, True, defer_loss=defer)
-            self._backward_kernels(st, self._loss_op() if defer else None)
+            self._backward_kernels(st, self._loss_op() if defer else None,
+                                   spread_opt=not split_optimizer)
             if not split_optimizer:
-                self._optim_kernels(st)
+                self._optim_kernels(st, spread_opt=True)
         self.graph_opt = None
         if split_optimizer:
             g2 = torch.cuda.CUDAGraph()
