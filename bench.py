@@ -135,6 +135,45 @@ def cpu_baseline(batch, seconds=12.0):
                       "%d threads, %.1f s)" % (n, batch, threads, dt)}
 
 
+def pmc_traffic(label):
+    """HBM bytes per launch of `label` from the committed rocprofv3 PMC summary
+    (scripts/gpu_pmc.sh -> profiles/*pmc_traffic.json): (2 x FETCH_SIZE + WRITE_SIZE) KiB, the
+    gfx950 FETCH_SIZE half-count correction applied as MI355X_MICROARCH.md's HBM section
+    prescribes (it is exact for 128-byte coalesced reads; for 64-byte row segments it can
+    over-count the reads up to 2x — the summary keeps the raw counters).  None when the summary
+    is for another launch."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("label") == label and d.get("traffic_bytes_per_launch"):
+            return d["traffic_bytes_per_launch"]
+    return None
+
+
+def batch_sweep(prec, batches=(1024, 4096), steps=30):
+    """Informational: the same step at larger frame batches — not `value`."""
+    out = {}
+    for b in batches:
+        eng, _, _, _ = build(prec, b, 0, 1)
+        for _ in range(3):
+            eng.train_step()
+        eng.capture()
+        for _ in range(5):
+            eng.train_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.train_step()
+        torch.cuda.synchronize()
+        out[str(b)] = round(steps * b / (time.perf_counter() - t0), 1)
+        del eng
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,6 +183,9 @@ def main():
     ap.add_argument("--prec", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-batch-sweep", action="store_true")
+    ap.add_argument("--pmc-replay", type=int, default=0,
+                    help="only replay the dominant launch N times (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -177,6 +219,32 @@ def main():
             a[3] += nb
     for v in agg.values():
         v[0] //= NPROF
+    # dominant kernel = the libpkc entry point with the largest in-step device time, measured
+    # live with HIP events as (step graph) - (step graph without its launches) for the three
+    # largest candidates by eager time (after this the weights are stale: it runs after the
+    # timed region, or alone in a counter run)
+    by_fn = {}
+    for label, fn, fl, nb, ms in prof:
+        f = by_fn.setdefault(fn, {"labels": set(), "launches": 0, "flops": 0.0, "bytes": 0.0,
+                                  "eager_ms": 0.0})
+        f["labels"].add(label)
+        f["launches"] += 1
+        f["flops"] += fl
+        f["bytes"] += nb
+        f["eager_ms"] += ms
+    cands = sorted(by_fn, key=lambda k: -by_fn[k]["eager_ms"])[:3]
+
+    def pick_dominant():
+        costs = {fn: eng.step_cost_of(by_fn[fn]["labels"])[0] for fn in cands}
+        fn = max(costs, key=costs.get)
+        return fn, costs[fn]
+
+    if args.pmc_replay:
+        # counter runs (scripts/gpu_pmc.sh): the dominant kernel's launches, N rounds, last
+        dom_fn, _ = pick_dominant()
+        nl = eng.replay_launches(dom_fn, args.pmc_replay)
+        print(json.dumps({"pmc_replay": dom_fn, "launches": nl * args.pmc_replay}), flush=True)
+        return
     eng.capture(split_optimizer=world > 1)
     for _ in range(args.warmup):
         eng.train_step(allreduce)
@@ -197,17 +265,23 @@ def main():
     loss_sum, err_sum = eng.chunk_totals()
     n_done = args.warmup + args.steps
 
-    # dominant kernel: re-measure it live with HIP events on its stream (50 launches)
-    dom = max(agg.items(), key=lambda kv: kv[1][1])
-    label, (cnt, ms_tot, fl_tot, nb_tot) = dom
-    dom_launches = [p for p in prof if p[0] == label]
-    per_launch_fl = dom_launches[0][2]
-    per_launch_nb = dom_launches[0][3]
-    avg_ms = ms_tot / cnt
+    dom_fn, dom_us = pick_dominant()
+    d = by_fn[dom_fn]
+    label = dom_fn
+    cnt = d["launches"]
+    per_launch_fl = d["flops"] / cnt
+    per_launch_nb = d["bytes"] / cnt
+    avg_ms = dom_us / cnt * 1e-3
+    traffic = pmc_traffic(label)
+    sweep = {}
+    if rank == 0 and world == 1 and not args.no_batch_sweep:
+        sweep = batch_sweep(prec)
     if rank == 0:
-        is_gemm = label.startswith("gemm")
-        if is_gemm and args.prec == "fp32":
-            bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS["fp32"], "TFLOP/s"
+        is_gemm = "gemm" in label
+        # MFMA-bound only where the launch's arithmetic intensity exceeds the machine balance
+        balance = MFMA_PEAK_TFLOPS[args.prec] * 1e12 / (HBM_PEAK_GBS * 1e9)
+        if is_gemm and per_launch_fl / max(per_launch_nb, 1.0) > balance:
+            bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS[args.prec], "TFLOP/s"
             achieved = per_launch_fl / (avg_ms * 1e-3) / 1e12
         else:
             bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
@@ -231,14 +305,16 @@ def main():
                                    "batch_size_train=128, dropout 0.15, SGD body + RMSprop heads",
                        "global_batch": args.batch * world, "parallelism": "dp%d" % world,
                        "chunk_frames_per_rank": chunk.n_rows},
-            "roofline": {"kernel": label, "bound": bound, "achieved": round(achieved, 2),
+            "roofline": {"kernel": label, "labels": sorted(d["labels"]), "bound": bound,
+                         "achieved": round(achieved, 2),
                          "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-                         "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 3),
+                         "traffic": traffic, "avg_launch_us": round(avg_ms * 1e3, 3),
                          "launches_per_step": cnt,
                          "algorithmic_bytes_per_launch": per_launch_nb,
                          "algorithmic_flops_per_launch": per_launch_fl},
             "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
                                   sorted(agg.items(), key=lambda kv: -kv[1][1])},
+            "batch_sweep_frames_per_s": sweep,
             "chunk_prep_s": round(prep_s, 3),
             "mean_loss": round(loss_sum / max(1, n_done), 4),
         }

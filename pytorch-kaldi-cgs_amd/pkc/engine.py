@@ -195,6 +195,7 @@ class Engine:
         self.graph = None
         self.graph_opt = None
         self.steps_done = 0
+        self.skip_labels = set()
 
     # ------------------------------------------------------------------ graph construction
     def _build_graph(self):
@@ -592,13 +593,15 @@ class Engine:
 
     def _k(self, label, flops, nbytes, fn, *args):
         """Launch one libpkc entry point; in profile mode bracket it with events."""
+        if label in self.skip_labels:     # measurement only (step_cost_of)
+            return
         if self.prof is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
             call(fn, *args)
             e1.record()
-            self.prof.append((label, fn, float(flops), float(nbytes), e0, e1))
+            self.prof.append((label, fn, float(flops), float(nbytes), e0, e1, args))
         else:
             call(fn, *args)
 
@@ -1070,10 +1073,59 @@ class Engine:
         self._set_rows(None)
         self._train_step_kernels()
         torch.cuda.synchronize()
-        out = [(l, f, fl, nb, e0.elapsed_time(e1)) for (l, f, fl, nb, e0, e1) in self.prof]
+        out = [(l, f, fl, nb, e0.elapsed_time(e1)) for (l, f, fl, nb, e0, e1, _) in self.prof]
+        self.last_prof_calls = [(l, f, a) for (l, f, _, _, _, _, a) in self.prof]
         self.prof = None
         self._after_step()
         return out
+
+    def step_cost_of(self, label, reps=50):
+        """In-step device time (us) of the launches labelled `label`: the captured step graph
+        timed with and without them (HIP events around `reps` replays each).  The launches are
+        measured where they run — after their real producers, inside the step — so this agrees
+        with rocprofv3's per-dispatch durations of the step graph.  Corrupts the training state
+        (the skipped outputs go stale): call it after the timed region only."""
+        def graph_us(skip):
+            self.skip_labels = set(skip)
+            self._set_rows(None)
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                s = self._stream()
+                self._forward_kernels(s, True, defer_loss=bool(self.loss_heads))
+                self._backward_kernels(s, self._loss_op() if self.loss_heads else None,
+                                       spread_opt=True)
+                self._optim_kernels(s, spread_opt=True)
+            torch.cuda.current_stream().wait_stream(st)
+            self.skip_labels = set()
+            for _ in range(3):
+                g.replay()
+            torch.cuda.synchronize()
+            best = None
+            for _ in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    g.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / reps
+                best = us if best is None else min(best, us)
+            return best
+        full = graph_us(())
+        without = graph_us(tuple(label) if isinstance(label, (list, tuple, set)) else (label,))
+        return full - without, full
+
+    def replay_launches(self, fn, reps):
+        """Re-issue every launch of entry point `fn` of the last profile_step, `reps` rounds
+        (eager; for PMC counter runs — corrupts the training state)."""
+        calls = [(f, a) for (l, f, a) in self.last_prof_calls if f == fn]
+        for _ in range(reps):
+            for f, a in calls:
+                call(f, *a[:-1], self._stream())
+        torch.cuda.synchronize()
+        return len(calls)
 
     def _after_step(self):
         self.steps_done += 1
