@@ -181,6 +181,22 @@ int pkc_batch_gather(const float* feats, int64_t ld_feats, int F, const int32_t*
                      int B, int64_t n_batches, int64_t* step_ctr, float* x_out, int32_t* lab_out,
                      int advance, void* x_bf16, void* stream);   /* x_bf16: optional bf16 copy */
 
+/* ---------------------------------------------------------------------------------------------
+ * LayerNorm of the reference (neural_networks.py:40-51, used by MLP dnn_use_laynorm /
+ * dnn_use_laynorm_inp): y = gamma * (x - mean) / (std + eps) + beta per row over N features,
+ * std unbiased, x = sum_s xslab[s] + bias.  Saves xhat = (x - mean)/(std + eps) and
+ * rowstat[2r] = std + eps, rowstat[2r+1] = std for the backward.
+ * ------------------------------------------------------------------------------------------- */
+int pkc_layernorm_fwd(int M, int N, int nslab, const float* xslab, int64_t slab_stride,
+                      const float* bias, const float* gamma, const float* beta, float eps,
+                      float* y, float* xhat, float* rowstat, void* stream);
+/* dx from dy = sum_s dy[s] (split-K slabs of the consumers' dX); dgamma = sum_rows dy*xhat,
+ * dbeta = sum_rows dy, dbias = sum_rows dx (each optional) */
+int pkc_layernorm_bwd(int M, int N, int nslab, const float* dy, int64_t slab_stride,
+                      const float* xhat, const float* gamma,
+                      const float* rowstat, float* dx, float* dgamma, float* dbeta, float* dbias,
+                      void* stream);
+
 /* dst (bf16) = src (fp32), n elements (bf16 operand copies for the MFMA matmuls) */
 int pkc_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 

@@ -77,6 +77,10 @@ OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM = 0, 1, 2, 3
 
 
 _SIGS = {
+    "pkc_layernorm_fwd": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_float, vp, vp,
+                                    vp, vp]),
+    "pkc_layernorm_bwd": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp, vp,
+                                    vp]),
     "pkc_gemm_grouped": (C.c_int, [C.c_int, vp, C.c_int, vp]),
     "pkc_fakequant_weight": (C.c_int, [vp, vp, i64, C.c_int, vp]),
     "pkc_fakequant_input": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, vp, vp]),

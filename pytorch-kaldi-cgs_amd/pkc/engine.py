@@ -73,8 +73,8 @@ class Layer:
         self.name = "%s.%d" % (arch, idx)
         if self.head and self.bn:
             raise NotImplementedError("%s: BatchNorm before LogSoftmax is not on the pkc path" % self.name)
-        if spec["ln"]:
-            raise NotImplementedError("%s: LayerNorm is not on the pkc path yet" % self.name)
+        self.ln = bool(spec["ln"])                # LayerNorm between the Linear and BN / act
+        self.ln_gamma, self.ln_beta = spec.get("ln_gamma"), spec.get("ln_beta")
         if self.act not in L.ACT and not self.head:
             raise NotImplementedError("%s: activation %s" % (self.name, self.act))
         self.qbits = int(spec["quant"] or 0)      # QuantizeLinear weight bits (0: nn.Linear)
@@ -84,12 +84,41 @@ class Layer:
 
     def params(self):
         out = [(self.W, "dW", self.mask), (self.b, "db", None)]
+        if self.ln:
+            out += [(self.ln_gamma, "dgamma_ln", None), (self.ln_beta, "dbeta_ln", None)]
         if self.bn:
             out += [(self.gamma, "dgamma", None), (self.beta, "dbeta", None)]
         return out
 
     def quant_of(self, p):
         return (self.Wq, self.qbits) if (p is self.W and self.qbits) else (None, 0)
+
+
+class NormLayer(Layer):
+    """An MLP's input LayerNorm / BatchNorm (dnn_use_laynorm_inp / dnn_use_batchnorm_inp,
+    neural_networks.py:246-251): a node with no matmul, normalising the arch's input."""
+
+    def __init__(self, arch, idx, spec, K):
+        self.arch, self.idx, self.K, self.N = arch, idx, K, K
+        self.spec = spec
+        self.kind = spec["kind"]
+        self.act, self.head, self.drop = "linear", False, 0.0
+        self.bn, self.ln = self.kind == "bn", self.kind == "ln"
+        self.gamma, self.beta = spec["gamma"], spec["beta"]
+        self.ln_gamma, self.ln_beta = spec["gamma"], spec["beta"]
+        self.rm, self.rv = spec.get("rm"), spec.get("rv")
+        self.W = self.b = self.mask = None
+        self.src, self.consumers, self.label_col = None, [], None
+        self.nbt0 = int(spec["nbt"].item()) if spec.get("nbt") is not None else 0
+        self.loss_weight = 0.0
+        self.name = "%s.inp_%s%d" % (arch, self.kind, idx)
+        self.qbits = self.ibits = self.reads = 0
+        self.Wq = None
+
+    def params(self):
+        if self.ln:
+            return [(self.gamma, "dgamma_ln", None), (self.beta, "dbeta_ln", None)]
+        return [(self.gamma, "dgamma", None), (self.beta, "dbeta", None)]
 
 
 class RecNode:
@@ -222,6 +251,14 @@ class Engine:
                 produced[out] = node
                 continue
             prev = src
+            for i, spec in enumerate(net.input_norm_specs() if hasattr(net, "input_norm_specs")
+                                     else []):
+                nl = NormLayer(a, i, spec, K)
+                nl.src = prev
+                if prev[0] == "node":
+                    prev[1].consumers.append(nl)
+                self.nodes.append(nl)
+                prev = ("node", nl)
             for i, spec in enumerate(net.layer_specs()):
                 lay = Layer(a, i, spec, K)
                 lay.src = prev
@@ -259,6 +296,16 @@ class Engine:
                 for k, w in scal[b].items():
                     d[k] = d.get(k, 0.0) + w
                 scal[out] = d
+            elif op in ("cost_l1", "cost_l2", "cost_gl"):
+                # utils.py:1954-1991: 0 when the first arch applies guided HCGS, else
+                # lambda * sum of norms over the dim>1 parameters of archs without
+                # skip_regularization (every CGS cfg sets it: the term is then exactly 0)
+                nets = list(self.nets.values())
+                if not (getattr(nets[0], "apply_guided_hcgs", False) or
+                        all(getattr(n, "skip_regularization", False) for n in nets)):
+                    raise NotImplementedError("%s over non-skipped parameters (it also trains the "
+                                              "HCGS mask Parameters) is not on the pkc path" % op)
+                scal[out] = {}
             elif op == "compute":
                 continue
             else:
@@ -314,8 +361,11 @@ class Engine:
                 continue
             N, K = n.N, n.K
             n.scap = self.cap or _splits(M, N, K, MAX_SPLITS)
-            n.zslab = _f32(n.scap * M * N, dev)
-            n.out = _f32(M * N, dev)
+            n.zslab = _f32(n.scap * M * N, dev) if n.W is not None else None
+            if n.ln:
+                n.ln_y, n.ln_xhat = _f32(M * N, dev), _f32(M * N, dev)
+                n.ln_stat, n.dz_ln = _f32(2 * M, dev), _f32(M * N, dev)
+            n.out = n.ln_y if (n.ln and n.W is None) else _f32(M * N, dev)
             n.xhat = None if n.head else _f32(M * N, dev)
             n.keep = torch.zeros(M * N, dtype=torch.uint8, device=dev) if n.drop > 0 else None
             n.save_mean = _f32(N, dev)
@@ -693,15 +743,31 @@ class Engine:
     def _fwd_epilogue(self, n, s, train, out=None):
         """The layer's epilogue launch (BN/act/dropout, or a head's LogSoftmax/NLL); with `out`
         the head's NllArgs are only filled in (for a grouped launch)."""
-        M, sf = self.M, n.sf
+        M = self.M
+        if n.W is None:                      # input normalisation: no matmul in front
+            x_ptr, ldx = self._src(n)
+            if ldx != n.N:
+                raise NotImplementedError("%s: input normalisation of one of several feature "
+                                          "streams" % n.name)
+            n.sf = 1
+            zp, sf, zs, bias = x_ptr, 1, 0, None
+        else:
+            zp, sf, zs, bias = n.zslab.data_ptr(), n.sf, M * n.N, n.b.data_ptr()
+        if n.ln:
+            self._k("layernorm_fwd N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 3), "pkc_layernorm_fwd", M,
+                    n.N, sf, C.c_void_p(zp), zs, C.c_void_p(bias) if bias else None, ptr(n.ln_gamma),
+                    ptr(n.ln_beta), C.c_float(1e-6), ptr(n.ln_y), ptr(n.ln_xhat), ptr(n.ln_stat), s)
+            zp, sf, zs, bias = n.ln_y.data_ptr(), 1, 0, None
+            if n.W is None:
+                return                       # out aliases ln_y
         if n.head:
             has_lab = n.label_col >= 0
-            a = L.NllArgs(M=M, N=n.N, nslab=sf, zslab=n.zslab.data_ptr(), slab_stride=M * n.N,
-                          bias=n.b.data_ptr(),
+            a = L.NllArgs(M=M, N=n.N, nslab=sf, zslab=zp, slab_stride=zs, bias=bias,
                           labels=(self.labs.data_ptr() + 4 * n.label_col) if has_lab else None,
                           label_stride=self.nlab, weight=n.loss_weight * self.grad_scale,
                           logp=n.out.data_ptr(), log_prior=None,
-                          dlogits=n.dz.data_ptr() if (train and has_lab) else None,
+                          dlogits=(n.dz_ln if n.ln else n.dz).data_ptr() if (train and has_lab)
+                          else None,
                           row_loss=n.row_loss.data_ptr(), row_err=n.row_err.data_ptr())
             if out is not None:
                 C.memmove(C.byref(out), C.byref(a), C.sizeof(a))
@@ -711,8 +777,7 @@ class Engine:
             return
         keep_in = self.drop_keep_in.get(n.name)
         a = L.DenseFwdArgs(
-            M=M, N=n.N, nslab=sf, zslab=n.zslab.data_ptr(), slab_stride=M * n.N,
-            bias=n.b.data_ptr(),
+            M=M, N=n.N, nslab=sf, zslab=zp, slab_stride=zs, bias=bias,
             norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if n.bn else L.NORM_NONE,
             gamma=n.gamma.data_ptr(), beta=n.beta.data_ptr(),
             running_mean=n.rm.data_ptr(), running_var=n.rv.data_ptr(),
@@ -814,6 +879,10 @@ class Engine:
                 self._rec_fwd(n, s, train)
                 i += 1
                 continue
+            if n.W is None:
+                self._fwd_epilogue(n, s, train)
+                i += 1
+                continue
             # output heads reading the same tensor (cd + mono senones) share one matmul launch
             grp = [n]
             while (n.head and i + len(grp) < len(nodes) and not nodes[i + len(grp)].rec
@@ -873,7 +942,12 @@ class Engine:
         consumers' dX slabs (a head's dlogits came from the forward; its bias gradient is an
         operation of the grouped backward launch, _bwd_problems)."""
         M = self.M
+        if n.W is None and n.ln:             # input LayerNorm: only its gamma / beta gradients
+            self._ln_bwd(n, s, ptr(n.gslab), n.sb, M * n.N, n.dz, None)
+            return
         if n.head:
+            if n.ln:                         # dlogits are the LayerNorm output's gradient
+                self._ln_bwd(n, s, ptr(n.dz_ln), 1, 0, n.dz, n.db)
             return
         a = L.DenseBwdArgs(M=M, N=n.N, nslab=n.sb, gslab=n.gslab.data_ptr(),
                            slab_stride=M * n.N,
@@ -882,20 +956,32 @@ class Engine:
                            beta=n.beta.data_ptr(), save_invstd=n.save_invstd.data_ptr(),
                            xhat=n.xhat.data_ptr(),
                            keep=n.keep.data_ptr() if n.keep is not None else None,
-                           drop_p=n.drop, dz=n.dz.data_ptr(),
+                           drop_p=n.drop, dz=(n.dz_ln if n.ln else n.dz).data_ptr(),
                            dgamma=n.dgamma.data_ptr() if n.bn else None,
                            dbeta=n.dbeta.data_ptr() if n.bn else None,
-                           dbias=n.db.data_ptr())
+                           dbias=n.db.data_ptr() if (n.b is not None and not n.ln) else None)
         self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (n.sb + 3), "pkc_dense_bwd",
                 C.byref(a), ptr(n.work), s)
+        if n.ln:
+            # the Linear's bias sits in front of the LayerNorm (per-row statistics): its gradient
+            # is the column sum of the LayerNorm's input gradient
+            self._ln_bwd(n, s, ptr(n.dz_ln), 1, 0, n.dz, n.db)
+
+    def _ln_bwd(self, n, s, dy, nslab, stride, dx, dbias):
+        M = self.M
+        self._k("layernorm_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (nslab + 4), "pkc_layernorm_bwd", M,
+                n.N, nslab, dy, stride, ptr(n.ln_xhat), ptr(n.ln_gamma), ptr(n.ln_stat), ptr(dx),
+                ptr(n.dgamma_ln), ptr(n.dbeta_ln), ptr(dbias), s)
 
     def _bwd_problems(self, n):
         """dW = dz^T X (into the flat gradient buffer) and, when the producer needs it,
         dX = dz W (into the producer's gradient slabs)."""
         M = self.M
+        if n.W is None:
+            return []
         a_ptr, lda = self._final_version(n) if self.qsrc[n.qkey]["Q"] else self._src(n)
         out = []
-        if n.head:
+        if n.head and not n.ln:
             out.append(("db %d" % n.N, 0.0, 4.0 * M * n.N,
                         L.GemmProblem(kind=L.OP_COLSUM, M=M, N=n.N, A=n.dz.data_ptr(),
                                       C=n.db.data_ptr())))
@@ -1247,6 +1333,12 @@ class ModuleRunner:
         net.check_supported()
         self.net, self.rows, self.dev = net, max_rows, next(net.parameters()).device
         self.specs = net.layer_specs()
+        self.norms = net.input_norm_specs() if hasattr(net, "input_norm_specs") else []
+        self.nbufs = [dict(y=_f32(max_rows * inp_dim, self.dev), xh=_f32(max_rows * inp_dim, self.dev),
+                           st=_f32(2 * max_rows, self.dev), sm=_f32(inp_dim, self.dev),
+                           si=_f32(inp_dim, self.dev),
+                           work=_f32(L.lib().pkc_dense_work_size(max_rows, inp_dim), self.dev))
+                      for _ in self.norms]
         self.bufs = []
         K = inp_dim
         for sp in self.specs:
@@ -1255,6 +1347,9 @@ class ModuleRunner:
                      xhat=_f32(max_rows * N, self.dev), sm=_f32(N, self.dev),
                      si=_f32(N, self.dev), out=_f32(max_rows * N, self.dev),
                      work=_f32(L.lib().pkc_dense_work_size(max_rows, N), self.dev))
+            if sp["ln"]:
+                b.update(ly=_f32(max_rows * N, self.dev), lxh=_f32(max_rows * N, self.dev),
+                         lst=_f32(2 * max_rows, self.dev))
             if sp["quant"]:
                 b["Wq"] = torch.zeros_like(sp["W"])
             if sp["inp_quant"]:
@@ -1283,6 +1378,23 @@ class ModuleRunner:
         s = Engine._stream()
         cur, cld = x_ptr, ld
         self.input_version = None
+        for ns, nb in zip(self.norms, self.nbufs):       # input LayerNorm / BatchNorm
+            K0 = self.bufs[0]["K"]
+            if cld != K0:
+                raise NotImplementedError("input normalisation of a strided feature stream")
+            if ns["kind"] == "ln":
+                call("pkc_layernorm_fwd", M, K0, 1, C.c_void_p(cur), 0, None, ptr(ns["gamma"]),
+                     ptr(ns["beta"]), C.c_float(1e-6), ptr(nb["y"]), ptr(nb["xh"]), ptr(nb["st"]), s)
+            else:
+                a = L.DenseFwdArgs(
+                    M=M, N=K0, nslab=1, zslab=cur, slab_stride=0, bias=None,
+                    norm=L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL, gamma=ns["gamma"].data_ptr(),
+                    beta=ns["beta"].data_ptr(), running_mean=ns["rm"].data_ptr(),
+                    running_var=ns["rv"].data_ptr(), momentum=0.05, eps=1e-5,
+                    save_mean=nb["sm"].data_ptr(), save_invstd=nb["si"].data_ptr(), act=0,
+                    xhat=nb["xh"].data_ptr(), out=nb["y"].data_ptr(), count_n=0)
+                call("pkc_dense_fwd", C.byref(a), ptr(nb["work"]), s)
+            cur = nb["y"].data_ptr()
         for li, (sp, b) in enumerate(zip(self.specs, self.bufs)):
             N, K = b["N"], b["K"]
             if sp["inp_quant"]:
@@ -1297,17 +1409,22 @@ class ModuleRunner:
             sf = _splits(M, N, K, MAX_SPLITS)
             call("pkc_gemm", L.PREC_FP32, 1, 1, M, N, K, C.c_void_p(cur), cld, ptr(W), K,
                  ptr(b["z"]), N, sf, M * N, s)
+            zp, zs, bias = b["z"].data_ptr(), M * N, sp["b"].data_ptr()
+            if sp["ln"]:
+                call("pkc_layernorm_fwd", M, N, sf, C.c_void_p(zp), zs, C.c_void_p(bias),
+                     ptr(sp["ln_gamma"]), ptr(sp["ln_beta"]), C.c_float(1e-6), ptr(b["ly"]),
+                     ptr(b["lxh"]), ptr(b["lst"]), s)
+                zp, zs, bias, sf = b["ly"].data_ptr(), 0, None, 1
             if sp["act"] == "softmax":
-                a = L.NllArgs(M=M, N=N, nslab=sf, zslab=b["z"].data_ptr(), slab_stride=M * N,
-                              bias=sp["b"].data_ptr(), labels=None, label_stride=0, weight=0.0,
+                a = L.NllArgs(M=M, N=N, nslab=sf, zslab=zp, slab_stride=zs,
+                              bias=bias, labels=None, label_stride=0, weight=0.0,
                               logp=b["out"].data_ptr(),
                               log_prior=log_prior.data_ptr() if log_prior is not None else None,
                               dlogits=None, row_loss=None, row_err=None)
                 call("pkc_nll_fused", C.byref(a), s)
             else:
                 a = L.DenseFwdArgs(
-                    M=M, N=N, nslab=sf, zslab=b["z"].data_ptr(), slab_stride=M * N,
-                    bias=sp["b"].data_ptr(),
+                    M=M, N=N, nslab=sf, zslab=zp, slab_stride=zs, bias=bias,
                     norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if sp["bn"] else L.NORM_NONE,
                     gamma=sp["gamma"].data_ptr(), beta=sp["beta"].data_ptr(),
                     running_mean=sp["rm"].data_ptr(), running_var=sp["rv"].data_ptr(), momentum=0.05,

@@ -150,14 +150,22 @@ class MLP(nn.Module):
                               rv=self.bn[i].running_var, nbt=self.bn[i].num_batches_tracked,
                               mask=self.hcgs[i].mask if self.mlp_hcgs else None,
                               quant=self.param_quant[i] if self.mlp_quant else 0,
-                              inp_quant=self.inp_quant[0] if (self.mlp_quant and self.mlp_quant_inp) else 0))
+                              inp_quant=self.inp_quant[0] if (self.mlp_quant and self.mlp_quant_inp) else 0,
+                              ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta))
         return specs
 
+    def input_norm_specs(self):
+        """Input normalisations in the reference's order: ln0 then bn0 (neural_networks.py:246-251)."""
+        out = []
+        if self.dnn_use_laynorm_inp:
+            out.append(dict(kind="ln", gamma=self.ln0.gamma, beta=self.ln0.beta))
+        if self.dnn_use_batchnorm_inp:
+            out.append(dict(kind="bn", gamma=self.bn0.weight, beta=self.bn0.bias,
+                            rm=self.bn0.running_mean, rv=self.bn0.running_var,
+                            nbt=self.bn0.num_batches_tracked))
+        return out
+
     def check_supported(self):
-        if self.dnn_use_laynorm_inp or self.dnn_use_batchnorm_inp:
-            raise NotImplementedError("input LayerNorm/BatchNorm is not on the pkc MLP path yet")
-        if any(self.dnn_use_laynorm):
-            raise NotImplementedError("LayerNorm layers are not on the pkc MLP path yet")
         if self.prune or self.if_pattern:
             raise NotImplementedError("pruned / pattern MLP layers are not on the pkc MLP path yet")
 

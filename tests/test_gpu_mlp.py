@@ -44,11 +44,20 @@ def out_version(eng, lay, M):
     return lay.out[:M * lay.N]
 
 
-@pytest.mark.parametrize("variant", ["plain", "hcgs", "quant"])
+@pytest.mark.parametrize("variant", ["plain", "hcgs", "quant", "ln", "plain_l1"])
 def test_engine_matches_reference_golden_steps(variant):
+    """plain_l1: the plain model with an L1 regulariser term over skip_regularization archs
+    (every CGS cfg): utils.py:1954-1964 makes it exactly 0."""
     from pkc.engine import Engine, parse_model
+    l1 = variant == "plain_l1"
+    variant = "plain" if l1 else variant
     g = G("mlp_%s.npz" % variant)
     cfg = build_mlp_config(variant)
+    if l1:
+        cfg["model"]["model"] = cfg["model"]["model"].replace(
+            "loss_final=sum(loss_cd,loss_mono_w)",
+            "loss_reg=cost_l1(out_dnn1,0.001)\nloss_tmp=sum(loss_cd,loss_mono_w)\n"
+            "loss_final=sum(loss_tmp,loss_reg)")
     nets, opts = build_nets(cfg, (("architecture1", 40), ("architecture2", 32), ("architecture3", 32)))
     for n in nets.values():
         n.to(DEV).train()
