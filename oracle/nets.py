@@ -195,6 +195,17 @@ class liGRU(_Rec):
         self.orth = _b(o["ligru_orthinit"])
         self.acts = _lst(o, "ligru_act")
         self.bidir = _b(o["ligru_bidir"])
+        # HCGS for liGRU: the reference liGRU has no CGS hook, so the
+        # LSTM hook is reused verbatim (neural_networks.py:858-861 / 980-983 semantics: masks drawn
+        # after the gate Linears of each layer, multiplied into W / U in place every forward).
+        # Parity of this extension is unpinned by the reference (no liGRU fixture can exist).
+        self.hcgs_on = _b(o.get("ligru_hcgs", "False"))
+        bx = _lst(o, "hcgsx_block", int) if self.hcgs_on else []
+        bh = _lst(o, "hcgsh_block", int) if self.hcgs_on else []
+        dx = _lst(o, "hcgsx_sparse", float) if self.hcgs_on else []
+        dh = _lst(o, "hcgsh_sparse", float) if self.hcgs_on else []
+        if self.hcgs_on:
+            self.hcgsx, self.hcgsh = nn.ModuleList(), nn.ModuleList()
         self.wh, self.uh, self.wz, self.uz = (nn.ModuleList() for _ in range(4))
         self.ln, self.bn_wh, self.bn_wz = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         if self.ln_inp:
@@ -206,8 +217,16 @@ class liGRU(_Rec):
             add_bias = not (self.use_ln[i] or self.use_bn[i])
             self.wh.append(nn.Linear(cur, n, bias=add_bias))
             self.wz.append(nn.Linear(cur, n, bias=add_bias))
+            if self.hcgs_on:
+                hm = nn.Module()
+                hm.mask = nn.Parameter(torch.from_numpy(M.hcgs_conn_mat(n, cur, bx, dx)))
+                self.hcgsx.append(hm)
             self.uh.append(nn.Linear(n, n, bias=False))
             self.uz.append(nn.Linear(n, n, bias=False))
+            if self.hcgs_on:
+                hm = nn.Module()
+                hm.mask = nn.Parameter(torch.from_numpy(M.hcgs_conn_mat(n, n, bh, dh)))
+                self.hcgsh.append(hm)
             if self.orth:
                 nn.init.orthogonal_(self.uh[i].weight)
                 nn.init.orthogonal_(self.uz[i].weight)
@@ -228,6 +247,11 @@ class liGRU(_Rec):
                 x = torch.cat([x, flip_time(x)], 1)
             T, B2, _ = x.shape
             dm = self._drop_mask(i, B2, H, drop_masks)
+            if self.hcgs_on:
+                for lin in (self.wh[i], self.wz[i]):
+                    lin.weight.data.mul_(self.hcgsx[i].mask.data)
+                for lin in (self.uh[i], self.uz[i]):
+                    lin.weight.data.mul_(self.hcgsh[i].mask.data)
             wh = self.wh[i](x)
             wz = self.wz[i](x)
             if self.use_bn[i]:
@@ -270,6 +294,9 @@ class LSTM(_Rec):
         self.quant_inp = _b(o.get("lstm_quant_inp", "False"))
         self.prune = _b(o.get("lstm_prune", "False"))
         self.if_pattern = _b(o["if_pattern"]) if "if_pattern" in o else False
+        # the reference forces bidir = 0 in forward (:835) and crashes on layer 2 of a bidir cfg;
+        # config C4's bidirectional LSTM follows the liGRU convention (shared W/U/BN, cat/flip)
+        self.bidir = _b(o.get("lstm_bidir", "False"))
         bits = _lst(o, "param_quant", int) if "param_quant" in o else [8] * len(self.lay)
         ibits = int(o["inp_quant"].split(",")[0]) if "inp_quant" in o else 16
         self.prune_perc = _lst(o, "lstm_prune_perc", float) if "lstm_prune_perc" in o else []
@@ -320,8 +347,8 @@ class LSTM(_Rec):
             for g in self.GATES:
                 getattr(self, "bn_w%sx" % g).append(nn.BatchNorm1d(n, momentum=0.05))
             self.ln.append(LayerNorm(n))
-            cur = n
-        self.out_dim = self.lay[-1]
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
         self.pattern_masks = None
 
     def _pattern_update(self):
@@ -347,6 +374,8 @@ class LSTM(_Rec):
             T, B, Fd = x.shape
             x = self.bn0(x.reshape(T * B, Fd)).view(T, B, Fd)
         for i, H in enumerate(self.lay):
+            if self.bidir:
+                x = torch.cat([x, flip_time(x)], 1)
             T, B, _ = x.shape
             dm = self._drop_mask(i, B, H, drop_masks)
             W = {g: getattr(self, "w%sx" % g)[i] for g in self.GATES}
@@ -383,6 +412,8 @@ class LSTM(_Rec):
                     h = self.ln[i](h)
                 hs.append(h)
             x = torch.stack(hs)
+            if self.bidir:
+                x = torch.cat([x[:, :B // 2], flip_time(x[:, B // 2:])], 2)
         return x
 
 

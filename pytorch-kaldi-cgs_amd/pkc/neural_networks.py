@@ -205,6 +205,16 @@ class liGRU(nn.Module):
         self.apply_guided_hcgs = False
         self.if_pattern = False
         self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
+        # pkc extension for config C3: the reference liGRU has no CGS hook; with
+        # ligru_hcgs the LSTM's HCGS hook is reused (same keys hcgsx_* / hcgsh_*, masks drawn
+        # after each layer's W and U Linears, applied in place every forward)
+        self.ligru_hcgs = strtobool(o.get("ligru_hcgs", "False"))
+        if self.ligru_hcgs:
+            self.hcgsx_block = _lst(o, "hcgsx_block", int)
+            self.hcgsh_block = _lst(o, "hcgsh_block", int)
+            self.hcgsx_sparse = _lst(o, "hcgsx_sparse", float)
+            self.hcgsh_sparse = _lst(o, "hcgsh_sparse", float)
+            self.hcgsx, self.hcgsh = nn.ModuleList(), nn.ModuleList()
         self.wh, self.uh = nn.ModuleList(), nn.ModuleList()
         self.wz, self.uz = nn.ModuleList(), nn.ModuleList()
         self.ln, self.bn_wh, self.bn_wz = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
@@ -217,8 +227,12 @@ class liGRU(nn.Module):
             add_bias = not (self.ligru_use_laynorm[i] or self.ligru_use_batchnorm[i])
             self.wh.append(nn.Linear(cur, n, bias=add_bias))
             self.wz.append(nn.Linear(cur, n, bias=add_bias))
+            if self.ligru_hcgs:
+                self.hcgsx.append(_Mask(hcgs_mask(n, cur, self.hcgsx_block, self.hcgsx_sparse)))
             self.uh.append(nn.Linear(n, n, bias=False))
             self.uz.append(nn.Linear(n, n, bias=False))
+            if self.ligru_hcgs:
+                self.hcgsh.append(_Mask(hcgs_mask(n, n, self.hcgsh_block, self.hcgsh_sparse)))
             if self.ligru_orthinit:
                 nn.init.orthogonal_(self.uh[i].weight)
                 nn.init.orthogonal_(self.uz[i].weight)
@@ -243,7 +257,9 @@ class liGRU(nn.Module):
                               W=[self.wz[i].weight, self.wh[i].weight],
                               b=[self.wz[i].bias, self.wh[i].bias],
                               U=[self.uz[i].weight, self.uh[i].weight],
-                              bnm=[self.bn_wz[i], self.bn_wh[i]], Wmask=None, Umask=None))
+                              bnm=[self.bn_wz[i], self.bn_wh[i]],
+                              Wmask=self.hcgsx[i].mask if self.ligru_hcgs else None,
+                              Umask=self.hcgsh[i].mask if self.ligru_hcgs else None))
         return specs
 
 

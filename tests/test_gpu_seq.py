@@ -20,6 +20,13 @@ def make_cfg(body):
                opt_eps="1e-8", opt_centered="False", opt_weight_decay="0.0", arch_freeze="False")
     if body == "ligru":
         cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2", **opt)
+    elif body == "lstm_bidir":     # config C4: bidirectional LSTM, liGRU convention
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="True", **opt)
+    elif body == "ligru_hcgs":     # config C3: liGRU with the LSTM's HCGS hook (8x4 / 50,50)
+        cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2",
+                         ligru_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
+                         hcgsh_block="8,4", hcgsh_sparse="25,50", **opt)
     else:
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", **opt)
@@ -35,7 +42,7 @@ def make_cfg(body):
     return cfg
 
 
-@pytest.mark.parametrize("body", ["ligru", "lstm"])
+@pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -51,7 +58,8 @@ def test_seq_engine_vs_oracle(body):
             inp = nets["rnn"].out_dim
         torch.manual_seed(3)
         np.random.seed(3)
-        cls = {"ligru": "liGRU", "lstm": "LSTM"}[body] if sec == "a1" else "MLP"
+        cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM"}[body]
+               if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
         onets[o["arch_name"]].load_state_dict(nets[o["arch_name"]].state_dict())
@@ -107,5 +115,11 @@ def test_seq_engine_vs_oracle(body):
             if name.endswith("num_batches_tracked"):
                 continue
             ref = onets[k].state_dict()[name].double()
+            # the reference re-masks W / U at the next forward; pkc stores W*mask right away
+            sd_o = onets[k].state_dict()
+            parts = name.split(".")
+            if body == "ligru_hcgs" and name.endswith("weight") and parts[0] in ("wh", "wz", "uh", "uz"):
+                mk = ("hcgsx" if parts[0][0] == "w" else "hcgsh") + ".%s.mask" % parts[1]
+                ref = ref * sd_o[mk].double()
             d = (v.cpu().double() - ref).norm().item()
             assert d <= 1e-3 * ref.norm().item() + 1e-7, "%s %s %.3g" % (k, name, d)

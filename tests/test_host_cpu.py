@@ -129,3 +129,26 @@ def test_ark_reader_roundtrip(tmp_path):
     assert list(got) == list(mats)
     for k in mats:
         np.testing.assert_array_equal(got[k], mats[k])
+
+
+def test_product_ligru_hcgs_init_matches_oracle():
+    """liGRU + HCGS (config C3, pkc extension reusing the LSTM hook): the product module draws
+    its masks and weights in the same order as the oracle restatement."""
+    import configparser
+    import numpy as np
+    import torch
+    import pkc.neural_networks as NN
+    from oracle import nets as ON
+    from cases import LIGRU_DEF
+    cp = configparser.ConfigParser()
+    cp["s"] = dict(LIGRU_DEF, ligru_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
+                   hcgsh_block="8,4", hcgsh_sparse="25,50")
+    sds = []
+    for cls in (NN.liGRU, ON.liGRU):
+        torch.manual_seed(9)
+        np.random.seed(9)
+        sds.append(cls(cp["s"], 20).state_dict())
+    assert sds[0].keys() == sds[1].keys()
+    assert any("hcgsx" in k for k in sds[0])
+    for k in sds[0]:
+        assert torch.equal(sds[0][k], sds[1][k]), k
