@@ -197,6 +197,14 @@ int pkc_layernorm_bwd(int M, int N, int nslab, const float* dy, int64_t slab_str
                       const float* rowstat, float* dx, float* dgamma, float* dbeta, float* dbias,
                       void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Magnitude pruning (quantized_modules.py:15-28): thr = np.percentile(|W|, perc) (numpy 'linear'),
+ * W *= (|W| > thr) in place; mask (optional) receives the {0,1} mask.  Exact order statistics by
+ * GPU radix select, no host round trip.  work: pkc_prune_work_size() bytes of device memory.
+ * ------------------------------------------------------------------------------------------- */
+int64_t pkc_prune_work_size(void);
+int pkc_prune(float* w, int64_t n, double perc, float* mask, void* work, void* stream);
+
 /* dst (bf16) = src (fp32), n elements (bf16 operand copies for the MFMA matmuls) */
 int pkc_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 

@@ -77,6 +77,8 @@ OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM = 0, 1, 2, 3
 
 
 _SIGS = {
+    "pkc_prune_work_size": (i64, []),
+    "pkc_prune": (C.c_int, [vp, i64, C.c_double, vp, vp, vp]),
     "pkc_layernorm_fwd": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_float, vp, vp,
                                     vp, vp]),
     "pkc_layernorm_bwd": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp, vp,

@@ -311,6 +311,10 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
 
     if to_do == "train" and ws_eff > 1:
         DP.average_buffers(list(nns.values()))
+    if to_do == "train" and if_prune:             # chunk-end pruning (core.py:291-296)
+        for net in nns.values():
+            if getattr(net, "prune", False):
+                net.prune_parameters()
     if rank == 0:
         if to_do == "train":
             for net_name, net in nns.items():

@@ -535,16 +535,49 @@ class Engine:
                     self.node_opt[nd] = self._chunk_map(idx) + (idx,)
             self.opt_desc = torch.zeros(n * C.sizeof(L.OptTensor), dtype=torch.uint8, device=self.dev)
             self._upload_opt_desc(step_inc=1)
+        # magnitude pruning (quantized_modules.py:15-28): recomputed from |W| before every
+        # forward, after the HCGS / pattern masks (neural_networks.py:256-278, 858-896)
+        self.prune_list = []
+        for n_ in self.nodes:
+            if n_.rec:
+                for li, sp in enumerate(n_.layers):
+                    if sp.get("prune") is not None:
+                        for p in list(sp["W"]) + list(sp["U"]):
+                            self.prune_list.append((p, float(sp["prune"])) + n_.quant_of(p))
+            elif n_.W is not None and n_.spec.get("prune") is not None:
+                self.prune_list.append((n_.W, float(n_.spec["prune"])) + n_.quant_of(n_.W))
+        self.prune_work = (torch.zeros(L.lib().pkc_prune_work_size(), dtype=torch.uint8,
+                                       device=self.dev) if self.prune_list else None)
+        pruned = {id(t[0]) for t in self.prune_list}
         # the reference multiplies the masks in (and QuantizeLinear clamps W to [-1, 1]) before
         # the first forward; do it once here, then fake-quantise the copy the GEMMs multiply with
         s = self._stream()
         for n_ in self.nodes:
             for p, key, m in n_.params():
                 q, qb = n_.quant_of(p)
+                if id(p) in pruned:
+                    if m is not None:
+                        call("pkc_apply_mask", ptr(p), ptr(m), p.numel(), C.c_float(0.0), s)
+                    call("pkc_prune", ptr(p), p.numel(), C.c_double(self._perc(p)), None,
+                         ptr(self.prune_work), s)
+                    m = None
                 if m is not None or qb:
                     call("pkc_apply_mask", ptr(p), ptr(m), p.numel(), C.c_float(1.0 if qb else 0.0), s)
                 if qb:
                     call("pkc_fakequant_weight", ptr(p), ptr(q), p.numel(), qb, s)
+
+    def _perc(self, p):
+        return next(t[1] for t in self.prune_list if t[0] is p)
+
+    def _prune_kernels(self, s):
+        """After the optimizer: each pruned weight re-thresholded at its percentile (and its
+        fake-quantised copy refreshed)."""
+        for p, perc, q, qb in self.prune_list:
+            self._k("prune %d" % p.numel(), 0, 4.0 * p.numel() * 7, "pkc_prune", ptr(p), p.numel(),
+                    C.c_double(perc), None, ptr(self.prune_work), s)
+            if qb:
+                self._k("fakequant_weight", 0, 8.0 * p.numel(), "pkc_fakequant_weight", ptr(p),
+                        ptr(q), p.numel(), qb, s)
 
     def _chunk_map(self, idx):
         """(n_chunks, device map) of pkc_optim_step work items over the entries idx (tensor ids
@@ -1103,10 +1136,12 @@ class Engine:
             return
         if spread_opt:
             self._gemms(self.spread_tail, s)
+            self._prune_kernels(s)
             return
         nparam = sum(e["p"].numel() for e in self.opt_entries)
         self._k("optim_step", 0, 4.0 * nparam * 5, "pkc_optim_step", ptr(self.opt_desc),
                 len(self.opt_entries), ptr(self.opt_map), self.opt_nchunks, s)
+        self._prune_kernels(s)
 
     def _train_step_kernels(self, allreduce=None, batch=None):
         s = self._stream()
@@ -1357,14 +1392,28 @@ class ModuleRunner:
                 b["qwork"] = _f32(256, self.dev)
             self.bufs.append(b)
             K = N
-        self.refresh()
+        self.prune_work = None
+        self.prunes = any(sp.get("prune") is not None for sp in self.specs)
+        if not self.prunes:          # else refreshed (pruned) at the top of every run()
+            self.refresh()
 
     def refresh(self):
         """Re-apply HCGS masks / the QuantizeLinear clamp and re-quantise (after weights change)."""
         s = Engine._stream()
         for sp, b in zip(self.specs, self.bufs):
             qb = int(sp["quant"] or 0)
-            if sp["mask"] is not None or qb:
+            if sp.get("prune") is not None:      # mask, then prune (neural_networks.py:256-278)
+                if sp["mask"] is not None:
+                    call("pkc_apply_mask", ptr(sp["W"]), ptr(sp["mask"]), sp["W"].numel(),
+                         C.c_float(0.0), s)
+                if self.prune_work is None:
+                    self.prune_work = torch.zeros(L.lib().pkc_prune_work_size(), dtype=torch.uint8,
+                                                  device=self.dev)
+                call("pkc_prune", ptr(sp["W"]), sp["W"].numel(), C.c_double(float(sp["prune"])), None,
+                     ptr(self.prune_work), s)
+                if qb:
+                    call("pkc_apply_mask", ptr(sp["W"]), None, sp["W"].numel(), C.c_float(1.0), s)
+            elif sp["mask"] is not None or qb:
                 call("pkc_apply_mask", ptr(sp["W"]), ptr(sp["mask"]), sp["W"].numel(),
                      C.c_float(1.0 if qb else 0.0), s)
             if qb:
@@ -1375,6 +1424,8 @@ class ModuleRunner:
         With input quantisation on the first layer, self.input_version holds the address of the
         quantised input (the value the reference leaves in the caller's tensor)."""
         assert M <= self.rows
+        if self.prunes:              # the reference re-prunes on every forward call
+            self.refresh()
         s = Engine._stream()
         cur, cld = x_ptr, ld
         self.input_version = None

@@ -45,6 +45,17 @@ class LayerNorm(nn.Module):
         self.eps = eps
 
 
+def _prune_params(params, perc):
+    """quantized_modules.prune + W.mul_(mask) on each parameter, on the GPU (pkc_prune)."""
+    import ctypes as C
+    from . import _lib as L
+    work = torch.zeros(L.lib().pkc_prune_work_size(), dtype=torch.uint8, device=params[0].device)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for p in params:
+        L.call("pkc_prune", L.ptr(p.data), p.numel(), C.c_double(perc), None, L.ptr(work), s)
+    torch.cuda.synchronize()
+
+
 class _Mask(nn.Module):
     """HCGS.HCGS: a non-learnable ``mask`` Parameter of shape (out, in) (HCGS.py:24-28)."""
 
@@ -133,8 +144,10 @@ class MLP(nn.Module):
 
     # --------------------------------------------------------------------- reference hooks
     def prune_parameters(self):
-        raise NotImplementedError("magnitude pruning (quantized_modules.prune) is not on the "
-                                  "pkc MLP path yet")
+        """Chunk-end pruning (neural_networks.py:321-327, called at core.py:291-296): every
+        layer's W pruned at prune_perc[0] (the reference uses the first entry for all layers)."""
+        _prune_params([self.wx[i].weight for i in range(len(self.dnn_lay))], self.prune_perc[0])
+        return 1
 
     def apply_ghcgs(self):
         raise NotImplementedError("guided HCGS is outside the pkc hot path")
@@ -151,7 +164,8 @@ class MLP(nn.Module):
                               mask=self.hcgs[i].mask if self.mlp_hcgs else None,
                               quant=self.param_quant[i] if self.mlp_quant else 0,
                               inp_quant=self.inp_quant[0] if (self.mlp_quant and self.mlp_quant_inp) else 0,
-                              ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta))
+                              ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta,
+                              prune=self.prune_perc[i] if self.prune else None))
         return specs
 
     def input_norm_specs(self):
@@ -166,8 +180,8 @@ class MLP(nn.Module):
         return out
 
     def check_supported(self):
-        if self.prune or self.if_pattern:
-            raise NotImplementedError("pruned / pattern MLP layers are not on the pkc MLP path yet")
+        if self.if_pattern:
+            raise NotImplementedError("pattern MLP layers are not on the pkc MLP path yet")
 
     def forward(self, x):
         """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
@@ -357,7 +371,11 @@ class LSTM(nn.Module):
         self.out_dim = cur
 
     def prune_parameters(self):
-        raise NotImplementedError("LSTM magnitude pruning is not on the pkc path yet")
+        """Chunk-end pruning (neural_networks.py:1114-1135): every gate W and U at prune_perc[0]."""
+        _prune_params([getattr(self, "%s" % nm)[i].weight for i in range(len(self.lstm_lay))
+                       for nm in ("wfx", "wix", "wox", "wcx", "ufh", "uih", "uoh", "uch")],
+                      self.prune_perc[0])
+        return 1
 
     def apply_ghcgs(self):
         raise NotImplementedError("guided HCGS is outside the pkc hot path")
@@ -365,8 +383,6 @@ class LSTM(nn.Module):
     def check_supported(self):
         if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp or any(self.lstm_use_laynorm):
             raise NotImplementedError("LayerNorm / input normalisation in LSTM is not on the pkc path yet")
-        if self.prune:
-            raise NotImplementedError("LSTM magnitude pruning is not on the pkc path yet")
         if self.if_pattern and self.pattern_kernels is None:
             raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option or "
                                       "patterns injected by run_nn)")
@@ -400,5 +416,6 @@ class LSTM(nn.Module):
                               Umask=self.hcgsh[i].mask if self.lstm_hcgs else None,
                               qbits=self.param_quant[i] if self.lstm_quant else 0,
                               ibits=self.inp_quant[0] if (self.lstm_quant and self.lstm_quant_inp) else 0,
+                              prune=self.prune_perc[i] if self.prune else None,
                               pattern=bool(self.if_pattern)))
         return specs

@@ -342,3 +342,24 @@ def test_context_window_chunk_prep(L, L_, R_):
     np.testing.assert_allclose(ch.feats.cpu().numpy(), ref[:, :C_].astype(np.float32), rtol=1e-6,
                                atol=1e-6)
     np.testing.assert_array_equal(ch.labels.cpu().numpy(), ref[:, C_:].astype(np.int32))
+
+
+@pytest.mark.parametrize("shape,perc,zeros", [((1024, 440), 70.0, 0.0), ((64, 64), 50.0, 0.5),
+                                              ((33, 17), 12.5, 0.0), ((128, 96), 99.9, 0.3),
+                                              ((40, 40), 0.0, 0.0), ((40, 40), 100.0, 0.0)])
+def test_prune_matches_numpy_percentile(L, shape, perc, zeros):
+    """pkc_prune == quantized_modules.prune (np.percentile 'linear' + strict >) bit for bit,
+    including matrices that are partly zero (HCGS-masked) and the 0 / 100 edges."""
+    from oracle.masks import prune_mask
+    g = torch.Generator().manual_seed(int(perc * 10) + shape[0])
+    w = torch.randn(*shape, generator=g)
+    if zeros:
+        w = w * (torch.rand(*shape, generator=g) > zeros).float()
+    ref_mask = prune_mask(w, perc)
+    wd = w.to(DEV).contiguous()
+    mask = torch.full(shape, 7.0, device=DEV)
+    work = torch.zeros(L.lib().pkc_prune_work_size(), dtype=torch.uint8, device=DEV)
+    L.call("pkc_prune", L.ptr(wd), w.numel(), C.c_double(perc), L.ptr(mask), L.ptr(work), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(mask.cpu(), ref_mask)
+    assert torch.equal(wd.cpu(), w * ref_mask)

@@ -213,3 +213,63 @@ def test_engine_graph_replay_equals_eager():
     assert res[0][0] == pytest.approx(res[1][0], rel=1e-6)
     for k in res[0][1]:
         torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=0, atol=0)
+
+
+def test_engine_prune_vs_oracle():
+    """mlp_prune: every forward re-thresholds |W| at np.percentile(prune_perc[i]) and zeroes the
+    rest (neural_networks.py:276-278) — combined with HCGS masks on the body; 3 steps vs the oracle."""
+    from oracle import nets as ON
+    from oracle import run as OR
+    from oracle.masks import prune_mask
+    from pkc.engine import Engine, parse_model
+    cfg = build_mlp_config("hcgs")
+    cfg["architecture1"]["mlp_prune"] = "True"
+    cfg["architecture1"]["mlp_prune_perc"] = "70,55"
+    cfg["architecture2"].update(mlp_prune="True", mlp_prune_perc="30")
+    dims = (("architecture1", 40), ("architecture2", 32), ("architecture3", 32))
+    nets, opts = build_nets(cfg, dims)
+    onets, _ = build_nets(cfg, dims, cls=ON.MLP)
+    for a in nets:
+        onets[a].load_state_dict(nets[a].state_dict())
+        nets[a].to(DEV).train()
+        onets[a].train()
+    B, steps = 16, 3
+    rs = np.random.RandomState(11)
+    X = rs.randn(B * steps, 40).astype(np.float32)
+    lab = np.stack([rs.randint(0, 96, B * steps), rs.randint(0, 8, B * steps)], 1).astype(np.int32)
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 40)},
+                 ["lab_cd", "lab_mono"], batch=B, seed=1)
+    eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), B * steps)
+    ooptim = {a: ON.make_optimizer(onets[a].parameters(), cfg[s]) for s, a in
+              zip(("architecture1", "architecture2", "architecture3"), nets)}
+    lines = OR.parse_model(cfg["model"]["model"])
+    for s in range(steps):
+        inp = torch.from_numpy(np.concatenate([X[s * B:(s + 1) * B],
+                                               lab[s * B:(s + 1) * B].astype(np.float32)], 1))
+        outs = OR.train_step(lines, onets, ooptim, {a: False for a in nets}, {"fmllr": (0, 40)},
+                             {"lab_cd": 40, "lab_mono": 41}, inp)
+        eng.train_step()
+        loss, err = eng.loss_values()
+        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-5)
+        np.testing.assert_allclose(err, outs["err_final"].item())
+        head = [l for l in eng.layers if l.arch == "MLP_layers2"][0]
+        post = head.out.view(B, -1).cpu()
+        ref = outs["out_dnn2"].detach()
+        rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
+        assert rel < 1e-4, "step %d posterior max rel err %.3g" % (s, rel)
+    eng.sync_state()
+    percs = {"MLP_layers1": (70.0, 55.0), "MLP_layers2": (30.0,)}
+    for a in nets:
+        sd_o = onets[a].state_dict()
+        for k, v in nets[a].state_dict().items():
+            ref = sd_o[k]
+            if k.startswith("wx.") and k.endswith("weight"):
+                i = int(k.split(".")[1])
+                mk = "hcgs.%d.mask" % i
+                if mk in sd_o:           # re-masked + re-pruned at the reference's next forward
+                    ref = ref * sd_o[mk]
+                if a in percs:
+                    ref = ref * prune_mask(ref, percs[a][i])
+                    assert float((v == 0).float().mean()) >= percs[a][i] / 100 - 0.01
+            np.testing.assert_allclose(v.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-6,
+                                       err_msg="%s %s" % (a, k))

@@ -27,6 +27,9 @@ def make_cfg(body):
         cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2",
                          ligru_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
                          hcgsh_block="8,4", hcgsh_sparse="25,50", **opt)
+    elif body == "lstm_prune":     # magnitude pruning every forward (neural_networks.py:886-1005)
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", lstm_prune="True", lstm_prune_perc="60,40", **opt)
     else:
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", **opt)
@@ -42,7 +45,7 @@ def make_cfg(body):
     return cfg
 
 
-@pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir"])
+@pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -58,7 +61,8 @@ def test_seq_engine_vs_oracle(body):
             inp = nets["rnn"].out_dim
         torch.manual_seed(3)
         np.random.seed(3)
-        cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM"}[body]
+        cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM",
+                "lstm_prune": "LSTM"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
@@ -121,5 +125,9 @@ def test_seq_engine_vs_oracle(body):
             if body == "ligru_hcgs" and name.endswith("weight") and parts[0] in ("wh", "wz", "uh", "uz"):
                 mk = ("hcgsx" if parts[0][0] == "w" else "hcgsh") + ".%s.mask" % parts[1]
                 ref = ref * sd_o[mk].double()
+            if body == "lstm_prune" and name.endswith("weight") and len(parts[0]) == 3 and k == "rnn":
+                from oracle.masks import prune_mask
+                perc = (60.0, 40.0)[int(parts[1])]
+                ref = ref * prune_mask(sd_o[name], perc).double()
             d = (v.cpu().double() - ref).norm().item()
             assert d <= 1e-3 * ref.norm().item() + 1e-7, "%s %s %.3g" % (k, name, d)
