@@ -135,6 +135,19 @@ class MLP(nn.Module):
             lin.bias = nn.Parameter(torch.zeros(n))
             cur = n
         self.out_dim = cur
+        self.if_pattern = _b(o["if_pattern"]) if "if_pattern" in o else False
+        self.pattern_kernels = None
+        self.pattern_masks = None
+
+    def _pattern_update(self):
+        """neural_networks.py:263-272, 350-361: masks computed once (at the first layer call) from
+        |W| of every layer, then every layer's W multiplied by its mask on every layer call."""
+        if self.pattern_masks is None:
+            self.pattern_masks = [torch.from_numpy(M.apply_patterns(self.wx[i].weight.data.numpy(),
+                                                                    self.pattern_kernels))
+                                  for i in range(len(self.lay))]
+        for i in range(len(self.lay)):
+            self.wx[i].weight.data.mul_(self.pattern_masks[i])
 
     def forward(self, x, drop_masks=None):
         if self.ln_inp:
@@ -145,6 +158,8 @@ class MLP(nn.Module):
             w = self.wx[i].weight
             if self.hcgs_on:
                 w.data.mul_(self.hcgs[i].mask.data)
+            if self.if_pattern:
+                self._pattern_update()
             if self.prune:
                 w.data.mul_(M.prune_mask(w, self.prune_perc[i]))
             z = self.wx[i](x)

@@ -206,6 +206,11 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         if pt != "none":
             ck = torch.load(pt, map_location="cuda", weights_only=True)
             nns[net_name].load_state_dict(ck["model_par"])
+        if getattr(nns[net_name], "prune", False) and if_prune:       # core.py:122-127
+            nns[net_name].prune_parameters()
+        if net_name in patterns:          # pattern sets / masks carried between chunks (129-131)
+            nns[net_name].pattern = patterns[net_name]
+            nns[net_name].pattern_mask = pattern_masks[net_name]
     seq_model = any(arch_dict[a][2] for a in arch_dict)
     lines = parse_model(config["model"]["model"])
     arch_opts = {a: config[arch_dict[a][0]] for a in nns}
@@ -315,6 +320,11 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         for net in nns.values():
             if getattr(net, "prune", False):
                 net.prune_parameters()
+    if to_do == "train":
+        for net_name, net in nns.items():
+            if getattr(net, "if_pattern", False):                    # core.py:304-306
+                patterns[net_name] = net.pattern
+                pattern_masks[net_name] = net.pattern_mask
     if rank == 0:
         if to_do == "train":
             for net_name, net in nns.items():

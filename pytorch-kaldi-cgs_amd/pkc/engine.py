@@ -181,6 +181,71 @@ class RecNode:
         return q[0] if q is not None else p
 
 
+def pattern_effective_masks(net, s):
+    """Pattern masks (neural_networks.py:263-272, 876-884; sparsity.py:1112-1146) of one
+    architecture: computed once, at the first layer call, from |W| of every pattern-masked weight —
+    layer 0's input weights already multiplied by their HCGS mask, every other weight raw — and
+    then multiplied into all of them once per layer call (L times per forward; {0,1} except on
+    tied tiles).  Masks already held in ``net.pattern_mask`` (carried between chunks by run_nn,
+    core.py:129-131, 304-306) are reused, as the reference does; new ones are stored there in the
+    reference's structure.  Returns {id(param): HCGS x pattern^L effective mask}."""
+    if not getattr(net, "if_pattern", False):
+        return {}
+    pk = net.pattern_kernels
+    if pk is None:
+        raise NotImplementedError("%s: pattern masks need a pattern set" % net.arch_name)
+    P, ph, pw = pk.shape
+    dev = next(net.parameters()).device
+    pat = torch.from_numpy(np.ascontiguousarray(pk, dtype=np.float32)).to(dev)
+    entries = net.pattern_params()
+    nl = 1 + max(e[1] for e in entries)
+    store = net.pattern_mask
+    have = all(_pm_get(store, key) is not None for key, _, _, _ in entries)
+    out = {}
+    for key, li, p, hmask in entries:
+        rows, cols = p.shape
+        if rows % ph or cols % pw:
+            raise NotImplementedError("%s: %dx%d weight not tiled by %dx%d patterns"
+                                      % (net.arch_name, rows, cols, ph, pw))
+        if have:
+            pm = _pm_get(store, key).to(dev, torch.float32).contiguous()
+        else:
+            pre = li == 0 and hmask is not None and _is_input_weight(key)
+            src = (p * hmask if pre else p).contiguous()
+            pm = torch.empty_like(p)
+            call("pkc_pattern_mask", ptr(src), rows, cols, ptr(pat), P, ph, pw, ptr(pm), s)
+            _pm_set(store, key, pm)
+        e = pm.pow(nl) if nl > 1 else pm.clone()
+        out[id(p)] = e * hmask if hmask is not None else e
+    if not have:
+        kern = pat.view(P, 1, ph, pw)
+        if isinstance(net.pattern, list):
+            net.pattern[:] = [kern] * nl
+        else:
+            for k in net.pattern:
+                net.pattern[k] = [kern] * nl
+    return out
+
+
+def _is_input_weight(key):
+    name, _ = key
+    return name is None or name.startswith("pattern_mask_w")
+
+
+def _pm_get(store, key):
+    name, i = key
+    lst = store if name is None else store.get(name, [])
+    return lst[i] if i < len(lst) else None
+
+
+def _pm_set(store, key, v):
+    name, i = key
+    lst = store if name is None else store.setdefault(name, [])
+    while len(lst) <= i:
+        lst.append(None)
+    lst[i] = v
+
+
 class Engine:
     """Training / validation executor of a [model] graph.
 
@@ -461,36 +526,19 @@ class Engine:
         n.out = n.lbuf[-1]["y"]
 
     def _build_masks(self):
-        """Pattern masks (neural_networks.py:876-884, sparsity.py:1112-1146): computed once, at the
-        first forward, from |W| of every layer's gate weights — W_0 already multiplied by its HCGS
-        mask, the other layers' W and every U raw — and then multiplied into W / U once per layer
-        call (L times per forward; the masks are {0,1} except on tied tiles).  Folded here with the
-        HCGS masks into one effective mask per parameter that the optimizer epilogue applies."""
+        """Pattern masks folded with the HCGS masks into one effective mask per parameter that the
+        optimizer epilogue applies (see pattern_effective_masks)."""
+        eff = {}
+        for net in self.nets.values():
+            eff.update(pattern_effective_masks(net, self._stream()))
         for n in self.nodes:
-            if not n.rec or not any(sp.get("pattern") for sp in n.layers):
-                continue
-            pk = n.net.pattern_kernels
-            P, ph, pw = pk.shape
-            pat = torch.from_numpy(np.ascontiguousarray(pk, dtype=np.float32)).to(self.dev)
-            nl = len(n.layers)
-            s = self._stream()
-            for li, sp in enumerate(n.layers):
-                for kind, hmask in (("W", sp["Wmask"]), ("U", sp["Umask"])):
-                    for g in range(n.G):
-                        p = sp[kind][g]
-                        src = p
-                        if kind == "W" and li == 0 and hmask is not None:
-                            src = p * hmask
-                        src = src.contiguous()
-                        rows, cols = p.shape
-                        if rows % ph or cols % pw:
-                            raise NotImplementedError("%s: %dx%d weight not tiled by %dx%d patterns"
-                                                      % (n.name, rows, cols, ph, pw))
-                        pm = torch.empty_like(p)
-                        call("pkc_pattern_mask", ptr(src), rows, cols, ptr(pat), P, ph, pw, ptr(pm), s)
-                        if nl > 1:
-                            pm = pm.pow(nl)
-                        n.emask[id(p)] = pm * hmask if hmask is not None else pm
+            if n.rec:
+                for li, sp in enumerate(n.layers):
+                    for p in list(sp["W"]) + list(sp["U"]):
+                        if id(p) in eff:
+                            n.emask[id(p)] = eff[id(p)]
+            elif n.W is not None and id(n.W) in eff:
+                n.mask = eff[id(n.W)]
 
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
@@ -1393,8 +1441,10 @@ class ModuleRunner:
             self.bufs.append(b)
             K = N
         self.prune_work = None
-        self.prunes = any(sp.get("prune") is not None for sp in self.specs)
-        if not self.prunes:          # else refreshed (pruned) at the top of every run()
+        self.eff = pattern_effective_masks(net, Engine._stream())
+        # the reference re-prunes / re-applies pattern^L on every forward call
+        self.prunes = any(sp.get("prune") is not None for sp in self.specs) or bool(self.eff)
+        if not self.prunes:          # else refreshed at the top of every run()
             self.refresh()
 
     def refresh(self):
@@ -1402,9 +1452,10 @@ class ModuleRunner:
         s = Engine._stream()
         for sp, b in zip(self.specs, self.bufs):
             qb = int(sp["quant"] or 0)
+            mask = self.eff.get(id(sp["W"]), sp["mask"])
             if sp.get("prune") is not None:      # mask, then prune (neural_networks.py:256-278)
-                if sp["mask"] is not None:
-                    call("pkc_apply_mask", ptr(sp["W"]), ptr(sp["mask"]), sp["W"].numel(),
+                if mask is not None:
+                    call("pkc_apply_mask", ptr(sp["W"]), ptr(mask), sp["W"].numel(),
                          C.c_float(0.0), s)
                 if self.prune_work is None:
                     self.prune_work = torch.zeros(L.lib().pkc_prune_work_size(), dtype=torch.uint8,
@@ -1413,8 +1464,8 @@ class ModuleRunner:
                      ptr(self.prune_work), s)
                 if qb:
                     call("pkc_apply_mask", ptr(sp["W"]), None, sp["W"].numel(), C.c_float(1.0), s)
-            elif sp["mask"] is not None or qb:
-                call("pkc_apply_mask", ptr(sp["W"]), ptr(sp["mask"]), sp["W"].numel(),
+            elif mask is not None or qb:
+                call("pkc_apply_mask", ptr(sp["W"]), ptr(mask), sp["W"].numel(),
                      C.c_float(1.0 if qb else 0.0), s)
             if qb:
                 call("pkc_fakequant_weight", ptr(sp["W"]), ptr(b["Wq"]), sp["W"].numel(), qb, s)
@@ -1424,7 +1475,7 @@ class ModuleRunner:
         With input quantisation on the first layer, self.input_version holds the address of the
         quantised input (the value the reference leaves in the caller's tensor)."""
         assert M <= self.rows
-        if self.prunes:              # the reference re-prunes on every forward call
+        if self.prunes:
             self.refresh()
         s = Engine._stream()
         cur, cld = x_ptr, ld

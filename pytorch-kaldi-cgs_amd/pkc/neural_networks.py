@@ -56,6 +56,41 @@ def _prune_params(params, perc):
     torch.cuda.synchronize()
 
 
+class _PatternSet:
+    """Pattern-set plumbing shared by MLP and LSTM (neural_networks.py:115-131, 513-529).
+    The reference searches the set with sklearn KMeans (sparsity.py:999-1049, no random_state:
+    parity unpinned); pkc takes it from ``pattern_from_file`` / ``pattern_file`` (an (P*ph, pw)
+    .npy such as pattern_file/b08b08_k04_n16_pattern.npy), from ``pattern_kernels = ...``, or
+    from the ``patterns`` dict run_nn carries between chunks (core.py:129-131, 304-306)."""
+
+    def _pattern_opts(self, o):
+        self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
+        self.pattern_shape = _lst(o, "pattern_shape", int) if "pattern_shape" in o else [8, 8]
+        self.pattern_from_file = o.get("pattern_from_file", o.get("pattern_file", None))
+
+    @property
+    def pattern_kernels(self):
+        """(P, ph, pw) float32 pattern set, or None."""
+        k = getattr(self, "_pattern_kernels", None)
+        if k is None and self.if_pattern:
+            pat = self.pattern
+            first = (pat[0] if isinstance(pat, list) and pat else
+                     next((v[0] for v in pat.values() if v), None) if isinstance(pat, dict) else None)
+            if first is not None:                   # (P, 1, ph, pw) kernel, as the reference keeps
+                t = first.detach().cpu().numpy() if torch.is_tensor(first) else np.asarray(first)
+                k = t.reshape(t.shape[0], t.shape[-2], t.shape[-1]).astype(np.float32)
+            elif self.pattern_from_file:
+                arr = np.load(self.pattern_from_file, allow_pickle=False).astype(np.float32)
+                ph, pw = self.pattern_shape
+                k = arr.reshape(-1, ph, pw)
+            self._pattern_kernels = k
+        return k
+
+    @pattern_kernels.setter
+    def pattern_kernels(self, v):
+        self._pattern_kernels = None if v is None else np.asarray(v, dtype=np.float32)
+
+
 class _Mask(nn.Module):
     """HCGS.HCGS: a non-learnable ``mask`` Parameter of shape (out, in) (HCGS.py:24-28)."""
 
@@ -79,7 +114,7 @@ class _QLinear(nn.Module):
         self.inp_quant = inp_bits
 
 
-class MLP(nn.Module):
+class MLP(_PatternSet, nn.Module):
     """neural_networks.py:81-361 (options per proto/MLP.proto + the CGS keys)."""
 
     seq_model = False
@@ -108,11 +143,11 @@ class MLP(nn.Module):
         self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
         self.guided_hcgs = strtobool(o.get("guided_hcgs", "False"))
         self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
-        self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
+        self._pattern_opts(o)
         self.arch_name = o.get("arch_name", "MLP")
         if self.guided_hcgs:
             raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
-        if self.if_pattern:
+        if self.if_pattern:                  # per-layer kernels / masks (neural_networks.py:159-161)
             self.pattern, self.pattern_mask = [], []
 
         if self.mlp_hcgs:                    # registered first, as neural_networks.py:151-152
@@ -165,8 +200,14 @@ class MLP(nn.Module):
                               quant=self.param_quant[i] if self.mlp_quant else 0,
                               inp_quant=self.inp_quant[0] if (self.mlp_quant and self.mlp_quant_inp) else 0,
                               ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta,
-                              prune=self.prune_perc[i] if self.prune else None))
+                              prune=self.prune_perc[i] if self.prune else None,
+                              pattern=bool(self.if_pattern)))
         return specs
+
+    def pattern_params(self):
+        """[(store key, layer, W, HCGS mask)] in the reference's update_mask order."""
+        return [((None, i), i, self.wx[i].weight, self.hcgs[i].mask if self.mlp_hcgs else None)
+                for i in range(len(self.dnn_lay))]
 
     def input_norm_specs(self):
         """Input normalisations in the reference's order: ln0 then bn0 (neural_networks.py:246-251)."""
@@ -180,8 +221,9 @@ class MLP(nn.Module):
         return out
 
     def check_supported(self):
-        if self.if_pattern:
-            raise NotImplementedError("pattern MLP layers are not on the pkc MLP path yet")
+        if self.if_pattern and self.pattern_kernels is None:
+            raise NotImplementedError("pattern MLP needs a pattern set (pattern_from_file option, "
+                                      "pattern_kernels, or patterns injected by run_nn)")
 
     def forward(self, x):
         """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
@@ -277,7 +319,7 @@ class liGRU(nn.Module):
         return specs
 
 
-class LSTM(nn.Module):
+class LSTM(_PatternSet, nn.Module):
     """neural_networks.py:468-1237.  The reference forces bidir off inside forward (:835), so a
     bidirectional cfg crashes there on layer 2; pkc runs bidirectional LSTMs with the liGRU
     shared-weight convention (BASELINE C4) and uni-directional ones exactly as the reference."""
@@ -314,9 +356,7 @@ class LSTM(nn.Module):
         self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
         self.guided_hcgs = strtobool(o.get("guided_hcgs", "False"))
         self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
-        self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
-        self.pattern_shape = _lst(o, "pattern_shape", int) if "pattern_shape" in o else [8, 8]
-        self.pattern_from_file = o.get("pattern_file", None)
+        self._pattern_opts(o)
         self.arch_name = o.get("arch_name", "LSTM")
         if self.guided_hcgs:
             raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
@@ -325,7 +365,8 @@ class LSTM(nn.Module):
         if self.if_pattern:
             self.pattern = {k: [] for k in ("pattern_w%sx" % g for g in self.GATES)}
             self.pattern.update({k: [] for k in ("pattern_u%sh" % g for g in self.GATES)})
-            self.pattern_mask = {}
+            self.pattern_mask = {k: [] for k in ("pattern_mask_w%sx" % g for g in self.GATES)}
+            self.pattern_mask.update({k: [] for k in ("pattern_mask_u%sh" % g for g in self.GATES)})
         for g in self.GATES:
             setattr(self, "w%sx" % g, nn.ModuleList())
             setattr(self, "u%sh" % g, nn.ModuleList())
@@ -387,21 +428,16 @@ class LSTM(nn.Module):
             raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option or "
                                       "patterns injected by run_nn)")
 
-    @property
-    def pattern_kernels(self):
-        """(P, ph, pw) pattern set: run_nn-injected, or loaded from the ``pattern_file`` option
-        (e.g. pattern_file/b08b08_k04_n16_pattern.npy, shape (P*ph, pw))."""
-        k = getattr(self, "_pattern_kernels", None)
-        if k is None and getattr(self, "pattern_from_file", None):
-            arr = np.load(self.pattern_from_file, allow_pickle=False).astype(np.float32)
-            ph, pw = self.pattern_shape
-            k = arr.reshape(-1, ph, pw)
-            self._pattern_kernels = k
-        return k
-
-    @pattern_kernels.setter
-    def pattern_kernels(self, v):
-        self._pattern_kernels = None if v is None else np.asarray(v, dtype=np.float32)
+    def pattern_params(self):
+        """[(store key, layer, W or U, HCGS mask)] in the reference's update_mask order
+        (neural_networks.py:1202-1223)."""
+        out = []
+        for i in range(len(self.lstm_lay)):
+            for nm, msk in [("w%sx" % g, "hcgsx") for g in self.GATES] + \
+                           [("u%sh" % g, "hcgsh") for g in self.GATES]:
+                m = getattr(self, msk)[i].mask if self.lstm_hcgs else None
+                out.append((("pattern_mask_" + nm, i), i, getattr(self, nm)[i].weight, m))
+        return out
 
     def layer_specs(self):
         specs = []

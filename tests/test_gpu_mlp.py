@@ -215,21 +215,34 @@ def test_engine_graph_replay_equals_eager():
         torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=0, atol=0)
 
 
-def test_engine_prune_vs_oracle():
-    """mlp_prune: every forward re-thresholds |W| at np.percentile(prune_perc[i]) and zeroes the
-    rest (neural_networks.py:276-278) — combined with HCGS masks on the body; 3 steps vs the oracle."""
+@pytest.mark.parametrize("variant", ["prune", "pattern"])
+def test_engine_sparsity_vs_oracle(variant):
+    """prune: every forward re-thresholds |W| at np.percentile(prune_perc[i]) and zeroes the rest
+    (neural_networks.py:276-278); pattern: 8x8/k4/n16 pattern masks from the pattern_file set,
+    computed at the first layer call and multiplied in once per layer call (263-272, 339-361).
+    Both on top of HCGS masks on the body; 3 training steps vs the oracle."""
     from oracle import nets as ON
     from oracle import run as OR
     from oracle.masks import prune_mask
     from pkc.engine import Engine, parse_model
     cfg = build_mlp_config("hcgs")
-    cfg["architecture1"]["mlp_prune"] = "True"
-    cfg["architecture1"]["mlp_prune_perc"] = "70,55"
-    cfg["architecture2"].update(mlp_prune="True", mlp_prune_perc="30")
+    pset = None
+    if variant == "prune":
+        cfg["architecture1"]["mlp_prune"] = "True"
+        cfg["architecture1"]["mlp_prune_perc"] = "70,55"
+        cfg["architecture2"].update(mlp_prune="True", mlp_prune_perc="30")
+    else:
+        pset = G("quant.npz")["pattern_set"].reshape(16, 8, 8)
+        for sec in ("architecture1", "architecture2"):
+            cfg[sec].update(if_pattern="True", pattern_mode="pattern", pattern_shape="8,8",
+                            pattern_nnz="4,4", pattern_num="16,16")
     dims = (("architecture1", 40), ("architecture2", 32), ("architecture3", 32))
     nets, opts = build_nets(cfg, dims)
     onets, _ = build_nets(cfg, dims, cls=ON.MLP)
     for a in nets:
+        if pset is not None and nets[a].if_pattern:
+            nets[a].pattern_kernels = pset
+            onets[a].pattern_kernels = pset
         onets[a].load_state_dict(nets[a].state_dict())
         nets[a].to(DEV).train()
         onets[a].train()
@@ -258,7 +271,11 @@ def test_engine_prune_vs_oracle():
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
         assert rel < 1e-4, "step %d posterior max rel err %.3g" % (s, rel)
     eng.sync_state()
-    percs = {"MLP_layers1": (70.0, 55.0), "MLP_layers2": (30.0,)}
+    percs = {"MLP_layers1": (70.0, 55.0), "MLP_layers2": (30.0,)} if variant == "prune" else {}
+    if variant == "pattern":         # the engine stored the reference-structured masks
+        for a in ("MLP_layers1", "MLP_layers2"):
+            for pm, opm in zip(nets[a].pattern_mask, onets[a].pattern_masks):
+                np.testing.assert_array_equal(pm.cpu().numpy(), opm.numpy())
     for a in nets:
         sd_o = onets[a].state_dict()
         for k, v in nets[a].state_dict().items():
@@ -268,6 +285,8 @@ def test_engine_prune_vs_oracle():
                 mk = "hcgs.%d.mask" % i
                 if mk in sd_o:           # re-masked + re-pruned at the reference's next forward
                     ref = ref * sd_o[mk]
+                if variant == "pattern" and onets[a].if_pattern:
+                    ref = ref * onets[a].pattern_masks[i] ** len(onets[a].lay)
                 if a in percs:
                     ref = ref * prune_mask(ref, percs[a][i])
                     assert float((v == 0).float().mean()) >= percs[a][i] / 100 - 0.01
