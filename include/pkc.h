@@ -205,6 +205,31 @@ int pkc_layernorm_bwd(int M, int N, int nslab, const float* dy, int64_t slab_str
 int64_t pkc_prune_work_size(void);
 int pkc_prune(float* w, int64_t n, double perc, float* mask, void* work, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * [model] regularisers cost_l1 / cost_l2 / cost_gl (utils.py:24-60, 1954-1991): the loss term
+ * lam * sum of block norms (l1: |.|_1 per parameter; l2: |.|_2 per parameter; gl: |.|_2 per
+ * torch.chunk block) and its gradient.  A block is cut into row-slice items; items of one block are
+ * contiguous and block_start[b]..block_start[b+1] indexes them.
+ *   pkc_reg_partial : partial[i] = sum |x| (L1) or sum x^2 (L2) over item i
+ *   pkc_reg_finalize: coef[b] = lam (L1) or lam / ||block b|| (L2, 0 for a zero block);
+ *                     loss_rows[0..nrows) = lam * sum_b ||block b||  (a pseudo loss head)
+ *   pkc_reg_grad    : g += coef[block] * sign(x) (L1) or coef[block] * x (L2), items with g set
+ * ------------------------------------------------------------------------------------------- */
+enum { PKC_REG_L1 = 1, PKC_REG_L2 = 2 };
+typedef struct pkc_reg_item_s {
+  const float* p;     /* parameter (row-major, leading dimension ld) */
+  float* g;           /* its gradient buffer (NULL: loss term only) */
+  int64_t ld;
+  int r0, r1, c0, c1; /* the item's rectangle */
+  int block;          /* block index */
+} pkc_reg_item;
+int pkc_reg_partial(int kind, const pkc_reg_item* items_dev, int nitems, float* partial,
+                    void* stream);
+int pkc_reg_finalize(int kind, const int32_t* block_start_dev, int nblocks, const float* partial,
+                     float lam, float* coef, float* loss_rows, int nrows, void* stream);
+int pkc_reg_grad(int kind, const pkc_reg_item* items_dev, int nitems, const float* coef,
+                 void* stream);
+
 /* dst (bf16) = src (fp32), n elements (bf16 operand copies for the MFMA matmuls) */
 int pkc_cast_bf16(const float* src, void* dst, int64_t n, void* stream);
 

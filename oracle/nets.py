@@ -92,6 +92,8 @@ class QLinear(nn.Module):
 class MLP(nn.Module):
     def __init__(self, o, inp_dim):
         super().__init__()
+        self.skip_regularization = _b(o.get("skip_regularization", "False"))
+        self.apply_guided_hcgs = _b(o.get("apply_guided_hcgs", "False"))
         self.input_dim = inp_dim
         self.lay = _lst(o, "dnn_lay", int)
         self.dropp = _lst(o, "dnn_drop", float)
@@ -201,6 +203,8 @@ class liGRU(_Rec):
 
     def __init__(self, o, inp_dim):
         super().__init__()
+        self.skip_regularization = _b(o.get("skip_regularization", "False"))
+        self.apply_guided_hcgs = _b(o.get("apply_guided_hcgs", "False"))
         self.lay = _lst(o, "ligru_lay", int)
         self.dropp = _lst(o, "ligru_drop", float)
         self.use_bn = _lst(o, "ligru_use_batchnorm", _b)
@@ -296,6 +300,8 @@ class LSTM(_Rec):
 
     def __init__(self, o, inp_dim):
         super().__init__()
+        self.skip_regularization = _b(o.get("skip_regularization", "False"))
+        self.apply_guided_hcgs = _b(o.get("apply_guided_hcgs", "False"))
         self.lay = _lst(o, "lstm_lay", int)
         self.dropp = _lst(o, "lstm_drop", float)
         self.use_bn = _lst(o, "lstm_use_batchnorm", _b)

@@ -13,8 +13,44 @@ from .nets import nll_err
 _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
 
 
+_PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
+
+
 def parse_model(text):
-    return [list(_PAT.findall(line)[0]) for line in text.split("\n") if line.strip()]
+    """utils.py:1898-1903: out=op(a,b) (greedy: the LAST comma splits); a line whose output name
+    starts with 'loss_gl' is re-read as out=op(a,b,c) and c rides in b as "b,c"."""
+    rows = []
+    for line in text.split("\n"):
+        if not line.strip():
+            continue
+        row = list(_PAT.findall(line)[0])
+        if row[0][:7] == "loss_gl":
+            o, op, a, b, c = _PAT3.findall(line)[0]
+            row = [o, op, a, b + "," + c]
+        rows.append(row)
+    return rows
+
+
+def _reg_norm(nets, op, lam):
+    """utils.py:24-60 (l1_norm / l2_norm / gl_norm) and the guided-HCGS zero (1954-1991)."""
+    first = next(iter(nets.values()))
+    if getattr(first, "apply_guided_hcgs", False):
+        return torch.tensor(0.0)
+    if op == "cost_gl":
+        lam, nblk = lam.split(",")
+    acc = torch.tensor(0.0, dtype=torch.float32)
+    for net in nets.values():
+        for p in net.parameters():
+            if p.dim() > 1 and not net.skip_regularization:
+                if op == "cost_l1":
+                    acc = acc + torch.norm(p, 1)
+                elif op == "cost_l2":
+                    acc = acc + torch.norm(p, 2)
+                else:
+                    for d1 in torch.chunk(p, int(nblk), 1):
+                        for blk in torch.chunk(d1, int(nblk), 0):
+                            acc = acc + torch.norm(blk, 2)
+    return acc * float(lam)
 
 
 def forward_model(lines, nets, seq, fea_cols, lab_cols, inp, max_len=0, batch=0, forward_out=None):
@@ -49,6 +85,8 @@ def forward_model(lines, nets, seq, fea_cols, lab_cols, inp, max_len=0, batch=0,
             outs[out_name] = outs[a] + outs[b]
         elif op == "mult_constant":
             outs[out_name] = outs[a] * float(b)
+        elif op in ("cost_l1", "cost_l2", "cost_gl"):
+            outs[out_name] = _reg_norm(nets, op, b)
         elif op == "concatenate":
             outs[out_name] = torch.cat((outs[a], outs[b]), outs[a].dim() - 1)
         else:

@@ -75,8 +75,18 @@ class GemmProblem(C.Structure):
 
 OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM = 0, 1, 2, 3
 
+REG_L1, REG_L2 = 1, 2
+
+
+class RegItem(C.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("ld", i64), ("r0", C.c_int), ("r1", C.c_int),
+                ("c0", C.c_int), ("c1", C.c_int), ("block", C.c_int)]
+
 
 _SIGS = {
+    "pkc_reg_partial": (C.c_int, [C.c_int, vp, C.c_int, vp, vp]),
+    "pkc_reg_finalize": (C.c_int, [C.c_int, vp, C.c_int, vp, C.c_float, vp, vp, C.c_int, vp]),
+    "pkc_reg_grad": (C.c_int, [C.c_int, vp, C.c_int, vp, vp]),
     "pkc_prune_work_size": (i64, []),
     "pkc_prune": (C.c_int, [vp, i64, C.c_double, vp, vp, vp]),
     "pkc_layernorm_fwd": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_float, vp, vp,

@@ -33,9 +33,55 @@ _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
 MAX_SPLITS = 8
 
 
+_PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
+
+
 def parse_model(text):
-    """utils.py:1888-1903 line grammar: out=op(in1,in2)."""
-    return [list(_PAT.findall(line)[0]) for line in text.split("\n") if line.strip()]
+    """utils.py:1888-1903 line grammar: out=op(in1,in2), split at the LAST comma (greedy); a line
+    whose output name starts with 'loss_gl' is re-read as out=op(in1,in2,in3) (1904-1906), and
+    in3 rides in in2 as "in2,in3"."""
+    rows = []
+    for line in text.split("\n"):
+        if not line.strip():
+            continue
+        row = list(_PAT.findall(line)[0])
+        if row[0][:7] == "loss_gl":
+            o, op, a, b, c = _PAT3.findall(line)[0]
+            row = [o, op, a, b + "," + c]
+        rows.append(row)
+    return rows
+
+
+class RegTerm:
+    """One cost_l1 / cost_l2 / cost_gl line of the [model] (utils.py:24-60): a pseudo loss head
+    whose per-row 'loss' is the regulariser value (pkc_reg_finalize broadcasts it)."""
+    head = False
+
+    def __init__(self, op, lam, nblk, params):
+        self.op, self.lam, self.nblk, self.params = op, float(lam), nblk, params
+        self.kind = L.REG_L1 if op == "cost_l1" else L.REG_L2
+        self.loss_weight = 0.0
+
+    def items(self, grads):
+        """Row-slice items of every block, blocks in parameter order (gl: the torch.chunk grid
+        along dim 1, then dim 0 — utils.py:49-54)."""
+        items, bstart = [], [0]
+        for p in self.params:
+            R, Cc = p.shape[0], int(np.prod(p.shape[1:]))
+            if self.op == "cost_gl":
+                cs, rs = -(-Cc // self.nblk), -(-R // self.nblk)
+                cgrid = [(c, min(c + cs, Cc)) for c in range(0, Cc, cs)]
+                rgrid = [(r, min(r + rs, R)) for r in range(0, R, rs)]
+                rects = [(r0, r1, c0, c1) for c0, c1 in cgrid for r0, r1 in rgrid]
+            else:
+                rects = [(0, R, 0, Cc)]
+            g = grads.get(id(p))
+            for r0, r1, c0, c1 in rects:
+                per = max(1, 4096 // max(1, c1 - c0))
+                for a in range(r0, r1, per):
+                    items.append((p, g, Cc, a, min(a + per, r1), c0, c1, len(bstart) - 1))
+                bstart.append(len(items))
+        return items, bstart
 
 
 def _f32(n, dev):
@@ -286,6 +332,7 @@ class Engine:
         self._alloc()
         self._build_masks()
         self._build_optim()
+        self._build_reg()
         self.graph = None
         self.graph_opt = None
         self.steps_done = 0
@@ -364,13 +411,31 @@ class Engine:
             elif op in ("cost_l1", "cost_l2", "cost_gl"):
                 # utils.py:1954-1991: 0 when the first arch applies guided HCGS, else
                 # lambda * sum of norms over the dim>1 parameters of archs without
-                # skip_regularization (every CGS cfg sets it: the term is then exactly 0)
+                # skip_regularization (every CGS cfg but TIMIT_CGS/*L1*, *groupLasso* sets it)
                 nets = list(self.nets.values())
-                if not (getattr(nets[0], "apply_guided_hcgs", False) or
-                        all(getattr(n, "skip_regularization", False) for n in nets)):
-                    raise NotImplementedError("%s over non-skipped parameters (it also trains the "
-                                              "HCGS mask Parameters) is not on the pkc path" % op)
-                scal[out] = {}
+                params = []
+                for net in nets:
+                    if getattr(net, "skip_regularization", False):
+                        continue
+                    for pn, p in net.named_parameters():
+                        if p.dim() > 1:
+                            if "mask" in pn.split(".")[-1]:
+                                raise NotImplementedError(
+                                    "%s over an HCGS mask Parameter (the reference then trains "
+                                    "the mask) is not on the pkc path" % op)
+                            params.append(p)
+                if getattr(nets[0], "apply_guided_hcgs", False) or not params:
+                    scal[out] = {}
+                    continue
+                if op == "cost_gl":
+                    if "," not in b:
+                        raise NotImplementedError("cost_gl needs an output named loss_gl* "
+                                                  "(utils.py:1904-1906)")
+                    lam, nblk = b.split(",")
+                    term = RegTerm(op, lam, int(nblk), params)
+                else:
+                    term = RegTerm(op, b, 0, params)
+                scal[out] = {term: 1.0}
             elif op == "compute":
                 continue
             else:
@@ -381,6 +446,8 @@ class Engine:
             raise ValueError("[model] has no loss_final")
         for lay, w in scal.get("loss_final", {}).items():
             lay.loss_weight = w
+        self.reg_terms = [t for t in scal.get("loss_final", {}) if isinstance(t, RegTerm)
+                          and t.loss_weight != 0.0]
         if self.err_layer is None and self.heads:
             self.err_layer = self.heads[0]
         for lay in self.nodes:
@@ -481,11 +548,15 @@ class Engine:
         if self.loss_heads:
             if self.err_layer not in self.loss_heads:
                 raise NotImplementedError("err head without labels")
-            self.loss_out = _f32(2 + len(self.loss_heads), dev)
+            terms = self.loss_heads + self.reg_terms
+            for t in self.reg_terms:
+                t.row_loss = _f32(M, dev)
+            self.n_loss_terms = len(terms)
+            self.loss_out = _f32(2 + len(terms), dev)
             self.loss_acc = _f32(2, dev)
-            ptrs = np.array([l.row_loss.data_ptr() for l in self.loss_heads], dtype=np.uint64)
+            ptrs = np.array([l.row_loss.data_ptr() for l in terms], dtype=np.uint64)
             self.loss_ptrs = torch.from_numpy(ptrs.view(np.int64)).to(dev)
-            self.loss_w = torch.tensor([l.loss_weight for l in self.loss_heads], dtype=torch.float32,
+            self.loss_w = torch.tensor([l.loss_weight for l in terms], dtype=torch.float32,
                                        device=dev)
         if self.seq:
             self.seq_meta = torch.zeros(4 * self.B, dtype=torch.int64, device=dev)
@@ -953,6 +1024,8 @@ class Engine:
 
     def _forward_kernels(self, s, train, batch=None, defer_loss=False):
         self._gather(s, batch)
+        if self.reg_terms and self.loss_heads:
+            self._reg_loss_kernels(s)
         nodes, i = self.nodes, 0
         while i < len(nodes):
             n = nodes[i]
@@ -978,19 +1051,19 @@ class Engine:
                 self._fwd_epilogue(n, s, train)
             i += len(grp)
         if self.loss_heads and not defer_loss:
-            self._k("loss_finalize", 0, 4.0 * self.M * (len(self.loss_heads) + 1),
-                    "pkc_loss_finalize", len(self.loss_heads), ptr(self.loss_ptrs), ptr(self.loss_w),
+            self._k("loss_finalize", 0, 4.0 * self.M * (self.n_loss_terms + 1),
+                    "pkc_loss_finalize", self.n_loss_terms, ptr(self.loss_ptrs), ptr(self.loss_w),
                     self.M, ptr(self.err_layer.row_err), ptr(self.loss_out), ptr(self.loss_acc),
                     None if self.seq else ptr(self.ctr), s)
 
     def _loss_op(self):
         """The loss reduction (and batch-counter advance) as an operation of the first backward
         launch: it only needs the forward's per-row losses."""
-        p = L.GemmProblem(kind=L.OP_LOSS, M=len(self.loss_heads), N=self.M,
+        p = L.GemmProblem(kind=L.OP_LOSS, M=self.n_loss_terms, N=self.M,
                           A=self.loss_ptrs.data_ptr(), B=self.loss_w.data_ptr(),
                           C=self.loss_out.data_ptr(), X1=self.err_layer.row_err.data_ptr(),
                           X2=self.loss_acc.data_ptr(), X3=None if self.seq else self.ctr.data_ptr())
-        return ("loss", 0.0, 4.0 * self.M * (len(self.loss_heads) + 1), p)
+        return ("loss", 0.0, 4.0 * self.M * (self.n_loss_terms + 1), p)
 
     def _nll_multi(self, heads, s, train):
         """LogSoftmax/NLL of several heads in one launch."""
@@ -1151,6 +1224,7 @@ class Engine:
         spread_opt: each layer's optimizer update joins the launch AFTER the one holding its dW
         and dX (dX still reads the old weights), so the bandwidth-bound update overlaps the
         latency-bound matmuls instead of running as its own launch at the end."""
+        spread_opt = spread_opt and not self.reg_terms
         for n in self.nodes:
             if n.gslab is not None:
                 n.sb = self._grad_slabs(n)
@@ -1179,9 +1253,45 @@ class Engine:
         flush()
         self.spread_tail = carry        # updates still to run (the last layers')
 
+    def _build_reg(self):
+        """Device descriptors of the regulariser terms (item lists, block starts, buffers)."""
+        grads = {id(e["p"]): e["g"] for e in self.opt_entries}
+        for t in self.reg_terms:
+            items, bstart = t.items(grads)
+            arr = (L.RegItem * len(items))()
+            for i, (p, g, ld, r0, r1, c0, c1, blk) in enumerate(items):
+                arr[i] = L.RegItem(p=p.data_ptr(), g=None if g is None else g.data_ptr(), ld=ld,
+                                   r0=r0, r1=r1, c0=c0, c1=c1, block=blk)
+            t.nitems, t.nblocks = len(items), len(bstart) - 1
+            t.items_dev = torch.frombuffer(bytearray(C.string_at(arr, C.sizeof(arr))),
+                                           dtype=torch.uint8).to(self.dev)
+            t.bstart = torch.tensor(bstart, dtype=torch.int32, device=self.dev)
+            t.partial = _f32(len(items), self.dev)
+            t.coef = _f32(t.nblocks, self.dev)
+            t.nparam = sum(p.numel() for p in t.params)
+
+    def _reg_loss_kernels(self, s):
+        """Regulariser values of the current weights (before the forward's loss reduction)."""
+        for t in self.reg_terms:
+            self._k("reg_partial", 0, 4.0 * t.nparam, "pkc_reg_partial", t.kind, ptr(t.items_dev),
+                    t.nitems, ptr(t.partial), s)
+            self._k("reg_finalize", 0, 4.0 * (t.nitems + self.Mmax), "pkc_reg_finalize", t.kind,
+                    ptr(t.bstart), t.nblocks, ptr(t.partial), C.c_float(t.lam), ptr(t.coef),
+                    ptr(t.row_loss), self.Mmax, s)
+
+    def _reg_grad_kernels(self, s):
+        """d(w * lam * norms)/dp added to the (all-reduced) gradients before the optimizer."""
+        for t in self.reg_terms:
+            if t.loss_weight != 1.0:
+                raise NotImplementedError("a weighted regulariser term in loss_final")
+            self._k("reg_grad", 0, 12.0 * t.nparam, "pkc_reg_grad", t.kind, ptr(t.items_dev),
+                    t.nitems, ptr(t.coef), s)
+
     def _optim_kernels(self, s, spread_opt=False):
         if not self.opt_entries:
             return
+        spread_opt = spread_opt and not self.reg_terms
+        self._reg_grad_kernels(s)
         if spread_opt:
             self._gemms(self.spread_tail, s)
             self._prune_kernels(s)

@@ -41,18 +41,30 @@ def build_mlp_config(variant):
     if variant == "ln":
         body.update(dnn_use_batchnorm="False,True", dnn_use_laynorm="True,True",
                     dnn_use_batchnorm_inp="True", dnn_act="relu,tanh")
+    reg = REG_LINES.get(variant)
+    if reg:                        # regularised body + mono head, skipped cd head (utils.py:24-60)
+        body.update(skip_regularization="False")
+        mono.update(skip_regularization="False")
     cfg["architecture1"] = body
     cfg["architecture2"] = head
     cfg["architecture3"] = mono
+    tail = ("loss_tmp=sum(loss_cd,loss_mono_w)\n" + reg + "\nloss_final=sum(loss_tmp,%s)\n"
+            % reg.split("=")[0]) if reg else "loss_final=sum(loss_cd,loss_mono_w)\n"
     cfg["model"] = {"model": "out_dnn1=compute(MLP_layers1,fmllr)\n"
                              "out_dnn2=compute(MLP_layers2,out_dnn1)\n"
                              "out_dnn3=compute(MLP_layers3,out_dnn1)\n"
                              "loss_mono=cost_nll(out_dnn3,lab_mono)\n"
                              "loss_mono_w=mult_constant(loss_mono,1.0)\n"
-                             "loss_cd=cost_nll(out_dnn2,lab_cd)\n"
-                             "loss_final=sum(loss_cd,loss_mono_w)\n"
+                             "loss_cd=cost_nll(out_dnn2,lab_cd)\n" + tail +
                              "err_final=cost_err(out_dnn2,lab_cd)"}
     return cfg
+
+
+# [model] lines of the regulariser variants (cfg/TIMIT_CGS/TIMIT_LSTM_fmllr_L1.cfg,
+# ..._groupLasso.cfg use these forms; lambdas scaled up so the term is visible at this size)
+REG_LINES = {"l1": "loss_l1=cost_l1(out_dnn2,0.01)",
+             "l2": "loss_l2=cost_l2(out_dnn2,0.05)",
+             "gl": "loss_gl=cost_gl(out_dnn2,0.02,3)"}
 
 
 

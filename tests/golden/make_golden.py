@@ -339,10 +339,15 @@ def gen_ark():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:          # e.g. `make_golden.py mlp:l1 mlp:l2 mlp:gl`
+        for a in sys.argv[1:]:
+            kind, _, v = a.partition(":")
+            {"mlp": gen_mlp}[kind](v)
+        sys.exit(0)
     gen_loader()
     gen_hcgs()
     gen_quant()
-    for v in ("plain", "hcgs", "quant", "ln"):
+    for v in ("plain", "hcgs", "quant", "ln", "l1", "l2", "gl"):
         gen_mlp(v)
     gen_rnn()
     gen_ark()

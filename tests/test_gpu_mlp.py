@@ -44,10 +44,11 @@ def out_version(eng, lay, M):
     return lay.out[:M * lay.N]
 
 
-@pytest.mark.parametrize("variant", ["plain", "hcgs", "quant", "ln", "plain_l1"])
+@pytest.mark.parametrize("variant", ["plain", "hcgs", "quant", "ln", "plain_l1", "l1", "l2", "gl"])
 def test_engine_matches_reference_golden_steps(variant):
     """plain_l1: the plain model with an L1 regulariser term over skip_regularization archs
-    (every CGS cfg): utils.py:1954-1964 makes it exactly 0."""
+    (every CGS cfg): utils.py:1954-1964 makes it exactly 0.  l1 / l2 / gl: cost_l1 / cost_l2 /
+    cost_gl over the body and mono head (utils.py:24-60) — loss term and its gradient."""
     from pkc.engine import Engine, parse_model
     l1 = variant == "plain_l1"
     variant = "plain" if l1 else variant

@@ -27,6 +27,9 @@ def make_cfg(body):
         cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2",
                          ligru_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
                          hcgsh_block="8,4", hcgsh_sparse="25,50", **opt)
+    elif body == "lstm_gl":        # TIMIT_CGS/TIMIT_LSTM_fmllr_groupLasso.cfg: group lasso on the LSTM
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", skip_regularization="False", **opt)
     elif body == "lstm_prune":     # magnitude pruning every forward (neural_networks.py:886-1005)
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", lstm_prune="True", lstm_prune_perc="60,40", **opt)
@@ -38,14 +41,16 @@ def make_cfg(body):
                 dnn_use_laynorm="False", dnn_act="softmax", **opt)
     cfg["a2"] = head
     cfg["a3"] = dict(head, arch_name="mono", dnn_lay="8", arch_lr="0.0004")
+    fin = ("lt=sum(lc,lmw)\nloss_gl=cost_gl(o2,0.01,4)\nloss_final=sum(lt,loss_gl)\n"
+           if body == "lstm_gl" else "loss_final=sum(lc,lmw)\n")
     cfg["model"] = {"model": "o1=compute(rnn,fea)\no2=compute(head,o1)\no3=compute(mono,o1)\n"
                              "lm=cost_nll(o3,lab_mono)\nlmw=mult_constant(lm,1.0)\n"
-                             "lc=cost_nll(o2,lab_cd)\nloss_final=sum(lc,lmw)\n"
-                             "err_final=cost_err(o2,lab_cd)"}
+                             "lc=cost_nll(o2,lab_cd)\n" + fin + "err_final=cost_err(o2,lab_cd)"}
     return cfg
 
 
-@pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune"])
+@pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune",
+                                  "lstm_gl"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -62,7 +67,7 @@ def test_seq_engine_vs_oracle(body):
         torch.manual_seed(3)
         np.random.seed(3)
         cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM",
-                "lstm_prune": "LSTM"}[body]
+                "lstm_prune": "LSTM", "lstm_gl": "LSTM"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
