@@ -214,6 +214,7 @@ int pkc_prune(float* w, int64_t n, double perc, float* mask, void* work, void* s
  *   pkc_reg_finalize: coef[b] = lam (L1) or lam / ||block b|| (L2, 0 for a zero block);
  *                     loss_rows[0..nrows) = lam * sum_b ||block b||  (a pseudo loss head)
  *   pkc_reg_grad    : g += coef[block] * sign(x) (L1) or coef[block] * x (L2), items with g set
+ *                     (g = ... for items with assign set)
  * ------------------------------------------------------------------------------------------- */
 enum { PKC_REG_L1 = 1, PKC_REG_L2 = 2 };
 typedef struct pkc_reg_item_s {
@@ -222,6 +223,7 @@ typedef struct pkc_reg_item_s {
   int64_t ld;
   int r0, r1, c0, c1; /* the item's rectangle */
   int block;          /* block index */
+  int assign;         /* 1: g = term gradient (a parameter only the term trains); 0: g += */
 } pkc_reg_item;
 int pkc_reg_partial(int kind, const pkc_reg_item* items_dev, int nitems, float* partial,
                     void* stream);

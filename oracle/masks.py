@@ -103,3 +103,38 @@ def apply_patterns(w, patterns):
     out = np.zeros((R, C), dtype=np.float32)
     out[:R // ph * ph, :C // pw * pw] = mask_t.transpose(0, 2, 1, 3).reshape(R // ph * ph, C // pw * pw)
     return out
+
+
+def guided_conn_mat(n_rows, n_cols, block_sizes, drop_ratios, w):
+    """guided_hcgs.py:9-77 / guided_cgs_base.py:5-58 / guided_choices.py:4-31 (equal_blks_for_input
+    branch): per block row keep the block columns with the largest AvgPool2d mean of |W|
+    (torch.nn.AvgPool2d itself computes the means here), recursively per level."""
+    wabs = torch.as_tensor(np.abs(np.asarray(w, dtype=np.float32)))
+    levels = list(zip(block_sizes, drop_ratios))
+
+    def rec(a, lv):
+        r, c = a.shape
+        if not lv:
+            return np.ones((r, c), dtype=np.float32)
+        bs, drop = lv[0]
+        out = np.zeros((r, c), dtype=np.float32)
+        nbr = r // bs + (r % bs != 0)
+        nbc = c // bs + (c % bs != 0)
+        nsel = int(round(nbc * (1 - float(drop) / 100)))
+        for i in range(nbr):
+            rows = a[i * bs:(i + 1) * bs]
+            rr = rows.shape[0]
+            pool = torch.nn.AvgPool2d((rr, bs), bs) if rr != bs else torch.nn.AvgPool2d(bs, bs)
+            K = pool(rows[None, None])[0, 0]
+            if c % bs:
+                x = (nbc - 1) * bs
+                K = torch.cat([K, torch.nn.AvgPool2d((rr, c - x), c - x)(rows[None, None, :, x:])[0, 0]], 1)
+            ch = np.argsort(K[0].numpy())[-nsel:]
+            for j in range(nsel):
+                c0 = ch[j] * bs
+                out[i * bs:(i + 1) * bs, c0:c0 + bs] = rec(rows[:, c0:c0 + bs], lv[1:])
+        return out
+
+    m = rec(wabs, levels)
+    assert m.shape == (n_rows, n_cols)
+    return m

@@ -114,6 +114,10 @@ class MLP(nn.Module):
         self.wx, self.bn, self.ln = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         if self.hcgs_on:
             self.hcgs = nn.ModuleList()
+        self.guided = _b(o.get("guided_hcgs", "False"))
+        self.gbd = (blocks, drops)
+        if self.guided:
+            self.ghcgs = nn.ModuleList()
         if self.ln_inp:
             self.ln0 = LayerNorm(inp_dim)
         if self.bn_inp:
@@ -135,11 +139,25 @@ class MLP(nn.Module):
             s = np.sqrt(0.01 / (cur + n))                         # neural_networks.py:233-235
             lin.weight = nn.Parameter(torch.Tensor(n, cur).uniform_(-s, s))
             lin.bias = nn.Parameter(torch.zeros(n))
+            if self.guided:                                       # :237-239
+                hm = nn.Module()
+                hm.mask = nn.Parameter(torch.from_numpy(
+                    M.guided_conn_mat(n, cur, blocks, drops, lin.weight.data.numpy())))
+                self.ghcgs.append(hm)
             cur = n
         self.out_dim = cur
         self.if_pattern = _b(o["if_pattern"]) if "if_pattern" in o else False
         self.pattern_kernels = None
         self.pattern_masks = None
+
+    def apply_ghcgs(self):
+        """neural_networks.py:329-337."""
+        cur = self.input_dim
+        for i, n in enumerate(self.lay):
+            self.ghcgs[i].mask.data = torch.from_numpy(
+                M.guided_conn_mat(n, cur, self.gbd[0], self.gbd[1], self.wx[i].weight.data.numpy()))
+            cur = n
+        return 20.0
 
     def _pattern_update(self):
         """neural_networks.py:263-272, 350-361: masks computed once (at the first layer call) from
@@ -160,6 +178,8 @@ class MLP(nn.Module):
             w = self.wx[i].weight
             if self.hcgs_on:
                 w.data.mul_(self.hcgs[i].mask.data)
+            if self.guided and self.apply_guided_hcgs:                # :261-262
+                w.data.mul_(self.ghcgs[i].mask.data)
             if self.if_pattern:
                 self._pattern_update()
             if self.prune:
@@ -302,6 +322,7 @@ class LSTM(_Rec):
         super().__init__()
         self.skip_regularization = _b(o.get("skip_regularization", "False"))
         self.apply_guided_hcgs = _b(o.get("apply_guided_hcgs", "False"))
+        self.input_dim = inp_dim
         self.lay = _lst(o, "lstm_lay", int)
         self.dropp = _lst(o, "lstm_drop", float)
         self.use_bn = _lst(o, "lstm_use_batchnorm", _b)
@@ -330,6 +351,13 @@ class LSTM(_Rec):
             setattr(self, "u%sh" % g, nn.ModuleList())
         if self.hcgs_on:
             self.hcgsx, self.hcgsh = nn.ModuleList(), nn.ModuleList()
+        self.guided = _b(o.get("guided_hcgs", "False"))
+        if self.guided:                      # guidedHCGS modules (neural_networks.py:553-564)
+            self.gx = (_lst(o, "hcgsx_block", int), _lst(o, "hcgsx_sparse", float))
+            self.gh = (_lst(o, "hcgsh_block", int), _lst(o, "hcgsh_sparse", float))
+            for g in self.GATES:
+                setattr(self, "ghcgs_w%sx" % g, nn.ModuleList())
+                setattr(self, "ghcgs_u%sh" % g, nn.ModuleList())
         self.ln = nn.ModuleList()
         for g in self.GATES:
             setattr(self, "bn_w%sx" % g, nn.ModuleList())
@@ -365,6 +393,14 @@ class LSTM(_Rec):
             if self.orth:
                 for g in self.GATES:
                     nn.init.orthogonal_(getattr(self, "u%sh" % g)[i].weight)
+            if self.guided:      # from the initial W (:727-735) and U after orthinit (:797-806)
+                for g in self.GATES:
+                    for nm, src, (b, d), fin in (("ghcgs_w%sx", "w%sx", self.gx, cur),
+                                                 ("ghcgs_u%sh", "u%sh", self.gh, n)):
+                        hm = nn.Module()
+                        hm.mask = nn.Parameter(torch.from_numpy(M.guided_conn_mat(
+                            n, fin, b, d, getattr(self, src % g)[i].weight.data.numpy())))
+                        getattr(self, nm % g).append(hm)
             for g in self.GATES:
                 getattr(self, "bn_w%sx" % g).append(nn.BatchNorm1d(n, momentum=0.05))
             self.ln.append(LayerNorm(n))
@@ -388,6 +424,19 @@ class LSTM(_Rec):
                 for i in range(len(self.lay)):
                     getattr(self, nm)[i].weight.data.mul_(self.pattern_masks[nm][i])
 
+    def apply_ghcgs(self):
+        """neural_networks.py:1137-1160: guided masks regenerated from the current W / U."""
+        cur = self.input_dim
+        for i, n in enumerate(self.lay):
+            for g in self.GATES:
+                for nm, src, (b, d), fin in (("ghcgs_w%sx", "w%sx", self.gx, cur),
+                                             ("ghcgs_u%sh", "u%sh", self.gh, n)):
+                    w = getattr(self, src % g)[i].weight.data
+                    getattr(self, nm % g)[i].mask.data = torch.from_numpy(
+                        M.guided_conn_mat(n, fin, b, d, w.numpy()))
+            cur = n
+        return 1
+
     def forward(self, x, drop_masks=None):
         if self.ln_inp:
             x = self.ln0(x)
@@ -404,6 +453,9 @@ class LSTM(_Rec):
             if self.hcgs_on:
                 for g in self.GATES:
                     W[g].weight.data.mul_(self.hcgsx[i].mask.data)
+            if self.guided and self.apply_guided_hcgs:          # :864-873
+                for g in self.GATES:
+                    W[g].weight.data.mul_(getattr(self, "ghcgs_w%sx" % g)[i].mask.data)
             if self.if_pattern:
                 self._pattern_update()
             if self.prune:
@@ -417,6 +469,9 @@ class LSTM(_Rec):
             if self.hcgs_on:
                 for g in self.GATES:
                     U[g].weight.data.mul_(self.hcgsh[i].mask.data)
+            if self.guided and self.apply_guided_hcgs:          # :989-994
+                for g in self.GATES:
+                    U[g].weight.data.mul_(getattr(self, "ghcgs_u%sh" % g)[i].mask.data)
             if self.prune:
                 for g in self.GATES:
                     U[g].weight.data.mul_(M.prune_mask(U[g].weight, self.prune_perc[i]))

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(RT) void reg_grad_kernel(int kind, const pkc_reg_it
     const int64_t i = (it.r0 + e / w) * it.ld + it.c0 + e % w;
     const float x = it.p[i];
     const float d = kind == PKC_REG_L1 ? k * (x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f)) : k * x;
-    it.g[i] += d;
+    it.g[i] = it.assign ? d : it.g[i] + d;
   }
 }
 

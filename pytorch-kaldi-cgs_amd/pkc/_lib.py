@@ -80,7 +80,7 @@ REG_L1, REG_L2 = 1, 2
 
 class RegItem(C.Structure):
     _fields_ = [("p", vp), ("g", vp), ("ld", i64), ("r0", C.c_int), ("r1", C.c_int),
-                ("c0", C.c_int), ("c1", C.c_int), ("block", C.c_int)]
+                ("c0", C.c_int), ("c1", C.c_int), ("block", C.c_int), ("assign", C.c_int)]
 
 
 _SIGS = {

@@ -49,3 +49,60 @@ def hcgs_mask(out_features, in_features, block_sizes, drop_ratios, rng=None):
     m = np.zeros((out_features, in_features), dtype=np.float32)
     _fill(m, 0, out_features, 0, in_features, list(zip(block_sizes, drop_ratios)), rng, True)
     return m
+
+
+# ------------------------------------------------------------------------------------------------
+# guided HCGS: the connectivity is chosen by weight magnitude instead of at random
+# (guided_hcgs.py:9-77 -> guided_cgs_base.py:5-58 -> guided_choices.py:4-31).  Each block row keeps
+# the n_sel block columns with the largest mean |W| (torch AvgPool2d: float32 sum in window order,
+# divided by the window size; np.argsort(...)[-n_sel:] picks them), recursively per level.  Used at
+# model construction (from the initial W) and at chunk end (apply_ghcgs, core.py:298-300).
+# ------------------------------------------------------------------------------------------------
+def _window_mean(a):
+    """torch.nn.AvgPool2d over one window: sequential float32 sum (row-major), / count."""
+    s = np.cumsum(a.reshape(-1), dtype=np.float32)[-1] if a.size else np.float32(0)
+    return np.float32(s / np.float32(a.size))
+
+
+def _guided_choices(wabs, n_blk, n_sel, bs):
+    """guided_choices.guided_array_rows: indices of the n_sel largest block means."""
+    r, c = wabs.shape
+    full = (c - bs) // bs + 1
+    if full < 1:
+        raise ValueError("guided HCGS: a %dx%d slice is narrower than its %d block" % (r, c, bs))
+    K = [_window_mean(wabs[:, j * bs:(j + 1) * bs]) for j in range(full)]
+    if c % bs != 0:
+        x = (n_blk - 1) * bs
+        K.append(_window_mean(wabs[:, x:c]))
+    return np.argsort(np.array(K, dtype=np.float32))[-n_sel:]
+
+
+def _guided_fill(out, wabs, levels):
+    n_in, n_out = wabs.shape
+    if not levels:
+        out[...] = 1.0
+        return
+    (bs, drop), rest = levels[0], levels[1:]
+    keep = 1.0 - float(drop) / 100.0
+    n_rows = n_in // bs + (1 if n_in % bs else 0)
+    n_cols = n_out // bs + (1 if n_out % bs else 0)
+    n_sel = int(round(n_cols * keep))
+    for i in range(n_rows):
+        r0, r1 = i * bs, min((i + 1) * bs, n_in)
+        ch = _guided_choices(wabs[r0:r1], n_cols, n_sel, bs)
+        for c in ch[:n_sel]:          # argsort(...)[-0:] is the whole array; range(0) is empty
+            c0, c1 = c * bs, min((c + 1) * bs, n_out)
+            _guided_fill(out[r0:r1, c0:c1], wabs[r0:r1, c0:c1], rest)
+
+
+def guided_hcgs_mask(out_features, in_features, block_sizes, drop_ratios, w):
+    """(out_features, in_features) float32 {0,1} mask guided by |w| (w: (out, in) array/tensor)."""
+    if len(block_sizes) != len(drop_ratios):
+        raise ValueError("block size and drop ratio should have the same length")
+    if hasattr(w, "detach"):
+        w = w.detach().float().cpu().numpy()
+    wabs = np.abs(np.asarray(w, dtype=np.float32))
+    assert wabs.shape == (out_features, in_features)
+    m = np.zeros((out_features, in_features), dtype=np.float32)
+    _guided_fill(m, wabs, list(zip(block_sizes, drop_ratios)))
+    return m

@@ -316,10 +316,12 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
 
     if to_do == "train" and ws_eff > 1:
         DP.average_buffers(list(nns.values()))
-    if to_do == "train" and if_prune:             # chunk-end pruning (core.py:291-296)
+    if to_do == "train":
         for net in nns.values():
-            if getattr(net, "prune", False):
+            if getattr(net, "prune", False) and if_prune:       # chunk-end pruning (291-296)
                 net.prune_parameters()
+            if getattr(net, "guided_hcgs", False) and not net.apply_guided_hcgs:   # (298-300)
+                net.apply_ghcgs()
     if to_do == "train":
         for net_name, net in nns.items():
             if getattr(net, "if_pattern", False):                    # core.py:304-306

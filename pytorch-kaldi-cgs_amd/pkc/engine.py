@@ -202,12 +202,14 @@ class RecNode:
         for li, sp in enumerate(self.layers):
             for g in range(self.G):
                 W = sp["W"][g]
-                out.append((W, ("dW", li, g), self.emask.get(id(W), sp["Wmask"])))
+                wm = sp["Wmasks"][g] if sp.get("Wmasks") else sp["Wmask"]
+                out.append((W, ("dW", li, g), self.emask.get(id(W), wm)))
                 if sp["b"][g] is not None:
                     out.append((sp["b"][g], ("db", li, g), None))
             for g in range(self.G):
                 U = sp["U"][g]
-                out.append((U, ("dU", li, g), self.emask.get(id(U), sp["Umask"])))
+                um = sp["Umasks"][g] if sp.get("Umasks") else sp["Umask"]
+                out.append((U, ("dU", li, g), self.emask.get(id(U), um)))
             if sp["bn"]:
                 for g in range(self.G):
                     out.append((sp["bnm"][g].weight, ("dgamma", li, g), None))
@@ -413,16 +415,24 @@ class Engine:
                 # lambda * sum of norms over the dim>1 parameters of archs without
                 # skip_regularization (every CGS cfg but TIMIT_CGS/*L1*, *groupLasso* sets it)
                 nets = list(self.nets.values())
-                params = []
-                for net in nets:
+                params, masks = [], []
+                for arch, net in self.nets.items():
+                    if getattr(nets[0], "apply_guided_hcgs", False):
+                        break                   # the whole term is 0 (utils.py:1962)
                     if getattr(net, "skip_regularization", False):
                         continue
                     for pn, p in net.named_parameters():
                         if p.dim() > 1:
                             if "mask" in pn.split(".")[-1]:
-                                raise NotImplementedError(
-                                    "%s over an HCGS mask Parameter (the reference then trains "
-                                    "the mask) is not on the pkc path" % op)
+                                # the mask Parameters are in the sum and in the optimizer, so the
+                                # reference trains them; supported while they are not multiplied
+                                # into W (guided masks before apply_guided_hcgs, which regenerates
+                                # them at chunk end anyway)
+                                if not (pn.startswith("ghcgs") and not net.apply_guided_hcgs):
+                                    raise NotImplementedError(
+                                        "%s over an applied mask Parameter %s.%s (the reference "
+                                        "then trains the mask it multiplies in)" % (op, arch, pn))
+                                masks.append((p, arch))
                             params.append(p)
                 if getattr(nets[0], "apply_guided_hcgs", False) or not params:
                     scal[out] = {}
@@ -435,6 +445,7 @@ class Engine:
                     term = RegTerm(op, lam, int(nblk), params)
                 else:
                     term = RegTerm(op, b, 0, params)
+                term.masks = masks
                 scal[out] = {term: 1.0}
             elif op == "compute":
                 continue
@@ -629,6 +640,17 @@ class Engine:
                 self.opt_entries.append(dict(arch=n.arch, p=p, g=g, mask=m, o=o, q=q, qbits=qb,
                                              s1=torch.zeros_like(p), s2=None, s3=None, step=0,
                                              node=n))
+        # mask Parameters trained by a regulariser term only (their gradient is the term's)
+        seen = {id(e["p"]) for e in self.opt_entries}
+        for t in getattr(self, "reg_terms", []):
+            for p, arch in t.masks:
+                o = self.arch_opts[arch]
+                if id(p) in seen or _b(o.get("arch_freeze", "False")) or not self.train:
+                    continue
+                seen.add(id(p))
+                self.opt_entries.append(dict(arch=arch, p=p, g=torch.zeros_like(p), mask=None, o=o,
+                                             q=None, qbits=0, s1=torch.zeros_like(p), s2=None,
+                                             s3=None, step=0, node=None, reg_only=True))
         for e in self.opt_entries:
             kind = e["o"]["arch_opt"]
             if kind == "rmsprop" and (float(e["o"]["opt_momentum"]) > 0):
@@ -1256,12 +1278,14 @@ class Engine:
     def _build_reg(self):
         """Device descriptors of the regulariser terms (item lists, block starts, buffers)."""
         grads = {id(e["p"]): e["g"] for e in self.opt_entries}
+        only = {id(e["p"]) for e in self.opt_entries if e.get("reg_only")}
         for t in self.reg_terms:
             items, bstart = t.items(grads)
             arr = (L.RegItem * len(items))()
             for i, (p, g, ld, r0, r1, c0, c1, blk) in enumerate(items):
                 arr[i] = L.RegItem(p=p.data_ptr(), g=None if g is None else g.data_ptr(), ld=ld,
-                                   r0=r0, r1=r1, c0=c0, c1=c1, block=blk)
+                                   r0=r0, r1=r1, c0=c0, c1=c1, block=blk,
+                                   assign=1 if id(p) in only else 0)
             t.nitems, t.nblocks = len(items), len(bstart) - 1
             t.items_dev = torch.frombuffer(bytearray(C.string_at(arr, C.sizeof(arr))),
                                            dtype=torch.uint8).to(self.dev)

@@ -19,7 +19,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .cgs import hcgs_mask
+from .cgs import guided_hcgs_mask, hcgs_mask
 
 
 def strtobool(v):
@@ -92,11 +92,26 @@ class _PatternSet:
 
 
 class _Mask(nn.Module):
-    """HCGS.HCGS: a non-learnable ``mask`` Parameter of shape (out, in) (HCGS.py:24-28)."""
+    """HCGS.HCGS / HCGS.guidedHCGS: a ``mask`` Parameter of shape (out, in) (HCGS.py:24-28, 55-59)."""
 
     def __init__(self, mask):
         super().__init__()
         self.mask = nn.Parameter(torch.from_numpy(mask))
+
+
+def _mask_product(*ms):
+    """Effective in-place mask of several masks multiplied into W one after the other."""
+    ms = [m for m in ms if m is not None]
+    if not ms:
+        return None
+    out = ms[0]
+    for m in ms[1:]:
+        out = out * m
+    return out.detach() if len(ms) > 1 else out
+
+
+def _set_mask(module, arr):
+    module.mask.data.copy_(torch.from_numpy(arr).to(module.mask.device))
 
 
 class _QLinear(nn.Module):
@@ -145,13 +160,13 @@ class MLP(_PatternSet, nn.Module):
         self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
         self._pattern_opts(o)
         self.arch_name = o.get("arch_name", "MLP")
-        if self.guided_hcgs:
-            raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
         if self.if_pattern:                  # per-layer kernels / masks (neural_networks.py:159-161)
             self.pattern, self.pattern_mask = [], []
 
-        if self.mlp_hcgs:                    # registered first, as neural_networks.py:151-152
+        if self.mlp_hcgs:                    # registered first, as neural_networks.py:151-156
             self.hcgs = nn.ModuleList()
+        if self.guided_hcgs:
+            self.ghcgs = nn.ModuleList()
         self.wx, self.bn, self.ln = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         if self.dnn_use_laynorm_inp:
             self.ln0 = LayerNorm(inp_dim)
@@ -173,6 +188,9 @@ class MLP(_PatternSet, nn.Module):
             s = np.sqrt(0.01 / (cur + n))                        # neural_networks.py:233-235
             lin.weight = nn.Parameter(torch.Tensor(n, cur).uniform_(-s, s))
             lin.bias = nn.Parameter(torch.zeros(n))
+            if self.guided_hcgs:             # from the initial W (neural_networks.py:237-239)
+                self.ghcgs.append(_Mask(guided_hcgs_mask(n, cur, self.hcgs_block, self.hcgs_sparse,
+                                                         lin.weight.data)))
             cur = n
         self.out_dim = cur
         self._engine = None
@@ -185,7 +203,21 @@ class MLP(_PatternSet, nn.Module):
         return 1
 
     def apply_ghcgs(self):
-        raise NotImplementedError("guided HCGS is outside the pkc hot path")
+        """Chunk-end regeneration of the guided masks from the current W (neural_networks.py:
+        329-337, called at core.py:298-300 while apply_guided_hcgs is off)."""
+        cur = self.input_dim
+        for i, n in enumerate(self.dnn_lay):
+            _set_mask(self.ghcgs[i], guided_hcgs_mask(n, cur, self.hcgs_block, self.hcgs_sparse,
+                                                      self.wx[i].weight.data))
+            cur = n
+        return 20.0
+
+    def _wmask(self, i):
+        """Masks multiplied into wx[i] before each forward: HCGS, then guided HCGS when applied
+        (neural_networks.py:256-262)."""
+        return _mask_product(self.hcgs[i].mask if self.mlp_hcgs else None,
+                             self.ghcgs[i].mask if (self.guided_hcgs and self.apply_guided_hcgs)
+                             else None)
 
     def layer_specs(self):
         """Per-layer description consumed by pkc.engine."""
@@ -196,7 +228,7 @@ class MLP(_PatternSet, nn.Module):
                               W=self.wx[i].weight, b=self.wx[i].bias, gamma=self.bn[i].weight,
                               beta=self.bn[i].bias, rm=self.bn[i].running_mean,
                               rv=self.bn[i].running_var, nbt=self.bn[i].num_batches_tracked,
-                              mask=self.hcgs[i].mask if self.mlp_hcgs else None,
+                              mask=self._wmask(i),
                               quant=self.param_quant[i] if self.mlp_quant else 0,
                               inp_quant=self.inp_quant[0] if (self.mlp_quant and self.mlp_quant_inp) else 0,
                               ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta,
@@ -206,8 +238,7 @@ class MLP(_PatternSet, nn.Module):
 
     def pattern_params(self):
         """[(store key, layer, W, HCGS mask)] in the reference's update_mask order."""
-        return [((None, i), i, self.wx[i].weight, self.hcgs[i].mask if self.mlp_hcgs else None)
-                for i in range(len(self.dnn_lay))]
+        return [((None, i), i, self.wx[i].weight, self._wmask(i)) for i in range(len(self.dnn_lay))]
 
     def input_norm_specs(self):
         """Input normalisations in the reference's order: ln0 then bn0 (neural_networks.py:246-251)."""
@@ -358,10 +389,12 @@ class LSTM(_PatternSet, nn.Module):
         self.apply_guided_hcgs = strtobool(o.get("apply_guided_hcgs", "False"))
         self._pattern_opts(o)
         self.arch_name = o.get("arch_name", "LSTM")
-        if self.guided_hcgs:
-            raise NotImplementedError("guided HCGS (guided_hcgs.py) is outside the pkc hot path")
         if self.lstm_hcgs:                      # registered first, as neural_networks.py:548-550
             self.hcgsx, self.hcgsh = nn.ModuleList(), nn.ModuleList()
+        if self.guided_hcgs:                    # then the guided lists (553-564)
+            for g in self.GATES:
+                setattr(self, "ghcgs_w%sx" % g, nn.ModuleList())
+                setattr(self, "ghcgs_u%sh" % g, nn.ModuleList())
         if self.if_pattern:
             self.pattern = {k: [] for k in ("pattern_w%sx" % g for g in self.GATES)}
             self.pattern.update({k: [] for k in ("pattern_u%sh" % g for g in self.GATES)})
@@ -393,6 +426,11 @@ class LSTM(_PatternSet, nn.Module):
                 getattr(self, "w%sx" % g).append(lin)
             if self.lstm_hcgs:
                 self.hcgsx.append(_Mask(hcgs_mask(n, cur, self.hcgsx_block, self.hcgsx_sparse)))
+            if self.guided_hcgs:                # from the initial W (neural_networks.py:727-735)
+                for g in self.GATES:
+                    getattr(self, "ghcgs_w%sx" % g).append(_Mask(guided_hcgs_mask(
+                        n, cur, self.hcgsx_block, self.hcgsx_sparse,
+                        getattr(self, "w%sx" % g)[i].weight.data)))
             for g in self.GATES:
                 if self.lstm_quant:
                     lin = _QLinear(n, n, self.param_quant[i], False,
@@ -405,6 +443,11 @@ class LSTM(_PatternSet, nn.Module):
             if self.lstm_orthinit:
                 for g in self.GATES:
                     nn.init.orthogonal_(getattr(self, "u%sh" % g)[i].weight)
+            if self.guided_hcgs:                # from the initial U (neural_networks.py:797-806)
+                for g in self.GATES:
+                    getattr(self, "ghcgs_u%sh" % g).append(_Mask(guided_hcgs_mask(
+                        n, n, self.hcgsh_block, self.hcgsh_sparse,
+                        getattr(self, "u%sh" % g)[i].weight.data)))
             for g in self.GATES:
                 getattr(self, "bn_w%sx" % g).append(nn.BatchNorm1d(n, momentum=0.05))
             self.ln.append(LayerNorm(n))
@@ -419,7 +462,27 @@ class LSTM(_PatternSet, nn.Module):
         return 1
 
     def apply_ghcgs(self):
-        raise NotImplementedError("guided HCGS is outside the pkc hot path")
+        """Chunk-end regeneration of the guided masks from the current W / U (neural_networks.py:
+        1137-1160, core.py:298-300)."""
+        cur = self.input_dim
+        for i, n in enumerate(self.lstm_lay):
+            for g in self.GATES:
+                _set_mask(getattr(self, "ghcgs_w%sx" % g)[i], guided_hcgs_mask(
+                    n, cur, self.hcgsx_block, self.hcgsx_sparse, getattr(self, "w%sx" % g)[i].weight.data))
+                _set_mask(getattr(self, "ghcgs_u%sh" % g)[i], guided_hcgs_mask(
+                    n, n, self.hcgsh_block, self.hcgsh_sparse, getattr(self, "u%sh" % g)[i].weight.data))
+            cur = 2 * n if self.bidir else n
+        return 1
+
+    def _gmask(self, kind, g, i):
+        """Masks multiplied into w<g>x[i] / u<g>h[i] before use: HCGS, then guided HCGS when
+        applied (neural_networks.py:858-873, 980-994)."""
+        h = (self.hcgsx if kind == "w" else self.hcgsh)[i].mask if self.lstm_hcgs else None
+        gm = None
+        if self.guided_hcgs and self.apply_guided_hcgs:
+            nm = ("ghcgs_w%sx" if kind == "w" else "ghcgs_u%sh") % g
+            gm = getattr(self, nm)[i].mask
+        return _mask_product(h, gm)
 
     def check_supported(self):
         if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp or any(self.lstm_use_laynorm):
@@ -433,10 +496,11 @@ class LSTM(_PatternSet, nn.Module):
         (neural_networks.py:1202-1223)."""
         out = []
         for i in range(len(self.lstm_lay)):
-            for nm, msk in [("w%sx" % g, "hcgsx") for g in self.GATES] + \
-                           [("u%sh" % g, "hcgsh") for g in self.GATES]:
-                m = getattr(self, msk)[i].mask if self.lstm_hcgs else None
-                out.append((("pattern_mask_" + nm, i), i, getattr(self, nm)[i].weight, m))
+            for kind in ("w", "u"):
+                for g in self.GATES:
+                    nm = ("w%sx" if kind == "w" else "u%sh") % g
+                    out.append((("pattern_mask_" + nm, i), i, getattr(self, nm)[i].weight,
+                                self._gmask(kind, g, i)))
         return out
 
     def layer_specs(self):
@@ -450,6 +514,8 @@ class LSTM(_PatternSet, nn.Module):
                               bnm=[getattr(self, "bn_w%sx" % g)[i] for g in self.GATES],
                               Wmask=self.hcgsx[i].mask if self.lstm_hcgs else None,
                               Umask=self.hcgsh[i].mask if self.lstm_hcgs else None,
+                              Wmasks=[self._gmask("w", g, i) for g in self.GATES],
+                              Umasks=[self._gmask("u", g, i) for g in self.GATES],
                               qbits=self.param_quant[i] if self.lstm_quant else 0,
                               ibits=self.inp_quant[0] if (self.lstm_quant and self.lstm_quant_inp) else 0,
                               prune=self.prune_perc[i] if self.prune else None,

@@ -83,3 +83,9 @@ LSTM_DEF = dict(lstm_lay="16,16", lstm_drop="0.0,0.0", lstm_use_laynorm_inp="Fal
                 if_hsigmoid="True", arch_name="LSTM_layers")
 
 
+
+
+# guided HCGS known answers (make_golden.gen_ghcgs): (shape, block sizes, drop ratios); case 4 has
+# exactly tied block means, case 1 selects no block at all (round(2 * 0.1875) = 0)
+GHCGS = [((48, 40), [16, 4], [50, 50]), ((64, 64), [32], [81.25]), ((30, 20), [8, 2], [50, 50]),
+         ((100, 70), [32, 4], [75, 50]), ((96, 96), [32, 8], [50, 25])]

@@ -204,6 +204,27 @@ def gen_quant():
 
 
 # ----------------------------------------------------------------------------------------------
+# guided HCGS masks (guided_hcgs.py:9-77): deterministic functions of |W|
+# ----------------------------------------------------------------------------------------------
+from cases import GHCGS  # noqa: E402
+
+
+def gen_ghcgs():
+    import guided_hcgs
+    out = {}
+    rs = np.random.RandomState(11)
+    for i, (shape, blocks, drops) in enumerate(GHCGS):
+        w = torch.from_numpy(rs.randn(*shape).astype(np.float32))
+        if i == 4:                                   # exact ties: equal block means
+            w[:, 32:64] = w[:, 0:32]
+        m = guided_hcgs.conn_mat(shape[0], shape[1], list(blocks), list(drops), w, str(i),
+                                 dir=_TMP, for_test=True)
+        out["w%d" % i] = w.numpy().copy()
+        out["mask%d" % i] = np.asarray(m, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "ghcgs.npz"), **out)
+
+
+# ----------------------------------------------------------------------------------------------
 # helpers to build reference modules from option dicts
 # ----------------------------------------------------------------------------------------------
 def section(d):
@@ -342,10 +363,11 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:          # e.g. `make_golden.py mlp:l1 mlp:l2 mlp:gl`
         for a in sys.argv[1:]:
             kind, _, v = a.partition(":")
-            {"mlp": gen_mlp}[kind](v)
+            {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs()}[kind](v)
         sys.exit(0)
     gen_loader()
     gen_hcgs()
+    gen_ghcgs()
     gen_quant()
     for v in ("plain", "hcgs", "quant", "ln", "l1", "l2", "gl"):
         gen_mlp(v)

@@ -216,7 +216,7 @@ def test_engine_graph_replay_equals_eager():
         torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("variant", ["prune", "pattern"])
+@pytest.mark.parametrize("variant", ["prune", "pattern", "ghcgs"])
 def test_engine_sparsity_vs_oracle(variant):
     """prune: every forward re-thresholds |W| at np.percentile(prune_perc[i]) and zeroes the rest
     (neural_networks.py:276-278); pattern: 8x8/k4/n16 pattern masks from the pattern_file set,
@@ -232,6 +232,8 @@ def test_engine_sparsity_vs_oracle(variant):
         cfg["architecture1"]["mlp_prune"] = "True"
         cfg["architecture1"]["mlp_prune_perc"] = "70,55"
         cfg["architecture2"].update(mlp_prune="True", mlp_prune_perc="30")
+    elif variant == "ghcgs":     # guided masks applied (apply_guided_hcgs, :261-262) on the body
+        cfg["architecture1"].update(guided_hcgs="True", apply_guided_hcgs="True")
     else:
         pset = G("quant.npz")["pattern_set"].reshape(16, 8, 8)
         for sec in ("architecture1", "architecture2"):
@@ -286,6 +288,8 @@ def test_engine_sparsity_vs_oracle(variant):
                 mk = "hcgs.%d.mask" % i
                 if mk in sd_o:           # re-masked + re-pruned at the reference's next forward
                     ref = ref * sd_o[mk]
+                if "ghcgs.%d.mask" % i in sd_o:
+                    ref = ref * sd_o["ghcgs.%d.mask" % i]
                 if variant == "pattern" and onets[a].if_pattern:
                     ref = ref * onets[a].pattern_masks[i] ** len(onets[a].lay)
                 if a in percs:

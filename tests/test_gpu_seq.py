@@ -30,6 +30,13 @@ def make_cfg(body):
     elif body == "lstm_gl":        # TIMIT_CGS/TIMIT_LSTM_fmllr_groupLasso.cfg: group lasso on the LSTM
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", skip_regularization="False", **opt)
+    elif body in ("lstm_ghcgs_l1", "lstm_ghcgs_apply"):
+        # TIMIT_CGS/TIMIT_LSTM_fmllr_ghcgs*.cfg: guided masks; before apply_guided_hcgs the L1 term
+        # also trains the (unapplied) mask Parameters, after it the term is 0
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", skip_regularization="False", guided_hcgs="True",
+                         apply_guided_hcgs=str(body == "lstm_ghcgs_apply"), hcgsx_block="8",
+                         hcgsx_sparse="50", hcgsh_block="8,4", hcgsh_sparse="75,50", **opt)
     elif body == "lstm_prune":     # magnitude pruning every forward (neural_networks.py:886-1005)
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", lstm_prune="True", lstm_prune_perc="60,40", **opt)
@@ -42,7 +49,9 @@ def make_cfg(body):
     cfg["a2"] = head
     cfg["a3"] = dict(head, arch_name="mono", dnn_lay="8", arch_lr="0.0004")
     fin = ("lt=sum(lc,lmw)\nloss_gl=cost_gl(o2,0.01,4)\nloss_final=sum(lt,loss_gl)\n"
-           if body == "lstm_gl" else "loss_final=sum(lc,lmw)\n")
+           if body == "lstm_gl" else
+           "lt=sum(lc,lmw)\nloss_l1=cost_l1(o2,0.0005)\nloss_final=sum(lt,loss_l1)\n"
+           if body.startswith("lstm_ghcgs") else "loss_final=sum(lc,lmw)\n")
     cfg["model"] = {"model": "o1=compute(rnn,fea)\no2=compute(head,o1)\no3=compute(mono,o1)\n"
                              "lm=cost_nll(o3,lab_mono)\nlmw=mult_constant(lm,1.0)\n"
                              "lc=cost_nll(o2,lab_cd)\n" + fin + "err_final=cost_err(o2,lab_cd)"}
@@ -50,7 +59,7 @@ def make_cfg(body):
 
 
 @pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune",
-                                  "lstm_gl"])
+                                  "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -67,7 +76,8 @@ def test_seq_engine_vs_oracle(body):
         torch.manual_seed(3)
         np.random.seed(3)
         cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM",
-                "lstm_prune": "LSTM", "lstm_gl": "LSTM"}[body]
+                "lstm_prune": "LSTM", "lstm_gl": "LSTM", "lstm_ghcgs_l1": "LSTM",
+                "lstm_ghcgs_apply": "LSTM"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
@@ -130,6 +140,9 @@ def test_seq_engine_vs_oracle(body):
             if body == "ligru_hcgs" and name.endswith("weight") and parts[0] in ("wh", "wz", "uh", "uz"):
                 mk = ("hcgsx" if parts[0][0] == "w" else "hcgsh") + ".%s.mask" % parts[1]
                 ref = ref * sd_o[mk].double()
+            if body == "lstm_ghcgs_apply" and k == "rnn" and name.endswith("weight") and \
+                    len(parts[0]) == 3:
+                ref = ref * sd_o["ghcgs_%s.%s.mask" % (parts[0], parts[1])].double()
             if body == "lstm_prune" and name.endswith("weight") and len(parts[0]) == 3 and k == "rnn":
                 from oracle.masks import prune_mask
                 perc = (60.0, 40.0)[int(parts[1])]

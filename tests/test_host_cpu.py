@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN, ROOT
-from cases import build_mlp_config
+from cases import GHCGS, build_mlp_config
 
 HDR = os.path.join(ROOT, "include", "pkc.h")
 
@@ -152,3 +152,49 @@ def test_product_ligru_hcgs_init_matches_oracle():
     assert any("hcgsx" in k for k in sds[0])
     for k in sds[0]:
         assert torch.equal(sds[0][k], sds[1][k]), k
+
+
+@pytest.mark.parametrize("i", range(len(GHCGS)))
+def test_product_guided_mask_matches_reference(i):
+    """guided_hcgs.conn_mat known answers (AvgPool2d float32 block means, argsort selection)."""
+    from pkc.cgs import guided_hcgs_mask
+    g = G("ghcgs.npz")
+    (r, c), bl, dr = GHCGS[i]
+    np.testing.assert_array_equal(guided_hcgs_mask(r, c, bl, dr, g["w%d" % i]), g["mask%d" % i])
+
+
+@pytest.mark.parametrize("cls", ["MLP", "LSTM"])
+def test_product_guided_init_matches_oracle(cls):
+    """guided_hcgs=True: the guidedHCGS mask Parameters are built from the initial W / U under
+    the reference's names, and apply_ghcgs regenerates them from the current weights."""
+    import pkc.neural_networks as NN
+    from oracle import nets as ON
+    from cases import LSTM_DEF, MLP_DEF
+    cp = configparser.ConfigParser()
+    if cls == "MLP":
+        cp["s"] = dict(MLP_DEF, dnn_lay="64,32", dnn_drop="0,0", dnn_use_batchnorm="True,True",
+                       dnn_use_laynorm="False,False", dnn_act="relu,relu", guided_hcgs="True",
+                       hcgs_block="16,4", hcgs_sparse="50,50")
+    else:
+        cp["s"] = dict(LSTM_DEF, guided_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
+                       hcgsh_block="8", hcgsh_sparse="75")
+    nets = []
+    for c in (getattr(NN, cls), getattr(ON, cls)):
+        torch.manual_seed(4)
+        np.random.seed(4)
+        nets.append(c(cp["s"], 40 if cls == "MLP" else 20))
+    sds = [n.state_dict() for n in nets]
+    assert sds[0].keys() == sds[1].keys()
+    assert any("ghcgs" in k for k in sds[0])
+    for k in sds[0]:
+        assert torch.equal(sds[0][k], sds[1][k]), k
+    for n in nets:                       # new weights -> regenerated masks agree
+        torch.manual_seed(5)
+        for pn, p in n.named_parameters():
+            if "mask" not in pn:
+                p.data.normal_()
+    nets[0].apply_ghcgs()
+    nets[1].apply_ghcgs()
+    for k, v in nets[0].state_dict().items():
+        if "ghcgs" in k:
+            assert torch.equal(v, nets[1].state_dict()[k]), k
