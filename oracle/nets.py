@@ -313,6 +313,80 @@ class liGRU(_Rec):
         return x
 
 
+class GRU(_Rec):
+    """neural_networks.py:1240-1426."""
+
+    def __init__(self, o, inp_dim):
+        super().__init__()
+        self.skip_regularization = _b(o.get("skip_regularization", "False"))
+        self.apply_guided_hcgs = False
+        self.lay = _lst(o, "gru_lay", int)
+        self.dropp = _lst(o, "gru_drop", float)
+        self.use_bn = _lst(o, "gru_use_batchnorm", _b)
+        self.use_ln = _lst(o, "gru_use_laynorm", _b)
+        self.ln_inp = _b(o["gru_use_laynorm_inp"])
+        self.bn_inp = _b(o["gru_use_batchnorm_inp"])
+        self.orth = _b(o["gru_orthinit"])
+        self.acts = _lst(o, "gru_act")
+        self.bidir = _b(o["gru_bidir"])
+        self.wh, self.uh, self.wz, self.uz, self.wr, self.ur = (nn.ModuleList() for _ in range(6))
+        self.ln = nn.ModuleList()
+        self.bn_wh, self.bn_wz, self.bn_wr = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        if self.ln_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.bn_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.lay):
+            add_bias = not (self.use_ln[i] or self.use_bn[i])
+            for lst in (self.wh, self.wz, self.wr):
+                lst.append(nn.Linear(cur, n, bias=add_bias))
+            for lst in (self.uh, self.uz, self.ur):
+                lst.append(nn.Linear(n, n, bias=False))
+            if self.orth:
+                for lst in (self.uh, self.uz, self.ur):
+                    nn.init.orthogonal_(lst[i].weight)
+            for lst in (self.bn_wh, self.bn_wz, self.bn_wr):
+                lst.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def forward(self, x, drop_masks=None):
+        if self.ln_inp:
+            x = self.ln0(x)
+        if self.bn_inp:
+            T, B, Fd = x.shape
+            x = self.bn0(x.reshape(T * B, Fd)).view(T, B, Fd)
+        for i, H in enumerate(self.lay):
+            if self.bidir:
+                x = torch.cat([x, flip_time(x)], 1)
+            T, B2, _ = x.shape
+            dm = self._drop_mask(i, B2, H, drop_masks)
+            pre = {}
+            for g in ("h", "z", "r"):
+                w = getattr(self, "w" + g)[i](x)
+                if self.use_bn[i]:
+                    w = getattr(self, "bn_w" + g)[i](w.reshape(T * B2, H)).view(T, B2, H)
+                pre[g] = w
+            h = torch.zeros(B2, H)
+            hs = []
+            for k in range(T):                                   # :1390-1396
+                z = torch.sigmoid(pre["z"][k] + self.uz[i](h))
+                r = torch.sigmoid(pre["r"][k] + self.ur[i](h))
+                a = pre["h"][k] + self.uh[i](r * h)
+                hc = act_fn(self.acts[i], a) * dm
+                h = z * h + (1 - z) * hc
+                if self.use_ln[i]:
+                    h = self.ln[i](h)
+                hs.append(h)
+            y = torch.stack(hs)
+            if self.bidir:
+                y = torch.cat([y[:, :B2 // 2], flip_time(y[:, B2 // 2:])], 2)
+            x = y
+        return x
+
+
 class LSTM(_Rec):
     """neural_networks.py:468-1112 (bidir forced 0 at :835, so only uni-directional)."""
 

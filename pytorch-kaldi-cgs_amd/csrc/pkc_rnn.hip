@@ -16,6 +16,12 @@
 //   dh_{t-1}[r][k] = sum_g sum_j da_g[t][r][j] * U_g[j][k]   (+ elementwise carry terms)
 // and immediately turns it into the gate gradients of step t-1 at (r, k), so the loop needs no
 // second launch per step.  dU and dW are big matmuls after the loop.
+//
+// GRU (neural_networks.py:1390-1396: z, r = sig(w + U h); a = wh + Uh (r*h); hc = act(a)*drop;
+// h = z*h + (1-z)*hc) multiplies Uh with r*h, which needs the r of every unit of the row first, so
+// a step is two launches: (z, r, r*h) then (Uh (r*h), update).  Its BPTT step is two launches as
+// well: d(rh) = Uh^T da (then dr), and dh_{t-1} = Uz^T dz + Ur^T dr + carries (then dz, da).
+// r*h is kept for every step (rh, (T, B2, H)): it is the input of the Uh gradient matmul.
 #include "pkc_common.h"
 
 namespace pkc {
@@ -157,6 +163,15 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
   const float m = drop_val(a, r, j, ix.B2);
   const float hp = hprev[(int64_t)r * H + j];
   float h;
+  if (CELL == PKC_CELL_GRU) {
+    // phase 1 of a GRU step: update / reset gates and r*h (the input of Uh)
+    const float z = sigm(a.wpre[pi] + acc[0]);
+    const float rg = sigm(a.wpre[TBH + pi] + acc[1]);
+    a.gates[si] = z;
+    a.gates[TB2H + si] = rg;
+    a.rh[si] = rg * hp;
+    return;
+  }
   if (CELL == PKC_CELL_LIGRU) {
     // gates (z, h) -- liGRU
     const float z = sigm(a.wpre[pi] + acc[0]);
@@ -180,6 +195,48 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
     a.gates[2 * TB2H + si] = o;
     a.gates[3 * TB2H + si] = cc;
   }
+  a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+  a.y[ix.out(t, r, j)] = h;
+}
+
+// phase 2 of a GRU step: a = wh + Uh (r*h_{t-1}); h = z*h_{t-1} + (1-z)*act(a)*drop
+__global__ __launch_bounds__(RT) void gru_fwd_h(pkc_rnn_args a, int t) {
+  __shared__ float hsm[RR][KC + 1];
+  __shared__ float usm[RU][KC + 1];
+  const RnnIdx ix = mkidx(a);
+  const int j = blockIdx.x * RU + threadIdx.x % RU;
+  const int r = blockIdx.y * RR + threadIdx.x / RU;
+  const int H = a.H;
+  const float* src = a.rh + (int64_t)t * ix.B2 * H;
+  const float* U = a.U[2];
+  float acc = 0.f;
+  for (int k0 = 0; k0 < H; k0 += KC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < RR * KC; e += RT) {
+      const int rr = e / KC, kk = e % KC;
+      const int R = blockIdx.y * RR + rr, K = k0 + kk;
+      hsm[rr][kk] = (R < ix.B2 && K < H) ? src[(int64_t)R * H + K] : 0.f;
+    }
+    for (int e = threadIdx.x; e < RU * KC; e += RT) {
+      const int jj = e / KC, kk = e % KC;
+      const int J = blockIdx.x * RU + jj, K = k0 + kk;
+      usm[jj][kk] = (J < H && K < H) ? U[(int64_t)J * H + K] : 0.f;
+    }
+    __syncthreads();
+    const int rl = threadIdx.x / RU, jl = threadIdx.x % RU;
+#pragma unroll 8
+    for (int kk = 0; kk < KC; ++kk) acc = fmaf(usm[jl][kk], hsm[rl][kk], acc);
+  }
+  if (r >= ix.B2 || j >= H) return;
+  const int64_t TBH = (int64_t)a.T * a.B * H;
+  const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
+  const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
+  const float m = drop_val(a, r, j, ix.B2);
+  const float hp = a.hs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
+  const float z = a.gates[si];
+  const float hcr = act_fwd(a.act, a.wpre[2 * TBH + pi] + acc);
+  const float h = z * hp + (1.f - z) * (hcr * m);
+  a.gates[2 * TB2H + si] = hcr;
   a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
   a.y[ix.out(t, r, j)] = h;
 }
@@ -223,6 +280,13 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
     dgo[0] = dz * z * (1.f - z);
     dgo[1] = dhc * m * act_bwd_out(a.act, hcr);   // act' from the post-activation value
     *g_out = g;
+  } else if (CELL == PKC_CELL_GRU) {
+    // dz and da now; dr needs Uh^T da over the whole row (gru_bwd_rh)
+    const float z = a.gates[si], hcr = a.gates[2 * TB2H + si];
+    const float hc = hcr * m;
+    dgo[0] = g * (hp - hc) * z * (1.f - z);
+    dgo[2] = g * (1.f - z) * m * act_bwd_out(a.act, hcr);
+    *g_out = g;
   } else {
     const float f = a.gates[si], i = a.gates[TB2H + si], o = a.gates[2 * TB2H + si];
     const float cc = a.gates[3 * TB2H + si];
@@ -252,8 +316,13 @@ __global__ void rnn_bwd_init(pkc_rnn_args a) {
     const float g = dy_at(a, ix.out(t, r, k));
     float dg[4], go, dco = 0.f;
     gate_grads<CELL>(a, ix, t, r, k, g, 0.f, dg, &go, &dco);
+    if (CELL == PKC_CELL_GRU) {
+      a.dgates[ix.st(t, r, k)] = dg[0];
+      a.dgates[2 * TB2H + ix.st(t, r, k)] = dg[2];
+    } else {
 #pragma unroll
-    for (int q = 0; q < G; ++q) a.dgates[q * TB2H + ix.st(t, r, k)] = dg[q];
+      for (int q = 0; q < G; ++q) a.dgates[q * TB2H + ix.st(t, r, k)] = dg[q];
+    }
     a.work[e] = go;                 // g ping  (step parity 1)
     a.work[2 * n + e] = dco;        // dc ping
   }
@@ -302,22 +371,70 @@ __global__ __launch_bounds__(RT) void rnn_bwd_step(pkc_rnn_args a, int tt) {
   float dc_carry = 0.f;
   if (CELL == PKC_CELL_LIGRU) {
     dh += a.work[src * n + e] * a.gates[ix.st(t, r, k)];     // g_t * z_t
+  } else if (CELL == PKC_CELL_GRU) {
+    // g_t * z_t + d(rh)_t * r_t  (acc = Uz^T dz_t + Ur^T dr_t)
+    dh += a.work[src * n + e] * a.gates[ix.st(t, r, k)] +
+          a.work[2 * n + e] * a.gates[TB2H + ix.st(t, r, k)];
   } else {
     dc_carry = a.work[2 * n + src * n + e];                  // dc_t * f_t
   }
   const float g = dy_at(a, ix.out(tt, r, k)) + dh;
   float dg[4], go, dco = 0.f;
   gate_grads<CELL>(a, ix, tt, r, k, g, dc_carry, dg, &go, &dco);
+  if (CELL == PKC_CELL_GRU) {
+    a.dgates[ix.st(tt, r, k)] = dg[0];
+    a.dgates[2 * TB2H + ix.st(tt, r, k)] = dg[2];
+    a.work[dst * n + e] = go;
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < G; ++q) a.dgates[q * TB2H + ix.st(tt, r, k)] = dg[q];
   a.work[dst * n + e] = go;
   a.work[2 * n + dst * n + e] = dco;
 }
 
+// GRU: d(rh)_t[r][k] = sum_j da_t[r][j] Uh[j][k]; dr_t = d(rh) * h_{t-1} * r (1 - r).
+// d(rh)_t is kept in work[2n..3n) for the carry term of the next (earlier) step.
+__global__ __launch_bounds__(RT) void gru_bwd_rh(pkc_rnn_args a, int t) {
+  __shared__ float dsm[RR][KC + 1];
+  __shared__ float usm[KC][RU + 1];
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H;
+  const int k = blockIdx.x * RU + threadIdx.x % RU;
+  const int r = blockIdx.y * RR + threadIdx.x / RU;
+  const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
+  const int64_t n = (int64_t)ix.B2 * H;
+  const float* U = a.U[2];
+  float acc = 0.f;
+  for (int j0 = 0; j0 < H; j0 += KC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < RR * KC; e += RT) {
+      const int rr = e / KC, jj = e % KC;
+      const int R = blockIdx.y * RR + rr, J = j0 + jj;
+      dsm[rr][jj] = (R < ix.B2 && J < H) ? a.dgates[2 * TB2H + ix.st(t, R, J)] : 0.f;
+    }
+    for (int e = threadIdx.x; e < KC * RU; e += RT) {
+      const int jj = e / RU, kk = e % RU;
+      const int J = j0 + jj, K = blockIdx.x * RU + kk;
+      usm[jj][kk] = (J < H && K < H) ? U[(int64_t)J * H + K] : 0.f;
+    }
+    __syncthreads();
+    const int rl = threadIdx.x / RU, kl = threadIdx.x % RU;
+#pragma unroll 8
+    for (int jj = 0; jj < KC; ++jj) acc = fmaf(dsm[rl][jj], usm[jj][kl], acc);
+  }
+  if (r >= ix.B2 || k >= H) return;
+  const int64_t e = (int64_t)r * H + k, si = ix.st(t, r, k);
+  const float hp = a.hs[(int64_t)t * ix.B2 * H + e];
+  const float rg = a.gates[TB2H + si];
+  a.dgates[TB2H + si] = acc * hp * rg * (1.f - rg);
+  a.work[2 * n + e] = acc;
+}
+
 // fold the per-direction gate gradients (G, T, B2, H) onto the (G, T, B, H) pre-activation rows
 __global__ void rnn_fold_kernel(pkc_rnn_args a, float* dpre) {
   const RnnIdx ix = mkidx(a);
-  const int G = a.cell == PKC_CELL_LSTM ? 4 : 2;
+  const int G = a.cell == PKC_CELL_LSTM ? 4 : (a.cell == PKC_CELL_GRU ? 3 : 2);
   const int64_t TBH = (int64_t)a.T * a.B * a.H;
   const int64_t TB2H = (int64_t)a.T * ix.B2 * a.H;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)G * TBH;
@@ -343,6 +460,14 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
     PKC_LAUNCH_CHECK("pkc_rnn_fwd drop mask");
   }
   dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
+  if (CELL == PKC_CELL_GRU) {
+    for (int t = 0; t < a->T; ++t) {
+      hipLaunchKernelGGL((rnn_fwd_step<2, PKC_CELL_GRU, false>), grid, dim3(RT), 0, s, *a, t);
+      hipLaunchKernelGGL(gru_fwd_h, grid, dim3(RT), 0, s, *a, t);
+    }
+    PKC_LAUNCH_CHECK("pkc_rnn_fwd gru step");
+    return PKC_OK;
+  }
   for (int t = 0; t < a->T; ++t) {
     if (a->qbits > 0)
       hipLaunchKernelGGL((rnn_fwd_step<G, CELL, true>), grid, dim3(RT), 0, s, *a, t);
@@ -359,8 +484,16 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
   dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
-  for (int tt = a->T - 2; tt >= 0; --tt)
-    hipLaunchKernelGGL((rnn_bwd_step<G, CELL>), grid, dim3(RT), 0, s, *a, tt);
+  if (CELL == PKC_CELL_GRU) {
+    hipLaunchKernelGGL(gru_bwd_rh, grid, dim3(RT), 0, s, *a, a->T - 1);
+    for (int tt = a->T - 2; tt >= 0; --tt) {
+      hipLaunchKernelGGL((rnn_bwd_step<2, PKC_CELL_GRU>), grid, dim3(RT), 0, s, *a, tt);
+      hipLaunchKernelGGL(gru_bwd_rh, grid, dim3(RT), 0, s, *a, tt);
+    }
+  } else {
+    for (int tt = a->T - 2; tt >= 0; --tt)
+      hipLaunchKernelGGL((rnn_bwd_step<G, CELL>), grid, dim3(RT), 0, s, *a, tt);
+  }
   PKC_LAUNCH_CHECK("pkc_rnn_bwd step");
   hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
@@ -369,10 +502,12 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
 
 static int check(const pkc_rnn_args* a, bool bwd) {
   PKC_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->H > 0, "pkc_rnn: bad shape");
-  PKC_CHECK_ARG(a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM, "pkc_rnn: bad cell %d", a->cell);
+  PKC_CHECK_ARG(a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM || a->cell == PKC_CELL_GRU,
+                "pkc_rnn: bad cell %d", a->cell);
+  PKC_CHECK_ARG(a->cell != PKC_CELL_GRU || (a->rh && a->qbits <= 0), "pkc_rnn: GRU needs rh, no qbits");
   PKC_CHECK_ARG(a->wpre && a->hs && a->gates && a->y, "pkc_rnn: null buffer");
   PKC_CHECK_ARG(a->cell != PKC_CELL_LSTM || a->cs, "pkc_rnn: LSTM needs cs");
-  const int G = a->cell == PKC_CELL_LSTM ? 4 : 2;
+  const int G = a->cell == PKC_CELL_LSTM ? 4 : (a->cell == PKC_CELL_GRU ? 3 : 2);
   for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U[g], "pkc_rnn: null U[%d]", g);
   PKC_CHECK_ARG(!a->train || a->drop_p <= 0.f || a->drop_mask, "pkc_rnn: dropout needs drop_mask");
   if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work, "pkc_rnn_bwd: null buffer");
@@ -388,6 +523,7 @@ extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
   int st = check(a, false);
   if (st) return st;
   if (a->cell == PKC_CELL_LIGRU) return fwd_impl<2, PKC_CELL_LIGRU>(a, S(stream));
+  if (a->cell == PKC_CELL_GRU) return fwd_impl<3, PKC_CELL_GRU>(a, S(stream));
   return fwd_impl<4, PKC_CELL_LSTM>(a, S(stream));
 }
 
@@ -397,5 +533,6 @@ extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
   if (st) return st;
   PKC_CHECK_ARG(dpre, "pkc_rnn_bwd: null dpre");
   if (a->cell == PKC_CELL_LIGRU) return bwd_impl<2, PKC_CELL_LIGRU>(a, dpre, S(stream));
+  if (a->cell == PKC_CELL_GRU) return bwd_impl<3, PKC_CELL_GRU>(a, dpre, S(stream));
   return bwd_impl<4, PKC_CELL_LSTM>(a, dpre, S(stream));
 }

@@ -54,7 +54,7 @@ class OptTensor(C.Structure):
                 ("qout", vp), ("qbits", C.c_int), ("bout", vp)]
 
 
-CELL_LIGRU, CELL_LSTM = 0, 1
+CELL_LIGRU, CELL_LSTM, CELL_GRU = 0, 1, 2
 
 
 class RnnArgs(C.Structure):
@@ -63,7 +63,7 @@ class RnnArgs(C.Structure):
                 ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp), ("stream_id", i64),
                 ("drop_mask_in", vp), ("drop_mask", vp), ("hs", vp), ("cs", vp), ("gates", vp),
                 ("y", vp), ("dy", vp), ("dy_nslab", C.c_int), ("dy_slab_stride", i64),
-                ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp)]
+                ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp), ("rh", vp)]
 
 
 class GemmProblem(C.Structure):

@@ -175,8 +175,8 @@ class RecNode:
     def __init__(self, arch, net, K):
         self.arch, self.net, self.K = arch, net, K
         self.name = arch
-        self.cell = L.CELL_LSTM if net.cell == "lstm" else L.CELL_LIGRU
-        self.G = 4 if self.cell == L.CELL_LSTM else 2
+        self.cell = {"lstm": L.CELL_LSTM, "gru": L.CELL_GRU, "ligru": L.CELL_LIGRU}[net.cell]
+        self.G = {L.CELL_LSTM: 4, L.CELL_GRU: 3, L.CELL_LIGRU: 2}[self.cell]
         self.layers = net.layer_specs()
         self.N = net.out_dim
         self.src = None
@@ -587,6 +587,7 @@ class Engine:
                       work=_f32(L.lib().pkc_dense_work_size(M, H), dev),
                       hs=_f32((T + 1) * B2 * H, dev),
                       cs=_f32((T + 1) * B2 * H, dev) if n.cell == L.CELL_LSTM else None,
+                      rh=_f32(T * B2 * H, dev) if n.cell == L.CELL_GRU else None,
                       gates=_f32(G * T * B2 * H, dev), y=_f32(M * D, dev),
                       drop=_f32(B2 * H, dev), dgates=_f32(G * T * B2 * H, dev),
                       dpre=_f32(G * M * H, dev), dz=_f32(G * M * H, dev),
@@ -985,6 +986,7 @@ class Engine:
         a.drop_mask = lb["drop"].data_ptr()
         a.hs = lb["hs"].data_ptr()
         a.cs = lb["cs"].data_ptr() if lb["cs"] is not None else None
+        a.rh = lb["rh"].data_ptr() if lb["rh"] is not None else None
         a.gates = lb["gates"].data_ptr()
         a.y = lb["y"].data_ptr()
         a.dgates = lb["dgates"].data_ptr()
@@ -1214,12 +1216,13 @@ class Engine:
                 self._k("rnn_gemm_dW %dx%dx%d" % (H, K, M), 2.0 * M * H * K,
                         4.0 * (M * H + M * K + H * K), "pkc_gemm", self.prec, 0, 0, H, K, M, dz, H,
                         C.c_void_p(x_ptr), ldx, ptr(lb["dW"][g]), K, 1, 0, s)
-                # dU = sum_t dgates[t]^T h_{t-1}: K = T*B2 rows of hs[0:T]
+                # dU = sum_t dgates[t]^T h_{t-1}: K = T*B2 rows of hs[0:T] (GRU Uh: r*h_{t-1})
                 R2 = T * lb["B2"]
+                usrc = lb["rh"] if (n.cell == L.CELL_GRU and g == 2) else hsrc
                 self._k("rnn_gemm_dU %dx%dx%d" % (H, H, R2), 2.0 * R2 * H * H,
                         4.0 * (2 * R2 * H + H * H), "pkc_gemm", self.prec, 0, 0, H, H, R2,
                         C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,
-                        ptr(hsrc), H, ptr(lb["dU"][g]), H, 1, 0, s)
+                        ptr(usrc), H, ptr(lb["dU"][g]), H, 1, 0, s)
                 if li > 0 or want_dx0:
                     sx = _splits(M, K, H, MAX_SPLITS)
                     self._k("rnn_gemm_dX %dx%dx%d" % (M, K, H), 2.0 * M * H * K,

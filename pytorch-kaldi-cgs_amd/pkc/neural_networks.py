@@ -350,6 +350,83 @@ class liGRU(nn.Module):
         return specs
 
 
+class GRU(nn.Module):
+    """neural_networks.py:1240-1426 (options per proto/GRU.proto).  Parameters: wh, uh, wz, uz, wr,
+    ur, ln, bn_wh, bn_wz, bn_wr (registration order and init draws of the reference)."""
+
+    seq_model = True
+    cell = "gru"
+    GATES = ("z", "r", "h")
+
+    def __init__(self, options, inp_dim):
+        super().__init__()
+        o = options
+        self.input_dim = inp_dim
+        self.gru_lay = _lst(o, "gru_lay", int)
+        self.gru_drop = _lst(o, "gru_drop", float)
+        self.gru_use_batchnorm = _lst(o, "gru_use_batchnorm", strtobool)
+        self.gru_use_laynorm = _lst(o, "gru_use_laynorm", strtobool)
+        self.gru_use_laynorm_inp = strtobool(o["gru_use_laynorm_inp"])
+        self.gru_use_batchnorm_inp = strtobool(o["gru_use_batchnorm_inp"])
+        self.gru_orthinit = strtobool(o["gru_orthinit"])
+        self.gru_act = _lst(o, "gru_act")
+        self.bidir = strtobool(o["gru_bidir"])
+        self.to_do = o.get("to_do", "train")
+        # core.run_nn / utils read these on every architecture; the reference GRU has no CGS hooks
+        self.prune = False
+        self.guided_hcgs = False
+        self.apply_guided_hcgs = False
+        self.if_pattern = False
+        self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
+        self.wh, self.uh = nn.ModuleList(), nn.ModuleList()
+        self.wz, self.uz = nn.ModuleList(), nn.ModuleList()
+        self.wr, self.ur = nn.ModuleList(), nn.ModuleList()
+        self.ln = nn.ModuleList()
+        self.bn_wh, self.bn_wz, self.bn_wr = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        if self.gru_use_laynorm_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.gru_use_batchnorm_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.gru_lay):
+            add_bias = not (self.gru_use_laynorm[i] or self.gru_use_batchnorm[i])
+            self.wh.append(nn.Linear(cur, n, bias=add_bias))
+            self.wz.append(nn.Linear(cur, n, bias=add_bias))
+            self.wr.append(nn.Linear(cur, n, bias=add_bias))
+            self.uh.append(nn.Linear(n, n, bias=False))
+            self.uz.append(nn.Linear(n, n, bias=False))
+            self.ur.append(nn.Linear(n, n, bias=False))
+            if self.gru_orthinit:
+                nn.init.orthogonal_(self.uh[i].weight)
+                nn.init.orthogonal_(self.uz[i].weight)
+                nn.init.orthogonal_(self.ur[i].weight)
+            self.bn_wh.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.bn_wz.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.bn_wr.append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def prune_parameters(self):
+        raise NotImplementedError("the reference GRU has no prune hook")
+
+    def check_supported(self):
+        if self.gru_use_laynorm_inp or self.gru_use_batchnorm_inp or any(self.gru_use_laynorm):
+            raise NotImplementedError("LayerNorm / input normalisation in GRU is not on the pkc path yet")
+
+    def layer_specs(self):
+        specs = []
+        for i, n in enumerate(self.gru_lay):
+            specs.append(dict(H=n, act=self.gru_act[i], bn=bool(self.gru_use_batchnorm[i]),
+                              drop=self.gru_drop[i], bidir=bool(self.bidir),
+                              W=[self.wz[i].weight, self.wr[i].weight, self.wh[i].weight],
+                              b=[self.wz[i].bias, self.wr[i].bias, self.wh[i].bias],
+                              U=[self.uz[i].weight, self.ur[i].weight, self.uh[i].weight],
+                              bnm=[self.bn_wz[i], self.bn_wr[i], self.bn_wh[i]],
+                              Wmask=None, Umask=None))
+        return specs
+
+
 class LSTM(_PatternSet, nn.Module):
     """neural_networks.py:468-1237.  The reference forces bidir off inside forward (:835), so a
     bidirectional cfg crashes there on layer 2; pkc runs bidirectional LSTMs with the liGRU

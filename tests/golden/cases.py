@@ -89,3 +89,13 @@ LSTM_DEF = dict(lstm_lay="16,16", lstm_drop="0.0,0.0", lstm_use_laynorm_inp="Fal
 # exactly tied block means, case 1 selects no block at all (round(2 * 0.1875) = 0)
 GHCGS = [((48, 40), [16, 4], [50, 50]), ((64, 64), [32], [81.25]), ((30, 20), [8, 2], [50, 50]),
          ((100, 70), [32, 4], [75, 50]), ((96, 96), [32, 8], [50, 25])]
+
+
+GRU_DEF = dict(gru_lay="16,16", gru_drop="0.0,0.0", gru_use_laynorm_inp="False",
+               gru_use_batchnorm_inp="False", gru_use_laynorm="False,False",
+               gru_use_batchnorm="True,True", gru_bidir="True", gru_act="relu,relu",
+               gru_orthinit="True", use_cuda="False", to_do="train")
+# (tag, options, T, B, F, seed) of the GRU golden cases (tests/golden/gru.npz)
+GRU_CASES = [("gru_bidir", GRU_DEF, 7, 3, 20, 31),
+             ("gru_uni_nobn", dict(GRU_DEF, gru_bidir="False", gru_use_batchnorm="False,False",
+                                   gru_act="tanh,tanh", gru_orthinit="False"), 6, 2, 12, 32)]

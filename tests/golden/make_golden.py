@@ -342,6 +342,14 @@ def gen_rnn():
     np.savez_compressed(os.path.join(OUT, "rnn.npz"), **out)
 
 
+def gen_gru():
+    from cases import GRU_CASES
+    out = {}
+    for tag, opts, T, B, F, seed in GRU_CASES:
+        run_rnn(neural_networks.GRU, opts, T, B, F, seed, out, tag)
+    np.savez_compressed(os.path.join(OUT, "gru.npz"), **out)
+
+
 # ----------------------------------------------------------------------------------------------
 # G6: posterior ark bytes (data_io.write_mat) incl. count normalisation (core.py:242-249)
 # ----------------------------------------------------------------------------------------------
@@ -363,7 +371,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:          # e.g. `make_golden.py mlp:l1 mlp:l2 mlp:gl`
         for a in sys.argv[1:]:
             kind, _, v = a.partition(":")
-            {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs()}[kind](v)
+            {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru()}[kind](v)
         sys.exit(0)
     gen_loader()
     gen_hcgs()
@@ -372,6 +380,7 @@ if __name__ == "__main__":
     for v in ("plain", "hcgs", "quant", "ln", "l1", "l2", "gl"):
         gen_mlp(v)
     gen_rnn()
+    gen_gru()
     gen_ark()
     total = sum(os.path.getsize(os.path.join(OUT, f)) for f in os.listdir(OUT))
     print("golden fixtures written to %s (%.1f KB)" % (OUT, total / 1024))

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN
-from cases import LIGRU_DEF, LSTM_DEF
+from cases import GRU_CASES, LIGRU_DEF, LSTM_DEF
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -55,14 +55,15 @@ CASES = [("ligru_bidir", "liGRU", LIGRU_DEF, 7, 3, 20, 21),
          ("lstm", "LSTM", LSTM_DEF, 7, 3, 20, 23),
          ("lstm_hcgs_quant", "LSTM", dict(LSTM_DEF, lstm_hcgs="True", lstm_quant="True",
                                           lstm_quant_inp="True"), 7, 3, 24, 24),
-         ("lstm_pattern", "LSTM", dict(LSTM_DEF, **PATTERN), 5, 2, 24, 25)]
+         ("lstm_pattern", "LSTM", dict(LSTM_DEF, **PATTERN), 5, 2, 24, 25)] + \
+        [(tag, "GRU", opts, T, B, F, seed) for tag, opts, T, B, F, seed in GRU_CASES]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_recurrent_layer_matches_reference(case):
     import pkc.neural_networks as NN
     tag, cls, opts, T, B, F, seed = case
-    g = np.load(os.path.join(GOLDEN, "rnn.npz"), allow_pickle=False)
+    g = np.load(os.path.join(GOLDEN, "gru.npz" if cls == "GRU" else "rnn.npz"), allow_pickle=False)
     torch.manual_seed(seed)
     np.random.seed(seed)
     net = getattr(NN, cls)(section(opts), F)
@@ -87,11 +88,14 @@ def test_recurrent_layer_matches_reference(case):
     grads = {}
     for li, lb in enumerate(node.lbuf):
         for gi, gate in enumerate(net.GATES):
-            if cls == "liGRU":
+            if cls in ("liGRU", "GRU"):
+                if lb["db"][gi] is not None:
+                    grads["w%s.%d.bias" % (gate, li)] = lb["db"][gi]
                 grads["w%s.%d.weight" % (gate, li)] = lb["dW"][gi]
                 grads["u%s.%d.weight" % (gate, li)] = lb["dU"][gi]
-                grads["bn_w%s.%d.weight" % (gate, li)] = lb["dgamma"][gi]
-                grads["bn_w%s.%d.bias" % (gate, li)] = lb["dbeta"][gi]
+                if node.layers[li]["bn"]:
+                    grads["bn_w%s.%d.weight" % (gate, li)] = lb["dgamma"][gi]
+                    grads["bn_w%s.%d.bias" % (gate, li)] = lb["dbeta"][gi]
             else:
                 grads["w%sx.%d.weight" % (gate, li)] = lb["dW"][gi]
                 grads["u%sh.%d.weight" % (gate, li)] = lb["dU"][gi]

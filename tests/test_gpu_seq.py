@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from cases import LIGRU_DEF, LSTM_DEF
+from cases import GRU_DEF, LIGRU_DEF, LSTM_DEF
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -27,6 +27,8 @@ def make_cfg(body):
         cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2",
                          ligru_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
                          hcgsh_block="8,4", hcgsh_sparse="25,50", **opt)
+    elif body == "gru":            # GRU (neural_networks.py:1240-1426), bidirectional
+        cfg["a1"] = dict(GRU_DEF, arch_name="rnn", gru_lay="32,24", gru_drop="0.2,0.2", **opt)
     elif body == "lstm_gl":        # TIMIT_CGS/TIMIT_LSTM_fmllr_groupLasso.cfg: group lasso on the LSTM
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", skip_regularization="False", **opt)
@@ -59,7 +61,7 @@ def make_cfg(body):
 
 
 @pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune",
-                                  "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply"])
+                                  "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply", "gru"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -77,7 +79,7 @@ def test_seq_engine_vs_oracle(body):
         np.random.seed(3)
         cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM",
                 "lstm_prune": "LSTM", "lstm_gl": "LSTM", "lstm_ghcgs_l1": "LSTM",
-                "lstm_ghcgs_apply": "LSTM"}[body]
+                "lstm_ghcgs_apply": "LSTM", "gru": "GRU"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
