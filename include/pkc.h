@@ -251,7 +251,8 @@ int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double*
 
 /* ---------------------------------------------------------------------------------------------
  * Recurrent layers: the per-time-step loops of liGRU (neural_networks.py:1573-1584), LSTM
- * (neural_networks.py:1077-1097) and GRU (neural_networks.py:1390-1396).  wpre holds the gate pre-activations W x (+BN) for the T*B input
+ * (neural_networks.py:1077-1097), GRU (:1390-1396, gates z, r, h), minimalGRU (:1751-1755, gates
+ * z, h) and RNN (:1905-1907, gate h).  wpre holds the gate pre-activations W x (+BN) for the T*B input
  * rows, gate-major (G, T, B, H): liGRU gates (z, h), LSTM gates (f, i, o, c).  Bidirectional
  * layers (liGRU's shared-weight cat/flip convention, :1536-1538) run 2B rows per step; rows >= B
  * read time T-1-t and write the second half of the (T, B, 2H) output y.  Forward saves
@@ -261,7 +262,7 @@ int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double*
  * per direction and dpre (G, T, B, H) = the same folded over directions (input of the BN / W
  * backward); work = 4*B2*H floats.
  * ------------------------------------------------------------------------------------------- */
-enum { PKC_CELL_LIGRU = 0, PKC_CELL_LSTM = 1, PKC_CELL_GRU = 2 };
+enum { PKC_CELL_LIGRU = 0, PKC_CELL_LSTM = 1, PKC_CELL_GRU = 2, PKC_CELL_MINGRU = 3, PKC_CELL_RNN = 4 };
 typedef struct {
   int cell, T, B, H, bidir, act, train;
   const float* wpre;
@@ -277,8 +278,8 @@ typedef struct {
    * at the fake-quantised weights.  hq (T+1, B2, H) receives q4(h_{t-1}) — the value the reference
    * keeps as hiddens[t-1] and as the saved input of the U backward. qbits = 0: off. */
   int qbits; float* hq;
-  /* GRU (cell 2, gates (z, r, h), neural_networks.py:1390-1396): r*h_{t-1} per step, (T, B2, H) —
-   * the input of the Uh product and of its gradient matmul.  NULL for the other cells. */
+  /* GRU / minimalGRU: r*h_{t-1} (z*h_{t-1}) per step, (T, B2, H) — the input of the Uh product
+   * and of its gradient matmul.  NULL for the other cells. */
   float* rh;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);

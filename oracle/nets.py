@@ -387,6 +387,97 @@ class GRU(_Rec):
         return x
 
 
+class _PlainRec(_Rec):
+    """minimalGRU / RNN construction (neural_networks.py:1602-1700, 1780-1861)."""
+    PREFIX, ORDER = "", ()
+
+    def __init__(self, o, inp_dim):
+        super().__init__()
+        p = self.PREFIX
+        self.skip_regularization = _b(o.get("skip_regularization", "False"))
+        self.apply_guided_hcgs = False
+        self.lay = _lst(o, p + "_lay", int)
+        self.dropp = _lst(o, p + "_drop", float)
+        self.use_bn = _lst(o, p + "_use_batchnorm", _b)
+        self.use_ln = _lst(o, p + "_use_laynorm", _b)
+        self.ln_inp = _b(o[p + "_use_laynorm_inp"])
+        self.bn_inp = _b(o[p + "_use_batchnorm_inp"])
+        self.orth = _b(o[p + "_orthinit"])
+        self.acts = _lst(o, p + "_act")
+        self.bidir = _b(o[p + "_bidir"])
+        for g in self.ORDER:
+            setattr(self, "w" + g, nn.ModuleList())
+            setattr(self, "u" + g, nn.ModuleList())
+        self.ln = nn.ModuleList()
+        for g in self.ORDER:
+            setattr(self, "bn_w" + g, nn.ModuleList())
+        if self.ln_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.bn_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.lay):
+            add_bias = not (self.use_ln[i] or self.use_bn[i])
+            for g in self.ORDER:
+                getattr(self, "w" + g).append(nn.Linear(cur, n, bias=add_bias))
+            for g in self.ORDER:
+                getattr(self, "u" + g).append(nn.Linear(n, n, bias=False))
+            if self.orth:
+                for g in self.ORDER:
+                    nn.init.orthogonal_(getattr(self, "u" + g)[i].weight)
+            for g in self.ORDER:
+                getattr(self, "bn_w" + g).append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def forward(self, x, drop_masks=None):
+        if self.ln_inp:
+            x = self.ln0(x)
+        if self.bn_inp:
+            T, B, Fd = x.shape
+            x = self.bn0(x.reshape(T * B, Fd)).view(T, B, Fd)
+        for i, H in enumerate(self.lay):
+            if self.bidir:
+                x = torch.cat([x, flip_time(x)], 1)
+            T, B2, _ = x.shape
+            dm = self._drop_mask(i, B2, H, drop_masks)
+            pre = {}
+            for g in self.ORDER:
+                w = getattr(self, "w" + g)[i](x)
+                if self.use_bn[i]:
+                    w = getattr(self, "bn_w" + g)[i](w.reshape(T * B2, H)).view(T, B2, H)
+                pre[g] = w
+            h = torch.zeros(B2, H)
+            hs = []
+            for k in range(T):
+                h = self.cell(pre, k, h, i, dm)
+                if self.use_ln[i]:
+                    h = self.ln[i](h)
+                hs.append(h)
+            y = torch.stack(hs)
+            if self.bidir:
+                y = torch.cat([y[:, :B2 // 2], flip_time(y[:, B2 // 2:])], 2)
+            x = y
+        return x
+
+
+class minimalGRU(_PlainRec):
+    PREFIX, ORDER = "minimalgru", ("h", "z")
+
+    def cell(self, pre, k, h, i, dm):                            # :1751-1755
+        z = torch.sigmoid(pre["z"][k] + self.uz[i](h))
+        a = pre["h"][k] + self.uh[i](z * h)
+        return z * h + (1 - z) * (act_fn(self.acts[i], a) * dm)
+
+
+class RNN(_PlainRec):
+    PREFIX, ORDER = "rnn", ("h",)
+
+    def cell(self, pre, k, h, i, dm):                            # :1905-1907
+        return act_fn(self.acts[i], pre["h"][k] + self.uh[i](h)) * dm
+
+
 class LSTM(_Rec):
     """neural_networks.py:468-1112 (bidir forced 0 at :835, so only uni-directional)."""
 

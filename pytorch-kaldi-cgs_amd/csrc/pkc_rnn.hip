@@ -22,11 +22,23 @@
 // a step is two launches: (z, r, r*h) then (Uh (r*h), update).  Its BPTT step is two launches as
 // well: d(rh) = Uh^T da (then dr), and dh_{t-1} = Uz^T dz + Ur^T dr + carries (then dz, da).
 // r*h is kept for every step (rh, (T, B2, H)): it is the input of the Uh gradient matmul.
+// minimalGRU (neural_networks.py:1751-1755) is the same two-phase step with r replaced by z
+// (a = wh + Uh (z*h)); the plain RNN (:1905-1907, h = act(wh + Uh h)*drop) is one gate, one
+// launch per step.
 #include "pkc_common.h"
 
 namespace pkc {
 
 constexpr int RU = 16, RR = 16, RT = RU * RR, KC = 64;
+
+__host__ __device__ constexpr int cell_gates(int cell) {
+  return cell == PKC_CELL_LSTM ? 4 : cell == PKC_CELL_GRU ? 3 : cell == PKC_CELL_RNN ? 1 : 2;
+}
+// index of the candidate ("h") gate whose U multiplies r*h / z*h (two-phase cells)
+__host__ __device__ constexpr int cand_gate(int cell) { return cell == PKC_CELL_GRU ? 2 : 1; }
+__host__ __device__ constexpr bool two_phase(int cell) {
+  return cell == PKC_CELL_GRU || cell == PKC_CELL_MINGRU;
+}
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
@@ -163,7 +175,7 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
   const float m = drop_val(a, r, j, ix.B2);
   const float hp = hprev[(int64_t)r * H + j];
   float h;
-  if (CELL == PKC_CELL_GRU) {
+  if constexpr (CELL == PKC_CELL_GRU) {
     // phase 1 of a GRU step: update / reset gates and r*h (the input of Uh)
     const float z = sigm(a.wpre[pi] + acc[0]);
     const float rg = sigm(a.wpre[TBH + pi] + acc[1]);
@@ -172,7 +184,22 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
     a.rh[si] = rg * hp;
     return;
   }
-  if (CELL == PKC_CELL_LIGRU) {
+  if constexpr (CELL == PKC_CELL_MINGRU) {
+    // phase 1 of a minimalGRU step: update gate and z*h (the input of Uh)
+    const float z = sigm(a.wpre[pi] + acc[0]);
+    a.gates[si] = z;
+    a.rh[si] = z * hp;
+    return;
+  }
+  if constexpr (CELL == PKC_CELL_RNN) {
+    const float hcr = act_fwd(a.act, a.wpre[pi] + acc[0]);
+    h = hcr * m;
+    a.gates[si] = hcr;
+    a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+    a.y[ix.out(t, r, j)] = h;
+    return;
+  }
+  if constexpr (CELL == PKC_CELL_LIGRU) {
     // gates (z, h) -- liGRU
     const float z = sigm(a.wpre[pi] + acc[0]);
     const float hcr = act_fwd(a.act, a.wpre[TBH + pi] + acc[1]);
@@ -180,7 +207,7 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
     h = z * hp + (1.f - z) * hc;
     a.gates[si] = z;
     a.gates[TB2H + si] = hcr;
-  } else {
+  } else if constexpr (CELL == PKC_CELL_LSTM) {
     // gates (f, i, o, c) -- LSTM; cs[t] = c_{t-1}
     const float f = sigm(a.wpre[pi] + acc[0]);
     const float i = sigm(a.wpre[TBH + pi] + acc[1]);
@@ -199,7 +226,9 @@ __global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
   a.y[ix.out(t, r, j)] = h;
 }
 
-// phase 2 of a GRU step: a = wh + Uh (r*h_{t-1}); h = z*h_{t-1} + (1-z)*act(a)*drop
+// phase 2 of a GRU / minimalGRU step: a = wh + Uh (r*h_{t-1} | z*h_{t-1});
+// h = z*h_{t-1} + (1-z)*act(a)*drop.  HG: index of the candidate gate.
+template <int HG>
 __global__ __launch_bounds__(RT) void gru_fwd_h(pkc_rnn_args a, int t) {
   __shared__ float hsm[RR][KC + 1];
   __shared__ float usm[RU][KC + 1];
@@ -208,7 +237,7 @@ __global__ __launch_bounds__(RT) void gru_fwd_h(pkc_rnn_args a, int t) {
   const int r = blockIdx.y * RR + threadIdx.x / RU;
   const int H = a.H;
   const float* src = a.rh + (int64_t)t * ix.B2 * H;
-  const float* U = a.U[2];
+  const float* U = a.U[HG];
   float acc = 0.f;
   for (int k0 = 0; k0 < H; k0 += KC) {
     __syncthreads();
@@ -234,9 +263,9 @@ __global__ __launch_bounds__(RT) void gru_fwd_h(pkc_rnn_args a, int t) {
   const float m = drop_val(a, r, j, ix.B2);
   const float hp = a.hs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
   const float z = a.gates[si];
-  const float hcr = act_fwd(a.act, a.wpre[2 * TBH + pi] + acc);
+  const float hcr = act_fwd(a.act, a.wpre[HG * TBH + pi] + acc);
   const float h = z * hp + (1.f - z) * (hcr * m);
-  a.gates[2 * TB2H + si] = hcr;
+  a.gates[HG * TB2H + si] = hcr;
   a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
   a.y[ix.out(t, r, j)] = h;
 }
@@ -272,7 +301,7 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
   const int64_t si = ix.st(t, r, k);
   const float m = drop_val(a, r, k, ix.B2);
   const float hp = a.hs[(int64_t)t * ix.B2 * H + (int64_t)r * H + k];
-  if (CELL == PKC_CELL_LIGRU) {
+  if constexpr (CELL == PKC_CELL_LIGRU) {
     const float z = a.gates[si], hcr = a.gates[TB2H + si];
     const float hc = hcr * m;
     const float dz = g * (hp - hc);
@@ -280,12 +309,20 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
     dgo[0] = dz * z * (1.f - z);
     dgo[1] = dhc * m * act_bwd_out(a.act, hcr);   // act' from the post-activation value
     *g_out = g;
-  } else if (CELL == PKC_CELL_GRU) {
+  } else if constexpr (CELL == PKC_CELL_GRU) {
     // dz and da now; dr needs Uh^T da over the whole row (gru_bwd_rh)
     const float z = a.gates[si], hcr = a.gates[2 * TB2H + si];
     const float hc = hcr * m;
     dgo[0] = g * (hp - hc) * z * (1.f - z);
     dgo[2] = g * (1.f - z) * m * act_bwd_out(a.act, hcr);
+    *g_out = g;
+  } else if constexpr (CELL == PKC_CELL_MINGRU) {
+    // da now; dz also needs Uh^T da (gru_bwd_rh), g is kept for it
+    const float z = a.gates[si], hcr = a.gates[TB2H + si];
+    dgo[1] = g * (1.f - z) * m * act_bwd_out(a.act, hcr);
+    *g_out = g;
+  } else if constexpr (CELL == PKC_CELL_RNN) {
+    dgo[0] = g * m * act_bwd_out(a.act, a.gates[si]);
     *g_out = g;
   } else {
     const float f = a.gates[si], i = a.gates[TB2H + si], o = a.gates[2 * TB2H + si];
@@ -316,9 +353,11 @@ __global__ void rnn_bwd_init(pkc_rnn_args a) {
     const float g = dy_at(a, ix.out(t, r, k));
     float dg[4], go, dco = 0.f;
     gate_grads<CELL>(a, ix, t, r, k, g, 0.f, dg, &go, &dco);
-    if (CELL == PKC_CELL_GRU) {
+    if constexpr (CELL == PKC_CELL_GRU) {
       a.dgates[ix.st(t, r, k)] = dg[0];
       a.dgates[2 * TB2H + ix.st(t, r, k)] = dg[2];
+    } else if constexpr (CELL == PKC_CELL_MINGRU) {
+      a.dgates[TB2H + ix.st(t, r, k)] = dg[1];
     } else {
 #pragma unroll
       for (int q = 0; q < G; ++q) a.dgates[q * TB2H + ix.st(t, r, k)] = dg[q];
@@ -369,21 +408,31 @@ __global__ __launch_bounds__(RT) void rnn_bwd_step(pkc_rnn_args a, int tt) {
   const int64_t e = (int64_t)r * H + k;
   float dh = acc;
   float dc_carry = 0.f;
-  if (CELL == PKC_CELL_LIGRU) {
+  if constexpr (CELL == PKC_CELL_LIGRU) {
     dh += a.work[src * n + e] * a.gates[ix.st(t, r, k)];     // g_t * z_t
-  } else if (CELL == PKC_CELL_GRU) {
+  } else if constexpr (CELL == PKC_CELL_GRU) {
     // g_t * z_t + d(rh)_t * r_t  (acc = Uz^T dz_t + Ur^T dr_t)
     dh += a.work[src * n + e] * a.gates[ix.st(t, r, k)] +
           a.work[2 * n + e] * a.gates[TB2H + ix.st(t, r, k)];
+  } else if constexpr (CELL == PKC_CELL_MINGRU) {
+    // (g_t + d(zh)_t) * z_t  (acc = Uz^T dz_t)
+    dh += (a.work[src * n + e] + a.work[2 * n + e]) * a.gates[ix.st(t, r, k)];
+  } else if constexpr (CELL == PKC_CELL_RNN) {
+    // acc = Uh^T da_t is the whole recurrent gradient
   } else {
     dc_carry = a.work[2 * n + src * n + e];                  // dc_t * f_t
   }
   const float g = dy_at(a, ix.out(tt, r, k)) + dh;
   float dg[4], go, dco = 0.f;
   gate_grads<CELL>(a, ix, tt, r, k, g, dc_carry, dg, &go, &dco);
-  if (CELL == PKC_CELL_GRU) {
+  if constexpr (CELL == PKC_CELL_GRU) {
     a.dgates[ix.st(tt, r, k)] = dg[0];
     a.dgates[2 * TB2H + ix.st(tt, r, k)] = dg[2];
+    a.work[dst * n + e] = go;
+    return;
+  }
+  if constexpr (CELL == PKC_CELL_MINGRU) {
+    a.dgates[TB2H + ix.st(tt, r, k)] = dg[1];
     a.work[dst * n + e] = go;
     return;
   }
@@ -395,7 +444,9 @@ __global__ __launch_bounds__(RT) void rnn_bwd_step(pkc_rnn_args a, int tt) {
 
 // GRU: d(rh)_t[r][k] = sum_j da_t[r][j] Uh[j][k]; dr_t = d(rh) * h_{t-1} * r (1 - r).
 // d(rh)_t is kept in work[2n..3n) for the carry term of the next (earlier) step.
+template <int CELL>
 __global__ __launch_bounds__(RT) void gru_bwd_rh(pkc_rnn_args a, int t) {
+  constexpr int HG = cand_gate(CELL);
   __shared__ float dsm[RR][KC + 1];
   __shared__ float usm[KC][RU + 1];
   const RnnIdx ix = mkidx(a);
@@ -404,14 +455,14 @@ __global__ __launch_bounds__(RT) void gru_bwd_rh(pkc_rnn_args a, int t) {
   const int r = blockIdx.y * RR + threadIdx.x / RU;
   const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
   const int64_t n = (int64_t)ix.B2 * H;
-  const float* U = a.U[2];
+  const float* U = a.U[HG];
   float acc = 0.f;
   for (int j0 = 0; j0 < H; j0 += KC) {
     __syncthreads();
     for (int e = threadIdx.x; e < RR * KC; e += RT) {
       const int rr = e / KC, jj = e % KC;
       const int R = blockIdx.y * RR + rr, J = j0 + jj;
-      dsm[rr][jj] = (R < ix.B2 && J < H) ? a.dgates[2 * TB2H + ix.st(t, R, J)] : 0.f;
+      dsm[rr][jj] = (R < ix.B2 && J < H) ? a.dgates[HG * TB2H + ix.st(t, R, J)] : 0.f;
     }
     for (int e = threadIdx.x; e < KC * RU; e += RT) {
       const int jj = e / RU, kk = e % RU;
@@ -426,15 +477,22 @@ __global__ __launch_bounds__(RT) void gru_bwd_rh(pkc_rnn_args a, int t) {
   if (r >= ix.B2 || k >= H) return;
   const int64_t e = (int64_t)r * H + k, si = ix.st(t, r, k);
   const float hp = a.hs[(int64_t)t * ix.B2 * H + e];
-  const float rg = a.gates[TB2H + si];
-  a.dgates[TB2H + si] = acc * hp * rg * (1.f - rg);
+  if constexpr (CELL == PKC_CELL_GRU) {
+    const float rg = a.gates[TB2H + si];
+    a.dgates[TB2H + si] = acc * hp * rg * (1.f - rg);
+  } else {
+    // minimalGRU: dz = g (h_{t-1} - hc) + d(zh) h_{t-1}; g_t sits in the ping-pong slot of step t
+    const float g = a.work[((a.T - 1 - t) & 1) * n + e];
+    const float z = a.gates[si], hc = a.gates[TB2H + si] * drop_val(a, r, k, ix.B2);
+    a.dgates[si] = (g * (hp - hc) + acc * hp) * z * (1.f - z);
+  }
   a.work[2 * n + e] = acc;
 }
 
 // fold the per-direction gate gradients (G, T, B2, H) onto the (G, T, B, H) pre-activation rows
 __global__ void rnn_fold_kernel(pkc_rnn_args a, float* dpre) {
   const RnnIdx ix = mkidx(a);
-  const int G = a.cell == PKC_CELL_LSTM ? 4 : (a.cell == PKC_CELL_GRU ? 3 : 2);
+  const int G = cell_gates(a.cell);
   const int64_t TBH = (int64_t)a.T * a.B * a.H;
   const int64_t TB2H = (int64_t)a.T * ix.B2 * a.H;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)G * TBH;
@@ -454,16 +512,17 @@ template <int G, int CELL>
 static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
   hipMemsetAsync(a->hs, 0, sizeof(float) * (size_t)B2 * a->H, s);            // h_init = 0
-  if (CELL == PKC_CELL_LSTM) hipMemsetAsync(a->cs, 0, sizeof(float) * (size_t)B2 * a->H, s);
+  if constexpr (CELL == PKC_CELL_LSTM) hipMemsetAsync(a->cs, 0, sizeof(float) * (size_t)B2 * a->H, s);
   if (a->train && a->drop_p > 0.f) {
     hipLaunchKernelGGL(rnn_drop_mask_kernel, dim3(64), dim3(256), 0, s, *a, B2);
     PKC_LAUNCH_CHECK("pkc_rnn_fwd drop mask");
   }
   dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
-  if (CELL == PKC_CELL_GRU) {
+  if constexpr (two_phase(CELL)) {
+    // phase 1 multiplies the gates that read h (GRU: z, r; minimalGRU: z) = all but the candidate
     for (int t = 0; t < a->T; ++t) {
-      hipLaunchKernelGGL((rnn_fwd_step<2, PKC_CELL_GRU, false>), grid, dim3(RT), 0, s, *a, t);
-      hipLaunchKernelGGL(gru_fwd_h, grid, dim3(RT), 0, s, *a, t);
+      hipLaunchKernelGGL((rnn_fwd_step<G - 1, CELL, false>), grid, dim3(RT), 0, s, *a, t);
+      hipLaunchKernelGGL(gru_fwd_h<cand_gate(CELL)>, grid, dim3(RT), 0, s, *a, t);
     }
     PKC_LAUNCH_CHECK("pkc_rnn_fwd gru step");
     return PKC_OK;
@@ -484,11 +543,11 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
   dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
-  if (CELL == PKC_CELL_GRU) {
-    hipLaunchKernelGGL(gru_bwd_rh, grid, dim3(RT), 0, s, *a, a->T - 1);
+  if constexpr (two_phase(CELL)) {
+    hipLaunchKernelGGL(gru_bwd_rh<CELL>, grid, dim3(RT), 0, s, *a, a->T - 1);
     for (int tt = a->T - 2; tt >= 0; --tt) {
-      hipLaunchKernelGGL((rnn_bwd_step<2, PKC_CELL_GRU>), grid, dim3(RT), 0, s, *a, tt);
-      hipLaunchKernelGGL(gru_bwd_rh, grid, dim3(RT), 0, s, *a, tt);
+      hipLaunchKernelGGL((rnn_bwd_step<G - 1, CELL>), grid, dim3(RT), 0, s, *a, tt);
+      hipLaunchKernelGGL(gru_bwd_rh<CELL>, grid, dim3(RT), 0, s, *a, tt);
     }
   } else {
     for (int tt = a->T - 2; tt >= 0; --tt)
@@ -502,12 +561,14 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
 
 static int check(const pkc_rnn_args* a, bool bwd) {
   PKC_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->H > 0, "pkc_rnn: bad shape");
-  PKC_CHECK_ARG(a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM || a->cell == PKC_CELL_GRU,
-                "pkc_rnn: bad cell %d", a->cell);
-  PKC_CHECK_ARG(a->cell != PKC_CELL_GRU || (a->rh && a->qbits <= 0), "pkc_rnn: GRU needs rh, no qbits");
+  PKC_CHECK_ARG(a->cell >= PKC_CELL_LIGRU && a->cell <= PKC_CELL_RNN, "pkc_rnn: bad cell %d", a->cell);
+  PKC_CHECK_ARG(!two_phase(a->cell) || (a->rh && a->qbits <= 0),
+                "pkc_rnn: GRU / minimalGRU need rh and no qbits");
+  PKC_CHECK_ARG(a->cell == PKC_CELL_LSTM || a->cell == PKC_CELL_LIGRU || a->qbits <= 0,
+                "pkc_rnn: input quantisation only for LSTM / liGRU");
   PKC_CHECK_ARG(a->wpre && a->hs && a->gates && a->y, "pkc_rnn: null buffer");
   PKC_CHECK_ARG(a->cell != PKC_CELL_LSTM || a->cs, "pkc_rnn: LSTM needs cs");
-  const int G = a->cell == PKC_CELL_LSTM ? 4 : (a->cell == PKC_CELL_GRU ? 3 : 2);
+  const int G = cell_gates(a->cell);
   for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U[g], "pkc_rnn: null U[%d]", g);
   PKC_CHECK_ARG(!a->train || a->drop_p <= 0.f || a->drop_mask, "pkc_rnn: dropout needs drop_mask");
   if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work, "pkc_rnn_bwd: null buffer");
@@ -524,6 +585,8 @@ extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
   if (st) return st;
   if (a->cell == PKC_CELL_LIGRU) return fwd_impl<2, PKC_CELL_LIGRU>(a, S(stream));
   if (a->cell == PKC_CELL_GRU) return fwd_impl<3, PKC_CELL_GRU>(a, S(stream));
+  if (a->cell == PKC_CELL_MINGRU) return fwd_impl<2, PKC_CELL_MINGRU>(a, S(stream));
+  if (a->cell == PKC_CELL_RNN) return fwd_impl<1, PKC_CELL_RNN>(a, S(stream));
   return fwd_impl<4, PKC_CELL_LSTM>(a, S(stream));
 }
 
@@ -534,5 +597,7 @@ extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
   PKC_CHECK_ARG(dpre, "pkc_rnn_bwd: null dpre");
   if (a->cell == PKC_CELL_LIGRU) return bwd_impl<2, PKC_CELL_LIGRU>(a, dpre, S(stream));
   if (a->cell == PKC_CELL_GRU) return bwd_impl<3, PKC_CELL_GRU>(a, dpre, S(stream));
+  if (a->cell == PKC_CELL_MINGRU) return bwd_impl<2, PKC_CELL_MINGRU>(a, dpre, S(stream));
+  if (a->cell == PKC_CELL_RNN) return bwd_impl<1, PKC_CELL_RNN>(a, dpre, S(stream));
   return bwd_impl<4, PKC_CELL_LSTM>(a, dpre, S(stream));
 }

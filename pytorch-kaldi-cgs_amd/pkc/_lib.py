@@ -54,7 +54,7 @@ class OptTensor(C.Structure):
                 ("qout", vp), ("qbits", C.c_int), ("bout", vp)]
 
 
-CELL_LIGRU, CELL_LSTM, CELL_GRU = 0, 1, 2
+CELL_LIGRU, CELL_LSTM, CELL_GRU, CELL_MINGRU, CELL_RNN = 0, 1, 2, 3, 4
 
 
 class RnnArgs(C.Structure):

@@ -175,8 +175,12 @@ class RecNode:
     def __init__(self, arch, net, K):
         self.arch, self.net, self.K = arch, net, K
         self.name = arch
-        self.cell = {"lstm": L.CELL_LSTM, "gru": L.CELL_GRU, "ligru": L.CELL_LIGRU}[net.cell]
-        self.G = {L.CELL_LSTM: 4, L.CELL_GRU: 3, L.CELL_LIGRU: 2}[self.cell]
+        self.cell = {"lstm": L.CELL_LSTM, "gru": L.CELL_GRU, "ligru": L.CELL_LIGRU,
+                     "minimalgru": L.CELL_MINGRU, "rnn": L.CELL_RNN}[net.cell]
+        self.G = {L.CELL_LSTM: 4, L.CELL_GRU: 3, L.CELL_LIGRU: 2, L.CELL_MINGRU: 2,
+                  L.CELL_RNN: 1}[self.cell]
+        # two-phase cells: the candidate gate's U multiplies r*h (GRU) / z*h (minimalGRU)
+        self.cand = {L.CELL_GRU: 2, L.CELL_MINGRU: 1}.get(self.cell)
         self.layers = net.layer_specs()
         self.N = net.out_dim
         self.src = None
@@ -587,7 +591,7 @@ class Engine:
                       work=_f32(L.lib().pkc_dense_work_size(M, H), dev),
                       hs=_f32((T + 1) * B2 * H, dev),
                       cs=_f32((T + 1) * B2 * H, dev) if n.cell == L.CELL_LSTM else None,
-                      rh=_f32(T * B2 * H, dev) if n.cell == L.CELL_GRU else None,
+                      rh=_f32(T * B2 * H, dev) if n.cand is not None else None,
                       gates=_f32(G * T * B2 * H, dev), y=_f32(M * D, dev),
                       drop=_f32(B2 * H, dev), dgates=_f32(G * T * B2 * H, dev),
                       dpre=_f32(G * M * H, dev), dz=_f32(G * M * H, dev),
@@ -1218,7 +1222,7 @@ class Engine:
                         C.c_void_p(x_ptr), ldx, ptr(lb["dW"][g]), K, 1, 0, s)
                 # dU = sum_t dgates[t]^T h_{t-1}: K = T*B2 rows of hs[0:T] (GRU Uh: r*h_{t-1})
                 R2 = T * lb["B2"]
-                usrc = lb["rh"] if (n.cell == L.CELL_GRU and g == 2) else hsrc
+                usrc = lb["rh"] if g == n.cand else hsrc
                 self._k("rnn_gemm_dU %dx%dx%d" % (H, H, R2), 2.0 * R2 * H * H,
                         4.0 * (2 * R2 * H + H * H), "pkc_gemm", self.prec, 0, 0, H, H, R2,
                         C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,

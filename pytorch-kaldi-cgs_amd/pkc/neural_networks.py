@@ -427,6 +427,109 @@ class GRU(nn.Module):
         return specs
 
 
+class _PlainRec(nn.Module):
+    """Shared construction of the reference's hook-free recurrent families (minimalGRU, RNN):
+    option keys <prefix>_lay/_drop/_use_batchnorm/..., input Linears w<g> (bias only without
+    BN/LN), recurrent Linears u<g> (no bias, optional orthogonal init), bn_w<g>, ln."""
+
+    seq_model = True
+    PREFIX = ""
+    GATES = ()
+    INIT_ORDER = ()         # reference registration / init order of the gate letters
+
+    def __init__(self, options, inp_dim):
+        super().__init__()
+        o, p = options, self.PREFIX
+        self.input_dim = inp_dim
+        self.lay = _lst(o, p + "_lay", int)
+        self.drop = _lst(o, p + "_drop", float)
+        self.use_bn = _lst(o, p + "_use_batchnorm", strtobool)
+        self.use_ln = _lst(o, p + "_use_laynorm", strtobool)
+        self.ln_inp = strtobool(o[p + "_use_laynorm_inp"])
+        self.bn_inp = strtobool(o[p + "_use_batchnorm_inp"])
+        self.orthinit = strtobool(o[p + "_orthinit"])
+        self.acts = _lst(o, p + "_act")
+        self.bidir = strtobool(o[p + "_bidir"])
+        self.to_do = o.get("to_do", "train")
+        self.prune = False
+        self.guided_hcgs = False
+        self.apply_guided_hcgs = False
+        self.if_pattern = False
+        self.skip_regularization = strtobool(o.get("skip_regularization", "False"))
+        for g in self.INIT_ORDER:
+            setattr(self, "w" + g, nn.ModuleList())
+            setattr(self, "u" + g, nn.ModuleList())
+        self.ln = nn.ModuleList()
+        for g in self.INIT_ORDER:
+            setattr(self, "bn_w" + g, nn.ModuleList())
+        if self.ln_inp:
+            self.ln0 = LayerNorm(inp_dim)
+        if self.bn_inp:
+            self.bn0 = nn.BatchNorm1d(inp_dim, momentum=0.05)
+        cur = inp_dim
+        for i, n in enumerate(self.lay):
+            add_bias = not (self.use_ln[i] or self.use_bn[i])
+            for g in self.INIT_ORDER:
+                getattr(self, "w" + g).append(nn.Linear(cur, n, bias=add_bias))
+            for g in self.INIT_ORDER:
+                getattr(self, "u" + g).append(nn.Linear(n, n, bias=False))
+            if self.orthinit:
+                for g in self.INIT_ORDER:
+                    nn.init.orthogonal_(getattr(self, "u" + g)[i].weight)
+            for g in self.INIT_ORDER:
+                getattr(self, "bn_w" + g).append(nn.BatchNorm1d(n, momentum=0.05))
+            self.ln.append(LayerNorm(n))
+            cur = 2 * n if self.bidir else n
+        self.out_dim = cur
+
+    def prune_parameters(self):
+        raise NotImplementedError("the reference %s has no prune hook" % type(self).__name__)
+
+    def check_supported(self):
+        if self.ln_inp or self.bn_inp or any(self.use_ln):
+            raise NotImplementedError("LayerNorm / input normalisation in %s is not on the pkc "
+                                      "path yet" % type(self).__name__)
+
+    def layer_specs(self):
+        specs = []
+        for i, n in enumerate(self.lay):
+            specs.append(dict(H=n, act=self.acts[i], bn=bool(self.use_bn[i]), drop=self.drop[i],
+                              bidir=bool(self.bidir),
+                              W=[getattr(self, "w" + g)[i].weight for g in self.GATES],
+                              b=[getattr(self, "w" + g)[i].bias for g in self.GATES],
+                              U=[getattr(self, "u" + g)[i].weight for g in self.GATES],
+                              bnm=[getattr(self, "bn_w" + g)[i] for g in self.GATES],
+                              Wmask=None, Umask=None))
+        return specs
+
+
+class minimalGRU(_PlainRec):
+    """neural_networks.py:1602-1777: z = sig(wz + Uz h); h = z h + (1-z) act(wh + Uh (z*h))*drop.
+    Reference attribute names (minimalgru_lay, ...) are aliased below."""
+
+    PREFIX = "minimalgru"
+    cell = "minimalgru"
+    GATES = ("z", "h")
+    INIT_ORDER = ("h", "z")
+
+    def __init__(self, options, inp_dim):
+        super().__init__(options, inp_dim)
+        self.minimalgru_lay, self.minimalgru_drop = self.lay, self.drop
+
+
+class RNN(_PlainRec):
+    """neural_networks.py:1780-1931: h = act(wh + Uh h) * drop."""
+
+    PREFIX = "rnn"
+    cell = "rnn"
+    GATES = ("h",)
+    INIT_ORDER = ("h",)
+
+    def __init__(self, options, inp_dim):
+        super().__init__(options, inp_dim)
+        self.rnn_lay, self.rnn_drop = self.lay, self.drop
+
+
 class LSTM(_PatternSet, nn.Module):
     """neural_networks.py:468-1237.  The reference forces bidir off inside forward (:835), so a
     bidirectional cfg crashes there on layer 2; pkc runs bidirectional LSTMs with the liGRU

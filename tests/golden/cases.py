@@ -99,3 +99,16 @@ GRU_DEF = dict(gru_lay="16,16", gru_drop="0.0,0.0", gru_use_laynorm_inp="False",
 GRU_CASES = [("gru_bidir", GRU_DEF, 7, 3, 20, 31),
              ("gru_uni_nobn", dict(GRU_DEF, gru_bidir="False", gru_use_batchnorm="False,False",
                                    gru_act="tanh,tanh", gru_orthinit="False"), 6, 2, 12, 32)]
+
+MINGRU_DEF = {k.replace("gru_", "minimalgru_"): v for k, v in GRU_DEF.items()}
+RNN_DEF = {k.replace("gru_", "rnn_"): v for k, v in GRU_DEF.items()}
+# (tag, class, options, T, B, F, seed): minimalGRU / RNN golden cases (tests/golden/gru.npz)
+PLAIN_CASES = [("mingru_bidir", "minimalGRU", MINGRU_DEF, 7, 3, 20, 33),
+               ("mingru_uni_nobn", "minimalGRU", dict(MINGRU_DEF, minimalgru_bidir="False",
+                                                       minimalgru_use_batchnorm="False,False",
+                                                       minimalgru_act="tanh,tanh",
+                                                       minimalgru_orthinit="False"), 6, 2, 12, 34),
+               ("rnn_bidir", "RNN", RNN_DEF, 7, 3, 20, 35),
+               ("rnn_uni_nobn", "RNN", dict(RNN_DEF, rnn_bidir="False",
+                                            rnn_use_batchnorm="False,False", rnn_act="tanh,relu",
+                                            rnn_orthinit="False"), 6, 2, 12, 36)]

@@ -347,6 +347,9 @@ def gen_gru():
     out = {}
     for tag, opts, T, B, F, seed in GRU_CASES:
         run_rnn(neural_networks.GRU, opts, T, B, F, seed, out, tag)
+    from cases import PLAIN_CASES
+    for tag, cls, opts, T, B, F, seed in PLAIN_CASES:
+        run_rnn(getattr(neural_networks, cls), opts, T, B, F, seed, out, tag)
     np.savez_compressed(os.path.join(OUT, "gru.npz"), **out)
 
 

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN
-from cases import GRU_CASES, LIGRU_DEF, LSTM_DEF
+from cases import GRU_CASES, PLAIN_CASES, LIGRU_DEF, LSTM_DEF
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -56,14 +56,15 @@ CASES = [("ligru_bidir", "liGRU", LIGRU_DEF, 7, 3, 20, 21),
          ("lstm_hcgs_quant", "LSTM", dict(LSTM_DEF, lstm_hcgs="True", lstm_quant="True",
                                           lstm_quant_inp="True"), 7, 3, 24, 24),
          ("lstm_pattern", "LSTM", dict(LSTM_DEF, **PATTERN), 5, 2, 24, 25)] + \
-        [(tag, "GRU", opts, T, B, F, seed) for tag, opts, T, B, F, seed in GRU_CASES]
+        [(tag, "GRU", opts, T, B, F, seed) for tag, opts, T, B, F, seed in GRU_CASES] + PLAIN_CASES
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_recurrent_layer_matches_reference(case):
     import pkc.neural_networks as NN
     tag, cls, opts, T, B, F, seed = case
-    g = np.load(os.path.join(GOLDEN, "gru.npz" if cls == "GRU" else "rnn.npz"), allow_pickle=False)
+    g = np.load(os.path.join(GOLDEN, "gru.npz" if cls in ("GRU", "minimalGRU", "RNN") else "rnn.npz"),
+                allow_pickle=False)
     torch.manual_seed(seed)
     np.random.seed(seed)
     net = getattr(NN, cls)(section(opts), F)
@@ -88,7 +89,7 @@ def test_recurrent_layer_matches_reference(case):
     grads = {}
     for li, lb in enumerate(node.lbuf):
         for gi, gate in enumerate(net.GATES):
-            if cls in ("liGRU", "GRU"):
+            if cls in ("liGRU", "GRU", "minimalGRU", "RNN"):
                 if lb["db"][gi] is not None:
                     grads["w%s.%d.bias" % (gate, li)] = lb["db"][gi]
                 grads["w%s.%d.weight" % (gate, li)] = lb["dW"][gi]

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from cases import GRU_DEF, LIGRU_DEF, LSTM_DEF
+from cases import GRU_DEF, LIGRU_DEF, LSTM_DEF, MINGRU_DEF, RNN_DEF
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -29,6 +29,12 @@ def make_cfg(body):
                          hcgsh_block="8,4", hcgsh_sparse="25,50", **opt)
     elif body == "gru":            # GRU (neural_networks.py:1240-1426), bidirectional
         cfg["a1"] = dict(GRU_DEF, arch_name="rnn", gru_lay="32,24", gru_drop="0.2,0.2", **opt)
+    elif body == "mingru":
+        cfg["a1"] = dict(MINGRU_DEF, arch_name="rnn", minimalgru_lay="32,24",
+                         minimalgru_drop="0.2,0.2", **opt)
+    elif body == "rnn":
+        cfg["a1"] = dict(RNN_DEF, arch_name="rnn", rnn_lay="32,24", rnn_drop="0.2,0.2",
+                         rnn_act="tanh,relu", **opt)
     elif body == "lstm_gl":        # TIMIT_CGS/TIMIT_LSTM_fmllr_groupLasso.cfg: group lasso on the LSTM
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", skip_regularization="False", **opt)
@@ -61,7 +67,8 @@ def make_cfg(body):
 
 
 @pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune",
-                                  "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply", "gru"])
+                                  "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply", "gru", "mingru",
+                                  "rnn"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -79,7 +86,8 @@ def test_seq_engine_vs_oracle(body):
         np.random.seed(3)
         cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM",
                 "lstm_prune": "LSTM", "lstm_gl": "LSTM", "lstm_ghcgs_l1": "LSTM",
-                "lstm_ghcgs_apply": "LSTM", "gru": "GRU"}[body]
+                "lstm_ghcgs_apply": "LSTM", "gru": "GRU", "mingru": "minimalGRU",
+                "rnn": "RNN"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)

@@ -200,17 +200,19 @@ def test_product_guided_init_matches_oracle(cls):
             assert torch.equal(v, nets[1].state_dict()[k]), k
 
 
-@pytest.mark.parametrize("case", ["gru_bidir", "gru_uni_nobn"])
+@pytest.mark.parametrize("case", ["gru_bidir", "gru_uni_nobn", "mingru_bidir", "mingru_uni_nobn",
+                                  "rnn_bidir", "rnn_uni_nobn"])
 def test_product_gru_init_matches_reference(case):
     import pkc.neural_networks as NN
-    from cases import GRU_CASES
-    tag, opts, T, B, F, seed = [c for c in GRU_CASES if c[0] == case][0]
+    from cases import GRU_CASES, PLAIN_CASES
+    allc = [(t, "GRU", o, T, B, F, sd) for t, o, T, B, F, sd in GRU_CASES] + PLAIN_CASES
+    tag, cls, opts, T, B, F, seed = [c for c in allc if c[0] == case][0]
     cp = configparser.ConfigParser()
     cp["s"] = {k: str(v) for k, v in opts.items()}
     g = G("gru.npz")
     torch.manual_seed(seed)
     np.random.seed(seed)
-    sd = NN.GRU(cp["s"], F).state_dict()
+    sd = getattr(NN, cls)(cp["s"], F).state_dict()
     ref_keys = sorted(k[len(tag) + 6:] for k in g.files if k.startswith(tag + "/init/"))
     assert sorted(sd) == ref_keys
     for k, v in sd.items():
