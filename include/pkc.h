@@ -260,7 +260,7 @@ int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double*
  * Dropout: bernoulli(1-p) mask per (row, unit), shared by all steps and NOT rescaled; (1-p) at eval.
  * pkc_rnn_bwd: dy = dL/dy (layer output layout); writes dgates (G, T, B2, H) = dL/d pre-activation
  * per direction and dpre (G, T, B, H) = the same folded over directions (input of the BN / W
- * backward); work = 4*B2*H floats.
+ * backward); work = 8*B2*H floats (carries + per-gate partial products).
  * ------------------------------------------------------------------------------------------- */
 enum { PKC_CELL_LIGRU = 0, PKC_CELL_LSTM = 1, PKC_CELL_GRU = 2, PKC_CELL_MINGRU = 3, PKC_CELL_RNN = 4 };
 typedef struct {
@@ -281,6 +281,8 @@ typedef struct {
   /* GRU / minimalGRU: r*h_{t-1} (z*h_{t-1}) per step, (T, B2, H) — the input of the Uh product
    * and of its gradient matmul.  NULL for the other cells. */
   float* rh;
+  /* pkc_rnn_bwd: G x H x H scratch for the transposed U (the B operand of the BPTT products) */
+  float* ut;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
 /* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that

@@ -1,35 +1,42 @@
-// pkc_rnn.hip — the serial time loops of liGRU and LSTM layers (forward and BPTT).
+// pkc_rnn.hip — the serial time loops of the recurrent layers (forward and BPTT).
 //
 // Reference: liGRU  neural_networks.py:1573-1584 (z = sig(wz+Uz h); hc = act(wh+Uh h)*drop;
 //                   h = z*h + (1-z)*hc), shared-weight bidirectional rows via cat/flip
 //                   (:1536-1538, :1590-1594);
 //            LSTM   neural_networks.py:1077-1097 (f,i,o = sig(w+U h); c = i*act(wc+Uc h)*drop + f*c;
-//                   h = o*act(c)).
+//                   h = o*act(c));
+//            GRU    :1390-1396 (z, r = sig(w + U h); h = z*h + (1-z)*act(wh + Uh (r*h))*drop);
+//            minimalGRU :1751-1755 (GRU with r replaced by z); RNN :1905-1907 (h = act(wh+Uh h)*drop).
 // The input projections W x (+BN) are one big MFMA matmul over all T*B rows outside the loop
-// (pkc_gemm + pkc_dense_fwd); here each time step is ONE launch that computes every gate's
-// recurrent product U h_{t-1} for a 16-unit x 16-row tile and applies the cell update in the
-// epilogue.  Bidirectional layers run both directions as one 2B-row batch: row r < B reads time t,
-// row r >= B reads time T-1-t of the same (T, B, H) pre-activations (the reference's flip), and
-// writes its h into the second half of the (T, B, 2H) output at T-1-t.
+// (pkc_gemm + pkc_dense_fwd).  Bidirectional layers run both directions as one 2B-row batch:
+// row r < B reads time t, row r >= B reads time T-1-t of the same (T, B, H) pre-activations (the
+// reference's flip) and writes its h into the second half of the (T, B, 2H) output at T-1-t.
 //
-// BPTT: one launch per step.  For its 16-unit column slice k the kernel forms
-//   dh_{t-1}[r][k] = sum_g sum_j da_g[t][r][j] * U_g[j][k]   (+ elementwise carry terms)
-// and immediately turns it into the gate gradients of step t-1 at (r, k), so the loop needs no
-// second launch per step.  dU and dW are big matmuls after the loop.
+// Per time step the recurrent products are skinny matmuls [B2 x H] x [H x G*H] — a few hundred
+// MFLOP for the 4x1024 LSTM, i.e. ~2 us of the chip's whole fp32 MFMA rate.  Each step is one
+// launch of 256-thread workgroups that each own a 32-row x 16-column output tile and run exact-fp32
+// v_mfma_f32_16x16x4_f32 chains over the whole contraction: the 4 waves x 4 lane groups split the
+// contraction into 16 contiguous k-blocks of S values, every lane streams its k-block of one A row
+// pair and one B row straight from global memory into registers (no LDS staging: each operand
+// byte is used by exactly one lane), the four waves' partial tiles are summed in LDS and the cell
+// update runs in the epilogue on the finished tile.  The forward tile holds all G gates of 16/G
+// units, so the update needs nothing from other workgroups.
 //
-// GRU (neural_networks.py:1390-1396: z, r = sig(w + U h); a = wh + Uh (r*h); hc = act(a)*drop;
-// h = z*h + (1-z)*hc) multiplies Uh with r*h, which needs the r of every unit of the row first, so
-// a step is two launches: (z, r, r*h) then (Uh (r*h), update).  Its BPTT step is two launches as
-// well: d(rh) = Uh^T da (then dr), and dh_{t-1} = Uz^T dz + Ur^T dr + carries (then dz, da).
-// r*h is kept for every step (rh, (T, B2, H)): it is the input of the Uh gradient matmul.
-// minimalGRU (neural_networks.py:1751-1755) is the same two-phase step with r replaced by z
-// (a = wh + Uh (z*h)); the plain RNN (:1905-1907, h = act(wh + Uh h)*drop) is one gate, one
-// launch per step.
+// BPTT: dh_{t-1}[r][k] = sum_g sum_j dg_g[t][r][j] U_g[j][k] contracts over G*H, so the step is
+// split by gate across workgroups (B operand from a per-layer transposed copy U^T, made once per
+// backward pass); the G partial tiles go to slabs and a small elementwise launch sums them and
+// applies the carries and the gate gradients of step t-1.  One-gate products (RNN, the minimalGRU
+// step, the d(r*h) / d(z*h) phases of the two-phase cells) finish in the matmul's own epilogue.
+//
+// GRU / minimalGRU multiply Uh with r*h (z*h), which needs r (z) of every unit of the row first:
+// their forward step is two launches (gates that read h, then the candidate), their BPTT step two
+// as well (d(rh) = Uh^T da then dr / dz, and dh_{t-1}).  r*h is kept per step (rh, (T, B2, H)):
+// it is the input of the Uh gradient matmul.
 #include "pkc_common.h"
 
 namespace pkc {
 
-constexpr int RU = 16, RR = 16, RT = RU * RR, KC = 64;
+constexpr int RT = 256;          // threads per workgroup (4 waves)
 
 __host__ __device__ constexpr int cell_gates(int cell) {
   return cell == PKC_CELL_LSTM ? 4 : cell == PKC_CELL_GRU ? 3 : cell == PKC_CELL_RNN ? 1 : 2;
@@ -112,163 +119,6 @@ __device__ void h_quant_vars(const float* hprev, int64_t n, float scale, float* 
   }
 }
 
-// ------------------------------------------------------------------------------- forward step
-template <int G, int CELL, bool QH>
-__global__ __launch_bounds__(RT) void rnn_fwd_step(pkc_rnn_args a, int t) {
-  __shared__ float hsm[QH ? G : 1][RR][KC + 1];
-  __shared__ float usm[G][RU][KC + 1];
-  const RnnIdx ix = mkidx(a);
-  const int j = blockIdx.x * RU + threadIdx.x % RU;
-  const int r = blockIdx.y * RR + threadIdx.x / RU;
-  const int H = a.H;
-  const float* hprev = a.hs + (int64_t)t * ix.B2 * H;     // hs[t] = h_{t-1}
-  float vars[4] = {0.f, 0.f, 0.f, 0.f};
-  const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
-  if (QH) h_quant_vars<G>(hprev, (int64_t)ix.B2 * H, qscale, vars);
-  float acc[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) acc[g] = 0.f;
-  for (int k0 = 0; k0 < H; k0 += KC) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < RR * KC; e += RT) {
-      const int rr = e / KC, kk = e % KC;
-      const int R = blockIdx.y * RR + rr, K = k0 + kk;
-      float v = (R < ix.B2 && K < H) ? hprev[(int64_t)R * H + K] : 0.f;
-      if (QH) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          v = qin(v, vars[g], qscale);
-          hsm[g][rr][kk] = v;
-        }
-      } else {
-        hsm[0][rr][kk] = v;
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-      for (int e = threadIdx.x; e < RU * KC; e += RT) {
-        const int jj = e / KC, kk = e % KC;
-        const int J = blockIdx.x * RU + jj, K = k0 + kk;
-        usm[g][jj][kk] = (J < H && K < H) ? a.U[g][(int64_t)J * H + K] : 0.f;
-      }
-    __syncthreads();
-    const int rl = threadIdx.x / RU, jl = threadIdx.x % RU;
-#pragma unroll 8
-    for (int kk = 0; kk < KC; ++kk) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) acc[g] = fmaf(usm[g][jl][kk], hsm[QH ? g : 0][rl][kk], acc[g]);
-    }
-  }
-  if (r >= ix.B2 || j >= H) return;
-  if (QH) {
-    // the hidden state the reference keeps for step t-1 (hiddens[t-1], and the saved input of the
-    // U backward) is the 4x re-quantised tensor; the last step's h is never quantised
-    float v = hprev[(int64_t)r * H + j];
-#pragma unroll
-    for (int g = 0; g < G; ++g) v = qin(v, vars[g], qscale);
-    a.hq[(int64_t)t * ix.B2 * H + (int64_t)r * H + j] = v;
-    if (t > 0) a.y[ix.out(t - 1, r, j)] = v;
-  }
-  const int64_t TBH = (int64_t)a.T * a.B * H;   // gate stride of the (G, T, B, H) pre-activations
-  const int64_t TB2H = (int64_t)a.T * ix.B2 * H; // gate stride of the saved activations
-  const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
-  const float m = drop_val(a, r, j, ix.B2);
-  const float hp = hprev[(int64_t)r * H + j];
-  float h;
-  if constexpr (CELL == PKC_CELL_GRU) {
-    // phase 1 of a GRU step: update / reset gates and r*h (the input of Uh)
-    const float z = sigm(a.wpre[pi] + acc[0]);
-    const float rg = sigm(a.wpre[TBH + pi] + acc[1]);
-    a.gates[si] = z;
-    a.gates[TB2H + si] = rg;
-    a.rh[si] = rg * hp;
-    return;
-  }
-  if constexpr (CELL == PKC_CELL_MINGRU) {
-    // phase 1 of a minimalGRU step: update gate and z*h (the input of Uh)
-    const float z = sigm(a.wpre[pi] + acc[0]);
-    a.gates[si] = z;
-    a.rh[si] = z * hp;
-    return;
-  }
-  if constexpr (CELL == PKC_CELL_RNN) {
-    const float hcr = act_fwd(a.act, a.wpre[pi] + acc[0]);
-    h = hcr * m;
-    a.gates[si] = hcr;
-    a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
-    a.y[ix.out(t, r, j)] = h;
-    return;
-  }
-  if constexpr (CELL == PKC_CELL_LIGRU) {
-    // gates (z, h) -- liGRU
-    const float z = sigm(a.wpre[pi] + acc[0]);
-    const float hcr = act_fwd(a.act, a.wpre[TBH + pi] + acc[1]);
-    const float hc = hcr * m;
-    h = z * hp + (1.f - z) * hc;
-    a.gates[si] = z;
-    a.gates[TB2H + si] = hcr;
-  } else if constexpr (CELL == PKC_CELL_LSTM) {
-    // gates (f, i, o, c) -- LSTM; cs[t] = c_{t-1}
-    const float f = sigm(a.wpre[pi] + acc[0]);
-    const float i = sigm(a.wpre[TBH + pi] + acc[1]);
-    const float o = sigm(a.wpre[2 * TBH + pi] + acc[2]);
-    const float cc = act_fwd(a.act, a.wpre[3 * TBH + pi] + acc[3]);
-    const float cp = a.cs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
-    const float c = i * cc * m + f * cp;
-    h = o * act_fwd(a.act, c);
-    a.cs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = c;
-    a.gates[si] = f;
-    a.gates[TB2H + si] = i;
-    a.gates[2 * TB2H + si] = o;
-    a.gates[3 * TB2H + si] = cc;
-  }
-  a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
-  a.y[ix.out(t, r, j)] = h;
-}
-
-// phase 2 of a GRU / minimalGRU step: a = wh + Uh (r*h_{t-1} | z*h_{t-1});
-// h = z*h_{t-1} + (1-z)*act(a)*drop.  HG: index of the candidate gate.
-template <int HG>
-__global__ __launch_bounds__(RT) void gru_fwd_h(pkc_rnn_args a, int t) {
-  __shared__ float hsm[RR][KC + 1];
-  __shared__ float usm[RU][KC + 1];
-  const RnnIdx ix = mkidx(a);
-  const int j = blockIdx.x * RU + threadIdx.x % RU;
-  const int r = blockIdx.y * RR + threadIdx.x / RU;
-  const int H = a.H;
-  const float* src = a.rh + (int64_t)t * ix.B2 * H;
-  const float* U = a.U[HG];
-  float acc = 0.f;
-  for (int k0 = 0; k0 < H; k0 += KC) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < RR * KC; e += RT) {
-      const int rr = e / KC, kk = e % KC;
-      const int R = blockIdx.y * RR + rr, K = k0 + kk;
-      hsm[rr][kk] = (R < ix.B2 && K < H) ? src[(int64_t)R * H + K] : 0.f;
-    }
-    for (int e = threadIdx.x; e < RU * KC; e += RT) {
-      const int jj = e / KC, kk = e % KC;
-      const int J = blockIdx.x * RU + jj, K = k0 + kk;
-      usm[jj][kk] = (J < H && K < H) ? U[(int64_t)J * H + K] : 0.f;
-    }
-    __syncthreads();
-    const int rl = threadIdx.x / RU, jl = threadIdx.x % RU;
-#pragma unroll 8
-    for (int kk = 0; kk < KC; ++kk) acc = fmaf(usm[jl][kk], hsm[rl][kk], acc);
-  }
-  if (r >= ix.B2 || j >= H) return;
-  const int64_t TBH = (int64_t)a.T * a.B * H;
-  const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
-  const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
-  const float m = drop_val(a, r, j, ix.B2);
-  const float hp = a.hs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
-  const float z = a.gates[si];
-  const float hcr = act_fwd(a.act, a.wpre[HG * TBH + pi] + acc);
-  const float h = z * hp + (1.f - z) * (hcr * m);
-  a.gates[HG * TB2H + si] = hcr;
-  a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
-  a.y[ix.out(t, r, j)] = h;
-}
 
 __global__ void rnn_drop_mask_kernel(pkc_rnn_args a, int B2) {
   const int64_t n = (int64_t)B2 * a.H;
@@ -282,6 +132,7 @@ __global__ void rnn_drop_mask_kernel(pkc_rnn_args a, int B2) {
     a.drop_mask[i] = v;
   }
 }
+
 
 // ------------------------------------------------------------------------------- backward
 __device__ __forceinline__ float dy_at(const pkc_rnn_args& a, int64_t i) {
@@ -367,45 +218,225 @@ __global__ void rnn_bwd_init(pkc_rnn_args a) {
   }
 }
 
-// launch for target step tt = t-1 (t = tt+1 already has its gate gradients)
-template <int G, int CELL>
-__global__ __launch_bounds__(RT) void rnn_bwd_step(pkc_rnn_args a, int tt) {
-  __shared__ float dsm[G][RR][KC + 1];
-  __shared__ float usm[G][KC][RU + 1];
-  const RnnIdx ix = mkidx(a);
+
+// ------------------------------------------------------------------------------- MFMA strips
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// v[s] = (ok && kb + s < kmax) ? row[kb + s] : 0 for s < S, with clamped (unconditional) loads;
+// vw: wave-uniform vector width (4 when kmax % 4 == 0 and rows are 16-B aligned, 2, or 1).
+template <int S>
+__device__ __forceinline__ void load_strip(const float* row, bool ok, int kb, int kmax, int vw,
+                                           float* v) {
+  if (vw == 4) {
+#pragma unroll
+    for (int s = 0; s < S; s += 4) {
+      const int k = kb + s;
+      const bool in = ok && k < kmax;
+      const float4 x = *reinterpret_cast<const float4*>(row + (in ? k : 0));
+      v[s] = in ? x.x : 0.f; v[s + 1] = in ? x.y : 0.f;
+      v[s + 2] = in ? x.z : 0.f; v[s + 3] = in ? x.w : 0.f;
+    }
+  } else if (vw == 2) {
+#pragma unroll
+    for (int s = 0; s < S; s += 2) {
+      const int k = kb + s;
+      const bool in = ok && k < kmax;
+      const float2 x = *reinterpret_cast<const float2*>(row + (in ? k : 0));
+      v[s] = in ? x.x : 0.f; v[s + 1] = in ? x.y : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int k = kb + s;
+      const bool in = ok && k < kmax;
+      const float x = row[in ? k : 0];
+      v[s] = in ? x : 0.f;
+    }
+  }
+}
+
+// Sum the four waves' 32x16 partial tiles (MFMA C layout: col = lane & 15, row = 4*(lane>>4)+i)
+// into tile[32][17]; red is [4][32][17] scratch.  Ends with a barrier.
+__device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1, float* red,
+                                            float* tile) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, q = lane >> 4;
+  float* rw = red + w * 32 * 17;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rw[(4 * q + i) * 17 + c] = acc0[i];
+    rw[(16 + 4 * q + i) * 17 + c] = acc1[i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 16; e += RT) {
+    const int r = e >> 4, cc = e & 15;
+    const int o = r * 17 + cc;
+    tile[o] = (red[o] + red[32 * 17 + o]) + (red[2 * 32 * 17 + o] + red[3 * 32 * 17 + o]);
+  }
+  __syncthreads();
+}
+
+template <int S>
+__device__ __forceinline__ void mfma_chain(const float* va, const float* vb, const float* vu,
+                                           f32x4& acc0, f32x4& acc1) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s], vu[s], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[s], vu[s], acc1, 0, 0, 0);
+  }
+}
+
+// ------------------------------------------------------------------------------- forward step
+// Cell update of step t at (r, j) from the recurrent products acc[g] = (U_g h_{t-1})[r][j].
+template <int CELL, bool QH>
+__device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
+                                        int j, const float* acc, const float* vars, float qscale) {
   const int H = a.H;
-  const int k = blockIdx.x * RU + threadIdx.x % RU;
-  const int r = blockIdx.y * RR + threadIdx.x / RU;
+  const float* hprev = a.hs + (int64_t)t * ix.B2 * H;
+  if constexpr (QH) {
+    // the hidden state the reference keeps for step t-1 (hiddens[t-1], and the saved input of the
+    // U backward) is the 4x re-quantised tensor; the last step's h is never quantised
+    float v = hprev[(int64_t)r * H + j];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v = qin(v, vars[g], qscale);
+    a.hq[(int64_t)t * ix.B2 * H + (int64_t)r * H + j] = v;
+    if (t > 0) a.y[ix.out(t - 1, r, j)] = v;
+  }
+  const int64_t TBH = (int64_t)a.T * a.B * H;   // gate stride of the (G, T, B, H) pre-activations
+  const int64_t TB2H = (int64_t)a.T * ix.B2 * H; // gate stride of the saved activations
+  const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
+  const float m = drop_val(a, r, j, ix.B2);
+  const float hp = hprev[(int64_t)r * H + j];
+  float h = 0.f;
+  if constexpr (CELL == PKC_CELL_GRU) {
+    // phase 1 of a GRU step: update / reset gates and r*h (the input of Uh)
+    const float z = sigm(a.wpre[pi] + acc[0]);
+    const float rg = sigm(a.wpre[TBH + pi] + acc[1]);
+    a.gates[si] = z;
+    a.gates[TB2H + si] = rg;
+    a.rh[si] = rg * hp;
+    return;
+  } else if constexpr (CELL == PKC_CELL_MINGRU) {
+    // phase 1 of a minimalGRU step: update gate and z*h (the input of Uh)
+    const float z = sigm(a.wpre[pi] + acc[0]);
+    a.gates[si] = z;
+    a.rh[si] = z * hp;
+    return;
+  } else if constexpr (CELL == PKC_CELL_RNN) {
+    const float hcr = act_fwd(a.act, a.wpre[pi] + acc[0]);
+    h = hcr * m;
+    a.gates[si] = hcr;
+  } else if constexpr (CELL == PKC_CELL_LIGRU) {
+    const float z = sigm(a.wpre[pi] + acc[0]);
+    const float hcr = act_fwd(a.act, a.wpre[TBH + pi] + acc[1]);
+    h = z * hp + (1.f - z) * (hcr * m);
+    a.gates[si] = z;
+    a.gates[TB2H + si] = hcr;
+  } else {
+    // LSTM gates (f, i, o, c); cs[t] = c_{t-1}
+    const float f = sigm(a.wpre[pi] + acc[0]);
+    const float i = sigm(a.wpre[TBH + pi] + acc[1]);
+    const float o = sigm(a.wpre[2 * TBH + pi] + acc[2]);
+    const float cc = act_fwd(a.act, a.wpre[3 * TBH + pi] + acc[3]);
+    const float cp = a.cs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
+    const float c = i * cc * m + f * cp;
+    h = o * act_fwd(a.act, c);
+    a.cs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = c;
+    a.gates[si] = f;
+    a.gates[TB2H + si] = i;
+    a.gates[2 * TB2H + si] = o;
+    a.gates[3 * TB2H + si] = cc;
+  }
+  a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+  a.y[ix.out(t, r, j)] = h;
+}
+
+// phase 2 of a GRU / minimalGRU step: h = z*h_{t-1} + (1-z)*act(wh + Uh (r|z)*h_{t-1})*drop
+template <int HG>
+__device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
+                                         int j, float acc) {
+  const int H = a.H;
+  const int64_t TBH = (int64_t)a.T * a.B * H;
+  const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
+  const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
+  const float m = drop_val(a, r, j, ix.B2);
+  const float hp = a.hs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
+  const float z = a.gates[si];
+  const float hcr = act_fwd(a.act, a.wpre[HG * TBH + pi] + acc);
+  const float h = z * hp + (1.f - z) * (hcr * m);
+  a.gates[HG * TB2H + si] = hcr;
+  a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+  a.y[ix.out(t, r, j)] = h;
+}
+
+// One forward step (PH = 0: the gates that read h_{t-1}; PH = 1: the candidate of a two-phase
+// cell, reading rh).  Tile: rows [32*blockIdx.y, +32) x NG gates of NU = 16/NG units.
+template <int NG, int CELL, int PH, int S, bool QH>
+__global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
+  __shared__ float red[4 * 32 * 17];
+  __shared__ float tile[32 * 17];
+  constexpr int NU = 16 / NG;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, q = lane >> 4;
+  const int u0 = blockIdx.x * NU, r0 = blockIdx.y * 32;
+  const float* src = (PH == 0 ? a.hs : a.rh) + (int64_t)t * B2 * H;
+  const int ra = r0 + c, rb = r0 + 16 + c;
+  const int gi = c / NU, u = u0 + c % NU;
+  const float* pu = a.U[PH == 0 ? gi : cand_gate(CELL)] + (int64_t)(u < H ? u : 0) * H;
+  const int kb = (w * 4 + q) * S;
+  float va[S], vb[S], vu[S];
+  load_strip<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
+  load_strip<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
+  load_strip<S>(pu, u < H, kb, H, vw, vu);
+  float vars[4] = {0.f, 0.f, 0.f, 0.f};
+  const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (QH) {
+    // each gate's QuantizeLinear re-quantises h in place (q1..q4): gate g's product reads q_{g+1}
+    h_quant_vars<NG>(src, (int64_t)B2 * H, qscale, vars);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      float vg[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        va[s] = qin(va[s], vars[g], qscale);
+        vb[s] = qin(vb[s], vars[g], qscale);
+        vg[s] = gi == g ? vu[s] : 0.f;
+      }
+      mfma_chain<S>(va, vb, vg, acc0, acc1);
+    }
+  } else {
+    mfma_chain<S>(va, vb, vu, acc0, acc1);
+  }
+  reduce_tile(acc0, acc1, red, tile);
+  for (int p = threadIdx.x; p < 32 * NU; p += RT) {
+    const int rl = p / NU, ul = p % NU;
+    const int r = r0 + rl, j = u0 + ul;
+    if (r >= B2 || j >= H) continue;
+    if constexpr (PH == 1) {
+      cand_epi<cand_gate(CELL)>(a, ix, t, r, j, tile[rl * 17 + ul]);
+    } else {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[g] = tile[rl * 17 + g * NU + ul];
+      fwd_epi<CELL, QH>(a, ix, t, r, j, acc, vars, qscale);
+    }
+  }
+}
+
+// BPTT step for target tt (t = tt + 1 has its gate gradients): dh = acc + carries, g = dy + dh,
+// then the gate gradients of step tt at (r, k).
+template <int G, int CELL>
+__device__ __forceinline__ void bwd_step_epi(const pkc_rnn_args& a, const RnnIdx& ix, int tt, int r,
+                                             int k, float acc) {
+  const int H = a.H;
   const int t = tt + 1;
   const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
   const int64_t n = (int64_t)ix.B2 * H;
-  const int src = (a.T - 1 - t) & 1, dst = src ^ 1;      // ping-pong slots of g / dc
-  float acc = 0.f;
-  for (int j0 = 0; j0 < H; j0 += KC) {
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      for (int e = threadIdx.x; e < RR * KC; e += RT) {
-        const int rr = e / KC, jj = e % KC;
-        const int R = blockIdx.y * RR + rr, J = j0 + jj;
-        dsm[g][rr][jj] = (R < ix.B2 && J < H) ? a.dgates[g * TB2H + ix.st(t, R, J)] : 0.f;
-      }
-      for (int e = threadIdx.x; e < KC * RU; e += RT) {
-        const int jj = e / RU, kk = e % RU;
-        const int J = j0 + jj, K = blockIdx.x * RU + kk;
-        usm[g][jj][kk] = (J < H && K < H) ? a.U[g][(int64_t)J * H + K] : 0.f;
-      }
-    }
-    __syncthreads();
-    const int rl = threadIdx.x / RU, kl = threadIdx.x % RU;
-#pragma unroll 4
-    for (int jj = 0; jj < KC; ++jj) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) acc = fmaf(dsm[g][rl][jj], usm[g][jj][kl], acc);
-    }
-  }
-  if (r >= ix.B2 || k >= H) return;
   const int64_t e = (int64_t)r * H + k;
+  const int src = (a.T - 1 - t) & 1, dst = src ^ 1;      // ping-pong slots of g / dc
   float dh = acc;
   float dc_carry = 0.f;
   if constexpr (CELL == PKC_CELL_LIGRU) {
@@ -417,64 +448,34 @@ __global__ __launch_bounds__(RT) void rnn_bwd_step(pkc_rnn_args a, int tt) {
   } else if constexpr (CELL == PKC_CELL_MINGRU) {
     // (g_t + d(zh)_t) * z_t  (acc = Uz^T dz_t)
     dh += (a.work[src * n + e] + a.work[2 * n + e]) * a.gates[ix.st(t, r, k)];
-  } else if constexpr (CELL == PKC_CELL_RNN) {
-    // acc = Uh^T da_t is the whole recurrent gradient
-  } else {
+  } else if constexpr (CELL == PKC_CELL_LSTM) {
     dc_carry = a.work[2 * n + src * n + e];                  // dc_t * f_t
   }
   const float g = dy_at(a, ix.out(tt, r, k)) + dh;
-  float dg[4], go, dco = 0.f;
+  float dg[4] = {0.f, 0.f, 0.f, 0.f}, go = 0.f, dco = 0.f;
   gate_grads<CELL>(a, ix, tt, r, k, g, dc_carry, dg, &go, &dco);
+  const int64_t si = ix.st(tt, r, k);
   if constexpr (CELL == PKC_CELL_GRU) {
-    a.dgates[ix.st(tt, r, k)] = dg[0];
-    a.dgates[2 * TB2H + ix.st(tt, r, k)] = dg[2];
-    a.work[dst * n + e] = go;
-    return;
-  }
-  if constexpr (CELL == PKC_CELL_MINGRU) {
-    a.dgates[TB2H + ix.st(tt, r, k)] = dg[1];
-    a.work[dst * n + e] = go;
-    return;
-  }
+    a.dgates[si] = dg[0];
+    a.dgates[2 * TB2H + si] = dg[2];
+  } else if constexpr (CELL == PKC_CELL_MINGRU) {
+    a.dgates[TB2H + si] = dg[1];
+  } else {
 #pragma unroll
-  for (int q = 0; q < G; ++q) a.dgates[q * TB2H + ix.st(tt, r, k)] = dg[q];
+    for (int q = 0; q < G; ++q) a.dgates[q * TB2H + si] = dg[q];
+  }
   a.work[dst * n + e] = go;
-  a.work[2 * n + dst * n + e] = dco;
+  if constexpr (CELL == PKC_CELL_LSTM) a.work[2 * n + dst * n + e] = dco;
 }
 
-// GRU: d(rh)_t[r][k] = sum_j da_t[r][j] Uh[j][k]; dr_t = d(rh) * h_{t-1} * r (1 - r).
-// d(rh)_t is kept in work[2n..3n) for the carry term of the next (earlier) step.
+// d(rh)_t = Uh^T da_t (acc) of a two-phase cell -> dr_t (GRU) or dz_t (minimalGRU); d(rh) is kept
+// in work[2n..3n) for the carry term of the next (earlier) step.
 template <int CELL>
-__global__ __launch_bounds__(RT) void gru_bwd_rh(pkc_rnn_args a, int t) {
-  constexpr int HG = cand_gate(CELL);
-  __shared__ float dsm[RR][KC + 1];
-  __shared__ float usm[KC][RU + 1];
-  const RnnIdx ix = mkidx(a);
+__device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r, int k,
+                                       float acc) {
   const int H = a.H;
-  const int k = blockIdx.x * RU + threadIdx.x % RU;
-  const int r = blockIdx.y * RR + threadIdx.x / RU;
   const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
   const int64_t n = (int64_t)ix.B2 * H;
-  const float* U = a.U[HG];
-  float acc = 0.f;
-  for (int j0 = 0; j0 < H; j0 += KC) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < RR * KC; e += RT) {
-      const int rr = e / KC, jj = e % KC;
-      const int R = blockIdx.y * RR + rr, J = j0 + jj;
-      dsm[rr][jj] = (R < ix.B2 && J < H) ? a.dgates[HG * TB2H + ix.st(t, R, J)] : 0.f;
-    }
-    for (int e = threadIdx.x; e < KC * RU; e += RT) {
-      const int jj = e / RU, kk = e % RU;
-      const int J = j0 + jj, K = blockIdx.x * RU + kk;
-      usm[jj][kk] = (J < H && K < H) ? U[(int64_t)J * H + K] : 0.f;
-    }
-    __syncthreads();
-    const int rl = threadIdx.x / RU, kl = threadIdx.x % RU;
-#pragma unroll 8
-    for (int jj = 0; jj < KC; ++jj) acc = fmaf(dsm[rl][jj], usm[jj][kl], acc);
-  }
-  if (r >= ix.B2 || k >= H) return;
   const int64_t e = (int64_t)r * H + k, si = ix.st(t, r, k);
   const float hp = a.hs[(int64_t)t * ix.B2 * H + e];
   if constexpr (CELL == PKC_CELL_GRU) {
@@ -489,6 +490,75 @@ __global__ __launch_bounds__(RT) void gru_bwd_rh(pkc_rnn_args a, int t) {
   a.work[2 * n + e] = acc;
 }
 
+// MODE 0: the product of gate g0 + blockIdx.z into slab blockIdx.z (a.work + (4 + z) n);
+// MODE 1: one-gate product + bwd_step_epi (t = tt + 1); MODE 2: one-gate product + rh_epi.
+// out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
+template <int G, int CELL, int MODE, int S>
+__global__ __launch_bounds__(RT) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
+  __shared__ float red[4 * 32 * 17];
+  __shared__ float tile[32 * 17];
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = lane & 15, q = lane >> 4;
+  const int k0 = blockIdx.x * 16, r0 = blockIdx.y * 32;
+  const int g = g0 + blockIdx.z;
+  const int64_t TB2H = (int64_t)a.T * B2 * H;
+  const float* dg = a.dgates + g * TB2H + (int64_t)t * B2 * H;
+  const int ra = r0 + c, rb = r0 + 16 + c, k = k0 + c;
+  const float* pu = a.ut + (int64_t)g * H * H + (int64_t)(k < H ? k : 0) * H;
+  const int kb = (w * 4 + q) * S;
+  float va[S], vb[S], vu[S];
+  load_strip<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
+  load_strip<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
+  load_strip<S>(pu, k < H, kb, H, vw, vu);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  mfma_chain<S>(va, vb, vu, acc0, acc1);
+  reduce_tile(acc0, acc1, red, tile);
+  const int64_t n = (int64_t)B2 * H;
+  for (int p = threadIdx.x; p < 32 * 16; p += RT) {
+    const int rl = p >> 4, kl = p & 15;
+    const int r = r0 + rl, kk = k0 + kl;
+    if (r >= B2 || kk >= H) continue;
+    const float v = tile[rl * 17 + kl];
+    if constexpr (MODE == 0) a.work[(4 + blockIdx.z) * n + (int64_t)r * H + kk] = v;
+    else if constexpr (MODE == 1) bwd_step_epi<G, CELL>(a, ix, t - 1, r, kk, v);
+    else rh_epi<CELL>(a, ix, t, r, kk, v);
+  }
+}
+
+// Sum of the NS gate slabs + bwd_step_epi for target tt (elementwise over B2 x H).
+template <int G, int CELL, int NS>
+__global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt) {
+  const RnnIdx ix = mkidx(a);
+  const int64_t n = (int64_t)ix.B2 * a.H;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc += a.work[(4 + s) * n + e];
+    bwd_step_epi<G, CELL>(a, ix, tt, (int)(e / a.H), (int)(e % a.H), acc);
+  }
+}
+
+// ut[g][k][j] = U[g][j][k] (the B operand of the backward products), 32 x 32 tiles through LDS
+__global__ __launch_bounds__(256) void rnn_transpose_u(pkc_rnn_args a) {
+  __shared__ float tl[32][33];
+  const int H = a.H, g = blockIdx.z;
+  const float* U = a.U[g];
+  float* ut = a.ut + (int64_t)g * H * H;
+  const int j0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int j = j0 + i, k = k0 + tx;
+    tl[i][tx] = (j < H && k < H) ? U[(int64_t)j * H + k] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int k = k0 + i, j = j0 + tx;
+    if (k < H && j < H) ut[(int64_t)k * H + j] = tl[tx][i];
+  }
+}
 // fold the per-direction gate gradients (G, T, B2, H) onto the (G, T, B, H) pre-activation rows
 __global__ void rnn_fold_kernel(pkc_rnn_args a, float* dpre) {
   const RnnIdx ix = mkidx(a);
@@ -508,6 +578,91 @@ __global__ void rnn_fold_kernel(pkc_rnn_args a, float* dpre) {
   }
 }
 
+
+template <int S>
+struct SCase {};
+
+static int pick_vw(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
+
+template <int G, int CELL, int S>
+static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
+  const int B2 = a->bidir ? 2 * a->B : a->B;
+  const int vw = pick_vw(a->H);
+  const unsigned rows = (unsigned)((B2 + 31) / 32);
+  if constexpr (two_phase(CELL)) {
+    constexpr int NG = G - 1;                        // gates that read h_{t-1}
+    dim3 g1((a->H + 16 / NG - 1) / (16 / NG), rows), g2((a->H + 15) / 16, rows);
+    for (int t = 0; t < a->T; ++t) {
+      hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
+      hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), g2, dim3(RT), 0, s, *a, t, vw);
+    }
+  } else {
+    dim3 g1((a->H + 16 / G - 1) / (16 / G), rows);
+    for (int t = 0; t < a->T; ++t) {
+      if (a->qbits > 0)
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
+      else
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
+    }
+  }
+  PKC_LAUNCH_CHECK("pkc_rnn_fwd step");
+  return PKC_OK;
+}
+
+template <int G, int CELL, int S>
+static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
+  const int B2 = a->bidir ? 2 * a->B : a->B;
+  const int vw = pick_vw(a->H);
+  const unsigned rows = (unsigned)((B2 + 31) / 32);
+  const int64_t n = (int64_t)B2 * a->H;
+  const unsigned eb = (unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024);
+  const dim3 tg((a->H + 31) / 32, (a->H + 31) / 32, G);
+  hipLaunchKernelGGL(rnn_transpose_u, tg, dim3(256), 0, s, *a);
+  hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
+  PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
+  const unsigned kt = (unsigned)((a->H + 15) / 16);
+  if constexpr (two_phase(CELL)) {
+    constexpr int HG = cand_gate(CELL);
+    hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                       a->T - 1, HG, vw);
+    for (int tt = a->T - 2; tt >= 0; --tt) {
+      if constexpr (CELL == PKC_CELL_GRU) {           // Uz^T dz + Ur^T dr: two gate slabs
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, 2), dim3(RT), 0, s, *a,
+                           tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, 2>), dim3(eb), dim3(256), 0, s, *a, tt);
+      } else {                                        // minimalGRU: Uz^T dz, one gate
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                           tt + 1, 0, vw);
+      }
+      hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a, tt,
+                         HG, vw);
+    }
+  } else {
+    for (int tt = a->T - 2; tt >= 0; --tt) {
+      if constexpr (G == 1) {
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                           tt + 1, 0, vw);
+      } else {
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
+                           tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
+      }
+    }
+  }
+  PKC_LAUNCH_CHECK("pkc_rnn_bwd step");
+  hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
+  PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
+  return PKC_OK;
+}
+
+// contraction strip per lane: 16 lane groups x S >= H
+#define PKC_S_DISPATCH(FN, ...)                                      \
+  (a->H <= 256 ? FN<G, CELL, 16>(__VA_ARGS__)                        \
+   : a->H <= 512 ? FN<G, CELL, 32>(__VA_ARGS__)                      \
+   : a->H <= 768 ? FN<G, CELL, 48>(__VA_ARGS__)                      \
+   : a->H <= 1024 ? FN<G, CELL, 64>(__VA_ARGS__)                     \
+   : FN<G, CELL, 128>(__VA_ARGS__))
+
 template <int G, int CELL>
 static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
@@ -517,63 +672,28 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
     hipLaunchKernelGGL(rnn_drop_mask_kernel, dim3(64), dim3(256), 0, s, *a, B2);
     PKC_LAUNCH_CHECK("pkc_rnn_fwd drop mask");
   }
-  dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
-  if constexpr (two_phase(CELL)) {
-    // phase 1 multiplies the gates that read h (GRU: z, r; minimalGRU: z) = all but the candidate
-    for (int t = 0; t < a->T; ++t) {
-      hipLaunchKernelGGL((rnn_fwd_step<G - 1, CELL, false>), grid, dim3(RT), 0, s, *a, t);
-      hipLaunchKernelGGL(gru_fwd_h<cand_gate(CELL)>, grid, dim3(RT), 0, s, *a, t);
-    }
-    PKC_LAUNCH_CHECK("pkc_rnn_fwd gru step");
-    return PKC_OK;
-  }
-  for (int t = 0; t < a->T; ++t) {
-    if (a->qbits > 0)
-      hipLaunchKernelGGL((rnn_fwd_step<G, CELL, true>), grid, dim3(RT), 0, s, *a, t);
-    else
-      hipLaunchKernelGGL((rnn_fwd_step<G, CELL, false>), grid, dim3(RT), 0, s, *a, t);
-  }
-  PKC_LAUNCH_CHECK("pkc_rnn_fwd step");
-  return PKC_OK;
+  return PKC_S_DISPATCH(fwd_impl_s, a, s);
 }
 
 template <int G, int CELL>
 static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
-  const int B2 = a->bidir ? 2 * a->B : a->B;
-  hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
-  PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
-  dim3 grid((a->H + RU - 1) / RU, (B2 + RR - 1) / RR);
-  if constexpr (two_phase(CELL)) {
-    hipLaunchKernelGGL(gru_bwd_rh<CELL>, grid, dim3(RT), 0, s, *a, a->T - 1);
-    for (int tt = a->T - 2; tt >= 0; --tt) {
-      hipLaunchKernelGGL((rnn_bwd_step<G - 1, CELL>), grid, dim3(RT), 0, s, *a, tt);
-      hipLaunchKernelGGL(gru_bwd_rh<CELL>, grid, dim3(RT), 0, s, *a, tt);
-    }
-  } else {
-    for (int tt = a->T - 2; tt >= 0; --tt)
-      hipLaunchKernelGGL((rnn_bwd_step<G, CELL>), grid, dim3(RT), 0, s, *a, tt);
-  }
-  PKC_LAUNCH_CHECK("pkc_rnn_bwd step");
-  hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
-  PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
-  return PKC_OK;
+  return PKC_S_DISPATCH(bwd_impl_s, a, dpre, s);
 }
 
 static int check(const pkc_rnn_args* a, bool bwd) {
-  PKC_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->H > 0, "pkc_rnn: bad shape");
+  PKC_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->H > 0 && a->H <= 2048, "pkc_rnn: bad shape (H <= 2048)");
   PKC_CHECK_ARG(a->cell >= PKC_CELL_LIGRU && a->cell <= PKC_CELL_RNN, "pkc_rnn: bad cell %d", a->cell);
   PKC_CHECK_ARG(!two_phase(a->cell) || (a->rh && a->qbits <= 0),
                 "pkc_rnn: GRU / minimalGRU need rh and no qbits");
-  PKC_CHECK_ARG(a->cell == PKC_CELL_LSTM || a->cell == PKC_CELL_LIGRU || a->qbits <= 0,
-                "pkc_rnn: input quantisation only for LSTM / liGRU");
+  PKC_CHECK_ARG(a->cell == PKC_CELL_LSTM || a->qbits <= 0, "pkc_rnn: input quantisation only for LSTM");
   PKC_CHECK_ARG(a->wpre && a->hs && a->gates && a->y, "pkc_rnn: null buffer");
   PKC_CHECK_ARG(a->cell != PKC_CELL_LSTM || a->cs, "pkc_rnn: LSTM needs cs");
   const int G = cell_gates(a->cell);
   for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U[g], "pkc_rnn: null U[%d]", g);
   PKC_CHECK_ARG(!a->train || a->drop_p <= 0.f || a->drop_mask, "pkc_rnn: dropout needs drop_mask");
-  if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work, "pkc_rnn_bwd: null buffer");
-  PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir && (a->bidir ? 2 * a->B : a->B) <= RR),
-                "pkc_rnn: quantised h needs hq, a uni-directional layer and <= %d rows", RR);
+  if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work && a->ut, "pkc_rnn_bwd: null buffer");
+  PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir), "pkc_rnn: quantised h needs hq and a "
+                "uni-directional layer");
   return PKC_OK;
 }
 
@@ -583,11 +703,13 @@ extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
   using namespace pkc;
   int st = check(a, false);
   if (st) return st;
-  if (a->cell == PKC_CELL_LIGRU) return fwd_impl<2, PKC_CELL_LIGRU>(a, S(stream));
-  if (a->cell == PKC_CELL_GRU) return fwd_impl<3, PKC_CELL_GRU>(a, S(stream));
-  if (a->cell == PKC_CELL_MINGRU) return fwd_impl<2, PKC_CELL_MINGRU>(a, S(stream));
-  if (a->cell == PKC_CELL_RNN) return fwd_impl<1, PKC_CELL_RNN>(a, S(stream));
-  return fwd_impl<4, PKC_CELL_LSTM>(a, S(stream));
+  switch (a->cell) {
+    case PKC_CELL_LIGRU: return fwd_impl<2, PKC_CELL_LIGRU>(a, S(stream));
+    case PKC_CELL_GRU: return fwd_impl<3, PKC_CELL_GRU>(a, S(stream));
+    case PKC_CELL_MINGRU: return fwd_impl<2, PKC_CELL_MINGRU>(a, S(stream));
+    case PKC_CELL_RNN: return fwd_impl<1, PKC_CELL_RNN>(a, S(stream));
+    default: return fwd_impl<4, PKC_CELL_LSTM>(a, S(stream));
+  }
 }
 
 extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
@@ -595,9 +717,11 @@ extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
   int st = check(a, true);
   if (st) return st;
   PKC_CHECK_ARG(dpre, "pkc_rnn_bwd: null dpre");
-  if (a->cell == PKC_CELL_LIGRU) return bwd_impl<2, PKC_CELL_LIGRU>(a, dpre, S(stream));
-  if (a->cell == PKC_CELL_GRU) return bwd_impl<3, PKC_CELL_GRU>(a, dpre, S(stream));
-  if (a->cell == PKC_CELL_MINGRU) return bwd_impl<2, PKC_CELL_MINGRU>(a, dpre, S(stream));
-  if (a->cell == PKC_CELL_RNN) return bwd_impl<1, PKC_CELL_RNN>(a, dpre, S(stream));
-  return bwd_impl<4, PKC_CELL_LSTM>(a, dpre, S(stream));
+  switch (a->cell) {
+    case PKC_CELL_LIGRU: return bwd_impl<2, PKC_CELL_LIGRU>(a, dpre, S(stream));
+    case PKC_CELL_GRU: return bwd_impl<3, PKC_CELL_GRU>(a, dpre, S(stream));
+    case PKC_CELL_MINGRU: return bwd_impl<2, PKC_CELL_MINGRU>(a, dpre, S(stream));
+    case PKC_CELL_RNN: return bwd_impl<1, PKC_CELL_RNN>(a, dpre, S(stream));
+    default: return bwd_impl<4, PKC_CELL_LSTM>(a, dpre, S(stream));
+  }
 }

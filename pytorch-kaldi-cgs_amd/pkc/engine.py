@@ -595,7 +595,7 @@ class Engine:
                       gates=_f32(G * T * B2 * H, dev), y=_f32(M * D, dev),
                       drop=_f32(B2 * H, dev), dgates=_f32(G * T * B2 * H, dev),
                       dpre=_f32(G * M * H, dev), dz=_f32(G * M * H, dev),
-                      rwork=_f32(4 * B2 * H, dev),
+                      rwork=_f32(8 * B2 * H, dev), ut=_f32(G * H * H, dev),
                       dx=_f32(G * MAX_SPLITS * M * K, dev),
                       dW=[None] * G, db=[None] * G, dU=[None] * G, dgamma=[None] * G,
                       dbeta=[None] * G)
@@ -995,6 +995,7 @@ class Engine:
         a.y = lb["y"].data_ptr()
         a.dgates = lb["dgates"].data_ptr()
         a.work = lb["rwork"].data_ptr()
+        a.ut = lb["ut"].data_ptr()
         return a
 
     def _rec_inputs(self, n, li):

@@ -1,0 +1,148 @@
+"""Training throughput of the sequence configurations of BASELINE.json (informational; the headline
+bench.py line is the C2 MLP):
+
+  C3  liGRU 4x550 bidirectional + HCGS [32,2]/[75,75] (16x) on W and U, B = 8 sentences, ReLU, BN,
+      dropout 0.2, heads 1100 -> 1928 cd + 48 mono                       (TIMIT_CGS liGRU)
+  C4  LSTM 4x1024 bidirectional (liGRU shared-weight convention), B = 16, tanh, BN, T <= 500
+                                                                          (Librispeech_baselines)
+  C5  LSTM 3x512 + Pattern 8x8/k4/n16 + 8-bit weights + 16-bit inputs, B = 12, T <= 200
+                                                                          (LibriSpeech_CGS)
+  plus GRU 4x550 bidirectional (north_star's GRU family) at the C3 shape.
+
+Synthetic TIMIT-shaped chunk: utterance lengths U[150, 450] (C5: U[100, 200]), 440-dim
+context-expanded features.  Metric: real (unpadded) frames / s of the batch loop, one sentence
+batch = one step (core.py:183-232), plus microseconds per recurrent time step and layer.
+
+Usage: python scripts/bench_seq.py [--configs c3,c4,c5,gru] [--steps K] [--warmup W]
+"""
+import argparse
+import configparser
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+OPT = dict(arch_opt="rmsprop", arch_lr="0.0016", opt_momentum="0.0", opt_alpha="0.95",
+           opt_eps="1e-8", opt_centered="False", opt_weight_decay="0.0", arch_freeze="False",
+           to_do="train", skip_regularization="True")
+
+
+def rec_opts(cfg_name):
+    n = {"c3": 4, "c4": 4, "c5": 3, "gru": 4}[cfg_name]
+    if cfg_name in ("c3", "gru"):
+        p = "ligru" if cfg_name == "c3" else "gru"
+        d = {p + "_lay": ",".join(["550"] * n), p + "_drop": ",".join(["0.2"] * n),
+             p + "_use_laynorm_inp": "False", p + "_use_batchnorm_inp": "False",
+             p + "_use_laynorm": ",".join(["False"] * n),
+             p + "_use_batchnorm": ",".join(["True"] * n), p + "_bidir": "True",
+             p + "_act": ",".join(["relu"] * n), p + "_orthinit": "True"}
+        if cfg_name == "c3":
+            d.update(ligru_hcgs="True", hcgsx_block="32,2", hcgsx_sparse="75,75",
+                     hcgsh_block="32,2", hcgsh_sparse="75,75")
+        return ("liGRU" if cfg_name == "c3" else "GRU"), d, 8
+    H = "1024" if cfg_name == "c4" else "512"
+    d = dict(lstm_lay=",".join([H] * n), lstm_drop=",".join(["0.2"] * n),
+             lstm_use_laynorm_inp="False", lstm_use_batchnorm_inp="False",
+             lstm_use_laynorm=",".join(["False"] * n), lstm_use_batchnorm=",".join(["True"] * n),
+             lstm_bidir="True" if cfg_name == "c4" else "False", lstm_act=",".join(["tanh"] * n),
+             lstm_orthinit="True", lstm_hcgs="False")
+    if cfg_name == "c5":
+        d.update(if_pattern="True", pattern_mode="pattern", pattern_shape="8,8",
+                 pattern_nnz=",".join(["4"] * n), pattern_num=",".join(["16"] * n),
+                 lstm_quant="True", lstm_quant_inp="True", param_quant=",".join(["8"] * n),
+                 inp_quant="16")
+    return "LSTM", d, (16 if cfg_name == "c4" else 12)
+
+
+def build(cfg_name, seed=2234):
+    import pkc.neural_networks as NN
+    from pkc.engine import Engine, parse_model
+    cls, ropts, B = rec_opts(cfg_name)
+    cfg = configparser.ConfigParser()
+    cfg["a1"] = dict(ropts, arch_name="rnn", **OPT)
+    head = dict(dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False", arch_name="head",
+                dnn_lay="1928", dnn_drop="0.0", dnn_use_batchnorm="False", dnn_use_laynorm="False",
+                dnn_act="softmax", **dict(OPT, arch_lr="0.0004"))
+    cfg["a2"] = head
+    cfg["a3"] = dict(head, arch_name="mono", dnn_lay="48")
+    model = ("o1=compute(rnn,fea)\no2=compute(head,o1)\no3=compute(mono,o1)\n"
+             "lm=cost_nll(o3,lab_mono)\nlmw=mult_constant(lm,1.0)\nlc=cost_nll(o2,lab_cd)\n"
+             "loss_final=sum(lc,lmw)\nerr_final=cost_err(o2,lab_cd)")
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    rnn = getattr(NN, cls)(cfg["a1"], 440)
+    if cfg_name == "c5":
+        pset = np.load(os.path.join(ROOT, "tests", "golden", "quant.npz"),
+                       allow_pickle=False)["pattern_set"]
+        rnn.pattern_kernels = pset.reshape(16, 8, 8)
+    nets = {"rnn": rnn, "head": NN.MLP(cfg["a2"], rnn.out_dim), "mono": NN.MLP(cfg["a3"], rnn.out_dim)}
+    for n in nets.values():
+        n.cuda().train()
+    opts = {"rnn": cfg["a1"], "head": cfg["a2"], "mono": cfg["a3"]}
+    rs = np.random.RandomState(seed)
+    lo, hi = (100, 200) if cfg_name == "c5" else (150, 450)
+    n_utt = 64 * B
+    lens = np.sort(rs.randint(lo, hi + 1, size=n_utt))          # length-sorted, as the loader
+    end = np.cumsum(lens)
+    N = int(end[-1])
+    feats = torch.randn(N, 440, device="cuda")
+    labs = torch.stack([torch.randint(0, 1928, (N,), device="cuda"),
+                        torch.randint(0, 48, (N,), device="cuda")], 1).to(torch.int32).contiguous()
+    eng = Engine(nets, opts, parse_model(model), {"fea": (0, 440)}, ["lab_cd", "lab_mono"],
+                 batch=B, max_len=int(lens.max()), seed=seed)
+    eng.bind_chunk(feats, labs, N, end_index=end)
+    return eng, nets, B
+
+
+def run(cfg_name, steps, warmup):
+    eng, nets, B = build(cfg_name)
+    rng = random.Random(7)
+    # sample the batches across the length-sorted chunk (short and long sentences alike)
+    nb = eng.n_batches
+    order = [int(i) for i in np.linspace(0, nb - 1, warmup + steps)]
+    batches = []
+    for i in order:
+        eng.snt = i * B
+        batches.append(eng.next_seq_batch(rng))
+    for b in batches[:warmup]:
+        eng.train_step(batch=b)
+    torch.cuda.synchronize()
+    frames, tsteps = 0, 0
+    t0 = time.time()
+    for b in batches[warmup:]:
+        eng.train_step(batch=b)
+        frames += int(b[1].sum())
+        tsteps += int(b[3])
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    nl = len(nets["rnn"].layer_specs())
+    return {"config": cfg_name, "batch_sentences": B, "steps": steps,
+            "frames_per_s": frames / dt, "ms_per_step": dt * 1e3 / steps,
+            "us_per_time_step_per_layer_fwd_bwd": dt * 1e6 / (tsteps * nl),
+            "mean_T": tsteps / steps}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c4,c5,gru")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    out = []
+    for c in a.configs.split(","):
+        r = run(c, a.steps, a.warmup)
+        print(json.dumps(r), flush=True)
+        out.append(r)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
