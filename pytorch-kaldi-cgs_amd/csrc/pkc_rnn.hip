@@ -91,33 +91,6 @@ __device__ __forceinline__ float qin(float x, float var, float scale) {
   return ceilf(fabsf(x / var) * scale) / scale * var * s;
 }
 
-template <int G>
-__device__ void h_quant_vars(const float* hprev, int64_t n, float scale, float* vars) {
-  // vars[g] = max(|max q_g|, |min q_g|) over all of h_{t-1}, q_0 = h (block-redundant reduction)
-  __shared__ float rmx[RT], rmn[RT];
-  for (int g = 0; g < G; ++g) {
-    float mx = -INFINITY, mn = INFINITY;
-    for (int64_t e = threadIdx.x; e < n; e += RT) {
-      float v = hprev[e];
-      for (int p = 0; p < g; ++p) v = qin(v, vars[p], scale);
-      mx = fmaxf(mx, v);
-      mn = fminf(mn, v);
-    }
-    rmx[threadIdx.x] = mx;
-    rmn[threadIdx.x] = mn;
-    __syncthreads();
-    for (int o = RT / 2; o > 0; o >>= 1) {
-      if (threadIdx.x < o) {
-        rmx[threadIdx.x] = fmaxf(rmx[threadIdx.x], rmx[threadIdx.x + o]);
-        rmn[threadIdx.x] = fminf(rmn[threadIdx.x], rmn[threadIdx.x + o]);
-      }
-      __syncthreads();
-    }
-    const float a = fabsf(rmx[0]), b = fabsf(rmn[0]);
-    vars[g] = a > b ? a : b;
-    __syncthreads();
-  }
-}
 
 
 __global__ void rnn_drop_mask_kernel(pkc_rnn_args a, int B2) {
@@ -394,10 +367,28 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
   const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   if constexpr (QH) {
-    // each gate's QuantizeLinear re-quantises h in place (q1..q4): gate g's product reads q_{g+1}
-    h_quant_vars<NG>(src, (int64_t)B2 * H, qscale, vars);
+    // each gate's QuantizeLinear re-quantises h in place (q1..q4): gate g's product reads
+    // q_{g+1} = Q(q_g) with var_g = max|q_g| over the whole tensor.  With all B2 <= 32 rows in this
+    // tile, the four waves' strips hold every element of h_{t-1} exactly once (rows >= B2 and
+    // k >= H are zeros, which change neither max nor min), so var_g is a block reduction of the
+    // registers: no second pass over global memory, and each element is quantised once per gate.
+    __shared__ float qred[8];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
+      float mx = -INFINITY, mn = INFINITY;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        mx = fmaxf(mx, fmaxf(va[s], vb[s]));
+        mn = fminf(mn, fminf(va[s], vb[s]));
+      }
+      mx = warp_max(mx);
+      mn = -warp_max(-mn);
+      if (lane == 0) { qred[w] = mx; qred[4 + w] = mn; }
+      __syncthreads();
+      mx = fmaxf(fmaxf(qred[0], qred[1]), fmaxf(qred[2], qred[3]));
+      mn = fminf(fminf(qred[4], qred[5]), fminf(qred[6], qred[7]));
+      __syncthreads();
+      vars[g] = fabsf(mx) > fabsf(mn) ? fabsf(mx) : fabsf(mn);
       float vg[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -692,8 +683,8 @@ static int check(const pkc_rnn_args* a, bool bwd) {
   for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U[g], "pkc_rnn: null U[%d]", g);
   PKC_CHECK_ARG(!a->train || a->drop_p <= 0.f || a->drop_mask, "pkc_rnn: dropout needs drop_mask");
   if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work && a->ut, "pkc_rnn_bwd: null buffer");
-  PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir), "pkc_rnn: quantised h needs hq and a "
-                "uni-directional layer");
+  PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir && a->B <= 32), "pkc_rnn: quantised h needs "
+                "hq, a uni-directional layer and B <= 32");
   return PKC_OK;
 }
 
