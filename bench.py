@@ -184,6 +184,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-batch-sweep", action="store_true")
+    ap.add_argument("--no-seq-configs", action="store_true",
+                    help="skip the informational C3/C4/C5 sequence-model throughputs")
     ap.add_argument("--pmc-replay", type=int, default=0,
                     help="only replay the dominant launch N times (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -246,14 +248,12 @@ def main():
         print(json.dumps({"pmc_replay": dom_fn, "launches": nl * args.pmc_replay}), flush=True)
         return
     eng.capture(split_optimizer=world > 1)
-    for _ in range(args.warmup):
-        eng.train_step(allreduce)
+    eng.train_steps(args.warmup, allreduce)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.train_step(allreduce)
+    eng.train_steps(args.steps, allreduce)        # exactly args.steps batches
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -276,6 +276,16 @@ def main():
     sweep = {}
     if rank == 0 and world == 1 and not args.no_batch_sweep:
         sweep = batch_sweep(prec)
+    seq = {}
+    if rank == 0 and world == 1 and not args.no_seq_configs:
+        # BASELINE configs C3-C5 (informational; scripts/bench_seq.py has the details)
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import bench_seq
+        for c in ("c3", "c4", "c5"):
+            r = bench_seq.run(c, steps=4, warmup=1)
+            seq[c] = {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()
+                      if k != "config"}
+            torch.cuda.empty_cache()
     if rank == 0:
         is_gemm = "gemm" in label
         # MFMA-bound only where the launch's arithmetic intensity exceeds the machine balance
@@ -315,6 +325,7 @@ def main():
             "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
                                   sorted(agg.items(), key=lambda kv: -kv[1][1])},
             "batch_sweep_frames_per_s": sweep,
+            "sequence_configs_frames_per_s": seq,
             "chunk_prep_s": round(prep_s, 3),
             "mean_loss": round(loss_sum / max(1, n_done), 4),
         }

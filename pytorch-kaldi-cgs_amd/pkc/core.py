@@ -283,8 +283,7 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         eng.n_batches = n_batches
         if to_do == "train":
             eng.capture(split_optimizer=allreduce is not None)
-            for i in range(n_batches):
-                eng.train_step(allreduce)
+            eng.train_steps(n_batches, allreduce)
         else:
             for i in range(n_batches):
                 eng.eval_step()

@@ -341,6 +341,7 @@ class Engine:
         self._build_reg()
         self.graph = None
         self.graph_opt = None
+        self.graph_multi, self.steps_per_graph = None, 1
         self.steps_done = 0
         self.skip_labels = set()
 
@@ -1370,6 +1371,19 @@ class Engine:
             self._train_step_kernels(allreduce)
         self._after_step()
 
+    def train_steps(self, n, allreduce=None):
+        """n consecutive training batches (core.py:216-232 per batch); whole multi-step graphs
+        where possible."""
+        if self.graph is not None and self.graph_multi is not None and allreduce is None:
+            k = self.steps_per_graph
+            while n >= k:
+                self.graph_multi.replay()
+                for _ in range(k):
+                    self._after_step()
+                n -= k
+        for _ in range(n):
+            self.train_step(allreduce)
+
     def eval_step(self, batch=None):
         """Validation batch: forward with running BN statistics, loss/err accumulated."""
         if self.seq:
@@ -1445,24 +1459,37 @@ class Engine:
         if self.opt_entries and not self.static_opt and self.graph is None:
             self._upload_opt_desc(step_inc=1)
 
-    def capture(self, split_optimizer=False):
+    def capture(self, split_optimizer=False, steps_per_graph=8):
         """Capture the training step into hipGraph(s) (non-sequential models with step-independent
         optimizer descriptors: RMSprop / momentum-free SGD).  split_optimizer=True captures
-        forward+backward and the optimizer separately so a gradient all-reduce fits in between."""
+        forward+backward and the optimizer separately so a gradient all-reduce fits in between.
+        Without the split, a second graph holds steps_per_graph consecutive steps (the batch
+        counter lives on the device), so train_steps() pays one graph launch per that many
+        batches instead of one per batch."""
         if not self.static_opt or self.seq:
             return False
         self._set_rows(None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            st = self._stream()
+
+        def one_step(st):
             defer = bool(self.loss_heads)
             self._forward_kernels(st, True, defer_loss=defer)
             self._backward_kernels(st, self._loss_op() if defer else None,
                                    spread_opt=not split_optimizer)
             if not split_optimizer:
                 self._optim_kernels(st, spread_opt=True)
+
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            one_step(self._stream())
+        self.graph_multi, self.steps_per_graph = None, 1
+        if not split_optimizer and steps_per_graph > 1:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, stream=s):
+                for _ in range(steps_per_graph):
+                    one_step(self._stream())
+            self.graph_multi, self.steps_per_graph = gm, steps_per_graph
         self.graph_opt = None
         if split_optimizer:
             g2 = torch.cuda.CUDAGraph()

@@ -9,7 +9,14 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 first = sys.argv[2] if len(sys.argv) > 2 else "batch_gather"
 starts = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
-steps = [rows[a:b] for a, b in zip(starts[-21:-1], starts[-20:])]  # last 20 complete steps
+# the bench's own steps: the most common launch count between consecutive gathers (other
+# workloads in the same trace — batch sweep, sequence configs — have other shapes)
+pairs = list(zip(starts, starts[1:]))
+lens = defaultdict(int)
+for a, b in pairs:
+    lens[b - a] += 1
+L = max(lens, key=lens.get)
+steps = [rows[a:b] for a, b in pairs if b - a == L][-200:]
 agg = defaultdict(lambda: [0.0, 0.0, 0])
 order = []
 tot = []

@@ -192,7 +192,7 @@ def test_engine_graph_replay_equals_eager():
     from pkc.engine import Engine, parse_model
     cfg = c1_config(drop="0.15")
     res = []
-    for use_graph in (False, True):
+    for use_graph in (False, True, "multi"):
         nets, opts = build_nets(cfg, C1_DIMS)
         for n in nets.values():
             n.to(DEV).train()
@@ -204,16 +204,20 @@ def test_engine_graph_replay_equals_eager():
                      ["lab_cd", "lab_mono"], batch=128, seed=3)
         eng.bind_chunk(X, lab, 512)
         if use_graph:
-            assert eng.capture()
+            assert eng.capture(steps_per_graph=3)
             eng.ctr.zero_()
             eng.loss_acc.zero_()
             # capture only records; re-bind the initial weights (capture did not execute kernels)
-        for _ in range(4):
-            eng.train_step()
+        if use_graph == "multi":
+            eng.train_steps(4)            # one 3-step graph replay + one single step
+        else:
+            for _ in range(4):
+                eng.train_step()
         res.append((eng.chunk_totals(), {k: v.cpu() for k, v in nets["MLP_layers2"].state_dict().items()}))
-    assert res[0][0] == pytest.approx(res[1][0], rel=1e-6)
-    for k in res[0][1]:
-        torch.testing.assert_close(res[0][1][k], res[1][1][k], rtol=0, atol=0)
+    for other in res[1:]:
+        assert res[0][0] == pytest.approx(other[0], rel=1e-6)
+        for k in res[0][1]:
+            torch.testing.assert_close(res[0][1][k], other[1][k], rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("variant", ["prune", "pattern", "ghcgs"])
