@@ -313,6 +313,10 @@ int pkc_ark_write_mat(const char* path, int append, const char* key, int64_t row
 int64_t pkc_ark_index(const char* path, int64_t* offsets, int64_t* rows, int64_t* cols, int64_t cap,
                       char* keys_buf, int64_t keys_cap);
 int pkc_ark_read_rows(const char* path, int64_t offset, int64_t rows, int64_t cols, float* dst);
+/* Kaldi "CM " compressed matrix (data_io.py:729-766): blob = the bytes after "\0BCM ";
+ * pkc_ark_cm_size -> its byte length; pkc_ark_decode_cm -> rows x cols float32, row-major. */
+int64_t pkc_ark_cm_size(const unsigned char* blob, int64_t nbytes);
+int pkc_ark_decode_cm(const unsigned char* blob, int64_t nbytes, float* out);
 
 #ifdef __cplusplus
 }

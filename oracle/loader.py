@@ -161,3 +161,17 @@ def load_counts(text):
     """data_io.py:148-152 (first line '[ c1 c2 ... ]')."""
     row = text.splitlines()[0].strip().strip("[]").strip()
     return np.array([np.float32(v) for v in row.split()])
+
+
+def decode_cm(blob):
+    """data_io.py:729-766 (_read_compressed_mat, "CM " only): blob = bytes after "\\0BCM "."""
+    gmin, grange, rows, cols = np.frombuffer(blob[:16], dtype="<f4,<f4,<i4,<i4", count=1)[0]
+    ph = np.frombuffer(blob[16:16 + 8 * cols], dtype="<u2").reshape(cols, 4)
+    hdr = (ph * grange * 1.52590218966964e-05 + gmin).astype(np.float32)
+    data = np.frombuffer(blob[16 + 8 * cols:16 + 8 * cols + rows * cols], dtype=np.uint8)
+    data = data.reshape(cols, rows)
+    p0, p25, p75, p100 = (hdr[:, i:i + 1] for i in range(4))
+    m = np.where(data <= 64, p0 + (p25 - p0) / 64. * data,
+                 np.where(data > 192, p75 + (p100 - p75) / 63. * (data - 192),
+                          p25 + (p75 - p25) / 128. * (data - 64)))
+    return np.ascontiguousarray(m.T, dtype=np.float32)

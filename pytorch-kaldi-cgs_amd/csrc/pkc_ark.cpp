@@ -129,3 +129,54 @@ extern "C" int pkc_ark_read_rows(const char* path, int64_t offset, int64_t rows,
   }
   return PKC_OK;
 }
+
+// Kaldi CompressedMatrix "CM " (data_io.py:729-766, kaldi compressed-matrix.h): global header
+// {min, range, rows, cols}, per-column uint16 percentiles {p0, p25, p75, p100} mapped to
+// min + range * q / 65535, then cols x rows uint8 codes (column-major) decoded piecewise-linearly.
+// Evaluated in float32 exactly as the reference's numpy expressions (no contraction into FMA).
+extern "C" int64_t pkc_ark_cm_size(const unsigned char* blob, int64_t nbytes) {
+  if (!blob || nbytes < 16) return PKC_ERR_ARG;
+  int32_t rows, cols;
+  memcpy(&rows, blob + 8, 4);
+  memcpy(&cols, blob + 12, 4);
+  if (rows < 0 || cols < 0) return PKC_ERR_ARG;
+  return 16 + (int64_t)cols * 8 + (int64_t)rows * cols;
+}
+
+extern "C" int pkc_ark_decode_cm(const unsigned char* blob, int64_t nbytes, float* out) {
+#pragma clang fp contract(off)
+  const int64_t need = pkc_ark_cm_size(blob, nbytes);
+  if (need < 0 || need > nbytes || !out) {
+    pkc::set_error("pkc_ark_decode_cm: truncated or bad compressed matrix");
+    return PKC_ERR_ARG;
+  }
+  float gmin, grange;
+  int32_t rows, cols;
+  memcpy(&gmin, blob, 4);
+  memcpy(&grange, blob + 4, 4);
+  memcpy(&rows, blob + 8, 4);
+  memcpy(&cols, blob + 12, 4);
+  const float scale = (float)1.52590218966964e-05;
+  const unsigned char* ch = blob + 16;
+  const unsigned char* data = ch + (int64_t)cols * 8;
+  for (int32_t c = 0; c < cols; ++c) {
+    float p[4];
+    for (int q = 0; q < 4; ++q) {
+      uint16_t v;
+      memcpy(&v, ch + (int64_t)c * 8 + 2 * q, 2);
+      float x = (float)v * grange;
+      x = x * scale;
+      p[q] = x + gmin;
+    }
+    const float s0 = (p[1] - p[0]) / 64.0f, s1 = (p[2] - p[1]) / 128.0f, s2 = (p[3] - p[2]) / 63.0f;
+    for (int32_t r = 0; r < rows; ++r) {
+      const unsigned b = data[(int64_t)c * rows + r];
+      float v;
+      if (b <= 64) v = p[0] + s0 * (float)b;
+      else if (b > 192) v = p[2] + s2 * (float)(b - 192);
+      else v = p[1] + s1 * (float)(b - 64);
+      out[(int64_t)r * cols + c] = v;
+    }
+  }
+  return PKC_OK;
+}

@@ -87,6 +87,8 @@ _SIGS = {
     "pkc_reg_partial": (C.c_int, [C.c_int, vp, C.c_int, vp, vp]),
     "pkc_reg_finalize": (C.c_int, [C.c_int, vp, C.c_int, vp, C.c_float, vp, vp, C.c_int, vp]),
     "pkc_reg_grad": (C.c_int, [C.c_int, vp, C.c_int, vp, vp]),
+    "pkc_ark_cm_size": (i64, [vp, i64]),
+    "pkc_ark_decode_cm": (C.c_int, [vp, i64, vp]),
     "pkc_prune_work_size": (i64, []),
     "pkc_prune": (C.c_int, [vp, i64, C.c_double, vp, vp, vp]),
     "pkc_layernorm_fwd": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_float, vp, vp,

@@ -24,9 +24,13 @@ def write_mat_path(path, m, key="", append=False):
 
 
 def read_mat_ark_path(path):
-    """Binary FM/DM ark -> generator of (key, float32 matrix) (data_io.py:645-711)."""
+    """Binary FM/DM/CM ark -> generator of (key, float32 matrix) (data_io.py:645-766)."""
     lib = L.lib()
     n = lib.pkc_ark_index(path.encode(), None, None, None, 0, None, 0)
+    if n == L.PKC_ERR_UNSUPPORTED:         # compressed matrices: parse the bytes (pkc_ark_decode_cm)
+        with open(path, "rb") as f:
+            yield from parse_mat_ark_bytes(f.read())
+        return
     if n < 0:
         raise L.PkcError(lib.pkc_last_error().decode())
     offs, rows, cols = (C.c_int64 * n)(), (C.c_int64 * n)(), (C.c_int64 * n)()
@@ -52,9 +56,14 @@ def parse_mat_ark_bytes(buf):
         if buf[pos:pos + 2] != b"\0B":
             raise ValueError("only binary matrices are supported")
         hdr = buf[pos + 2:pos + 5]
+        if hdr == b"CM ":
+            out.append((key, decode_cm(buf, pos + 5)))
+            pos += 5 + int(L.lib().pkc_ark_cm_size(_addr(buf, pos + 5), len(buf) - pos - 5))
+            continue
         dt = {b"FM ": np.float32, b"DM ": np.float64}.get(hdr)
         if dt is None:
-            raise ValueError("compressed / unknown matrix type %r" % hdr)
+            raise ValueError("unsupported matrix type %r (CM2 / CM3 are not supported, as in "
+                             "data_io.py:736)" % hdr)
         rows = struct.unpack("<i", buf[pos + 6:pos + 10])[0]
         cols = struct.unpack("<i", buf[pos + 11:pos + 15])[0]
         pos += 15
@@ -62,6 +71,24 @@ def parse_mat_ark_bytes(buf):
         out.append((key, np.frombuffer(buf[pos:pos + n], dtype=dt).reshape(rows, cols)
                     .astype(np.float32)))
         pos += n
+    return out
+
+
+def _addr(buf, off):
+    a = np.frombuffer(buf, dtype=np.uint8)
+    return C.c_void_p(a.ctypes.data + off)
+
+
+def decode_cm(buf, off):
+    """One "CM " compressed matrix whose global header starts at buf[off] -> float32 matrix."""
+    lib = L.lib()
+    n = len(buf) - off
+    size = lib.pkc_ark_cm_size(_addr(buf, off), n)
+    if size < 0 or size > n:
+        raise ValueError("truncated compressed matrix")
+    rows, cols = struct.unpack("<ii", buf[off + 8:off + 16])
+    out = np.empty((rows, cols), dtype=np.float32)
+    call("pkc_ark_decode_cm", _addr(buf, off), n, out.ctypes.data_as(C.c_void_p))
     return out
 
 

@@ -342,6 +342,25 @@ def gen_rnn():
     np.savez_compressed(os.path.join(OUT, "rnn.npz"), **out)
 
 
+def gen_cm():
+    """Kaldi CM compressed matrices (data_io.py:729-766): hand-built blobs decoded by the
+    reference's _read_compressed_mat."""
+    import io
+    out = {}
+    rs = np.random.RandomState(17)
+    for i, (rows, cols) in enumerate([(7, 5), (40, 13), (1, 3)]):
+        gh = np.array([(rs.randn() * 3, abs(rs.randn()) * 10 + 0.5, rows, cols)],
+                      dtype=[("minvalue", "<f4"), ("range", "<f4"), ("num_rows", "<i4"), ("num_cols", "<i4")])
+        ph = np.sort(rs.randint(0, 65536, size=(cols, 4)), axis=1).astype("<u2")
+        data = rs.randint(0, 256, size=cols * rows).astype(np.uint8)
+        data[:min(6, data.size)] = [0, 64, 65, 192, 193, 255][:min(6, data.size)]
+        blob = gh.tobytes() + ph.tobytes() + data.tobytes()
+        m = data_io._read_compressed_mat(io.BytesIO(blob), "CM ")
+        out["blob%d" % i] = np.frombuffer(blob, dtype=np.uint8).copy()
+        out["mat%d" % i] = np.asarray(m, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "cm.npz"), **out)
+
+
 def gen_gru():
     from cases import GRU_CASES
     out = {}
@@ -374,7 +393,8 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:          # e.g. `make_golden.py mlp:l1 mlp:l2 mlp:gl`
         for a in sys.argv[1:]:
             kind, _, v = a.partition(":")
-            {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru()}[kind](v)
+            {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru(),
+             "cm": lambda _v: gen_cm()}[kind](v)
         sys.exit(0)
     gen_loader()
     gen_hcgs()
@@ -384,6 +404,7 @@ if __name__ == "__main__":
         gen_mlp(v)
     gen_rnn()
     gen_gru()
+    gen_cm()
     gen_ark()
     total = sum(os.path.getsize(os.path.join(OUT, f)) for f in os.listdir(OUT))
     print("golden fixtures written to %s (%.1f KB)" % (OUT, total / 1024))

@@ -217,3 +217,21 @@ def test_product_gru_init_matches_reference(case):
     assert sorted(sd) == ref_keys
     for k, v in sd.items():
         np.testing.assert_array_equal(v.numpy(), g[tag + "/init/" + k], err_msg=k)
+
+
+def test_product_cm_decode_matches_reference(tmp_path):
+    """Kaldi CM compressed feature matrices (data_io.py:729-766) through the C ABI, from an ark
+    file and from pipe bytes."""
+    from pkc import data_io as D
+    g = G("cm.npz")
+    ark = b""
+    for i in range(3):
+        ark += b"utt%d \0BCM " % i + g["blob%d" % i].tobytes()
+    path = str(tmp_path / "cm.ark")
+    open(path, "wb").write(ark)
+    got = list(D.read_mat_ark_path(path))
+    assert [k for k, _ in got] == ["utt0", "utt1", "utt2"]
+    for i, (_, m) in enumerate(got):
+        np.testing.assert_array_equal(m, g["mat%d" % i])
+    for i, (_, m) in enumerate(D.parse_mat_ark_bytes(ark)):
+        np.testing.assert_array_equal(m, g["mat%d" % i])
