@@ -119,7 +119,11 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
             lab_names.append(lname)
     seq = any(a[2] for a in arch_dict.values())
     rng = np.random if (not seq and to_do != "forward") else None
-    shared_list.append(("raw", fea, labs, lab_names, int(fd[3]), int(fd[4]), max_seq, rng, fname))
+    # sort / split the utterances and start the pinned-memory upload on a side stream here, in
+    # the loader thread, so it overlaps the current chunk's training; the frame shuffle (global
+    # np.random) stays on the main thread in _finish_chunk, in a deterministic order
+    staged = D.stage_chunk(fea, labs, max_seq)
+    shared_list.append(("raw", staged, labs, lab_names, int(fd[3]), int(fd[4]), max_seq, rng, fname))
     shared_list.append(None)
     shared_list.append(fea_dict)
     shared_list.append(lab_dict)
@@ -129,8 +133,9 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
 
 def _finish_chunk(shared_list):
     """GPU half of the loader: context window + normalisation + shuffle (pkc_cw_*)."""
-    _, fea, labs, lab_names, L, R, max_seq, rng, fname = shared_list[0]
-    ch = D.prepare_chunk(fea, labs, lab_names, L, R, max_seq, shuffle_rng=rng, fea_name=fname)
+    _, staged, labs, lab_names, L, R, max_seq, rng, fname = shared_list[0]
+    ch = D.prepare_chunk(None, labs, lab_names, L, R, max_seq, shuffle_rng=rng, fea_name=fname,
+                         staged=staged)
     fea_dict, lab_dict = shared_list[2], shared_list[3]
     c0, c1 = ch.fea_cols[fname]
     fea_dict[fname] = fea_dict[fname][:5] + [c0, c1, c1 - c0]

@@ -186,13 +186,42 @@ class Chunk:
         return self.feats.shape[0]
 
 
+class StagedChunk:
+    """A chunk after the host half of loading: utterances sorted / split (load_dataset) and the
+    raw frames on their way to HBM — copied from pinned host memory by an asynchronous copy on a
+    dedicated stream (hipMemcpyAsync underneath), so the upload of chunk k+1 overlaps the
+    training of chunk k (run_nn stages the next chunk from its loader thread)."""
+
+    def __init__(self, names, raw, lab_arrays, end_index, device):
+        self.names, self.lab_arrays, self.end_index = names, lab_arrays, end_index
+        self.shape = raw.shape
+        dev = torch.device(device)
+        self.stream = torch.cuda.Stream(device=dev)
+        pinned = torch.empty(raw.shape, dtype=torch.float32, pin_memory=True)
+        pinned.numpy()[...] = raw
+        with torch.cuda.stream(self.stream):
+            self.raw_d = pinned.to(dev, non_blocking=True)
+            self.done = torch.cuda.Event()
+            self.done.record(self.stream)
+        self._pinned = pinned           # alive until the copy has completed (finish_chunk)
+
+
+def stage_chunk(fea, labs, max_sequence_length, device="cuda"):
+    names, raw, lab_arrays, end_index = load_dataset(fea, labs, max_sequence_length)
+    return StagedChunk(names, np.ascontiguousarray(raw, dtype=np.float32), lab_arrays, end_index,
+                       device)
+
+
 def prepare_chunk(fea, labs, lab_names, left, right, max_sequence_length, shuffle_rng=None,
-                  device="cuda", fea_name="fea"):
+                  device="cuda", fea_name="fea", staged=None):
     """data_io.load_chunk + read_lab_fea for one feature stream (data_io.py:121-145, 155-282):
     context window, chunk z-normalisation, label shift by the chunk minimum, optional frame
-    shuffle (rng: the RandomState the reference's global np.random would be, seeded by run_nn)."""
-    names, raw, lab_arrays, end_index = load_dataset(fea, labs, max_sequence_length)
-    N, D = raw.shape
+    shuffle (rng: the RandomState the reference's global np.random would be, seeded by run_nn).
+    staged: the StagedChunk of these utterances when the loader thread already uploaded them."""
+    if staged is None:
+        staged = stage_chunk(fea, labs, max_sequence_length, device)
+    names, lab_arrays, end_index = staged.names, staged.lab_arrays, staged.end_index
+    N, D = staged.shape
     Nout = N - left - right
     end_index = end_index - left
     end_index[-1] = end_index[-1] - right
@@ -208,7 +237,9 @@ def prepare_chunk(fea, labs, lab_names, left, right, max_sequence_length, shuffl
         shuffle_rng.shuffle(perm)
         labels = labels[perm]
     dev = torch.device(device)
-    raw_d = torch.from_numpy(raw).to(dev, non_blocking=False)
+    torch.cuda.current_stream(dev).wait_event(staged.done)
+    raw_d = staged.raw_d
+    raw_d.record_stream(torch.cuda.current_stream(dev))
     mean = torch.empty(Cc, dtype=torch.float64, device=dev)
     std = torch.empty(Cc, dtype=torch.float64, device=dev)
     work = torch.empty(int(L.lib().pkc_cw_stats_work_size(N, D, left, right)), dtype=torch.float64,
