@@ -283,6 +283,11 @@ typedef struct {
   float* rh;
   /* pkc_rnn_bwd: G x H x H scratch for the transposed U (the B operand of the BPTT products) */
   float* ut;
+  /* LayerNorm of h after every step (use_laynorm; neural_networks.py:40-51 applied at :1093-1094,
+   * :1581-1582 ...): gamma / beta (H), NULL = off; xhat (T, B2, H) and stat (T, B2, 2) saved by the
+   * forward; g (T, B2, H) the post-norm gradients, dgamma / dbeta (H) written by the backward. */
+  const float* ln_gamma; const float* ln_beta; float ln_eps;
+  float* ln_xhat; float* ln_stat; float* ln_g; float* ln_dgamma; float* ln_dbeta;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
 /* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that

@@ -269,7 +269,10 @@ __global__ __launch_bounds__(ET) void colsum_kernel(int M, int N, int nslab, con
 // workgroup reduction (wave shuffles + 4-entry LDS merge) and the layer epilogue is ONE launch
 // with every load issued up front: split-K slabs are summed in registers (NS = power-of-two bound
 // on the slab count, loads clamped to the last slab instead of branched, so none is serialised).
-constexpr int FG = 4, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
+#ifndef PKC_DENSE_FG
+#define PKC_DENSE_FG 4
+#endif
+constexpr int FG = PKC_DENSE_FG, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {

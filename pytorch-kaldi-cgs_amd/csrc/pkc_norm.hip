@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64 * NW) void ln_bwd_rows_kernel(int M, int N, int 
   sgx = warp_sum(sgx);
   const float den = rowstat[2 * r], sd = rowstat[2 * r + 1];
   const float mg = sg / (float)N;
-  const float k = sgx / ((float)(N - 1) * sd);
+  const float k = sd > 0.f ? sgx / ((float)(N - 1) * sd) : 0.f;   // torch masks std == 0 to 0
   for (int j = lane; j < N; j += 64) {
     const float gh = slabs(g + j, ns, ss) * gamma[j];
     dx[(int64_t)r * N + j] = (gh - mg) / den - xh[j] * k;

@@ -164,30 +164,134 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
   }
 }
 
-// first backward launch: step T-1, no recurrent gradient yet
+// The gate gradients of step tt from the total dL/dh_tt = g (LSTM: plus the carried dc), into
+// dgates and the ping-pong slot of step tt ((T-1-tt) & 1) of the g / dc carries.
+template <int G, int CELL>
+__device__ __forceinline__ void gate_part(const pkc_rnn_args& a, const RnnIdx& ix, int tt, int r,
+                                          int k, float g, float dc_carry) {
+  const int64_t TB2H = (int64_t)a.T * ix.B2 * a.H;
+  const int64_t n = (int64_t)ix.B2 * a.H;
+  const int64_t e = (int64_t)r * a.H + k;
+  const int p = (a.T - 1 - tt) & 1;
+  float dg[4] = {0.f, 0.f, 0.f, 0.f}, go = 0.f, dco = 0.f;
+  gate_grads<CELL>(a, ix, tt, r, k, g, dc_carry, dg, &go, &dco);
+  const int64_t si = ix.st(tt, r, k);
+  if constexpr (CELL == PKC_CELL_GRU) {
+    a.dgates[si] = dg[0];
+    a.dgates[2 * TB2H + si] = dg[2];
+  } else if constexpr (CELL == PKC_CELL_MINGRU) {
+    a.dgates[TB2H + si] = dg[1];
+  } else {
+#pragma unroll
+    for (int q = 0; q < G; ++q) a.dgates[q * TB2H + si] = dg[q];
+  }
+  a.work[p * n + e] = go;
+  if constexpr (CELL == PKC_CELL_LSTM) a.work[2 * n + p * n + e] = dco;
+}
+
+// first backward launch: step T-1, no recurrent gradient yet (with LayerNorm on h: only the
+// post-norm gradient, the norm's backward and the gate gradients follow in rnn_ln_bwd_gates)
 template <int G, int CELL>
 __global__ void rnn_bwd_init(pkc_rnn_args a) {
   const RnnIdx ix = mkidx(a);
   const int64_t n = (int64_t)ix.B2 * a.H;
-  const int64_t TB2H = (int64_t)a.T * ix.B2 * a.H;
   const int t = a.T - 1;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(e / a.H), k = (int)(e % a.H);
     const float g = dy_at(a, ix.out(t, r, k));
-    float dg[4], go, dco = 0.f;
-    gate_grads<CELL>(a, ix, t, r, k, g, 0.f, dg, &go, &dco);
-    if constexpr (CELL == PKC_CELL_GRU) {
-      a.dgates[ix.st(t, r, k)] = dg[0];
-      a.dgates[2 * TB2H + ix.st(t, r, k)] = dg[2];
-    } else if constexpr (CELL == PKC_CELL_MINGRU) {
-      a.dgates[TB2H + ix.st(t, r, k)] = dg[1];
-    } else {
-#pragma unroll
-      for (int q = 0; q < G; ++q) a.dgates[q * TB2H + ix.st(t, r, k)] = dg[q];
+    if (a.ln_gamma) a.ln_g[ix.st(t, r, k)] = g;
+    else gate_part<G, CELL>(a, ix, t, r, k, g, 0.f);
+  }
+}
+
+// LayerNorm of the new hidden state (neural_networks.py:1093-1094, 1399-1400, 1581-1582,
+// 1758-1759, 1909-1910): h_t <- gamma (h_t - mean) / (std + eps) + beta per row, std unbiased.
+// One wave per row; saves xhat and (std + eps, std) for the backward.
+__global__ __launch_bounds__(256) void rnn_ln_fwd(pkc_rnn_args a, int t) {
+  const RnnIdx ix = mkidx(a);
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= ix.B2) return;
+  const int H = a.H;
+  float* h = a.hs + (int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H;
+  float sum = 0.f;
+  for (int j = lane; j < H; j += 64) sum += h[j];
+  const float mean = warp_sum(sum) / (float)H;
+  float sq = 0.f;
+  for (int j = lane; j < H; j += 64) {
+    const float d = h[j] - mean;
+    sq += d * d;
+  }
+  const float sd = sqrtf(warp_sum(sq) / (float)(H - 1));
+  const float den = sd + a.ln_eps;
+  for (int j = lane; j < H; j += 64) {
+    const float xh = (h[j] - mean) / den;
+    const float v = a.ln_gamma[j] * xh + a.ln_beta[j];
+    a.ln_xhat[ix.st(t, r, j)] = xh;
+    h[j] = v;
+    a.y[ix.out(t, r, j)] = v;
+  }
+  if (lane == 0) {
+    a.ln_stat[2 * ((int64_t)t * ix.B2 + r)] = den;
+    a.ln_stat[2 * ((int64_t)t * ix.B2 + r) + 1] = sd;
+  }
+}
+
+// Backward of that LayerNorm for step tt (row-wise), then the gate gradients of step tt:
+//   gh = g gamma, dh_raw = (gh - mean(gh)) / (std + eps) - xhat sum(gh xhat) / ((H - 1) std)
+template <int G, int CELL>
+__global__ __launch_bounds__(256) void rnn_ln_bwd_gates(pkc_rnn_args a, int tt) {
+  const RnnIdx ix = mkidx(a);
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= ix.B2) return;
+  const int H = a.H;
+  const int64_t n = (int64_t)ix.B2 * H;
+  const int64_t s0 = ix.st(tt, r, 0);
+  float sg = 0.f, sgx = 0.f;
+  for (int j = lane; j < H; j += 64) {
+    const float gh = a.ln_g[s0 + j] * a.ln_gamma[j];
+    sg += gh;
+    sgx += gh * a.ln_xhat[s0 + j];
+  }
+  sg = warp_sum(sg);
+  sgx = warp_sum(sgx);
+  const float den = a.ln_stat[2 * ((int64_t)tt * ix.B2 + r)];
+  const float sd = a.ln_stat[2 * ((int64_t)tt * ix.B2 + r) + 1];
+  const float mg = sg / (float)H;
+  // torch's std backward masks the zero-std case to 0 (a zero row: e.g. leading padding)
+  const float kk = sd > 0.f ? sgx / ((float)(H - 1) * sd) : 0.f;
+  const int src = (a.T - 1 - (tt + 1)) & 1;          // carry slot of step tt + 1
+  for (int j = lane; j < H; j += 64) {
+    const float gh = a.ln_g[s0 + j] * a.ln_gamma[j];
+    const float g = (gh - mg) / den - a.ln_xhat[s0 + j] * kk;
+    float dc_carry = 0.f;
+    if constexpr (CELL == PKC_CELL_LSTM)
+      if (tt < a.T - 1) dc_carry = a.work[2 * n + src * n + (int64_t)r * H + j];
+    gate_part<G, CELL>(a, ix, tt, r, j, g, dc_carry);
+  }
+}
+
+// dgamma = sum_{t,r} g_post * xhat, dbeta = sum_{t,r} g_post over the T * B2 rows of the layer
+__global__ __launch_bounds__(256) void rnn_ln_param_grads(pkc_rnn_args a) {
+  __shared__ float red[2][256];
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H;
+  const int c = blockIdx.x * 64 + threadIdx.x % 64, q = threadIdx.x / 64;
+  const int64_t rows = (int64_t)a.T * ix.B2;
+  float dg = 0.f, db = 0.f;
+  if (c < H)
+    for (int64_t r = q; r < rows; r += 4) {
+      const float g = a.ln_g[r * H + c];
+      dg += g * a.ln_xhat[r * H + c];
+      db += g;
     }
-    a.work[e] = go;                 // g ping  (step parity 1)
-    a.work[2 * n + e] = dco;        // dc ping
+  red[0][threadIdx.x] = dg;
+  red[1][threadIdx.x] = db;
+  __syncthreads();
+  if (q == 0 && c < H) {
+    const int l = threadIdx.x;
+    a.ln_dgamma[c] = (red[0][l] + red[0][64 + l]) + (red[0][128 + l] + red[0][192 + l]);
+    a.ln_dbeta[c] = (red[1][l] + red[1][64 + l]) + (red[1][128 + l] + red[1][192 + l]);
   }
 }
 
@@ -427,7 +531,7 @@ __device__ __forceinline__ void bwd_step_epi(const pkc_rnn_args& a, const RnnIdx
   const int64_t TB2H = (int64_t)a.T * ix.B2 * H;
   const int64_t n = (int64_t)ix.B2 * H;
   const int64_t e = (int64_t)r * H + k;
-  const int src = (a.T - 1 - t) & 1, dst = src ^ 1;      // ping-pong slots of g / dc
+  const int src = (a.T - 1 - t) & 1;                     // ping-pong slot of g / dc of step t
   float dh = acc;
   float dc_carry = 0.f;
   if constexpr (CELL == PKC_CELL_LIGRU) {
@@ -443,20 +547,11 @@ __device__ __forceinline__ void bwd_step_epi(const pkc_rnn_args& a, const RnnIdx
     dc_carry = a.work[2 * n + src * n + e];                  // dc_t * f_t
   }
   const float g = dy_at(a, ix.out(tt, r, k)) + dh;
-  float dg[4] = {0.f, 0.f, 0.f, 0.f}, go = 0.f, dco = 0.f;
-  gate_grads<CELL>(a, ix, tt, r, k, g, dc_carry, dg, &go, &dco);
-  const int64_t si = ix.st(tt, r, k);
-  if constexpr (CELL == PKC_CELL_GRU) {
-    a.dgates[si] = dg[0];
-    a.dgates[2 * TB2H + si] = dg[2];
-  } else if constexpr (CELL == PKC_CELL_MINGRU) {
-    a.dgates[TB2H + si] = dg[1];
-  } else {
-#pragma unroll
-    for (int q = 0; q < G; ++q) a.dgates[q * TB2H + si] = dg[q];
+  if (a.ln_gamma) {                  // gradient of the normalised h: rnn_ln_bwd_gates goes on
+    a.ln_g[ix.st(tt, r, k)] = g;
+    return;
   }
-  a.work[dst * n + e] = go;
-  if constexpr (CELL == PKC_CELL_LSTM) a.work[2 * n + dst * n + e] = dco;
+  gate_part<G, CELL>(a, ix, tt, r, k, g, dc_carry);
 }
 
 // d(rh)_t = Uh^T da_t (acc) of a two-phase cell -> dr_t (GRU) or dz_t (minimalGRU); d(rh) is kept
@@ -586,6 +681,7 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     for (int t = 0; t < a->T; ++t) {
       hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
       hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), g2, dim3(RT), 0, s, *a, t, vw);
+      if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
   } else {
     dim3 g1((a->H + 16 / G - 1) / (16 / G), rows);
@@ -594,6 +690,7 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
       else
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
+      if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
   }
   PKC_LAUNCH_CHECK("pkc_rnn_fwd step");
@@ -610,6 +707,9 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   const dim3 tg((a->H + 31) / 32, (a->H + 31) / 32, G);
   hipLaunchKernelGGL(rnn_transpose_u, tg, dim3(256), 0, s, *a);
   hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
+  const bool ln = a->ln_gamma != nullptr;
+  const dim3 lg((B2 + 3) / 4);
+  if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, a->T - 1);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
   const unsigned kt = (unsigned)((a->H + 15) / 16);
   if constexpr (two_phase(CELL)) {
@@ -625,6 +725,7 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
       }
+      if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
       hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a, tt,
                          HG, vw);
     }
@@ -638,8 +739,10 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
                            tt + 1, 0, vw);
         hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       }
+      if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
     }
   }
+  if (ln) hipLaunchKernelGGL(rnn_ln_param_grads, dim3((a->H + 63) / 64), dim3(256), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd step");
   hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
@@ -683,6 +786,9 @@ static int check(const pkc_rnn_args* a, bool bwd) {
   for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U[g], "pkc_rnn: null U[%d]", g);
   PKC_CHECK_ARG(!a->train || a->drop_p <= 0.f || a->drop_mask, "pkc_rnn: dropout needs drop_mask");
   if (bwd) PKC_CHECK_ARG(a->dy && a->dgates && a->work && a->ut, "pkc_rnn_bwd: null buffer");
+  PKC_CHECK_ARG(!a->ln_gamma || (a->ln_beta && a->ln_xhat && a->ln_stat && a->H > 1 &&
+                                 (!bwd || (a->ln_g && a->ln_dgamma && a->ln_dbeta))),
+                "pkc_rnn: LayerNorm needs beta, xhat, stat (+ g, dgamma, dbeta for the backward)");
   PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir && a->B <= 32), "pkc_rnn: quantised h needs "
                 "hq, a uni-directional layer and B <= 32");
   return PKC_OK;

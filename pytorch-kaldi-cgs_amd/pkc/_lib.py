@@ -63,7 +63,9 @@ class RnnArgs(C.Structure):
                 ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp), ("stream_id", i64),
                 ("drop_mask_in", vp), ("drop_mask", vp), ("hs", vp), ("cs", vp), ("gates", vp),
                 ("y", vp), ("dy", vp), ("dy_nslab", C.c_int), ("dy_slab_stride", i64),
-                ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp), ("rh", vp), ("ut", vp)]
+                ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp), ("rh", vp), ("ut", vp),
+                ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", C.c_float), ("ln_xhat", vp),
+                ("ln_stat", vp), ("ln_g", vp), ("ln_dgamma", vp), ("ln_dbeta", vp)]
 
 
 class GemmProblem(C.Structure):

@@ -218,6 +218,9 @@ class RecNode:
                 for g in range(self.G):
                     out.append((sp["bnm"][g].weight, ("dgamma", li, g), None))
                     out.append((sp["bnm"][g].bias, ("dbeta", li, g), None))
+            if sp.get("ln"):
+                out.append((sp["ln_gamma"], ("dgamma_ln", li, 0), None))
+                out.append((sp["ln_beta"], ("dbeta_ln", li, 0), None))
         return out
 
     def quant_of(self, p):
@@ -599,7 +602,10 @@ class Engine:
                       rwork=_f32(8 * B2 * H, dev), ut=_f32(G * H * H, dev),
                       dx=_f32(G * MAX_SPLITS * M * K, dev),
                       dW=[None] * G, db=[None] * G, dU=[None] * G, dgamma=[None] * G,
-                      dbeta=[None] * G)
+                      dbeta=[None] * G, dgamma_ln=[None], dbeta_ln=[None])
+            if sp.get("ln"):
+                lb.update(ln_xhat=_f32(T * B2 * H, dev), ln_stat=_f32(2 * T * B2, dev),
+                          ln_g=_f32(T * B2 * H, dev), ln_pg=_f32(2 * H, dev))
             if sp["ibits"]:
                 lb["hq"] = _f32((T + 1) * B2 * H, dev)      # q4(h_{t-1}) per step
                 if n.lbuf:                                   # layers >= 1: q1..qG of y_{l-1}
@@ -997,6 +1003,15 @@ class Engine:
         a.dgates = lb["dgates"].data_ptr()
         a.work = lb["rwork"].data_ptr()
         a.ut = lb["ut"].data_ptr()
+        if sp.get("ln"):
+            a.ln_gamma, a.ln_beta, a.ln_eps = sp["ln_gamma"].data_ptr(), sp["ln_beta"].data_ptr(), 1e-6
+            a.ln_xhat, a.ln_stat = lb["ln_xhat"].data_ptr(), lb["ln_stat"].data_ptr()
+            a.ln_g = lb["ln_g"].data_ptr()
+            if lb["dgamma_ln"][0] is not None:
+                a.ln_dgamma, a.ln_dbeta = lb["dgamma_ln"][0].data_ptr(), lb["dbeta_ln"][0].data_ptr()
+            else:                        # no optimizer for this arch: gradients to scratch
+                a.ln_dgamma = lb["ln_pg"].data_ptr()
+                a.ln_dbeta = lb["ln_pg"].data_ptr() + 4 * H
         return a
 
     def _rec_inputs(self, n, li):

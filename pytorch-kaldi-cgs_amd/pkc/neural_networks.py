@@ -333,8 +333,8 @@ class liGRU(nn.Module):
         raise NotImplementedError("the reference liGRU has no prune hook")
 
     def check_supported(self):
-        if self.ligru_use_laynorm_inp or self.ligru_use_batchnorm_inp or any(self.ligru_use_laynorm):
-            raise NotImplementedError("LayerNorm / input normalisation in liGRU is not on the pkc path yet")
+        if self.ligru_use_laynorm_inp or self.ligru_use_batchnorm_inp:
+            raise NotImplementedError("input normalisation in liGRU is not on the pkc path yet")
 
     def layer_specs(self):
         specs = []
@@ -346,7 +346,9 @@ class liGRU(nn.Module):
                               U=[self.uz[i].weight, self.uh[i].weight],
                               bnm=[self.bn_wz[i], self.bn_wh[i]],
                               Wmask=self.hcgsx[i].mask if self.ligru_hcgs else None,
-                              Umask=self.hcgsh[i].mask if self.ligru_hcgs else None))
+                              Umask=self.hcgsh[i].mask if self.ligru_hcgs else None,
+                              ln=bool(self.ligru_use_laynorm[i]), ln_gamma=self.ln[i].gamma,
+                              ln_beta=self.ln[i].beta))
         return specs
 
 
@@ -411,8 +413,8 @@ class GRU(nn.Module):
         raise NotImplementedError("the reference GRU has no prune hook")
 
     def check_supported(self):
-        if self.gru_use_laynorm_inp or self.gru_use_batchnorm_inp or any(self.gru_use_laynorm):
-            raise NotImplementedError("LayerNorm / input normalisation in GRU is not on the pkc path yet")
+        if self.gru_use_laynorm_inp or self.gru_use_batchnorm_inp:
+            raise NotImplementedError("input normalisation in GRU is not on the pkc path yet")
 
     def layer_specs(self):
         specs = []
@@ -423,7 +425,8 @@ class GRU(nn.Module):
                               b=[self.wz[i].bias, self.wr[i].bias, self.wh[i].bias],
                               U=[self.uz[i].weight, self.ur[i].weight, self.uh[i].weight],
                               bnm=[self.bn_wz[i], self.bn_wr[i], self.bn_wh[i]],
-                              Wmask=None, Umask=None))
+                              Wmask=None, Umask=None, ln=bool(self.gru_use_laynorm[i]),
+                              ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta))
         return specs
 
 
@@ -486,9 +489,9 @@ class _PlainRec(nn.Module):
         raise NotImplementedError("the reference %s has no prune hook" % type(self).__name__)
 
     def check_supported(self):
-        if self.ln_inp or self.bn_inp or any(self.use_ln):
-            raise NotImplementedError("LayerNorm / input normalisation in %s is not on the pkc "
-                                      "path yet" % type(self).__name__)
+        if self.ln_inp or self.bn_inp:
+            raise NotImplementedError("input normalisation in %s is not on the pkc path yet"
+                                      % type(self).__name__)
 
     def layer_specs(self):
         specs = []
@@ -499,7 +502,8 @@ class _PlainRec(nn.Module):
                               b=[getattr(self, "w" + g)[i].bias for g in self.GATES],
                               U=[getattr(self, "u" + g)[i].weight for g in self.GATES],
                               bnm=[getattr(self, "bn_w" + g)[i] for g in self.GATES],
-                              Wmask=None, Umask=None))
+                              Wmask=None, Umask=None, ln=bool(self.use_ln[i]),
+                              ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta))
         return specs
 
 
@@ -665,8 +669,8 @@ class LSTM(_PatternSet, nn.Module):
         return _mask_product(h, gm)
 
     def check_supported(self):
-        if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp or any(self.lstm_use_laynorm):
-            raise NotImplementedError("LayerNorm / input normalisation in LSTM is not on the pkc path yet")
+        if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp:
+            raise NotImplementedError("input normalisation in LSTM is not on the pkc path yet")
         if self.if_pattern and self.pattern_kernels is None:
             raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option or "
                                       "patterns injected by run_nn)")
@@ -699,5 +703,6 @@ class LSTM(_PatternSet, nn.Module):
                               qbits=self.param_quant[i] if self.lstm_quant else 0,
                               ibits=self.inp_quant[0] if (self.lstm_quant and self.lstm_quant_inp) else 0,
                               prune=self.prune_perc[i] if self.prune else None,
-                              pattern=bool(self.if_pattern)))
+                              pattern=bool(self.if_pattern), ln=bool(self.lstm_use_laynorm[i]),
+                              ln_gamma=self.ln[i].gamma, ln_beta=self.ln[i].beta))
         return specs

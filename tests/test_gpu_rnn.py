@@ -52,6 +52,9 @@ def dx0(eng, node):
 PATTERN = dict(if_pattern="True", pattern_mode="pattern", pattern_shape="8,8", pattern_nnz="4,4",
                pattern_num="16,16")
 CASES = [("ligru_bidir", "liGRU", LIGRU_DEF, 7, 3, 20, 21),
+         ("ligru_uni_ln", "liGRU", dict(LIGRU_DEF, ligru_bidir="False", ligru_act="tanh,relu",
+                                        ligru_orthinit="False", ligru_use_laynorm="True,False"),
+          6, 2, 12, 22),
          ("lstm", "LSTM", LSTM_DEF, 7, 3, 20, 23),
          ("lstm_hcgs_quant", "LSTM", dict(LSTM_DEF, lstm_hcgs="True", lstm_quant="True",
                                           lstm_quant_inp="True"), 7, 3, 24, 24),
@@ -88,6 +91,11 @@ def test_recurrent_layer_matches_reference(case):
                                rtol=1e-3, atol=1e-5)
     grads = {}
     for li, lb in enumerate(node.lbuf):
+        if node.layers[li].get("ln"):        # LayerNorm of h
+            H = lb["H"]
+            own = lb["dgamma_ln"][0] is not None
+            grads["ln.%d.gamma" % li] = lb["dgamma_ln"][0] if own else lb["ln_pg"][:H]
+            grads["ln.%d.beta" % li] = lb["dbeta_ln"][0] if own else lb["ln_pg"][H:2 * H]
         for gi, gate in enumerate(net.GATES):
             if cls in ("liGRU", "GRU", "minimalGRU", "RNN"):
                 if lb["db"][gi] is not None:

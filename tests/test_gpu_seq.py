@@ -35,6 +35,19 @@ def make_cfg(body):
     elif body == "rnn":
         cfg["a1"] = dict(RNN_DEF, arch_name="rnn", rnn_lay="32,24", rnn_drop="0.2,0.2",
                          rnn_act="tanh,relu", **opt)
+    elif body == "lstm_ln":        # LayerNorm of h instead of BN (neural_networks.py:1093-1094)
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", lstm_use_batchnorm="False,True",
+                         lstm_use_laynorm="True,True", **opt)
+    elif body == "gru_nobn":       # no BN, no LN: the input Linears carry biases
+        cfg["a1"] = dict(GRU_DEF, arch_name="rnn", gru_lay="32,24", gru_drop="0.2,0.2",
+                         gru_use_batchnorm="False,False", **opt)
+    elif body == "lstm_ln_bn":
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", lstm_use_laynorm="True,True", **opt)
+    elif body == "gru_ln":
+        cfg["a1"] = dict(GRU_DEF, arch_name="rnn", gru_lay="32,24", gru_drop="0.2,0.2",
+                         gru_use_laynorm="True,False", gru_use_batchnorm="False,True", **opt)
     elif body == "lstm_gl":        # TIMIT_CGS/TIMIT_LSTM_fmllr_groupLasso.cfg: group lasso on the LSTM
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", skip_regularization="False", **opt)
@@ -68,7 +81,7 @@ def make_cfg(body):
 
 @pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune",
                                   "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply", "gru", "mingru",
-                                  "rnn"])
+                                  "rnn", "lstm_ln", "gru_ln", "gru_nobn", "lstm_ln_bn"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -87,7 +100,8 @@ def test_seq_engine_vs_oracle(body):
         cls = ({"ligru": "liGRU", "ligru_hcgs": "liGRU", "lstm": "LSTM", "lstm_bidir": "LSTM",
                 "lstm_prune": "LSTM", "lstm_gl": "LSTM", "lstm_ghcgs_l1": "LSTM",
                 "lstm_ghcgs_apply": "LSTM", "gru": "GRU", "mingru": "minimalGRU",
-                "rnn": "RNN"}[body]
+                "rnn": "RNN", "lstm_ln": "LSTM", "gru_ln": "GRU", "gru_nobn": "GRU",
+                "lstm_ln_bn": "LSTM"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
