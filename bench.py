@@ -193,15 +193,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PKC_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
+    backend = os.environ.get("PKC_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     allreduce = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
-        def allreduce(t):
-            dist.all_reduce(t)
+        def allreduce(t, async_op=False):
+            return dist.all_reduce(t, async_op=async_op)
     from pkc import _lib
     prec = _lib.PREC_BF16 if args.prec == "bf16" else _lib.PREC_FP32
     eng, chunk, prep_s, nets = build(prec, args.batch, rank, world)

@@ -91,9 +91,12 @@ class GradAllReduce:
         self.group = group
         self.calls = 0
 
-    def __call__(self, gflat):
-        dist.all_reduce(gflat, group=self.group)
+    def __call__(self, gflat, async_op=False):
+        """async_op=True returns the work handle: the collective runs on the communicator's own
+        stream, overlapping the backward kernels the caller queues meanwhile, and
+        handle.wait() makes the caller's current stream wait for it (the host does not block)."""
         self.calls += 1
+        return dist.all_reduce(gflat, group=self.group, async_op=async_op)
 
 
 def average_buffers(modules, device=None):

@@ -345,6 +345,7 @@ class Engine:
         self.graph = None
         self.graph_opt = None
         self.graph_multi, self.steps_per_graph = None, 1
+        self.graph_tail = None
         self.steps_done = 0
         self.skip_labels = set()
 
@@ -556,7 +557,9 @@ class Engine:
         self.gflat = _f32(sum(p.numel() for _, p, _, _ in plist), dev)
         off = 0
         self.grads = {}
+        self.grad_off = {}
         for n, p, key, m in plist:
+            self.grad_off.setdefault(n, off)
             g = self.gflat[off:off + p.numel()].view_as(p)
             off += p.numel()
             if isinstance(key, tuple):
@@ -1263,7 +1266,24 @@ class Engine:
                  L.GemmProblem(kind=L.OP_OPTIM, M=nch, A=self.opt_desc.data_ptr(),
                                B=cmap.data_ptr()))]
 
-    def _backward_kernels(self, s, loss_op=None, spread_opt=False):
+    def _bucket_cut(self):
+        """Data parallelism: the node after whose dW launch the gradients of it and every later
+        node (the tail of gflat: heads and top layers, finished first in the reverse pass) form
+        the first all-reduce bucket — about a third of the buffer or more — so that collective
+        overlaps the rest of the backward.  Returns (node, gflat offset) or (None, 0)."""
+        if not hasattr(self, "_cut"):
+            self._cut = (None, 0)
+            total = self.gflat.numel()
+            for n in reversed(self.nodes):
+                if not self.needs_grad[n] or n.rec or n not in self.grad_off:
+                    continue
+                off = self.grad_off[n]
+                if total - off >= total // 3 and off > 0:
+                    self._cut = (n, off)
+                    break
+        return self._cut
+
+    def _backward_kernels(self, s, loss_op=None, spread_opt=False, on_cut=None):
         """Reverse pass.  The matmuls of a layer (dW, dX) are queued and launched together with
         those of the layers after it that are still pending, right before the first kernel that
         needs one of their results (the producer's BatchNorm backward reads the dX slabs).
@@ -1276,12 +1296,18 @@ class Engine:
                 n.sb = self._grad_slabs(n)
         pend = [loss_op] if loss_op is not None else []
         carry, carry_next = [], []
+        cut_node = self._bucket_cut()[0] if on_cut is not None else None
+        pend_nodes = []
 
         def flush():
-            nonlocal pend, carry, carry_next
+            nonlocal pend, carry, carry_next, pend_nodes, cut_node
             if pend or carry:
                 self._gemms(pend + carry, s)
             pend, carry, carry_next = [], carry_next, []
+            if cut_node is not None and cut_node in pend_nodes:
+                cut_node = None
+                on_cut()                # the first bucket's gradients are final
+            pend_nodes = []
 
         for n in reversed(self.nodes):
             if not self.needs_grad[n]:
@@ -1294,6 +1320,7 @@ class Engine:
                 flush()
             self._dense_bwd_pre(n, s)
             pend += self._bwd_problems(n)
+            pend_nodes.append(n)
             if spread_opt:
                 carry_next += self._opt_op(n)
         flush()
@@ -1354,9 +1381,22 @@ class Engine:
         defer = bool(self.loss_heads)
         spread = not self.seq and allreduce is None
         self._forward_kernels(s, True, batch, defer_loss=defer)
-        self._backward_kernels(s, self._loss_op() if defer else None, spread_opt=spread)
+        works = []
+        cut_off = self._bucket_cut()[1] if allreduce is not None else 0
+
+        def first_bucket():             # overlaps the rest of the backward
+            works.append(allreduce(self.gflat[cut_off:], async_op=True))
+
+        self._backward_kernels(s, self._loss_op() if defer else None, spread_opt=spread,
+                               on_cut=first_bucket if (allreduce is not None and cut_off) else None)
         if allreduce is not None:
-            allreduce(self.gflat)
+            if works:
+                works.append(allreduce(self.gflat[:cut_off], async_op=True))
+            else:
+                works.append(allreduce(self.gflat, async_op=True))
+            for w in works:
+                if w is not None:
+                    w.wait()
         self._optim_kernels(s, spread_opt=spread)
 
     # ------------------------------------------------------------------ public API
@@ -1376,11 +1416,24 @@ class Engine:
             self._train_step_kernels(allreduce, batch)
             self.ctr.add_(1)           # step counter of the dropout RNG streams
         elif self.graph is not None:
-            self.graph.replay()
-            if self.graph_opt is not None:
-                if allreduce is not None:
-                    allreduce(self.gflat)
+            if self.graph_opt is not None and self.graph_tail is not None:
+                # bucketed: first bucket all-reduced while the rest of the backward replays
+                self.graph.replay()
+                off = self._bucket_cut()[1]
+                works = [allreduce(self.gflat[off:], async_op=True)] if allreduce else []
+                self.graph_tail.replay()
+                if allreduce:
+                    works.append(allreduce(self.gflat[:off], async_op=True))
+                for w in works:
+                    if w is not None:
+                        w.wait()
                 self.graph_opt.replay()
+            else:
+                self.graph.replay()
+                if self.graph_opt is not None:
+                    if allreduce is not None:
+                        allreduce(self.gflat)
+                    self.graph_opt.replay()
         else:
             self._set_rows(None)
             self._train_step_kernels(allreduce)
@@ -1495,9 +1548,30 @@ class Engine:
             if not split_optimizer:
                 self._optim_kernels(st, spread_opt=True)
 
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            one_step(self._stream())
+        self.graph_tail = None
+        if split_optimizer and self._bucket_cut()[0] is not None:
+            # data parallelism: forward + backward up to the first bucket's last dW launch, then
+            # the rest of the backward, as two graphs with the first all-reduce between them
+            pool = torch.cuda.graph_pool_handle()
+            g, gt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                g.capture_begin(pool=pool)
+
+                def cut():
+                    g.capture_end()
+                    gt.capture_begin(pool=pool)
+
+                st = self._stream()
+                defer = bool(self.loss_heads)
+                self._forward_kernels(st, True, defer_loss=defer)
+                self._backward_kernels(st, self._loss_op() if defer else None, spread_opt=False,
+                                       on_cut=cut)
+                gt.capture_end()
+            self.graph_tail = gt
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                one_step(self._stream())
         self.graph_multi, self.steps_per_graph = None, 1
         if not split_optimizer and steps_per_graph > 1:
             gm = torch.cuda.CUDAGraph()

@@ -192,7 +192,11 @@ def test_engine_graph_replay_equals_eager():
     from pkc.engine import Engine, parse_model
     cfg = c1_config(drop="0.15")
     res = []
-    for use_graph in (False, True, "multi"):
+
+    def no_op_allreduce(t, async_op=False):     # world size 1: the data-parallel code path
+        return None
+
+    for use_graph in (False, True, "multi", "dp_eager", "dp_graph"):
         nets, opts = build_nets(cfg, C1_DIMS)
         for n in nets.values():
             n.to(DEV).train()
@@ -203,13 +207,21 @@ def test_engine_graph_replay_equals_eager():
         eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
                      ["lab_cd", "lab_mono"], batch=128, seed=3)
         eng.bind_chunk(X, lab, 512)
-        if use_graph:
+        if use_graph in (True, "multi"):
             assert eng.capture(steps_per_graph=3)
             eng.ctr.zero_()
             eng.loss_acc.zero_()
             # capture only records; re-bind the initial weights (capture did not execute kernels)
+        if use_graph == "dp_graph":
+            assert eng.capture(split_optimizer=True)
+            assert eng.graph_tail is not None       # bucketed: two backward graphs
+            eng.ctr.zero_()
+            eng.loss_acc.zero_()
         if use_graph == "multi":
             eng.train_steps(4)            # one 3-step graph replay + one single step
+        elif use_graph in ("dp_eager", "dp_graph"):
+            for _ in range(4):
+                eng.train_step(no_op_allreduce)
         else:
             for _ in range(4):
                 eng.train_step()
