@@ -368,8 +368,19 @@ class Engine:
             if getattr(net, "seq_model", False):
                 if src[0] != "fea":
                     raise NotImplementedError("%s: a recurrent arch must read a feature stream" % a)
+                # input LayerNorm / BatchNorm over the T*B rows (neural_networks.py:1511-1516 ...)
+                for i, spec in enumerate(net.input_norm_specs() if hasattr(net, "input_norm_specs")
+                                         else []):
+                    nl = NormLayer(a, i, spec, K)
+                    nl.src = src
+                    if src[0] == "node":
+                        src[1].consumers.append(nl)
+                    self.nodes.append(nl)
+                    src = ("node", nl)
                 node = RecNode(a, net, K)
                 node.src = src
+                if src[0] == "node":
+                    src[1].rec_consumer = node      # its gradient: the rec layer-0 dX slabs
                 self.nodes.append(node)
                 produced[out] = node
                 continue
@@ -545,13 +556,15 @@ class Engine:
         for n in self.nodes:
             cap = 0
             for c in n.consumers:
-                c.sxcap = self.cap or _splits(M, n.N, c.N, MAX_SPLITS)
+                # an input norm (no matmul) writes its input gradient into one slab
+                c.sxcap = 1 if c.W is None else (self.cap or _splits(M, n.N, c.N, MAX_SPLITS))
                 cap += c.sxcap
             n.gslab = _f32(cap * M * n.N, dev) if cap else None
         self.needs_grad = {}
         for n in reversed(self.nodes):
+            rc = getattr(n, "rec_consumer", None)
             self.needs_grad[n] = (n.head and n.loss_weight != 0.0) or any(
-                self.needs_grad[c] for c in n.consumers)
+                self.needs_grad[c] for c in n.consumers) or (rc is not None and self.needs_grad[rc])
         # all gradients in ONE flat buffer (a single RCCL all-reduce under data parallelism)
         plist = [(n, p, key, m) for n in self.nodes for (p, key, m) in n.params()]
         self.gflat = _f32(sum(p.numel() for _, p, _, _ in plist), dev)
@@ -1128,7 +1141,7 @@ class Engine:
         consumers share a budget of MAX_SPLITS slabs (the fused small-batch BN backward sums at
         most that many in registers); the widest consumer gives up splits first."""
         M = self.M
-        want = [_splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
+        want = [1 if c.W is None else _splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
         while sum(want) > MAX_SPLITS and max(want) > 1:
             want[want.index(max(want))] -= 1
         off = 0
@@ -1144,30 +1157,48 @@ class Engine:
         consumers' dX slabs (a head's dlogits came from the forward; its bias gradient is an
         operation of the grouped backward launch, _bwd_problems)."""
         M = self.M
-        if n.W is None and n.ln:             # input LayerNorm: only its gamma / beta gradients
-            self._ln_bwd(n, s, ptr(n.gslab), n.sb, M * n.N, n.dz, None)
+        # gradient of n's output: its consumers' dX slabs (an input norm consumer writes one), or
+        # a recurrent node's layer-0 dX slabs when n is that node's input norm
+        gs = getattr(n, "gsrc", None)
+        if gs is not None:
+            g_ptr, g_ns, g_st = gs[0].data_ptr(), gs[1], gs[2]
+        else:
+            g_ptr, g_ns, g_st = ((n.gslab.data_ptr(), n.sb, M * n.N) if n.gslab is not None
+                                 else (None, 0, 0))
+        if n.W is None and n.ln:             # input LayerNorm: gamma / beta and input gradients
+            self._ln_bwd(n, s, C.c_void_p(g_ptr), g_ns, g_st, self._norm_dx(n), None)
             return
         if n.head:
             if n.ln:                         # dlogits are the LayerNorm output's gradient
                 self._ln_bwd(n, s, ptr(n.dz_ln), 1, 0, n.dz, n.db)
             return
-        a = L.DenseBwdArgs(M=M, N=n.N, nslab=n.sb, gslab=n.gslab.data_ptr(),
-                           slab_stride=M * n.N,
+        a = L.DenseBwdArgs(M=M, N=n.N, nslab=g_ns, gslab=g_ptr,
+                           slab_stride=g_st,
                            norm=L.NORM_BN_TRAIN if n.bn else L.NORM_NONE,
                            act=L.ACT[n.act], gamma=n.gamma.data_ptr(),
                            beta=n.beta.data_ptr(), save_invstd=n.save_invstd.data_ptr(),
                            xhat=n.xhat.data_ptr(),
                            keep=n.keep.data_ptr() if n.keep is not None else None,
-                           drop_p=n.drop, dz=(n.dz_ln if n.ln else n.dz).data_ptr(),
+                           drop_p=n.drop,
+                           dz=(n.dz_ln if n.ln else self._norm_dx(n) if n.W is None else n.dz).data_ptr(),
                            dgamma=n.dgamma.data_ptr() if n.bn else None,
                            dbeta=n.dbeta.data_ptr() if n.bn else None,
                            dbias=n.db.data_ptr() if (n.b is not None and not n.ln) else None)
-        self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (n.sb + 3), "pkc_dense_bwd",
+        self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 3), "pkc_dense_bwd",
                 C.byref(a), ptr(n.work), s)
         if n.ln:
             # the Linear's bias sits in front of the LayerNorm (per-row statistics): its gradient
             # is the column sum of the LayerNorm's input gradient
             self._ln_bwd(n, s, ptr(n.dz_ln), 1, 0, n.dz, n.db)
+
+    def _norm_dx(self, n):
+        """Where an input normalisation writes its input gradient: its slab of the producer's
+        gradient slabs (own dz when it reads a feature stream)."""
+        if n.src[0] == "node" and n.src[1].gslab is not None:
+            P = n.src[1]
+            off = P.cons_off[P.consumers.index(n)]
+            return P.gslab[off * self.M * P.N:(off + 1) * self.M * P.N]
+        return n.dz
 
     def _ln_bwd(self, n, s, dy, nslab, stride, dx, dbias):
         M = self.M
@@ -1255,6 +1286,8 @@ class Engine:
                             C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
                     nx += sx
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
+            if li == 0 and n.src[0] == "node":
+                n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
 
     def _opt_op(self, n):
         """The optimizer update of node n's parameters as an operation of a grouped launch."""
@@ -1314,7 +1347,7 @@ class Engine:
                 continue
             if n.rec:
                 flush()
-                self._rec_bwd(n, s)
+                self._rec_bwd(n, s, want_dx0=n.src[0] == "node")
                 continue
             if not n.head:
                 flush()

@@ -56,6 +56,19 @@ def _prune_params(params, perc):
     torch.cuda.synchronize()
 
 
+def _input_norm_specs(net, ln, bn):
+    """ln0 (per row) then bn0 (over all rows; T*B rows, padding included, for a recurrent
+    architecture: neural_networks.py:826-831) as engine NormLayer specs."""
+    out = []
+    if ln:
+        out.append(dict(kind="ln", gamma=net.ln0.gamma, beta=net.ln0.beta))
+    if bn:
+        out.append(dict(kind="bn", gamma=net.bn0.weight, beta=net.bn0.bias,
+                        rm=net.bn0.running_mean, rv=net.bn0.running_var,
+                        nbt=net.bn0.num_batches_tracked))
+    return out
+
+
 class _PatternSet:
     """Pattern-set plumbing shared by MLP and LSTM (neural_networks.py:115-131, 513-529).
     The reference searches the set with sklearn KMeans (sparsity.py:999-1049, no random_state:
@@ -242,14 +255,7 @@ class MLP(_PatternSet, nn.Module):
 
     def input_norm_specs(self):
         """Input normalisations in the reference's order: ln0 then bn0 (neural_networks.py:246-251)."""
-        out = []
-        if self.dnn_use_laynorm_inp:
-            out.append(dict(kind="ln", gamma=self.ln0.gamma, beta=self.ln0.beta))
-        if self.dnn_use_batchnorm_inp:
-            out.append(dict(kind="bn", gamma=self.bn0.weight, beta=self.bn0.bias,
-                            rm=self.bn0.running_mean, rv=self.bn0.running_var,
-                            nbt=self.bn0.num_batches_tracked))
-        return out
+        return _input_norm_specs(self, self.dnn_use_laynorm_inp, self.dnn_use_batchnorm_inp)
 
     def check_supported(self):
         if self.if_pattern and self.pattern_kernels is None:
@@ -333,8 +339,10 @@ class liGRU(nn.Module):
         raise NotImplementedError("the reference liGRU has no prune hook")
 
     def check_supported(self):
-        if self.ligru_use_laynorm_inp or self.ligru_use_batchnorm_inp:
-            raise NotImplementedError("input normalisation in liGRU is not on the pkc path yet")
+        pass
+
+    def input_norm_specs(self):
+        return _input_norm_specs(self, self.ligru_use_laynorm_inp, self.ligru_use_batchnorm_inp)
 
     def layer_specs(self):
         specs = []
@@ -413,8 +421,10 @@ class GRU(nn.Module):
         raise NotImplementedError("the reference GRU has no prune hook")
 
     def check_supported(self):
-        if self.gru_use_laynorm_inp or self.gru_use_batchnorm_inp:
-            raise NotImplementedError("input normalisation in GRU is not on the pkc path yet")
+        pass
+
+    def input_norm_specs(self):
+        return _input_norm_specs(self, self.gru_use_laynorm_inp, self.gru_use_batchnorm_inp)
 
     def layer_specs(self):
         specs = []
@@ -489,9 +499,10 @@ class _PlainRec(nn.Module):
         raise NotImplementedError("the reference %s has no prune hook" % type(self).__name__)
 
     def check_supported(self):
-        if self.ln_inp or self.bn_inp:
-            raise NotImplementedError("input normalisation in %s is not on the pkc path yet"
-                                      % type(self).__name__)
+        pass
+
+    def input_norm_specs(self):
+        return _input_norm_specs(self, self.ln_inp, self.bn_inp)
 
     def layer_specs(self):
         specs = []
@@ -668,9 +679,10 @@ class LSTM(_PatternSet, nn.Module):
             gm = getattr(self, nm)[i].mask
         return _mask_product(h, gm)
 
+    def input_norm_specs(self):
+        return _input_norm_specs(self, self.lstm_use_laynorm_inp, self.lstm_use_batchnorm_inp)
+
     def check_supported(self):
-        if self.lstm_use_laynorm_inp or self.lstm_use_batchnorm_inp:
-            raise NotImplementedError("input normalisation in LSTM is not on the pkc path yet")
         if self.if_pattern and self.pattern_kernels is None:
             raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option or "
                                       "patterns injected by run_nn)")

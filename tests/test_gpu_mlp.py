@@ -68,7 +68,7 @@ def test_engine_matches_reference_golden_steps(variant):
     eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 40)},
                  ["lab_cd", "lab_mono"], batch=16, seed=1)
     eng.bind_chunk(feats, labels, data.shape[0])
-    head = [l for l in eng.layers if l.arch == "MLP_layers2"][0]
+    head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
     body = [l for l in eng.layers if l.arch == "MLP_layers1"][-1]
     for s in range(3):
         eng.train_step()
@@ -165,7 +165,7 @@ def test_engine_c1_full_size_vs_oracle():
         body.forward = orig_fwd
         eng.train_step()
         loss, err = eng.loss_values()
-        head = [l for l in eng.layers if l.arch == "MLP_layers2"][0]
+        head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
         post = head.out.view(B, -1).cpu()
         ref = outs["out_dnn2"].detach()
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
@@ -232,19 +232,27 @@ def test_engine_graph_replay_equals_eager():
             torch.testing.assert_close(res[0][1][k], other[1][k], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("variant", ["prune", "pattern", "ghcgs"])
+@pytest.mark.parametrize("variant", ["prune", "pattern", "ghcgs", "inpnorm"])
 def test_engine_sparsity_vs_oracle(variant):
     """prune: every forward re-thresholds |W| at np.percentile(prune_perc[i]) and zeroes the rest
     (neural_networks.py:276-278); pattern: 8x8/k4/n16 pattern masks from the pattern_file set,
     computed at the first layer call and multiplied in once per layer call (263-272, 339-361).
-    Both on top of HCGS masks on the body; 3 training steps vs the oracle."""
+    Both on top of HCGS masks on the body; 3 training steps vs the oracle.  inpnorm: ln0 then bn0
+    on the body and on the head that reads it (neural_networks.py:246-251): the head's input
+    norms hand their input gradient down to the body."""
     from oracle import nets as ON
     from oracle import run as OR
     from oracle.masks import prune_mask
     from pkc.engine import Engine, parse_model
-    cfg = build_mlp_config("hcgs")
+    cfg = build_mlp_config("plain" if variant == "inpnorm" else "hcgs")
     pset = None
-    if variant == "prune":
+    if variant == "inpnorm":
+        # ln0's beta feeds bn0, which removes it: its gradient is 0 up to rounding, which RMSprop
+        # would scale up to full steps — SGD keeps the comparison about the norms
+        for sec in ("architecture1", "architecture2"):
+            cfg[sec].update(dnn_use_laynorm_inp="True", dnn_use_batchnorm_inp="True",
+                            arch_opt="sgd", opt_dampening="0.0", opt_nesterov="False")
+    elif variant == "prune":
         cfg["architecture1"]["mlp_prune"] = "True"
         cfg["architecture1"]["mlp_prune_perc"] = "70,55"
         cfg["architecture2"].update(mlp_prune="True", mlp_prune_perc="30")
@@ -284,7 +292,7 @@ def test_engine_sparsity_vs_oracle(variant):
         loss, err = eng.loss_values()
         np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-5)
         np.testing.assert_allclose(err, outs["err_final"].item())
-        head = [l for l in eng.layers if l.arch == "MLP_layers2"][0]
+        head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
         post = head.out.view(B, -1).cpu()
         ref = outs["out_dnn2"].detach()
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
