@@ -46,12 +46,17 @@ def build(verbose=False):
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(_compile, srcs))
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+    stamp = os.path.join(BUILD, "libpkc.objs")
+    listing = "\n".join(objs)
+    same = os.path.exists(stamp) and open(stamp).read() == listing
+    if same and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB
     cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n%s" % r.stderr[-6000:])
+    with open(stamp, "w") as f:            # a removed source also forces the next relink
+        f.write(listing)
     if verbose:
         print("built", LIB)
     return LIB
