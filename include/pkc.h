@@ -288,6 +288,15 @@ typedef struct {
    * forward; g (T, B2, H) the post-norm gradients, dgamma / dbeta (H) written by the backward. */
   const float* ln_gamma; const float* ln_beta; float ln_eps;
   float* ln_xhat; float* ln_stat; float* ln_g; float* ln_dgamma; float* ln_dbeta;
+  /* Block-sparse U (static HCGS masks, HCGS.py:24-28; liGRU / LSTM, no quantised h): per
+   * workgroup tile, the indices of the 16-wide contraction blocks holding a nonzero of the mask
+   * (-1 = empty slot), kmap_s* slots per tile (16, 32 or 64; 16 lane groups x kmap_s/16 blocks).
+   *   kmap_fwd [ceil(H / (16/G))][kmap_s_fwd]: blocks of k (h_{t-1} / U columns) that the forward
+   *     tile of 16/G units x G gates reads;
+   *   kmap_bwd [G][ceil(H/16)][kmap_s_bwd]: blocks of j (U rows) that the BPTT tile of 16 columns k
+   *     of gate g reads.
+   * NULL: dense contraction over all H. */
+  const int32_t* kmap_fwd; const int32_t* kmap_bwd; int kmap_s_fwd, kmap_s_bwd;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
 /* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that

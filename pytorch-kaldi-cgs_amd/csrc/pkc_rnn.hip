@@ -332,6 +332,31 @@ __device__ __forceinline__ void load_strip(const float* row, bool ok, int kb, in
   }
 }
 
+// Block-sparse form of load_strip: S/16 blocks of 16 contiguous k at blk[i] * 16 (blk < 0: zeros).
+template <int S>
+__device__ __forceinline__ void load_blocks(const float* row, bool ok, const int* blk, int kmax,
+                                            int vw, float* v) {
+#pragma unroll
+  for (int i = 0; i < S / 16; ++i)
+    load_strip<16>(row, ok && blk[i] >= 0, blk[i] >= 0 ? blk[i] * 16 : 0, kmax, vw, v + 16 * i);
+}
+
+// This lane group's S/16 block indices of a kmap tile row (S slots: lane group w*4+q owns slots
+// [(w*4+q)*S/16, +S/16)).  The wave index is made uniform so the table is read with scalar loads
+// (constant cache) — the same tiles are re-read every time step.
+template <int S>
+__device__ __forceinline__ void tile_blocks(const int32_t* row, int* blk) {
+  typedef const __attribute__((address_space(4))) int32_t cint;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = (threadIdx.x & 63) >> 4;
+  cint* sl = (cint*)(row + wu * 4 * (S / 16));
+#pragma unroll
+  for (int i = 0; i < S / 16; ++i) {
+    const int b0 = sl[i], b1 = sl[S / 16 + i], b2 = sl[2 * (S / 16) + i], b3 = sl[3 * (S / 16) + i];
+    blk[i] = q == 0 ? b0 : (q == 1 ? b1 : (q == 2 ? b2 : b3));
+  }
+}
+
 // Sum the four waves' 32x16 partial tiles (MFMA C layout: col = lane & 15, row = 4*(lane>>4)+i)
 // into tile[32][17]; red is [4][32][17] scratch.  Ends with a barrier.
 __device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1, float* red,
@@ -448,7 +473,7 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 
 // One forward step (PH = 0: the gates that read h_{t-1}; PH = 1: the candidate of a two-phase
 // cell, reading rh).  Tile: rows [32*blockIdx.y, +32) x NG gates of NU = 16/NG units.
-template <int NG, int CELL, int PH, int S, bool QH>
+template <int NG, int CELL, int PH, int S, bool QH, bool SP = false>
 __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
   __shared__ float red[4 * 32 * 17];
   __shared__ float tile[32 * 17];
@@ -462,11 +487,20 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
   const int ra = r0 + c, rb = r0 + 16 + c;
   const int gi = c / NU, u = u0 + c % NU;
   const float* pu = a.U[PH == 0 ? gi : cand_gate(CELL)] + (int64_t)(u < H ? u : 0) * H;
-  const int kb = (w * 4 + q) * S;
   float va[S], vb[S], vu[S];
-  load_strip<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
-  load_strip<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
-  load_strip<S>(pu, u < H, kb, H, vw, vu);
+  if constexpr (SP) {
+    static_assert(!QH && PH == 0, "block-sparse U: no quantised h, one-phase cells");
+    int blk[S / 16];
+    tile_blocks<S>(a.kmap_fwd + (int64_t)blockIdx.x * S, blk);
+    load_blocks<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
+    load_blocks<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
+    load_blocks<S>(pu, u < H, blk, H, vw, vu);
+  } else {
+    const int kb = (w * 4 + q) * S;
+    load_strip<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
+    load_strip<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
+    load_strip<S>(pu, u < H, kb, H, vw, vu);
+  }
   float vars[4] = {0.f, 0.f, 0.f, 0.f};
   const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -579,7 +613,7 @@ __device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, 
 // MODE 0: the product of gate g0 + blockIdx.z into slab blockIdx.z (a.work + (4 + z) n);
 // MODE 1: one-gate product + bwd_step_epi (t = tt + 1); MODE 2: one-gate product + rh_epi.
 // out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
-template <int G, int CELL, int MODE, int S>
+template <int G, int CELL, int MODE, int S, bool SP = false>
 __global__ __launch_bounds__(RT) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
   __shared__ float red[4 * 32 * 17];
   __shared__ float tile[32 * 17];
@@ -593,11 +627,20 @@ __global__ __launch_bounds__(RT) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, 
   const float* dg = a.dgates + g * TB2H + (int64_t)t * B2 * H;
   const int ra = r0 + c, rb = r0 + 16 + c, k = k0 + c;
   const float* pu = a.ut + (int64_t)g * H * H + (int64_t)(k < H ? k : 0) * H;
-  const int kb = (w * 4 + q) * S;
   float va[S], vb[S], vu[S];
-  load_strip<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
-  load_strip<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
-  load_strip<S>(pu, k < H, kb, H, vw, vu);
+  if constexpr (SP) {
+    static_assert(MODE == 0, "block-sparse U: gate-split BPTT products only");
+    int blk[S / 16];
+    tile_blocks<S>(a.kmap_bwd + ((int64_t)g * gridDim.x + blockIdx.x) * S, blk);
+    load_blocks<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
+    load_blocks<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
+    load_blocks<S>(pu, k < H, blk, H, vw, vu);
+  } else {
+    const int kb = (w * 4 + q) * S;
+    load_strip<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
+    load_strip<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
+    load_strip<S>(pu, k < H, kb, H, vw, vu);
+  }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   mfma_chain<S>(va, vb, vu, acc0, acc1);
   reduce_tile(acc0, acc1, red, tile);
@@ -670,7 +713,7 @@ struct SCase {};
 
 static int pick_vw(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
 
-template <int G, int CELL, int S>
+template <int G, int CELL, int S, bool SP = false>
 static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
   const int vw = pick_vw(a->H);
@@ -686,7 +729,9 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   } else {
     dim3 g1((a->H + 16 / G - 1) / (16 / G), rows);
     for (int t = 0; t < a->T; ++t) {
-      if (a->qbits > 0)
+      if constexpr (SP)
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), g1, dim3(RT), 0, s, *a, t, vw);
+      else if (a->qbits > 0)
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
       else
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
@@ -697,7 +742,7 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   return PKC_OK;
 }
 
-template <int G, int CELL, int S>
+template <int G, int CELL, int S, bool SP = false>
 static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
   const int vw = pick_vw(a->H);
@@ -735,7 +780,7 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
       } else {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
         hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       }
@@ -766,11 +811,25 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
     hipLaunchKernelGGL(rnn_drop_mask_kernel, dim3(64), dim3(256), 0, s, *a, B2);
     PKC_LAUNCH_CHECK("pkc_rnn_fwd drop mask");
   }
+  if constexpr (!two_phase(CELL) && G > 1) {
+    if (a->kmap_fwd) {
+      if (a->kmap_s_fwd == 16) return fwd_impl_s<G, CELL, 16, true>(a, s);
+      if (a->kmap_s_fwd == 32) return fwd_impl_s<G, CELL, 32, true>(a, s);
+      return fwd_impl_s<G, CELL, 64, true>(a, s);
+    }
+  }
   return PKC_S_DISPATCH(fwd_impl_s, a, s);
 }
 
 template <int G, int CELL>
 static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
+  if constexpr (!two_phase(CELL) && G > 1) {
+    if (a->kmap_bwd) {
+      if (a->kmap_s_bwd == 16) return bwd_impl_s<G, CELL, 16, true>(a, dpre, s);
+      if (a->kmap_s_bwd == 32) return bwd_impl_s<G, CELL, 32, true>(a, dpre, s);
+      return bwd_impl_s<G, CELL, 64, true>(a, dpre, s);
+    }
+  }
   return PKC_S_DISPATCH(bwd_impl_s, a, dpre, s);
 }
 
@@ -791,6 +850,13 @@ static int check(const pkc_rnn_args* a, bool bwd) {
                 "pkc_rnn: LayerNorm needs beta, xhat, stat (+ g, dgamma, dbeta for the backward)");
   PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir && a->B <= 32), "pkc_rnn: quantised h needs "
                 "hq, a uni-directional layer and B <= 32");
+  if (a->kmap_fwd || a->kmap_bwd) {
+    PKC_CHECK_ARG((a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM) && a->qbits <= 0,
+                  "pkc_rnn: block-sparse U only for liGRU / LSTM without quantised h");
+    const int sf = a->kmap_s_fwd, sb = a->kmap_s_bwd;
+    PKC_CHECK_ARG(!a->kmap_fwd || sf == 16 || sf == 32 || sf == 64, "pkc_rnn: kmap_s_fwd %d", sf);
+    PKC_CHECK_ARG(!a->kmap_bwd || sb == 16 || sb == 32 || sb == 64, "pkc_rnn: kmap_s_bwd %d", sb);
+  }
   return PKC_OK;
 }
 

@@ -65,7 +65,8 @@ class RnnArgs(C.Structure):
                 ("y", vp), ("dy", vp), ("dy_nslab", C.c_int), ("dy_slab_stride", i64),
                 ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp), ("rh", vp), ("ut", vp),
                 ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", C.c_float), ("ln_xhat", vp),
-                ("ln_stat", vp), ("ln_g", vp), ("ln_dgamma", vp), ("ln_dbeta", vp)]
+                ("ln_stat", vp), ("ln_g", vp), ("ln_dgamma", vp), ("ln_dbeta", vp),
+                ("kmap_fwd", vp), ("kmap_bwd", vp), ("kmap_s_fwd", C.c_int), ("kmap_s_bwd", C.c_int)]
 
 
 class GemmProblem(C.Structure):

@@ -19,6 +19,7 @@ Design (MI355X-first):
     every architecture in one pkc_optim_step that also re-applies HCGS masks.
 """
 import ctypes as C
+import os
 import random
 import re
 import zlib
@@ -138,6 +139,11 @@ class Layer:
 
     def quant_of(self, p):
         return (self.Wq, self.qbits) if (p is self.W and self.qbits) else (None, 0)
+
+
+# Block-sparse U in the recurrent step kernels for static HCGS masks: "auto" (when it cuts the
+# contraction), "force" (whenever the tiles fit, used by the parity tests) or "off".
+RNN_SPARSE = os.environ.get("PKC_RNN_SPARSE", "auto")
 
 
 class NormLayer(Layer):
@@ -340,6 +346,7 @@ class Engine:
         self._build_graph()
         self._alloc()
         self._build_masks()
+        self._build_kmaps()
         self._build_optim()
         self._build_reg()
         self.graph = None
@@ -649,6 +656,54 @@ class Engine:
                             n.emask[id(p)] = eff[id(p)]
             elif n.W is not None and id(n.W) in eff:
                 n.mask = eff[id(n.W)]
+
+    def _build_kmaps(self):
+        """Block-sparse U for static HCGS masks (liGRU / LSTM; no prune, pattern or quantised h,
+        whose zeros move): per step-kernel tile, the 16-wide contraction blocks that hold a
+        nonzero of the mask (pkc_rnn_args.kmap_*).  The optimizer keeps masked entries at zero, so
+        skipping the other blocks changes only the order of the fp32 sums."""
+        for n in self.nodes:
+            if not n.rec or n.cell not in (L.CELL_LIGRU, L.CELL_LSTM):
+                continue
+            for sp, lb in zip(n.layers, n.lbuf):
+                lb["kmap_fwd"] = lb["kmap_bwd"] = None
+                if RNN_SPARSE == "off" or sp.get("prune") is not None or sp["ibits"]:
+                    continue
+                um = [sp["Umasks"][g] if sp.get("Umasks") else sp["Umask"] for g in range(n.G)]
+                if any(m is None or id(U) in n.emask for m, U in zip(um, sp["U"])):
+                    continue
+                H = lb["H"]
+                nb = -(-H // 16)
+                rowp, pres = [], []
+                for m in um:
+                    mb = torch.zeros(nb * 16, nb * 16, device=self.dev)
+                    mb[:H, :H] = (m.detach().reshape(H, H) != 0).float()
+                    rowp.append(mb.view(nb * 16, nb, 16).amax(2) > 0)          # [row][col blk]
+                    pres.append(mb.view(nb, 16, nb, 16).amax(dim=(1, 3)) > 0)  # [row blk][col blk]
+                NU = 16 // n.G
+                nt = -(-H // NU)
+                acc = torch.zeros(nt * NU, nb, dtype=torch.bool, device=self.dev)
+                for rp in rowp:
+                    acc[:H] |= rp[:H]
+                fwd = acc.view(nt, NU, nb).any(1)                   # [tile][k blk]
+                # BPTT tile (gate g, columns k-block kt) reads the row blocks j with a nonzero
+                bwd = torch.stack([p_.t() for p_ in pres])          # [g][kt][j blk]
+                dense_s = 16 if H <= 256 else 32 if H <= 512 else 48 if H <= 768 else 64 if H <= 1024 else 128
+
+                def table(presence, rows):
+                    kept = int(presence.sum(-1).max().item())
+                    S = next((c for c in (16, 32, 64) if c >= kept), None)
+                    if S is None or (RNN_SPARSE != "force" and S >= dense_s):
+                        return None, 0
+                    tab = torch.full((rows, S), -1, dtype=torch.int32)
+                    pc = presence.reshape(rows, -1).cpu()
+                    for i in range(rows):
+                        idx = torch.nonzero(pc[i]).flatten()
+                        tab[i, :len(idx)] = idx.to(torch.int32)
+                    return tab.to(self.dev), S
+
+                lb["kmap_fwd"], lb["kmap_s_fwd"] = table(fwd, nt)
+                lb["kmap_bwd"], lb["kmap_s_bwd"] = table(bwd, n.G * nb)
 
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
@@ -1019,6 +1074,10 @@ class Engine:
         a.dgates = lb["dgates"].data_ptr()
         a.work = lb["rwork"].data_ptr()
         a.ut = lb["ut"].data_ptr()
+        if lb.get("kmap_fwd") is not None:
+            a.kmap_fwd, a.kmap_s_fwd = lb["kmap_fwd"].data_ptr(), lb["kmap_s_fwd"]
+        if lb.get("kmap_bwd") is not None:
+            a.kmap_bwd, a.kmap_s_bwd = lb["kmap_bwd"].data_ptr(), lb["kmap_s_bwd"]
         if sp.get("ln"):
             a.ln_gamma, a.ln_beta, a.ln_eps = sp["ln_gamma"].data_ptr(), sp["ln_beta"].data_ptr(), 1e-6
             a.ln_xhat, a.ln_stat = lb["ln_xhat"].data_ptr(), lb["ln_stat"].data_ptr()

@@ -75,6 +75,26 @@ def bench_gemm(rows):
                                                            k, sp), us))
 
 
+def bench_biggemm(rows):
+    """The sequence configs' non-recurrent matmuls (C4: T*B = 5440 rows, 4 gates x 1024, bidir
+    input 2048), fp32 exact MFMA: achieved TFLOP/s."""
+    R, N, K = 5440, 1024, 2048
+    for name, akc, bkc, m, n, k in (("fwd", 1, 1, R, N, K), ("dX", 1, 0, R, K, N),
+                                    ("dW", 0, 0, N, K, R), ("dU", 0, 0, N, N, R)):
+        A = f32(m * k)
+        B = f32(n * k)
+        Cb = f32(m * n)
+        lda = k if akc else m
+        ldb = k if bkc else n
+        for prec in (L.PREC_FP32, L.PREC_BF16):
+            def fn():
+                call("pkc_gemm", prec, akc, bkc, m, n, k, ptr(A), lda, ptr(B), ldb, ptr(Cb), n, 1,
+                     m * n, stream())
+            us = timed(fn, reps=5)
+            rows.append(("big_%s_%s %dx%dx%d (%.0f TF/s)" % (name, ["fp32", "bf16"][prec], m, n, k,
+                                                             2.0 * m * n * k / us / 1e6), us))
+
+
 def bench_dense(rows):
     M = 128
     for N, ns in ((1024, 1), (1024, 4), (1024, 8)):
@@ -159,7 +179,7 @@ def main():
     flt = sys.argv[1] if len(sys.argv) > 1 else ""
     rows = []
     bench_floor(rows)
-    for name, fn in (("gemm", bench_gemm), ("dense", bench_dense),
+    for name, fn in (("gemm", bench_gemm), ("biggemm", bench_biggemm), ("dense", bench_dense),
                      ("heads", bench_heads), ("optim", bench_optim)):
         if flt and flt not in name:
             continue

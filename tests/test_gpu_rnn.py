@@ -121,3 +121,44 @@ def test_recurrent_layer_matches_reference(case):
             # BN statistics, and W / U after the forward's in-place masking + clamping
             np.testing.assert_allclose(v.cpu().numpy(), g[tag + "/post/" + k], rtol=1e-4, atol=1e-6,
                                        err_msg=k)
+
+
+SPARSE_CASES = [("ligru_hcgs96", "liGRU", dict(LIGRU_DEF, ligru_lay="96,80", ligru_hcgs="True",
+                                               hcgsx_block="32,4", hcgsx_sparse="50,50",
+                                               hcgsh_block="32,4", hcgsh_sparse="50,50"), 9, 3, 24),
+                ("lstm_hcgs96", "LSTM", dict(LSTM_DEF, lstm_lay="96,64", lstm_hcgs="True",
+                                             hcgsx_block="32,4", hcgsx_sparse="50,50",
+                                             hcgsh_block="32,4", hcgsh_sparse="50,75"), 8, 2, 24)]
+
+
+@pytest.mark.parametrize("case", SPARSE_CASES, ids=[c[0] for c in SPARSE_CASES])
+def test_block_sparse_u_matches_dense(case):
+    """HCGS-masked U: the step kernels that read only the 16-wide blocks holding a nonzero of the
+    mask (kmap tables) give the dense kernels' outputs and gradients up to fp32 summation order."""
+    import pkc.engine as E
+    import pkc.neural_networks as NN
+    tag, cls, opts, T, B, F = case
+    res = []
+    for mode in ("off", "force"):
+        torch.manual_seed(7)
+        np.random.seed(7)
+        net = getattr(NN, cls)(section(opts), F).to(DEV).train()
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(T, B, F, generator=g).to(DEV)
+        r = torch.randn(T, B, net.out_dim, generator=g).to(DEV)
+        old = E.RNN_SPARSE
+        E.RNN_SPARSE = mode
+        try:
+            eng, node, y = run_block(net, x, r)
+        finally:
+            E.RNN_SPARSE = old
+        if mode == "force":
+            maps = [lb["kmap_fwd"] for lb in node.lbuf]
+            assert all(m is not None for m in maps)
+            assert any(bool((m < 0).any()) for m in maps), "no block skipped: the case tests nothing"
+        res.append([y, dx0(eng, node)] + [u for lb in node.lbuf for u in lb["dU"]] +
+                   [w for lb in node.lbuf for w in lb["dW"]])
+    for i, (a, b) in enumerate(zip(*res)):
+        # fp32 sums in another order: differences relative to the tensor's scale
+        err = (b - a).abs().max().item()
+        assert err <= 2e-5 * a.abs().max().item() + 1e-7, "tensor %d: %.3g" % (i, err)

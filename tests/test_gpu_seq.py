@@ -23,7 +23,7 @@ def make_cfg(body):
     elif body == "lstm_bidir":     # config C4: bidirectional LSTM, liGRU convention
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="True", **opt)
-    elif body == "ligru_hcgs":     # config C3: liGRU with the LSTM's HCGS hook (8x4 / 50,50)
+    elif body in ("ligru_hcgs", "ligru_hcgs_sparse"):   # C3: liGRU + the LSTM's HCGS hook
         cfg["a1"] = dict(LIGRU_DEF, arch_name="rnn", ligru_lay="32,24", ligru_drop="0.2,0.2",
                          ligru_hcgs="True", hcgsx_block="8,4", hcgsx_sparse="50,50",
                          hcgsh_block="8,4", hcgsh_sparse="25,50", **opt)
@@ -102,7 +102,8 @@ def make_cfg(body):
 @pytest.mark.parametrize("body", ["ligru", "lstm", "ligru_hcgs", "lstm_bidir", "lstm_prune",
                                   "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply", "gru", "mingru",
                                   "rnn", "lstm_ln", "gru_ln", "gru_nobn", "lstm_ln_bn",
-                                  "ligru_inpnorm", "lstm_bninp", "gru_lninp", "mingru_inpnorm"])
+                                  "ligru_inpnorm", "lstm_bninp", "gru_lninp", "mingru_inpnorm",
+                                  "ligru_hcgs_sparse"])
 def test_seq_engine_vs_oracle(body):
     import pkc.neural_networks as NN
     from oracle import nets as ON
@@ -123,7 +124,8 @@ def test_seq_engine_vs_oracle(body):
                 "lstm_ghcgs_apply": "LSTM", "gru": "GRU", "mingru": "minimalGRU",
                 "rnn": "RNN", "lstm_ln": "LSTM", "gru_ln": "GRU", "gru_nobn": "GRU",
                 "lstm_ln_bn": "LSTM", "ligru_inpnorm": "liGRU", "lstm_bninp": "LSTM",
-                "gru_lninp": "GRU", "mingru_inpnorm": "minimalGRU"}[body]
+                "gru_lninp": "GRU", "mingru_inpnorm": "minimalGRU",
+                "ligru_hcgs_sparse": "liGRU"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
@@ -141,8 +143,17 @@ def test_seq_engine_vs_oracle(body):
     bid = 2 if H[0]["bidir"] else 1
     masks = {(("rnn", li)): torch.from_numpy((rs.rand(bid * B, sp["H"]) > 0.2).astype(np.float32))
              for li, sp in enumerate(H)}
-    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fea": (0, F)}, ["lab_cd", "lab_mono"],
-                 batch=B, max_len=16, seed=1, rnn_drop_in={k: v.to(DEV) for k, v in masks.items()})
+    import pkc.engine as E
+    old_sparse = E.RNN_SPARSE
+    E.RNN_SPARSE = "force" if body.endswith("_sparse") else old_sparse
+    try:
+        eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fea": (0, F)},
+                     ["lab_cd", "lab_mono"], batch=B, max_len=16, seed=1,
+                     rnn_drop_in={k: v.to(DEV) for k, v in masks.items()})
+    finally:
+        E.RNN_SPARSE = old_sparse
+    if body.endswith("_sparse"):
+        assert all(lb["kmap_fwd"] is not None for lb in eng.nodes[0].lbuf)
     eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), end[-1], end_index=end)
     oopt = {k: ON.make_optimizer(onets[k].parameters(), opts[k]) for k in onets}
     lines = OR.parse_model(cfg["model"]["model"])
@@ -183,7 +194,7 @@ def test_seq_engine_vs_oracle(body):
             # the reference re-masks W / U at the next forward; pkc stores W*mask right away
             sd_o = onets[k].state_dict()
             parts = name.split(".")
-            if body == "ligru_hcgs" and name.endswith("weight") and parts[0] in ("wh", "wz", "uh", "uz"):
+            if body.startswith("ligru_hcgs") and name.endswith("weight") and parts[0] in ("wh", "wz", "uh", "uz"):
                 mk = ("hcgsx" if parts[0][0] == "w" else "hcgsh") + ".%s.mask" % parts[1]
                 ref = ref * sd_o[mk].double()
             if body == "lstm_ghcgs_apply" and k == "rnn" and name.endswith("weight") and \
