@@ -250,6 +250,22 @@ int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double*
                  const double* std, const int64_t* perm, float* out, int64_t ld_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Kaldi feature front-end (replaces the `apply-cmvn ... | add-deltas ...` stages of the fea_opts
+ * pipe that data_io.py:18 runs through read_mat_ark, data_io.py:645-664; Kaldi's ApplyCmvn and
+ * DeltaFeatures restated).  raw: Nsrc x D frames of whole utterances; output row r (of Nout, in
+ * the sorted / split load_dataset order) is source frame src_row[r] of utterance u = utt_of_row[r],
+ * whose frames are [utt_beg[u], utt_end[u]) of raw.  cmvn_mode 0 none, 1 means (x + offset),
+ * 2 means+vars (x * scale + offset); norm[utt_norm[u]] = {offset[D], scale[D]} (fp32, computed by
+ * the host as ApplyCmvn does in double).  scales: (order+1) x (2*maxoff+1) delta windows (zero
+ * outside each order's own window); frames clamp to the utterance.  out: Nout x D*(order+1).
+ * order <= 7.
+ * ------------------------------------------------------------------------------------------- */
+int pkc_feat_frontend(const float* raw, int D, int64_t Nout, const int32_t* src_row,
+                      const int32_t* utt_of_row, const int32_t* utt_beg, const int32_t* utt_end,
+                      const int32_t* utt_norm, const float* norm, int cmvn_mode,
+                      const float* scales, int order, int maxoff, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Recurrent layers: the per-time-step loops of liGRU (neural_networks.py:1573-1584), LSTM
  * (neural_networks.py:1077-1097), GRU (:1390-1396, gates z, r, h), minimalGRU (:1751-1755, gates
  * z, h) and RNN (:1905-1907, gate h).  wpre holds the gate pre-activations W x (+BN) for the T*B input

@@ -127,6 +127,8 @@ _SIGS = {
     "pkc_cw_stats": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]),
     "pkc_cw_stats_work_size": (i64, [i64, C.c_int, C.c_int, C.c_int]),
     "pkc_cw_apply": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, i64, vp]),
+    "pkc_feat_frontend": (C.c_int, [vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, C.c_int, vp, C.c_int,
+                                    C.c_int, vp, vp]),
     "pkc_ark_write_mat": (C.c_int, [C.c_char_p, C.c_int, C.c_char_p, i64, i64, vp]),
     "pkc_ark_index": (i64, [C.c_char_p, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), i64,
                             C.c_char_p, i64]),

@@ -26,6 +26,7 @@ import torch
 
 from . import data_io as D
 from . import dist as DP
+from . import frontend as FE
 from . import neural_networks as NN
 from .engine import Engine, ForwardRunner, parse_model
 from .neural_networks import strtobool
@@ -63,13 +64,17 @@ def dict_fea_lab_arch(config):
 
 def _read_features(fea_scp, fea_opts, output_folder):
     """Feature stream of one chunk: ``copy-feats scp:<scp> ark:- |<opts>`` as data_io.py:18.
-    Without Kaldi on the box, an scp of binary arks ("key path:offset" or "key path") is read
-    directly; with fea_opts set the Kaldi pipeline is run exactly as the reference does."""
-    if fea_opts.strip():
+
+    The scp's binary arks ("key path:offset" or "key path") are read directly.  An
+    ``apply-cmvn ... | add-deltas ...`` fea_opts pipe (every shipped cfg) is parsed into a
+    pkc.frontend.FeaFrontend that pkc_feat_frontend applies on the GPU after the upload; any other
+    pipe is run through Kaldi exactly as the reference does.  Returns (feats, frontend or None)."""
+    if fea_opts.strip() and not FE.is_native_pipe(fea_opts):
         import subprocess
         cmd = "copy-feats scp:" + fea_scp + " ark:- |" + fea_opts
         out = subprocess.run(cmd, shell=True, capture_output=True, check=True).stdout
-        return dict(D.parse_mat_ark_bytes(out))
+        return dict(D.parse_mat_ark_bytes(out)), None
+    frontend = FE.FeaFrontend.parse(fea_opts) if fea_opts.strip() else None
     feats = {}
     by_file = {}
     with open(fea_scp) as f:
@@ -83,7 +88,7 @@ def _read_features(fea_scp, fea_opts, output_folder):
         for k, m in D.read_mat_ark_path(path):
             if k in keys:
                 feats[k] = m
-    return feats
+    return feats, frontend
 
 
 def _read_labels(lab_folder, lab_opts, output_folder):
@@ -111,7 +116,7 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
     if len(fea_dict) != 1:
         raise NotImplementedError("pkc chunk preparation handles one feature stream per model")
     (fname, fd), = fea_dict.items()
-    fea = _read_features(fd[1], fd[2], output_folder)
+    fea, frontend = _read_features(fd[1], fd[2], output_folder)
     labs, lab_names = [], []
     if not fea_only:
         for lname, ld in lab_dict.items():
@@ -122,7 +127,7 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
     # sort / split the utterances and start the pinned-memory upload on a side stream here, in
     # the loader thread, so it overlaps the current chunk's training; the frame shuffle (global
     # np.random) stays on the main thread in _finish_chunk, in a deterministic order
-    staged = D.stage_chunk(fea, labs, max_seq)
+    staged = D.stage_chunk(fea, labs, max_seq, frontend=frontend)
     shared_list.append(("raw", staged, labs, lab_names, int(fd[3]), int(fd[4]), max_seq, rng, fname))
     shared_list.append(None)
     shared_list.append(fea_dict)

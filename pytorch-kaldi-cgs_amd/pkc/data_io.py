@@ -131,46 +131,54 @@ def load_counts(path):
 
 
 # --------------------------------------------------------------------------------- chunk assembly
-def load_dataset(fea, labs, max_sequence_length):
-    """Utterance bookkeeping of data_io.py:16-88 on in-memory dicts.
+def dataset_pieces(lengths, labs, max_sequence_length):
+    """Utterance bookkeeping of data_io.py:16-88 on lengths only.
 
-    fea: {key: (T, D) float32}; labs: list of {key: (T,) int} (one per label stream) or [].
-    Returns names, raw (N, D) float32, [label arrays (N,)], end_index."""
+    lengths: {key: T}; labs: list of {key: (T,) int} (one per label stream) or [].
+    Returns names (first-sort order, as the reference returns snt_name), pieces [(key, start,
+    stop)] in the final (length-sorted) order, [label arrays (N,)], end_index."""
     if labs:
-        keep = set(fea)
+        keep = set(lengths)
         for l in labs:
             keep &= set(l)
-        fea = {k: v for k, v in fea.items() if k in keep}
-    names, fc, lc = [], [], [[] for _ in labs]
-    for k in sorted(sorted(fea), key=lambda k: len(fea[k])):
-        f = fea[k]
-        T = len(f)
+        lengths = {k: v for k, v in lengths.items() if k in keep}
+    names, pieces = [], []
+    for k in sorted(sorted(lengths), key=lambda k: lengths[k]):       # data_io.py:34
+        T = lengths[k]
         m = max_sequence_length
-        if m > 0 and T > m:
+        if m > 0 and T > m:                                            # data_io.py:41-60
             start, j = 0, 0
             while True:
                 if T - start > m + m / 4:
                     stop = start + m
                 else:
                     stop = T
-                fc.append(f[start:stop])
-                for li, l in enumerate(labs):
-                    lc[li].append(l[k][start:stop])
+                pieces.append((k, start, stop))
                 names.append("%s_split%d" % (k, j))
                 if stop == T:
                     break
                 start, j = stop, j + 1
         else:
-            fc.append(f)
-            for li, l in enumerate(labs):
-                lc[li].append(l[k])
+            pieces.append((k, 0, T))
             names.append(k)
-    order = sorted(range(len(fc)), key=lambda i: fc[i].shape[0])
-    fc = [fc[i] for i in order]
-    names = [names[i] for i in order]
-    lab_arrays = [np.concatenate([l[i] for i in order]) for l in lc]
-    end_index = np.cumsum([x.shape[0] for x in fc])
-    return names, np.concatenate(fc).astype(np.float32), lab_arrays, end_index
+    # :77-79 re-sorts the pieces by length (stable) but NOT snt_name, which keeps the order of
+    # the first sort (visible once pieces were split; forward mode never splits, data_io.py:176)
+    order = sorted(range(len(pieces)), key=lambda i: pieces[i][2] - pieces[i][1])
+    pieces = [pieces[i] for i in order]
+    lab_arrays = [np.concatenate([l[k][a:b] for k, a, b in pieces]) for l in labs]
+    end_index = np.cumsum([b - a for _, a, b in pieces])
+    return names, pieces, lab_arrays, end_index
+
+
+def load_dataset(fea, labs, max_sequence_length):
+    """data_io.py:16-88 on in-memory dicts.
+
+    fea: {key: (T, D) float32}; labs: list of {key: (T,) int} (one per label stream) or [].
+    Returns names, raw (N, D) float32, [label arrays (N,)], end_index."""
+    names, pieces, lab_arrays, end_index = dataset_pieces({k: len(v) for k, v in fea.items()},
+                                                          labs, max_sequence_length)
+    raw = np.concatenate([fea[k][a:b] for k, a, b in pieces]).astype(np.float32)
+    return names, raw, lab_arrays, end_index
 
 
 class Chunk:
@@ -190,36 +198,96 @@ class StagedChunk:
     """A chunk after the host half of loading: utterances sorted / split (load_dataset) and the
     raw frames on their way to HBM — copied from pinned host memory by an asynchronous copy on a
     dedicated stream (hipMemcpyAsync underneath), so the upload of chunk k+1 overlaps the
-    training of chunk k (run_nn stages the next chunk from its loader thread)."""
+    training of chunk k (run_nn stages the next chunk from its loader thread).
 
-    def __init__(self, names, raw, lab_arrays, end_index, device):
+    With a Kaldi front-end (pkc.frontend.FeaFrontend: apply-cmvn / add-deltas), whole utterances
+    are uploaded in their own order and pkc_feat_frontend writes the processed frames in the
+    sorted / split order on the same stream."""
+
+    def __init__(self, names, raw, lab_arrays, end_index, device, fe_args=None):
         self.names, self.lab_arrays, self.end_index = names, lab_arrays, end_index
-        self.shape = raw.shape
         dev = torch.device(device)
         self.stream = torch.cuda.Stream(device=dev)
-        pinned = torch.empty(raw.shape, dtype=torch.float32, pin_memory=True)
-        pinned.numpy()[...] = raw
+        host = [raw] + ([] if fe_args is None else list(fe_args["arrays"]))
+        pinned = []
+        for a in host:
+            t = torch.empty(a.shape, dtype=torch.float32 if a.dtype == np.float32 else torch.int32,
+                            pin_memory=True)
+            t.numpy()[...] = a
+            pinned.append(t)
         with torch.cuda.stream(self.stream):
-            self.raw_d = pinned.to(dev, non_blocking=True)
+            dev_t = [t.to(dev, non_blocking=True) for t in pinned]
+            if fe_args is None:
+                self.raw_d = dev_t[0]
+            else:
+                raw_src, srow, urow, ubeg, uend, unorm, norm, scales = dev_t
+                Nout, Dout = fe_args["out_shape"]
+                self.raw_d = torch.empty(Nout, Dout, dtype=torch.float32, device=dev)
+                call("pkc_feat_frontend", ptr(raw_src), int(raw.shape[1]), Nout, ptr(srow),
+                     ptr(urow), ptr(ubeg), ptr(uend), ptr(unorm), ptr(norm), fe_args["cmvn_mode"],
+                     ptr(scales), fe_args["order"], fe_args["maxoff"], ptr(self.raw_d),
+                     C.c_void_p(self.stream.cuda_stream))
+                self._dev_inputs = dev_t
             self.done = torch.cuda.Event()
             self.done.record(self.stream)
+        self.shape = tuple(self.raw_d.shape)
         self._pinned = pinned           # alive until the copy has completed (finish_chunk)
 
 
-def stage_chunk(fea, labs, max_sequence_length, device="cuda"):
-    names, raw, lab_arrays, end_index = load_dataset(fea, labs, max_sequence_length)
-    return StagedChunk(names, np.ascontiguousarray(raw, dtype=np.float32), lab_arrays, end_index,
-                       device)
+def frontend_args(fea, pieces, frontend):
+    """Host tables of pkc_feat_frontend for these pieces: the utterances' raw frames in one array
+    (each utterance whole, in order of first use), per-output-row source frame and utterance,
+    per-utterance frame range and cmvn table index, the cmvn tables and the delta windows."""
+    from .frontend import delta_scales
+    keys = list(dict.fromkeys(k for k, _, _ in pieces))
+    if not keys:
+        raise ValueError("empty chunk: no utterance survived the feature / label / cmvn filters")
+    D = fea[keys[0]].shape[1]
+    uid = {k: i for i, k in enumerate(keys)}
+    lens = np.array([len(fea[k]) for k in keys], dtype=np.int64)
+    ubeg = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    if int(lens.sum()) >= 2 ** 31:
+        raise ValueError("chunk too large for the int32 front-end row maps")
+    raw = np.ascontiguousarray(np.concatenate([fea[k] for k in keys]), dtype=np.float32)
+    srow = np.concatenate([np.arange(a, b) + ubeg[uid[k]] for k, a, b in pieces]).astype(np.int32)
+    urow = np.concatenate([np.full(b - a, uid[k]) for k, a, b in pieces]).astype(np.int32)
+    kept, norm, nidx, mode = frontend.norm_tables(keys, D)
+    if kept != keys:
+        raise ValueError("utterances without cmvn statistics reached the front-end")
+    if mode == 0:
+        norm = np.zeros((1, 2, D), np.float32)
+        nidx = np.zeros(len(keys), np.int32)
+    scales, maxoff = delta_scales(frontend.order, frontend.window)
+    arrays = [srow, urow, ubeg.astype(np.int32), (ubeg + lens).astype(np.int32),
+              nidx.astype(np.int32), norm.astype(np.float32), scales.astype(np.float32)]
+    return dict(raw=raw, arrays=arrays, cmvn_mode=mode, order=frontend.order, maxoff=maxoff,
+                out_shape=(len(srow), frontend.out_dim(D)))
+
+
+def stage_chunk(fea, labs, max_sequence_length, device="cuda", frontend=None):
+    if frontend is None:
+        names, raw, lab_arrays, end_index = load_dataset(fea, labs, max_sequence_length)
+        return StagedChunk(names, np.ascontiguousarray(raw, dtype=np.float32), lab_arrays,
+                           end_index, device)
+    # apply-cmvn writes nothing for utterances it has no statistics for: drop them before the
+    # label filter / sort / split of load_dataset
+    D = next(iter(fea.values())).shape[1] if fea else 0
+    kept = set(frontend.norm_tables(sorted(fea), D)[0])
+    fea = {k: v for k, v in fea.items() if k in kept}
+    names, pieces, lab_arrays, end_index = dataset_pieces({k: len(v) for k, v in fea.items()}, labs,
+                                                          max_sequence_length)
+    fa = frontend_args(fea, pieces, frontend)
+    return StagedChunk(names, fa["raw"], lab_arrays, end_index, device, fe_args=fa)
 
 
 def prepare_chunk(fea, labs, lab_names, left, right, max_sequence_length, shuffle_rng=None,
-                  device="cuda", fea_name="fea", staged=None):
+                  device="cuda", fea_name="fea", staged=None, frontend=None):
     """data_io.load_chunk + read_lab_fea for one feature stream (data_io.py:121-145, 155-282):
     context window, chunk z-normalisation, label shift by the chunk minimum, optional frame
     shuffle (rng: the RandomState the reference's global np.random would be, seeded by run_nn).
     staged: the StagedChunk of these utterances when the loader thread already uploaded them."""
     if staged is None:
-        staged = stage_chunk(fea, labs, max_sequence_length, device)
+        staged = stage_chunk(fea, labs, max_sequence_length, device, frontend=frontend)
     names, lab_arrays, end_index = staged.names, staged.lab_arrays, staged.end_index
     N, D = staged.shape
     Nout = N - left - right
