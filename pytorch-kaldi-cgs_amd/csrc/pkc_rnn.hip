@@ -85,10 +85,48 @@ __device__ __forceinline__ float drop_val(const pkc_rnn_args& a, int r, int j, i
 // Dynamic input quantisation of h_{t-1} (quantized_modules.py:99-119), applied in place by each of
 // the four recurrent QuantizeLinear calls of a step (neural_networks.py:1086-1091): gate g reads
 // q_{g+1} = Q(q_g) with its own per-tensor max-abs var_{g+1}.
-__device__ __forceinline__ float qin(float x, float var, float scale) {
-  if (var == 0.f) return x;
+//   q = sign(x) * ceil(|x / var| * 2^(b-1)) / 2^(b-1) * var      (var = max|x|; identity if var == 0)
+// Every element of a call divides by the same var, so the quotient is formed from the correctly
+// rounded reciprocal y = RN(1/var) and one fma correction (Markstein: q0 = RN(x*y),
+// e = x - q0*var exact, RN(q0 + e*y) == RN(x/var) whenever the remainder does not underflow,
+// i.e. |x| >= 2^-100), and / 2^(b-1) is the exact * 2^-(b-1).  For 2^-80 <= var <= 1 (an LSTM's
+// h = o * tanh(c) has |h| < 1) a smaller |x| has x/var < 2^-20, where both quotients give
+// ceil(.) = 1 (x != 0) or 0: the FAST form is bit-identical to the IEEE one (the sign of a zero
+// quotient is dropped by the fabsf either way); any other var takes the IEEE division.
+struct QParams {
+  float var, rcp, scale, iscale;
+  bool fast;
+};
+__device__ __forceinline__ QParams qparams(float var, float scale) {
+  QParams p;
+  p.var = var;
+  p.rcp = var != 0.f ? 1.f / var : 0.f;
+  p.scale = scale;
+  p.iscale = 1.f / scale;
+  p.fast = var >= 0x1p-80f && var <= 1.f;
+  return p;
+}
+template <bool FAST>
+__device__ __forceinline__ float qin(float x, const QParams& p) {
+  float q;
+  if constexpr (FAST) {
+    q = x * p.rcp;
+    const float e = __builtin_fmaf(-q, p.var, x);
+    q = __builtin_fmaf(e, p.rcp, q);
+  } else {
+    q = x / p.var;
+  }
   const float s = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
-  return ceilf(fabsf(x / var) * scale) / scale * var * s;
+  return ceilf(fabsf(q) * p.scale) * p.iscale * p.var * s;
+}
+
+template <bool FAST, int S>
+__device__ __forceinline__ void qin_strips(float* va, float* vb, const QParams& p) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    va[s] = qin<FAST>(va[s], p);
+    vb[s] = qin<FAST>(vb[s], p);
+  }
 }
 
 
@@ -399,8 +437,16 @@ __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix,
     // the hidden state the reference keeps for step t-1 (hiddens[t-1], and the saved input of the
     // U backward) is the 4x re-quantised tensor; the last step's h is never quantised
     float v = hprev[(int64_t)r * H + j];
+    if (vars[0] != 0.f) {           // every var_g equals var_1 (see rnn_fwd_mm)
+      const QParams qp = qparams(vars[0], qscale);
+      if (qp.fast) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) v = qin(v, vars[g], qscale);
+        for (int g = 0; g < 4; ++g) v = qin<true>(v, qp);
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v = qin<false>(v, qp);
+      }
+    }
     a.hq[(int64_t)t * ix.B2 * H + (int64_t)r * H + j] = v;
     if (t > 0) a.y[ix.out(t - 1, r, j)] = v;
   }
@@ -510,9 +556,12 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
     // tile, the four waves' strips hold every element of h_{t-1} exactly once (rows >= B2 and
     // k >= H are zeros, which change neither max nor min), so var_g is a block reduction of the
     // registers: no second pass over global memory, and each element is quantised once per gate.
+    //
+    // Only var_1 needs the reduction: Q maps the max-abs element x* (|x*| = var) to exactly
+    // +-var (x*/var = +-1, ceil(2^(b-1)) / 2^(b-1) = 1) and every other element to a magnitude
+    // <= var (monotone rounding of ceil(.) / 2^(b-1) <= 1), so var_{g+1} = max|q_{g+1}| = var_g.
     __shared__ float qred[8];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
+    {
       float mx = -INFINITY, mn = INFINITY;
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -525,15 +574,21 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
       __syncthreads();
       mx = fmaxf(fmaxf(qred[0], qred[1]), fmaxf(qred[2], qred[3]));
       mn = fminf(fminf(qred[4], qred[5]), fminf(qred[6], qred[7]));
-      __syncthreads();
-      vars[g] = fabsf(mx) > fabsf(mn) ? fabsf(mx) : fabsf(mn);
+      const float v1 = fabsf(mx) > fabsf(mn) ? fabsf(mx) : fabsf(mn);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) vars[g] = v1;
+    }
+    const QParams qp = qparams(vars[0], qscale);
+    const bool qon = vars[0] != 0.f;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (qon) {
+        if (qp.fast) qin_strips<true, S>(va, vb, qp);
+        else qin_strips<false, S>(va, vb, qp);
+      }
       float vg[S];
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        va[s] = qin(va[s], vars[g], qscale);
-        vb[s] = qin(vb[s], vars[g], qscale);
-        vg[s] = gi == g ? vu[s] : 0.f;
-      }
+      for (int s = 0; s < S; ++s) vg[s] = gi == g ? vu[s] : 0.f;
       mfma_chain<S>(va, vb, vg, acc0, acc1);
     }
   } else {
