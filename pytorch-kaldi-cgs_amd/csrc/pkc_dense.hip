@@ -8,7 +8,9 @@
 //   stats : grid (ceil(N/64), ceil(M/16)), 64 columns x 4 row-threads x 4 rows per workgroup;
 //           sums the split-K slabs (independent loads, fixed order), writes z, and per 16-row block
 //           the column mean / M2 (forward, merged with Chan's formula) or sum(dy) / sum(dy*xhat).
-//   apply : same grid; merges the partials of its columns, normalises / applies the BN backward.
+//   finalize: one workgroup per 64 columns merges each column's partials once (Chan / fixed-order
+//           sums) and writes the BN side outputs / parameter gradients.
+//   apply : same grid as stats; normalises / applies the BN backward from the merged statistics.
 #include "pkc_common.h"
 
 namespace pkc {
@@ -77,8 +79,89 @@ __global__ __launch_bounds__(ET) void dense_stats_kernel(pkc_dense_fwd_args a, f
   }
 }
 
+// Chan merge of one column's per-16-row partials, ONCE per column (not once per apply workgroup):
+// 4 row-threads merge every 4th partial in order, then the four in a fixed order (deterministic).
+// -> part[nrb*2N + c] = mean, part[nrb*2N + N + c] = population variance; the BN training side
+// outputs (save_mean / save_invstd / running statistics) are written here.
+__global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a, float* part) {
+  __shared__ float sn[ET], smu[ET], sm2[ET];
+  const int cl = threadIdx.x % EC, t = threadIdx.x / EC;
+  const int c = blockIdx.x * EC + cl;
+  const int64_t N = a.N;
+  const int nrb = (a.M + ERB - 1) / ERB;
+  float n = 0.f, mu = 0.f, M2 = 0.f;
+  if (c < a.N)
+    for (int k = t; k < nrb; k += ER) {
+      const float nk = (float)min(ERB, a.M - k * ERB);
+      const float mk = part[(int64_t)k * 2 * N + c];
+      const float M2k = part[(int64_t)k * 2 * N + N + c];
+      const float nn = n + nk;
+      const float d = mk - mu;
+      mu += d * nk / nn;
+      M2 += M2k + d * d * n * nk / nn;
+      n = nn;
+    }
+  sn[threadIdx.x] = n;
+  smu[threadIdx.x] = mu;
+  sm2[threadIdx.x] = M2;
+  __syncthreads();
+  if (t != 0 || c >= a.N) return;
+  for (int j = 1; j < ER; ++j) {
+    const float nk = sn[j * EC + cl];
+    if (nk == 0.f) continue;
+    const float nn = n + nk;
+    const float d = smu[j * EC + cl] - mu;
+    mu += d * nk / nn;
+    M2 += sm2[j * EC + cl] + d * d * n * nk / nn;
+    n = nn;
+  }
+  const float var = M2 / (float)a.M;
+  float* fin = part + (int64_t)nrb * 2 * N;
+  fin[c] = mu;
+  fin[N + c] = var;
+  a.save_mean[c] = mu;
+  a.save_invstd[c] = 1.f / sqrtf(var + a.eps);
+  const float cn = (float)(a.count_n > 0 ? a.count_n : a.M);
+  const float unb = cn > 1.f ? var * cn / (cn - 1.f) : var;
+  a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
+  a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
+}
+
+// Column sums of the backward stats pass's per-16-row partials, once per column (same split as
+// dense_finalize_kernel): part[nrb*2N + c] = sum dy, part[nrb*2N + N + c] = sum dy * xhat; the
+// parameter gradients are written here.
+__global__ __launch_bounds__(ET) void dense_bwd_finalize_kernel(pkc_dense_bwd_args a, float* part) {
+  __shared__ float s1[ET], s2[ET];
+  const int cl = threadIdx.x % EC, t = threadIdx.x / EC;
+  const int c = blockIdx.x * EC + cl;
+  const int64_t N = a.N;
+  const int nrb = (a.M + ERB - 1) / ERB;
+  float tdy = 0.f, tdyx = 0.f;
+  if (c < a.N)
+    for (int k = t; k < nrb; k += ER) {
+      tdy += part[(int64_t)k * 2 * N + c];
+      tdyx += part[(int64_t)k * 2 * N + N + c];
+    }
+  s1[threadIdx.x] = tdy;
+  s2[threadIdx.x] = tdyx;
+  __syncthreads();
+  if (t != 0 || c >= a.N) return;
+  tdy = (s1[cl] + s1[EC + cl]) + (s1[2 * EC + cl] + s1[3 * EC + cl]);
+  tdyx = (s2[cl] + s2[EC + cl]) + (s2[2 * EC + cl] + s2[3 * EC + cl]);
+  float* fin = part + (int64_t)nrb * 2 * N;
+  fin[c] = tdy;
+  fin[N + c] = tdyx;
+  if (a.norm == PKC_NORM_BN_TRAIN) {
+    if (a.dgamma) a.dgamma[c] = tdyx;
+    if (a.dbeta) a.dbeta[c] = tdy;
+    // a bias in front of BatchNorm cancels in (z - mean): its gradient is exactly zero
+    if (a.dbias) a.dbias[c] = 0.f;
+  } else if (a.dbias) {
+    a.dbias[c] = tdy;
+  }
+}
+
 __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, const float* part) {
-  __shared__ float stat[2 * EC];
   const int c = blockIdx.x * EC + threadIdx.x % EC;
   const int t = threadIdx.x / EC;
   const int r0 = blockIdx.y * ERB;
@@ -86,37 +169,10 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
   const int64_t N = a.N;
   float mean = 0.f, invstd = 1.f, gam = 1.f, bet = 0.f;
   if (a.norm == PKC_NORM_BN_TRAIN) {
-    if (t == 0 && cok) {   // Chan merge of the per-16-row partials of this column
-      const int nrb = (a.M + ERB - 1) / ERB;
-      float n = 0.f, mu = 0.f, M2 = 0.f;
-      for (int k = 0; k < nrb; ++k) {
-        const float nk = (float)min(ERB, a.M - k * ERB);
-        const float mk = part[(int64_t)k * 2 * N + c];
-        const float M2k = part[(int64_t)k * 2 * N + N + c];
-        const float nn = n + nk;
-        const float d = mk - mu;
-        mu += d * nk / nn;
-        M2 += M2k + d * d * n * nk / nn;
-        n = nn;
-      }
-      const float var = M2 / (float)a.M;
-      stat[threadIdx.x] = mu;
-      stat[EC + threadIdx.x] = var;
-      if (blockIdx.y == 0) {
-        const float is = 1.f / sqrtf(var + a.eps);
-        a.save_mean[c] = mu;
-        a.save_invstd[c] = is;
-        const float cn = (float)(a.count_n > 0 ? a.count_n : a.M);
-        const float unb = cn > 1.f ? var * cn / (cn - 1.f) : var;
-        a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
-        a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
-      }
-    }
-    __syncthreads();
-    if (cok) {
-      const int cl = threadIdx.x % EC;
-      mean = stat[cl];
-      invstd = 1.f / sqrtf(stat[EC + cl] + a.eps);
+    if (cok) {   // the column statistics, merged once per column by dense_finalize_kernel
+      const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+      mean = fin[c];
+      invstd = 1.f / sqrtf(fin[N + c] + a.eps);
       gam = a.gamma[c];
       bet = a.beta[c];
     }
@@ -198,23 +254,9 @@ __global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args 
   const int r0 = blockIdx.y * ERB;
   if (c >= a.N) return;
   const int64_t N = a.N;
-  const int nrb = (a.M + ERB - 1) / ERB;
-  float tdy = 0.f, tdyx = 0.f;
-  for (int k = 0; k < nrb; ++k) {      // fixed order -> deterministic
-    tdy += part[(int64_t)k * 2 * N + c];
-    tdyx += part[(int64_t)k * 2 * N + N + c];
-  }
+  const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;   // dense_bwd_finalize
+  const float tdy = fin[c], tdyx = fin[N + c];
   const bool bn = a.norm == PKC_NORM_BN_TRAIN;
-  if (blockIdx.y == 0 && t == 0) {
-    if (bn) {
-      if (a.dgamma) a.dgamma[c] = tdyx;
-      if (a.dbeta) a.dbeta[c] = tdy;
-      // a bias in front of BatchNorm cancels in (z - mean): its gradient is exactly zero
-      if (a.dbias) a.dbias[c] = 0.f;
-    } else if (a.dbias) {
-      a.dbias[c] = tdy;
-    }
-  }
   if (!bn) return;
   const float invM = 1.f / (float)a.M;
   const float k = a.gamma[c] * a.save_invstd[c];
@@ -551,7 +593,7 @@ static bool small_ok(int M, int N, int nslab, const void* p0, const void* p1, in
 }  // namespace pkc
 
 extern "C" int64_t pkc_dense_work_size(int M, int N) {
-  return 2 * (int64_t)((M + pkc::ERB - 1) / pkc::ERB) * N;
+  return 2 * (int64_t)((M + pkc::ERB - 1) / pkc::ERB + 1) * N;   // partials + the merged stats
 }
 
 extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream) {
@@ -583,6 +625,8 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   if (a->norm == PKC_NORM_BN_TRAIN) {
     hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
     PKC_LAUNCH_CHECK("pkc_dense_fwd stats");
+    hipLaunchKernelGGL(dense_finalize_kernel, dim3(grid.x), dim3(ET), 0, S(stream), *a, work);
+    PKC_LAUNCH_CHECK("pkc_dense_fwd finalize");
   }
   hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_fwd apply");
@@ -610,7 +654,10 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd stats");
-  hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3(grid.x), dim3(ET), 0, S(stream), *a, work);
+  PKC_LAUNCH_CHECK("pkc_dense_bwd finalize");
+  if (a->norm == PKC_NORM_BN_TRAIN)      // without BN, dz = dy is final after the stats pass
+    hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd apply");
   return PKC_OK;
 }

@@ -119,19 +119,21 @@ extern "C" int pkc_fakequant_input(const float* x, float* out, int64_t n, int bi
   using namespace pkc;
   PKC_CHECK_ARG(x && out && work && n > 0 && bits > 0 && bits < 31 && reps >= 1 && reps <= 8,
                 "pkc_fakequant_input: bad arguments");
-  // out holds reps consecutive tensors q1..q_reps; work >= 2*64 + 8 floats
+  // out holds reps consecutive tensors q1..q_reps; work >= 2*64 + 8 floats.  Only q1 needs the
+  // max-abs reduction: Q maps the max-abs element x* to exactly +-var (x*/var = +-1) and every
+  // other element to a magnitude <= var, so every later call's per-tensor var is the same.
   const float scale = ldexpf(1.f, bits - 1);
   const int nparts = 64;
+  hipLaunchKernelGGL(absmax_partial_kernel, dim3(nparts), dim3(256), 0, S(stream), x, n, work);
+  hipLaunchKernelGGL(absmax_finish_kernel, dim3(1), dim3(64), 0, S(stream), work, nparts,
+                     work + 2 * nparts);
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
   const float* src = x;
   for (int r = 0; r < reps; ++r) {
     float* dst = out + (int64_t)r * n;
-    hipLaunchKernelGGL(absmax_partial_kernel, dim3(nparts), dim3(256), 0, S(stream), src, n, work);
-    hipLaunchKernelGGL(absmax_finish_kernel, dim3(1), dim3(64), 0, S(stream), work, nparts,
-                       work + 2 * nparts + r);
-    int64_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(fq_input_kernel, dim3((unsigned)blocks), dim3(256), 0, S(stream), src, dst, n,
-                       work + 2 * nparts + r, scale);
+                       work + 2 * nparts, scale);
     src = dst;
   }
   PKC_LAUNCH_CHECK("pkc_fakequant_input");

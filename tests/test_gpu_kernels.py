@@ -111,7 +111,8 @@ def _bn_ref(z, gamma, beta, act, keep, p):
 
 @pytest.mark.parametrize("act", ["relu", "tanh", "sigmoid", "linear"])
 @pytest.mark.parametrize("p", [0.0, 0.15])
-@pytest.mark.parametrize("M,N,S", [(128, 1024, 4), (16, 48, 1), (50, 70, 3), (100, 1028, 7), (300, 64, 2)])
+@pytest.mark.parametrize("M,N,S", [(128, 1024, 4), (16, 48, 1), (50, 70, 3), (100, 1028, 7), (300, 64, 2),
+                                   (2000, 256, 1), (1700, 100, 3)])
 def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
     g = torch.Generator().manual_seed(M + N + S)
     slabs = torch.randn(S, M, N, generator=g)
@@ -153,13 +154,16 @@ def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
     # a pre-activation within rounding of a kink (ReLU at 0) may take the other branch on the GPU;
     # through the BN mean terms that changes its whole column: compare the other columns
     y = torch.nn.functional.batch_norm(z, None, None, gamma, beta, training=True, eps=1e-5)
-    cols = (y.abs() > 1e-4).all(0) if act == "relu" else torch.ones(N, dtype=torch.bool)
+    # (fp32 differences here are ~1e-6 of y's scale; at M = 2000 rows a 1e-4 margin would drop
+    # a fifth of the columns)
+    cols = (y.abs() > 1e-5).all(0) if act == "relu" else torch.ones(N, dtype=torch.bool)
     assert cols.float().mean() > 0.95
     torch.testing.assert_close(dz.cpu()[:, cols], zz.grad[:, cols], rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(dgam.cpu()[cols], gg.grad[cols], rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dbet.cpu()[cols], bb.grad[cols], rtol=1e-4, atol=1e-4)
     assert (dbias.cpu() == 0).all()          # bias before BN: exact zero gradient
-    assert zz.grad.sum(0).abs().max() < 1e-4  # ... which autograd reproduces up to rounding
+    # ... which autograd reproduces up to the rounding of an M-term fp32 sum
+    assert zz.grad.sum(0).abs().max() < 1e-4 * max(1.0, M / 256)
 
 
 def test_dense_dropout_rate_and_determinism(L):
