@@ -427,16 +427,40 @@ __device__ __forceinline__ void mfma_chain(const float* va, const float* vb, con
 }
 
 // ------------------------------------------------------------------------------- forward step
+// The cell update's inputs at (r, j) that do not depend on this step's products: the gate
+// pre-activations W x (+BN), h_{t-1}, c_{t-1} (LSTM) and the dropout mask.  rnn_fwd_mm requests
+// them before its operand strips, so they arrive while the MFMA chain runs instead of after it.
+struct EpiIn {
+  float w[4];
+  float hp, cp, m;
+};
+template <int CELL, int NG>
+__device__ __forceinline__ EpiIn epi_load(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
+                                          int j) {
+  EpiIn e;
+  const int H = a.H;
+  const int64_t TBH = (int64_t)a.T * a.B * H;   // gate stride of the (G, T, B, H) pre-activations
+  const int64_t pi = ix.pre(t, r, j);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) e.w[g] = g < NG ? a.wpre[g * TBH + pi] : 0.f;
+  const int64_t hi = (int64_t)t * ix.B2 * H + (int64_t)r * H + j;
+  e.hp = a.hs[hi];
+  if constexpr (CELL == PKC_CELL_LSTM) e.cp = a.cs[hi];
+  else e.cp = 0.f;
+  e.m = drop_val(a, r, j, ix.B2);
+  return e;
+}
+
 // Cell update of step t at (r, j) from the recurrent products acc[g] = (U_g h_{t-1})[r][j].
 template <int CELL, bool QH>
 __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
-                                        int j, const float* acc, const float* vars, float qscale) {
+                                        int j, const float* acc, const float* vars, float qscale,
+                                        const EpiIn& e) {
   const int H = a.H;
-  const float* hprev = a.hs + (int64_t)t * ix.B2 * H;
   if constexpr (QH) {
     // the hidden state the reference keeps for step t-1 (hiddens[t-1], and the saved input of the
     // U backward) is the 4x re-quantised tensor; the last step's h is never quantised
-    float v = hprev[(int64_t)r * H + j];
+    float v = e.hp;
     if (vars[0] != 0.f) {           // every var_g equals var_1 (see rnn_fwd_mm)
       const QParams qp = qparams(vars[0], qscale);
       if (qp.fast) {
@@ -453,40 +477,40 @@ __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix,
   const int64_t TBH = (int64_t)a.T * a.B * H;   // gate stride of the (G, T, B, H) pre-activations
   const int64_t TB2H = (int64_t)a.T * ix.B2 * H; // gate stride of the saved activations
   const int64_t pi = ix.pre(t, r, j), si = ix.st(t, r, j);
-  const float m = drop_val(a, r, j, ix.B2);
-  const float hp = hprev[(int64_t)r * H + j];
+  const float m = e.m;
+  const float hp = e.hp;
   float h = 0.f;
   if constexpr (CELL == PKC_CELL_GRU) {
     // phase 1 of a GRU step: update / reset gates and r*h (the input of Uh)
-    const float z = sigm(a.wpre[pi] + acc[0]);
-    const float rg = sigm(a.wpre[TBH + pi] + acc[1]);
+    const float z = sigm(e.w[0] + acc[0]);
+    const float rg = sigm(e.w[1] + acc[1]);
     a.gates[si] = z;
     a.gates[TB2H + si] = rg;
     a.rh[si] = rg * hp;
     return;
   } else if constexpr (CELL == PKC_CELL_MINGRU) {
     // phase 1 of a minimalGRU step: update gate and z*h (the input of Uh)
-    const float z = sigm(a.wpre[pi] + acc[0]);
+    const float z = sigm(e.w[0] + acc[0]);
     a.gates[si] = z;
     a.rh[si] = z * hp;
     return;
   } else if constexpr (CELL == PKC_CELL_RNN) {
-    const float hcr = act_fwd(a.act, a.wpre[pi] + acc[0]);
+    const float hcr = act_fwd(a.act, e.w[0] + acc[0]);
     h = hcr * m;
     a.gates[si] = hcr;
   } else if constexpr (CELL == PKC_CELL_LIGRU) {
-    const float z = sigm(a.wpre[pi] + acc[0]);
-    const float hcr = act_fwd(a.act, a.wpre[TBH + pi] + acc[1]);
+    const float z = sigm(e.w[0] + acc[0]);
+    const float hcr = act_fwd(a.act, e.w[1] + acc[1]);
     h = z * hp + (1.f - z) * (hcr * m);
     a.gates[si] = z;
     a.gates[TB2H + si] = hcr;
   } else {
     // LSTM gates (f, i, o, c); cs[t] = c_{t-1}
-    const float f = sigm(a.wpre[pi] + acc[0]);
-    const float i = sigm(a.wpre[TBH + pi] + acc[1]);
-    const float o = sigm(a.wpre[2 * TBH + pi] + acc[2]);
-    const float cc = act_fwd(a.act, a.wpre[3 * TBH + pi] + acc[3]);
-    const float cp = a.cs[(int64_t)t * ix.B2 * H + (int64_t)r * H + j];
+    const float f = sigm(e.w[0] + acc[0]);
+    const float i = sigm(e.w[1] + acc[1]);
+    const float o = sigm(e.w[2] + acc[2]);
+    const float cc = act_fwd(a.act, e.w[3] + acc[3]);
+    const float cp = e.cp;
     const float c = i * cc * m + f * cp;
     h = o * act_fwd(a.act, c);
     a.cs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = c;
@@ -533,6 +557,14 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
   const int ra = r0 + c, rb = r0 + 16 + c;
   const int gi = c / NU, u = u0 + c % NU;
   const float* pu = a.U[PH == 0 ? gi : cand_gate(CELL)] + (int64_t)(u < H ? u : 0) * H;
+  // one epilogue element per thread (LSTM, liGRU, GRU phase 1): its inputs are requested first
+  constexpr bool PF = PH == 0 && 32 * NU <= RT;
+  EpiIn pre;
+  if constexpr (PF) {
+    const int rl = (int)threadIdx.x / NU, ul = (int)threadIdx.x % NU;
+    const int rr = min(r0 + rl, B2 - 1), jj = min(u0 + ul, H - 1);
+    if ((int)threadIdx.x < 32 * NU) pre = epi_load<CELL, NG>(a, ix, t, rr, jj);
+  }
   float va[S], vb[S], vu[S];
   if constexpr (SP) {
     static_assert(!QH && PH == 0, "block-sparse U: no quantised h, one-phase cells");
@@ -605,7 +637,8 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < NG; ++g) acc[g] = tile[rl * 17 + g * NU + ul];
-      fwd_epi<CELL, QH>(a, ix, t, r, j, acc, vars, qscale);
+      if constexpr (PF) fwd_epi<CELL, QH>(a, ix, t, r, j, acc, vars, qscale, pre);
+      else fwd_epi<CELL, QH>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
     }
   }
 }
