@@ -188,6 +188,8 @@ def main():
                     help="skip the informational C3/C4/C5 sequence-model throughputs")
     ap.add_argument("--pmc-replay", type=int, default=0,
                     help="only replay the dominant launch N times (for rocprofv3 --pmc passes)")
+    ap.add_argument("--pmc-kernel", default="",
+                    help="entry point to replay with --pmc-replay (default: pick the dominant one)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -250,7 +252,7 @@ def main():
 
     if args.pmc_replay:
         # counter runs (scripts/gpu_pmc.sh): the dominant kernel's launches, N rounds, last
-        dom_fn, _ = pick_dominant()
+        dom_fn = args.pmc_kernel or pick_dominant()[0]
         nl = eng.replay_launches(dom_fn, args.pmc_replay)
         print(json.dumps({"pmc_replay": dom_fn, "launches": nl * args.pmc_replay}), flush=True)
         return

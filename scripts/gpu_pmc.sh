@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 N=20
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc/fetch -o f -- python3 bench.py --pmc-replay $N > gpurun_out/pmc/fetch.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc/write -o w -- python3 bench.py --pmc-replay $N > gpurun_out/pmc/write.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc/fetch -o f -- python3 bench.py --pmc-replay $N --pmc-kernel ${PMC_KERNEL:-pkc_gemm_grouped} > gpurun_out/pmc/fetch.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc/write -o w -- python3 bench.py --pmc-replay $N --pmc-kernel ${PMC_KERNEL:-pkc_gemm_grouped} > gpurun_out/pmc/write.log 2>&1 || exit $?
 python3 scripts/pmc_summary.py gpurun_out/pmc $N > gpurun_out/pmc_traffic.json
 cat gpurun_out/pmc_traffic.json
