@@ -34,6 +34,7 @@ _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
 # split-K slab budget of a layer output (<= 8: the small-batch dense kernels sum them in
 # registers); on the C2 step 4 gives 0.197 ms per step, 8 and 5 0.201, 3 0.211, 2 0.233
 MAX_SPLITS = int(os.environ.get("PKC_MAX_SPLITS", "4"))
+MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", str(MAX_SPLITS)))   # forward Z = X W^T
 
 
 _PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
@@ -532,7 +533,7 @@ class Engine:
                 self._alloc_rec(n)
                 continue
             N, K = n.N, n.K
-            n.scap = self.cap or _splits(M, N, K, MAX_SPLITS)
+            n.scap = self.cap or _splits(M, N, K, MAX_SPLITS_FWD)
             n.zslab = _f32(n.scap * M * N, dev) if n.W is not None else None
             if n.ln:
                 n.ln_y, n.ln_xhat = _f32(M * N, dev), _f32(M * N, dev)
