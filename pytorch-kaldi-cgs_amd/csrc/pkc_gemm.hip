@@ -42,6 +42,15 @@ struct Lds<PKC_PREC_BF16> {
   __bf16 b[BN * LD];
 };
 
+// LDS swizzle of an m-contiguous (not k-contiguous) fp32 operand.  Its register stage holds 4
+// consecutive ROWS of one k, so the store into the [row][k] tile is a column write: with the plain
+// layout the rows of a wave's 64 lanes fall into two banks (8-way conflicts on every such store,
+// the cost that dominated the sequence models' dW / dU matmuls).  Rotating each row's 16-byte
+// k-chunks by row / 4 spreads them (2-way).  k-contiguous operands keep the plain layout, which
+// their conflict-free 16-byte stores and fragment reads prefer; measured on the box, the same
+// rotation of the bf16 tiles made the C2 step slower (0.204 vs 0.197 ms), so bf16 keeps it too.
+__device__ __forceinline__ int swz4(int row, int c4) { return (c4 + (row >> 2)) & 7; }
+
 // Register staging of one 64x32 operand tile (8 floats per thread).  Loads are issued
 // unconditionally from clamped (always valid) addresses and out-of-range values are zeroed by a
 // select afterwards: a load guarded by a runtime condition makes hipcc branch around it and drain
@@ -97,8 +106,14 @@ struct Stage {
           for (int j = 0; j < 4; ++j) s[r * LD + k + j] = (T)v[4 * i + j];
         } else {
           const int k = idx >> 4, r = (idx & 15) * 4;
+          if constexpr (sizeof(T) == 4) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) s[(r + j) * LD + k] = (T)v[4 * i + j];
+            for (int j = 0; j < 4; ++j)
+              s[(r + j) * LD + 4 * swz4(r + j, k >> 2) + (k & 3)] = (T)v[4 * i + j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[(r + j) * LD + k] = (T)v[4 * i + j];
+          }
         }
       }
     } else {
@@ -110,7 +125,8 @@ struct Stage {
           s[r * LD + k] = (T)v[i];
         } else {
           const int k = idx >> 6, r = idx & 63;
-          s[r * LD + k] = (T)v[i];
+          if constexpr (sizeof(T) == 4) s[r * LD + 4 * swz4(r, k >> 2) + (k & 3)] = (T)v[i];
+          else s[r * LD + k] = (T)v[i];
         }
       }
     }
@@ -178,17 +194,22 @@ struct StageSel<true, KC, VEC> {
   using E = __bf16;
 };
 
-template <int PREC>
+template <int PREC, bool AKC, bool BKC>
 __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, int r, int h,
                                           f32x16& acc) {
   constexpr int LD = Lds<PREC>::LD;
+  const int ra = wm * 32 + r, rb = wn * 32 + r;
   if constexpr (PREC == PKC_PREC_FP32) {
-    const float4* pa = reinterpret_cast<const float4*>(&sm.a[(wm * 32 + r) * LD + 16 * h]);
-    const float4* pb = reinterpret_cast<const float4*>(&sm.b[(wn * 32 + r) * LD + 16 * h]);
+    const float4* pa = reinterpret_cast<const float4*>(&sm.a[ra * LD + 16 * h]);
+    const float4* pb = reinterpret_cast<const float4*>(&sm.b[rb * LD + 16 * h]);
     float av[16], bv[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float4 x = pa[q], y = pb[q];
+      float4 x, y;
+      if constexpr (AKC) x = pa[q];
+      else x = *reinterpret_cast<const float4*>(&sm.a[ra * LD + 4 * swz4(ra, 4 * h + q)]);
+      if constexpr (BKC) y = pb[q];
+      else y = *reinterpret_cast<const float4*>(&sm.b[rb * LD + 4 * swz4(rb, 4 * h + q)]);
       av[4 * q] = x.x; av[4 * q + 1] = x.y; av[4 * q + 2] = x.z; av[4 * q + 3] = x.w;
       bv[4 * q] = y.x; bv[4 * q + 1] = y.y; bv[4 * q + 2] = y.z; bv[4 * q + 3] = y.w;
     }
@@ -249,7 +270,7 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
         const int kn = kt + (d + DEPTH) * BK;
         sa[d].load(A, lda, m0, M, kn, kend);
         sb[d].load(B, ldb, n0, N, kn, kend);
-        mfma_tile<PREC>(sm, wm, wn, r, h, acc);
+        mfma_tile<PREC, AKC, BKC>(sm, wm, wn, r, h, acc);
       }
     }
   }
