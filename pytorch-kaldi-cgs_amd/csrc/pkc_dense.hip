@@ -317,6 +317,20 @@ __global__ __launch_bounds__(ET) void colsum_kernel(int M, int N, int nslab, con
 constexpr int FG = PKC_DENSE_FG, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Column group of a workgroup (PKC_DENSE_XCD, measured 0.1976 -> 0.1957 ms per C2 step): workgroup
+// w runs on XCD w % 8 (round-robin
+// dispatch), so give each XCD a contiguous run of groups — the two 64-byte halves of a slab's
+// 128-byte line are then read through one L2 instead of two.
+#ifndef PKC_DENSE_XCD
+#define PKC_DENSE_XCD 1
+#endif
+__device__ __forceinline__ int col_group(int b, int nb) {
+  if (!PKC_DENSE_XCD) return b;
+  const int per = nb >> 3;
+  if (b >= per * 8) return b;
+  return (b & 7) * per + (b >> 3);
+}
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
@@ -375,7 +389,7 @@ template <int NS, int RI>
 __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args a) {
   __shared__ float4 red[4 * FG];
   const int c4 = threadIdx.x % FG, rg = threadIdx.x / FG;
-  const int c = blockIdx.x * FC + c4 * 4;
+  const int c = col_group(blockIdx.x, gridDim.x) * FC + c4 * 4;
   const bool cok = c < a.N;
   const int64_t N = a.N;
   const int M = a.M;
@@ -486,7 +500,7 @@ template <int NS, int RI>
 __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args a) {
   __shared__ float4 red[4 * FG];
   const int c4 = threadIdx.x % FG, rg = threadIdx.x / FG;
-  const int c = blockIdx.x * FC + c4 * 4;
+  const int c = col_group(blockIdx.x, gridDim.x) * FC + c4 * 4;
   const bool cok = c < a.N;
   const int64_t N = a.N;
   const int M = a.M;
