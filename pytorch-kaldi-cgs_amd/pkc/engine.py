@@ -35,6 +35,10 @@ _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
 # registers); on the C2 step 4 gives 0.197 ms per step, 8 and 5 0.201, 3 0.211, 2 0.233
 MAX_SPLITS = int(os.environ.get("PKC_MAX_SPLITS", "4"))
 MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", str(MAX_SPLITS)))   # forward Z = X W^T
+# spread optimizer updates: a layer's update larger than this many parameters is cut into parts
+# that ride in successive backward launches (0: one part).  C2, frames/s: 0 -> 653-657k,
+# 1.2M -> 663k, 700k -> 666-667k, 400k-520k -> 669-671k, 250k -> 644k (the tail launch grows)
+OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "500000"))
 
 
 _PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
@@ -1351,15 +1355,23 @@ class Engine:
             if li == 0 and n.src[0] == "node":
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
 
-    def _opt_op(self, n):
-        """The optimizer update of node n's parameters as an operation of a grouped launch."""
+    def _opt_op(self, n, parts=1):
+        """The optimizer update of node n's parameters as operations of grouped launches: `parts`
+        consecutive slices of its work-item list (int32 pairs), one per launch."""
         if n not in self.node_opt:
             return []
         nch, cmap, idx = self.node_opt[n]
         nparam = sum(self.opt_entries[i]["p"].numel() for i in idx)
-        return [("opt %s" % n.name, 0.0, 20.0 * nparam,
-                 L.GemmProblem(kind=L.OP_OPTIM, M=nch, A=self.opt_desc.data_ptr(),
-                               B=cmap.data_ptr()))]
+        parts = max(1, min(parts, nch))
+        ops, b = [], 0
+        for k in range(parts):
+            e = (nch * (k + 1)) // parts
+            ops.append(("opt %s%s" % (n.name, "" if parts == 1 else " [%d/%d]" % (k + 1, parts)), 0.0,
+                        20.0 * nparam * (e - b) / nch,
+                        L.GemmProblem(kind=L.OP_OPTIM, M=e - b, A=self.opt_desc.data_ptr(),
+                                      B=cmap.data_ptr() + 8 * b)))
+            b = e
+        return ops
 
     def _bucket_cut(self):
         """Data parallelism: the node after whose dW launch the gradients of it and every later
@@ -1384,21 +1396,26 @@ class Engine:
         needs one of their results (the producer's BatchNorm backward reads the dX slabs).
         spread_opt: each layer's optimizer update joins the launch AFTER the one holding its dW
         and dX (dX still reads the old weights), so the bandwidth-bound update overlaps the
-        latency-bound matmuls instead of running as its own launch at the end."""
+        latency-bound matmuls instead of running as its own launch at the end.  An update of more
+        than OPT_SPREAD_PARAMS parameters is cut into parts over the following launches, so no
+        single launch carries a whole output head's update."""
         spread_opt = spread_opt and not self.reg_terms
         for n in self.nodes:
             if n.gslab is not None:
                 n.sb = self._grad_slabs(n)
         pend = [loss_op] if loss_op is not None else []
-        carry, carry_next = [], []
+        future = [[], []]       # future[i]: operations riding in the i-th launch from now
         cut_node = self._bucket_cut()[0] if on_cut is not None else None
         pend_nodes = []
 
         def flush():
-            nonlocal pend, carry, carry_next, pend_nodes, cut_node
-            if pend or carry:
-                self._gemms(pend + carry, s)
-            pend, carry, carry_next = [], carry_next, []
+            nonlocal pend, future, pend_nodes, cut_node
+            now = future.pop(0)
+            if pend or now:
+                self._gemms(pend + now, s)
+            pend = []
+            while len(future) < 2:
+                future.append([])
             if cut_node is not None and cut_node in pend_nodes:
                 cut_node = None
                 on_cut()                # the first bucket's gradients are final
@@ -1417,9 +1434,14 @@ class Engine:
             pend += self._bwd_problems(n)
             pend_nodes.append(n)
             if spread_opt:
-                carry_next += self._opt_op(n)
+                nparam = sum(self.opt_entries[i]["p"].numel() for i in self.node_opt.get(n, (0, 0, []))[2])
+                parts = -(-nparam // OPT_SPREAD_PARAMS) if OPT_SPREAD_PARAMS > 0 else 1
+                for k, op in enumerate(self._opt_op(n, parts)):
+                    while len(future) <= 1 + k:
+                        future.append([])
+                    future[1 + k].append(op)
         flush()
-        self.spread_tail = carry        # updates still to run (the last layers')
+        self.spread_tail = [op for f in future for op in f]   # updates still to run
 
     def _build_reg(self):
         """Device descriptors of the regulariser terms (item lists, block starts, buffers)."""
