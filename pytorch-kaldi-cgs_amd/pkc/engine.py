@@ -34,6 +34,10 @@ _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
 # split-K slab budget of a layer output (<= 8: the small-batch dense kernels sum them in
 # registers); on the C2 step 4 gives 0.197 ms per step, 8 and 5 0.201, 3 0.211, 2 0.233
 MAX_SPLITS = int(os.environ.get("PKC_MAX_SPLITS", "4"))
+# slab budget of a layer output read by several matmul layers (the output heads' shared input:
+# the 1928-wide head's dX gets 7 K-splits instead of 3).  C2, same run, frames/s: 4 -> 668-670k,
+# 5 -> 674-677k, 6 -> 675-677k, 8 -> 682-683k
+SLAB_BUDGET_MULTI = min(8, int(os.environ.get("PKC_SLAB_BUDGET_MULTI", "8")))
 MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", str(MAX_SPLITS)))   # forward Z = X W^T
 # spread optimizer updates: a layer's update larger than this many parameters is cut into parts
 # that ride in successive backward launches (0: one part).  C2, frames/s: 0 -> 653-657k,
@@ -571,7 +575,8 @@ class Engine:
             cap = 0
             for c in n.consumers:
                 # an input norm (no matmul) writes its input gradient into one slab
-                c.sxcap = 1 if c.W is None else (self.cap or _splits(M, n.N, c.N, MAX_SPLITS))
+                c.sxcap = 1 if c.W is None else (self.cap or _splits(
+                    M, n.N, c.N, SLAB_BUDGET_MULTI if len(n.consumers) > 1 else MAX_SPLITS))
                 cap += c.sxcap
             n.gslab = _f32(cap * M * n.N, dev) if cap else None
         self.needs_grad = {}
@@ -1208,7 +1213,8 @@ class Engine:
         most that many in registers); the widest consumer gives up splits first."""
         M = self.M
         want = [1 if c.W is None else _splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
-        while sum(want) > MAX_SPLITS and max(want) > 1:
+        budget = SLAB_BUDGET_MULTI if len(n.consumers) > 1 and not self.cap else MAX_SPLITS
+        while sum(want) > budget and max(want) > 1:
             want[want.index(max(want))] -= 1
         off = 0
         n.cons_off = []
