@@ -125,28 +125,24 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
     seq = any(a[2] for a in arch_dict.values())
     rng = np.random if (not seq and to_do != "forward") else None
     # sort / split the utterances and start the pinned-memory upload on a side stream here, in
-    # the loader thread, so it overlaps the current chunk's training; the frame shuffle (global
-    # np.random) stays on the main thread in _finish_chunk, in a deterministic order
+    # the loader thread, so it overlaps the current chunk's training.  The GPU half of load_chunk
+    # (context window, normalisation, frame shuffle) is item 5's finish(): run_nn calls it where the
+    # reference's thread shuffles (after the model init draws), keeping np.random's draw order
     staged = D.stage_chunk(fea, labs, max_seq, frontend=frontend)
-    shared_list.append(("raw", staged, labs, lab_names, int(fd[3]), int(fd[4]), max_seq, rng, fname))
-    shared_list.append(None)
-    shared_list.append(fea_dict)
-    shared_list.append(lab_dict)
-    shared_list.append(arch_dict)
-    shared_list.append(None)
+    L, R = int(fd[3]), int(fd[4])
+    data_set = D.PendingChunk(staged, labs, lab_names, L, R, max_seq, rng, fname)
+    c0, c1 = data_set.fea_cols[fname]
+    fea_dict[fname] = fea_dict[fname][:5] + [c0, c1, c1 - c0]        # data_io.py:225-228
+    for i, ln in enumerate(lab_names):
+        lab_dict[ln] = lab_dict[ln][:3] + [c1 + i]                     # data_io.py:259-261
+    # data_io.py:277-282: [data_name, data_end_index, fea_dict, lab_dict, arch_dict, data_set]
+    shared_list.extend([data_set.names, data_set.end_index, fea_dict, lab_dict, arch_dict, data_set])
 
 
 def _finish_chunk(shared_list):
-    """GPU half of the loader: context window + normalisation + shuffle (pkc_cw_*)."""
-    _, staged, labs, lab_names, L, R, max_seq, rng, fname = shared_list[0]
-    ch = D.prepare_chunk(None, labs, lab_names, L, R, max_seq, shuffle_rng=rng, fea_name=fname,
-                         staged=staged)
-    fea_dict, lab_dict = shared_list[2], shared_list[3]
-    c0, c1 = ch.fea_cols[fname]
-    fea_dict[fname] = fea_dict[fname][:5] + [c0, c1, c1 - c0]
-    for i, ln in enumerate(lab_names):
-        lab_dict[ln] = lab_dict[ln][:3] + [c1 + i]
-    return [ch.names, ch, ch.end_index, fea_dict, lab_dict, shared_list[4]]
+    """core.py:349-362: the six loader items in run_nn's return order, the chunk prepared."""
+    data_name, data_end_index, fea_dict, lab_dict, arch_dict, data_set = shared_list
+    return [data_name, data_set.finish(), data_end_index, fea_dict, lab_dict, arch_dict]
 
 
 def model_init(config, arch_dict, fea_dims, to_do):
@@ -180,6 +176,12 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
            if_apply_ghcgs=False, if_pattern_search=False):
     patterns = {} if patterns is None else patterns
     pattern_masks = {} if pattern_masks is None else pattern_masks
+    if if_pattern_search:
+        # core.py:149-151 imports pattern_prun_model from pattern_search, which the reference does
+        # not define (pattern_search.py has no such function): the call cannot run there either
+        raise NotImplementedError("if_pattern_search: pattern_search.pattern_prun_model does not "
+                                  "exist in the reference")
+    # if_apply_ghcgs is accepted and unused, as in the reference (core.py:25)
     if not os.path.exists(cfg_file):
         sys.stderr.write("ERROR: The config file %s does not exist!\n" % cfg_file)
         sys.exit(0)
@@ -332,6 +334,7 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
             if getattr(net, "guided_hcgs", False) and not net.apply_guided_hcgs:   # (298-300)
                 net.apply_ghcgs()
     if to_do == "train":
+        patterns, pattern_masks = {}, {}                             # core.py:287-288
         for net_name, net in nns.items():
             if getattr(net, "if_pattern", False):                    # core.py:304-306
                 patterns[net_name] = net.pattern

@@ -193,6 +193,68 @@ class Chunk:
     def n_rows(self):
         return self.feats.shape[0]
 
+    @property
+    def shape(self):
+        """(rows, feature columns + label columns), the shape of the reference's data_set."""
+        return (self.n_rows, self.feats.shape[1] + self.labels.shape[1])
+
+    def __array__(self, dtype=None, copy=None):
+        """The reference's data_set (data_io.py:236-282): float64 [features | labels] rows, for
+        callers that read item 5 of read_lab_fea's shared list as an array (a host copy)."""
+        a = np.concatenate([self.feats.cpu().numpy().astype(np.float64),
+                            self.labels.cpu().numpy().astype(np.float64)], 1)
+        return a if dtype is None else a.astype(dtype)
+
+    def finish(self):
+        return self
+
+
+def trim_end_index(end_index, left, right):
+    """load_chunk's end_index after the context window (data_io.py:130-131)."""
+    end_index = np.asarray(end_index) - left
+    end_index[-1] = end_index[-1] - right
+    return end_index
+
+
+class PendingChunk(Chunk):
+    """Item 5 of read_lab_fea's shared list: a chunk whose utterances are sorted / split and whose
+    raw frames are uploading (StagedChunk); the GPU half of load_chunk (context window, chunk
+    normalisation, label shift, frame shuffle) runs on finish() — which run_nn calls where the
+    reference's loader thread shuffles, so the np.random draws keep the reference's order — or on
+    first use of the device tensors."""
+
+    def __init__(self, staged, labs, lab_names, left, right, max_seq, shuffle_rng, fea_name):
+        self._pending = (staged, labs, list(lab_names), left, right, max_seq, shuffle_rng, fea_name)
+        N, D = staged.shape
+        Cc = D * (left + right + 1)
+        super().__init__(staged.names, trim_end_index(staged.end_index, left, right), None, None,
+                         {fea_name: (0, Cc)}, list(lab_names))
+
+    def finish(self):
+        if self._pending is not None:
+            staged, labs, lab_names, L, R, max_seq, rng, fname = self._pending
+            self._pending = None
+            ch = prepare_chunk(None, labs, lab_names, L, R, max_seq, shuffle_rng=rng, fea_name=fname,
+                               staged=staged)
+            self._feats, self._labels = ch.feats, ch.labels
+        return self
+
+    @property
+    def feats(self):
+        return self.finish()._feats
+
+    @feats.setter
+    def feats(self, v):
+        self._feats = v
+
+    @property
+    def labels(self):
+        return self.finish()._labels
+
+    @labels.setter
+    def labels(self, v):
+        self._labels = v
+
 
 class StagedChunk:
     """A chunk after the host half of loading: utterances sorted / split (load_dataset) and the
@@ -291,8 +353,7 @@ def prepare_chunk(fea, labs, lab_names, left, right, max_sequence_length, shuffl
     names, lab_arrays, end_index = staged.names, staged.lab_arrays, staged.end_index
     N, D = staged.shape
     Nout = N - left - right
-    end_index = end_index - left
-    end_index[-1] = end_index[-1] - right
+    end_index = trim_end_index(end_index, left, right)
     Cc = D * (left + right + 1)
     lab_cols = []
     for la in lab_arrays:                      # data_io.py:137-141

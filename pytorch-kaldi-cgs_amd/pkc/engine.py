@@ -859,6 +859,8 @@ class Engine:
             t.qout = e["q"].data_ptr() if e["qbits"] else None
             t.qbits = e["qbits"]
             t.step = e["step"] + step_inc
+            if kind == "sgd" and e.get("has_buf"):
+                t.step = max(t.step, 2)   # torch SGD starts buf = g only when it has no buffer
         host = torch.frombuffer(bytearray(C.string_at(arr, C.sizeof(arr))), dtype=torch.uint8)
         self.opt_desc.copy_(host)
 
@@ -1209,8 +1211,9 @@ class Engine:
     # ------------------------------------------------------------------ backward
     def _grad_slabs(self, n):
         """(pointer, nslab) of dL/d(out of n) as the consumers' dX slabs, with their offsets.  The
-        consumers share a budget of MAX_SPLITS slabs (the fused small-batch BN backward sums at
-        most that many in registers); the widest consumer gives up splits first."""
+        consumers share a budget of MAX_SPLITS slabs, or SLAB_BUDGET_MULTI (8) when several matmul
+        layers read the output (the heads' shared input; the fused small-batch BN backward sums at
+        most 8 in registers); the widest consumer gives up splits first."""
         M = self.M
         want = [1 if c.W is None else _splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
         budget = SLAB_BUDGET_MULTI if len(n.consumers) > 1 and not self.cap else MAX_SPLITS
@@ -1740,34 +1743,43 @@ class Engine:
                 n.spec["nbt"].fill_(n.nbt0 + self.steps_done)
 
     def optimizer_state_dict(self, arch):
-        """torch.optim-compatible state_dict of one architecture's optimizer (core.py:317-322)."""
+        """torch.optim state_dict of one architecture's optimizer (core.py:317-322).
+
+        param_groups come from the torch.optim class utils.optimizer_init would build
+        (utils.py:1833-1881) over the same parameters, so every hyperparameter key of the running
+        torch version is present and the dict loads into the reference's optimizer and steps."""
         net = self.nets[arch]
         params = list(net.parameters())
         index = {id(p): i for i, p in enumerate(params)}
         o = self.arch_opts[arch]
+        kind = o["arch_opt"]
         state = {}
         for e in self.opt_entries:
-            if e["arch"] != arch or e["step"] == 0:
+            if e["arch"] != arch or (e["step"] == 0 and not e.get("has_buf")):
                 continue
-            st = {"step": torch.tensor(float(e["step"]))}
-            kind = o["arch_opt"]
-            if kind == "rmsprop":
-                st["square_avg"] = e["s1"].detach().cpu().clone()
+            if kind == "sgd":
+                if float(o["opt_momentum"]) == 0:
+                    continue                      # torch SGD keeps no state without momentum
+                st = {"momentum_buffer": e["s1"].detach().cpu().clone()}
+            elif kind == "rmsprop":
+                st = {"step": torch.tensor(float(e["step"])),
+                      "square_avg": e["s1"].detach().cpu().clone()}
                 if e["s3"] is not None:
                     st["momentum_buffer"] = e["s3"].detach().cpu().clone()
                 if e["s2"] is not None:
                     st["grad_avg"] = e["s2"].detach().cpu().clone()
-            elif kind == "sgd":
-                st = {"momentum_buffer": e["s1"].detach().cpu().clone()
-                      if float(o["opt_momentum"]) != 0 else None}
             else:
-                st["exp_avg"] = e["s1"].detach().cpu().clone()
-                st["exp_avg_sq"] = e["s2"].detach().cpu().clone()
+                st = {"step": torch.tensor(float(e["step"])),
+                      "exp_avg": e["s1"].detach().cpu().clone(),
+                      "exp_avg_sq": e["s2"].detach().cpu().clone()}
+                if e["s3"] is not None:
+                    st["max_exp_avg_sq"] = e["s3"].detach().cpu().clone()
             state[index[id(e["p"])]] = st
-        group = {"params": list(range(len(params))), "lr": float(o["arch_lr"])}
+        group = torch_optimizer(params, o).state_dict()["param_groups"][0]
         return {"state": state, "param_groups": [group]}
 
     def load_optimizer_state_dict(self, arch, sd):
+        """optimizers[net].load_state_dict(checkpoint['optimizer_par']) (core.py:114-121)."""
         net = self.nets[arch]
         params = list(net.parameters())
         index = {id(p): i for i, p in enumerate(params)}
@@ -1779,14 +1791,40 @@ class Engine:
                 continue
             if "square_avg" in st:
                 e["s1"].copy_(st["square_avg"])
+            if "grad_avg" in st and e["s2"] is not None:
+                e["s2"].copy_(st["grad_avg"])
             if "exp_avg" in st:
                 e["s1"].copy_(st["exp_avg"])
                 e["s2"].copy_(st["exp_avg_sq"])
+            if "max_exp_avg_sq" in st and e["s3"] is not None:
+                e["s3"].copy_(st["max_exp_avg_sq"])
             if st.get("momentum_buffer") is not None:
                 (e["s3"] if e["s3"] is not None else e["s1"]).copy_(st["momentum_buffer"])
+                e["has_buf"] = True       # torch SGD: a loaded buffer is continued, not reset
             if "step" in st:
                 e["step"] = int(float(st["step"]))
         self._upload_opt_desc(step_inc=1)
+
+
+def torch_optimizer(params, o):
+    """The torch.optim object utils.optimizer_init (utils.py:1833-1881) builds for cfg section o."""
+    lr = float(o["arch_lr"])
+    kind = o["arch_opt"]
+    if kind == "sgd":
+        return torch.optim.SGD(params, lr=lr, momentum=float(o["opt_momentum"]),
+                               weight_decay=float(o["opt_weight_decay"]),
+                               dampening=float(o["opt_dampening"]),
+                               nesterov=_b(o["opt_nesterov"]))
+    if kind == "adam":
+        return torch.optim.Adam(params, lr=lr, betas=[float(v) for v in o["opt_betas"].split(",")],
+                                eps=float(o["opt_eps"]), weight_decay=float(o["opt_weight_decay"]),
+                                amsgrad=_b(o["opt_amsgrad"]))
+    if kind == "rmsprop":
+        return torch.optim.RMSprop(params, lr=lr, momentum=float(o["opt_momentum"]),
+                                   alpha=float(o["opt_alpha"]), eps=float(o["opt_eps"]),
+                                   centered=_b(o["opt_centered"]),
+                                   weight_decay=float(o["opt_weight_decay"]))
+    raise NotImplementedError("arch_opt=%s" % kind)
 
 
 class ModuleRunner:

@@ -4,6 +4,7 @@ Option names and values follow the reference's cfg schema (proto/MLP.proto, prot
 proto/LSTM.proto plus the CGS keys read at neural_networks.py:98-131, 490-529).
 """
 import configparser
+import os
 
 _TMP = "/tmp"
 
@@ -112,3 +113,73 @@ PLAIN_CASES = [("mingru_bidir", "minimalGRU", MINGRU_DEF, 7, 3, 20, 33),
                ("rnn_uni_nobn", "RNN", dict(RNN_DEF, rnn_bidir="False",
                                             rnn_use_batchnorm="False,False", rnn_act="tanh,relu",
                                             rnn_orthinit="False"), 6, 2, 12, 36)]
+
+
+# run_nn chunk-lifecycle golden cases (make_golden.gen_run_nn / tests/test_gpu_run_nn_parity.py)
+RUN_NN_CASES = ("mlp", "ligru", "lstm_quant")
+
+
+def run_nn_cfg(d, name, to_do, scp, case, pretrain=None, counts="none"):
+    """A chunk cfg in the reference's schema (what utils.create_chunks writes) for the run_nn
+    golden case `case`; pretrain: {section: pkl path}."""
+    cfg = configparser.ConfigParser()
+    cfg["exp"] = {"seed": "2234", "out_folder": d, "use_cuda": "False", "multi_gpu": "False",
+                  "to_do": to_do, "out_info": os.path.join(d, name + ".info"),
+                  "save_gpumem": "False", "production": "False", "run_nn_script": "run_nn.py"}
+    seq = case != "mlp"
+    cfg["batches"] = {"batch_size_train": "4" if seq else "16",
+                      "batch_size_valid": "4" if seq else "16",
+                      "max_seq_length_train": "30", "max_seq_length_valid": "1000"}
+    cfg["data_chunk"] = {
+        "fea": "fea_name=fmllr\nfea_lst=%s\nfea_opts=\ncw_left=2\ncw_right=2\n" % scp,
+        "lab": "lab_name=lab_cd\nlab_folder=%s\nlab_opts=ali-to-pdf\n\n"
+               "lab_name=lab_mono\nlab_folder=%s\nlab_opts=ali-to-phones --per-frame=true\n"
+               % (scp + ".ali", scp + ".ali")}
+    common = dict(arch_library="neural_networks", arch_freeze="False", out_folder=d,
+                  arch_pretrain_file="none", use_cuda="False")
+    if case == "mlp":
+        body = dict(MLP_DEF, **common, arch_name="MLP_layers1", arch_class="MLP",
+                    arch_seq_model="False", dnn_lay="64,64", dnn_act="relu,relu",
+                    dnn_drop="0.0,0.0", dnn_use_batchnorm="True,True",
+                    dnn_use_laynorm="False,False", param_quant="8,8", mlp_prune_perc="70,70",
+                    arch_lr="0.08", arch_opt="sgd", opt_momentum="0.5", opt_weight_decay="0.0",
+                    opt_dampening="0.0", opt_nesterov="False")
+    elif case == "ligru":
+        body = dict(LIGRU_DEF, **common, arch_name="RNN_layers", arch_class="liGRU",
+                    arch_seq_model="True", ligru_lay="24,24", arch_lr="0.0016", arch_opt="rmsprop",
+                    opt_momentum="0.0", opt_alpha="0.95", opt_eps="1e-8", opt_centered="False",
+                    opt_weight_decay="0.0")
+    else:
+        body = dict(LSTM_DEF, **common, arch_name="RNN_layers", arch_class="LSTM",
+                    arch_seq_model="True", lstm_lay="24,24", lstm_quant="True",
+                    lstm_quant_inp="True", arch_lr="0.0016", arch_opt="rmsprop",
+                    opt_momentum="0.0", opt_alpha="0.95", opt_eps="1e-8", opt_centered="False",
+                    opt_weight_decay="0.0")
+    head = dict(MLP_DEF, **common, arch_name="MLP_layers2", arch_class="MLP",
+                arch_seq_model="False", dnn_lay="48", dnn_act="softmax",
+                dnn_use_batchnorm="False", arch_lr="0.0004", arch_opt="rmsprop",
+                opt_momentum="0.0", opt_alpha="0.95", opt_eps="1e-8", opt_centered="False",
+                opt_weight_decay="0.0")
+    mono = dict(head, arch_name="MLP_layers3", dnn_lay="8", arch_opt="adam", opt_betas="0.9,0.999",
+                opt_eps="1e-8", opt_weight_decay="0.0", opt_amsgrad="False", arch_lr="0.001")
+    for sec, a in (("architecture1", body), ("architecture2", head), ("architecture3", mono)):
+        cfg[sec] = a
+        cfg[sec]["to_do"] = to_do
+        if pretrain:
+            cfg[sec]["arch_pretrain_file"] = pretrain[sec]
+    b = body["arch_name"]
+    cfg["model"] = {"model": "out_dnn1=compute(%s,fmllr)\n"
+                             "out_dnn2=compute(MLP_layers2,out_dnn1)\n"
+                             "out_dnn3=compute(MLP_layers3,out_dnn1)\n"
+                             "loss_mono=cost_nll(out_dnn3,lab_mono)\n"
+                             "loss_mono_w=mult_constant(loss_mono,1.0)\n"
+                             "loss_cd=cost_nll(out_dnn2,lab_cd)\n"
+                             "loss_final=sum(loss_cd,loss_mono_w)\n"
+                             "err_final=cost_err(out_dnn2,lab_cd)" % b}
+    cfg["forward"] = {"forward_out": "out_dnn2", "normalize_posteriors": "True",
+                      "normalize_with_counts_from": counts, "save_out_file": "True",
+                      "require_decoding": "True"}
+    path = os.path.join(d, name + ".cfg")
+    with open(path, "w") as f:
+        cfg.write(f)
+    return path

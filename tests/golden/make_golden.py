@@ -7,6 +7,8 @@ source or bytecode is copied.  Shims used (all monkeypatches of *this* process o
   * torch.Tensor.cuda -> identity           (reference hard-codes .cuda(), e.g. sparsity.py:1045)
   * hcgs.conn_mat(...) -> for_test=True path (hcgs.py:134-137 returns numpy instead of .to("cuda"))
   * data_io.read_mat_ark / read_vec_int_ark -> synthetic dicts  (Kaldi binaries are absent)
+  * neural_networks.liGRU.{prune, guided_hcgs, if_pattern} = False (class attributes core.run_nn
+    reads and the reference's liGRU never defines; only for the run_nn golden cases)
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
 """
@@ -33,7 +35,8 @@ import utils              # noqa: E402
 from sparsity import sparsity  # noqa: E402
 
 sys.path.insert(0, OUT)
-from cases import (LIGRU_DEF, LSTM_DEF, MLP_DEF, build_mlp_config)  # noqa: E402,F401
+from cases import (LIGRU_DEF, LSTM_DEF, MLP_DEF, RUN_NN_CASES, build_mlp_config,  # noqa: E402,F401
+                   run_nn_cfg)
 
 _TMP = tempfile.mkdtemp(prefix="pkc_golden_")
 _orig_conn_mat = hcgs.conn_mat
@@ -389,12 +392,85 @@ def gen_ark():
     np.savez_compressed(os.path.join(OUT, "post_inputs.npz"), counts=counts, m0=mats[0], m1=mats[1])
 
 
+# ----------------------------------------------------------------------------------------------
+# G9: the reference's own core.run_nn over a chunk lifecycle (train ck0 -> train ck1 resumed from
+# the reference-written .pkl -> valid -> forward ark), on CPU with the Kaldi reads shimmed
+# ----------------------------------------------------------------------------------------------
+def gen_run_nn(case):
+    import core
+    out = {}
+    rs = np.random.RandomState({"mlp": 41, "ligru": 42, "lstm_quant": 43}[case])
+    data = {}
+    for tag, n in (("ck0", 14), ("ck1", 14)):
+        names, fea, cd, mono = synth_utts(rs, n, 12, 40, n_cd=48, n_mono=8)
+        data[tag] = (fea, cd, mono)
+        pack_dict(tag + "_fea", fea, out)
+        pack_dict(tag + "_cd", cd, out)
+        pack_dict(tag + "_mono", mono, out)
+    counts = rs.randint(1, 500, size=48)
+    out["counts"] = counts
+    d = tempfile.mkdtemp(prefix="pkc_runnn_")
+    cpath = os.path.join(d, "counts")
+    with open(cpath, "w") as f:
+        f.write("[ " + " ".join(str(int(c)) for c in counts) + " ]\n")
+
+    def fake_read_mat_ark(spec, output_folder):
+        tag = spec.split("scp:")[1].split()[0]
+        for k, v in data[os.path.basename(tag)][0].items():
+            yield k, v
+
+    def fake_read_vec_int_ark(spec, output_folder):
+        tag = os.path.basename(spec.split("gunzip -c ")[1].split("/ali*")[0]).replace(".ali", "")
+        src = data[tag][2] if "phones" in spec else data[tag][1]
+        for k, v in src.items():
+            yield k, v
+
+    data_io.read_mat_ark = fake_read_mat_ark
+    data_io.read_vec_int_ark = fake_read_vec_int_ark
+    # the reference's liGRU lacks the .prune / .guided_hcgs / .if_pattern attributes core.run_nn
+    # reads (core.py:123, 299, 304): run_nn raises AttributeError on any liGRU cfg.  Shim them as
+    # class attributes with the value every other architecture has when the feature is off
+    for attr in ("prune", "guided_hcgs", "if_pattern"):
+        if not hasattr(neural_networks.liGRU, attr):
+            setattr(neural_networks.liGRU, attr, False)
+    secs = ("architecture1", "architecture2", "architecture3")
+    pk0 = {s: os.path.join(d, "train_ck0_%s.pkl" % s) for s in secs}
+    pk1 = {s: os.path.join(d, "train_ck1_%s.pkl" % s) for s in secs}
+    c_tr0 = run_nn_cfg(d, "train_ck0", "train", "ck0", case)
+    c_tr1 = run_nn_cfg(d, "train_ck1", "train", "ck1", case, pretrain=pk0)
+    c_va = run_nn_cfg(d, "valid", "valid", "ck0", case, pretrain=pk1)
+    c_fw = run_nn_cfg(d, "forward", "forward", "ck0", case, pretrain=pk1, counts=cpath)
+    nxt, pats, pms = core.run_nn(None, None, None, None, None, None, c_tr0, True, c_tr1)
+    nxt, pats, pms = core.run_nn(*nxt, c_tr1, False, c_va, patterns=pats, pattern_masks=pms)
+    nxt, pats, pms = core.run_nn(*nxt, c_va, False, c_fw, patterns=pats, pattern_masks=pms)
+    core.run_nn(*nxt, c_fw, False, c_fw, patterns=pats, pattern_masks=pms)
+    for tag in ("train_ck0", "train_ck1", "valid"):
+        info = configparser.ConfigParser()
+        info.read(os.path.join(d, tag + ".info"))
+        out["info_" + tag] = np.array([float(info["results"]["loss"]), float(info["results"]["err"])])
+    sub = os.path.join(OUT, "run_nn_" + case)
+    os.makedirs(sub, exist_ok=True)
+    import shutil
+    for s in secs:       # the reference-written checkpoints: ck0 is the resume input of the test
+        shutil.copy(pk0[s], os.path.join(sub, "train_ck0_%s.pkl" % s))
+        ck = torch.load(pk1[s], weights_only=True)
+        for k, v in ck["model_par"].items():
+            out["ck1/%s/model/%s" % (s, k)] = v.numpy().copy()
+        for pi, st in ck["optimizer_par"]["state"].items():
+            for k, v in st.items():
+                if torch.is_tensor(v):
+                    out["ck1/%s/opt/%d/%s" % (s, pi, k)] = v.numpy().copy()
+    shutil.copy(os.path.join(d, "forward_out_dnn2_to_decode.ark"),
+                os.path.join(sub, "forward_out_dnn2_to_decode.ark"))
+    np.savez_compressed(os.path.join(sub, "expected.npz"), **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:          # e.g. `make_golden.py mlp:l1 mlp:l2 mlp:gl`
         for a in sys.argv[1:]:
             kind, _, v = a.partition(":")
             {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru(),
-             "cm": lambda _v: gen_cm()}[kind](v)
+             "cm": lambda _v: gen_cm(), "run_nn": gen_run_nn}[kind](v)
         sys.exit(0)
     gen_loader()
     gen_hcgs()
@@ -406,5 +482,7 @@ if __name__ == "__main__":
     gen_gru()
     gen_cm()
     gen_ark()
+    for c in RUN_NN_CASES:
+        gen_run_nn(c)
     total = sum(os.path.getsize(os.path.join(OUT, f)) for f in os.listdir(OUT))
     print("golden fixtures written to %s (%.1f KB)" % (OUT, total / 1024))
