@@ -682,3 +682,37 @@ def make_optimizer(params, o):
                                 eps=float(o["opt_eps"]), weight_decay=float(o["opt_weight_decay"]),
                                 amsgrad=_b(o["opt_amsgrad"]))
     raise ValueError(kind)
+
+
+def _bf16(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+class _BF16Linear(torch.autograd.Function):
+    """F.linear with every matmul operand rounded to bf16 (round-to-nearest-even) and fp32
+    accumulation, in all three products of the layer's training step (Y = X W^T + b,
+    dX = dY W, dW = dY^T X): the arithmetic of pkc's bf16 mode (pkc_gemm PREC_BF16), used as the
+    tight reference for the bench headline's precision.  Not a reference function: the reference
+    computes these products in fp32 (neural_networks.py:306-317)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        y = _bf16(x) @ _bf16(w).t()
+        return y + b if b is not None else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        g = _bf16(dy)
+        dx = g @ _bf16(w)
+        dw = g.t() @ _bf16(x)
+        return dx, dw, (dy.sum(0) if ctx.has_b else None)
+
+
+def use_bf16_matmuls(net):
+    """Route every nn.Linear of an oracle MLP through _BF16Linear."""
+    for lin in net.wx:
+        lin.forward = (lambda x, _l=lin: _BF16Linear.apply(x, _l.weight, _l.bias))
+    return net

@@ -225,8 +225,8 @@ def test_engine_graph_replay_equals_eager():
         else:
             for _ in range(4):
                 eng.train_step()
-        # every architecture: the one-GPU steps update W in the dW epilogue (PKC_OP_GEMM_OPT),
-        # the data-parallel ones in the separate optimizer pass — bit-identical
+        # the one-GPU steps spread the optimizer updates over the backward's grouped launches,
+        # the data-parallel ones run them in a separate pass after the all-reduce — bit-identical
         res.append((eng.chunk_totals(), {a + "/" + k: v.cpu() for a in nets
                                          for k, v in nets[a].state_dict().items()}))
     for other in res[1:]:
@@ -324,3 +324,83 @@ def test_engine_sparsity_vs_oracle(variant):
                     assert float((v == 0).float().mean()) >= percs[a][i] / 100 - 0.01
             np.testing.assert_allclose(v.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-6,
                                        err_msg="%s %s" % (a, k))
+
+
+@pytest.mark.parametrize("steps", [3])
+def test_engine_c2_bf16_vs_oracle(steps):
+    """BASELINE C2 (the bench headline): the C1 model at B = 128 with bf16 matmul operands
+    (PREC_BF16: every operand of Y = X W^T, dX = dY W, dW = dY^T X rounded to bf16 RNE, fp32
+    accumulation, fp32 master weights / BN / loss / optimizer).
+
+    (i) the first step's posteriors within 1e-4 relative of the oracle with the same bf16
+        rounding of its matmul operands (oracle.nets.use_bf16_matmuls): only the fp32 summation
+        order differs (measured 5.6e-5); vs the fp32 oracle (the reference's arithmetic) the bf16
+        rounding itself shows: 1.5e-4, held to 1e-3;
+    (ii) later steps: this model's training is chaotic at init on random labels — the heads'
+        RMSprop makes its first steps lr * g / sqrt((1 - alpha) g^2), full-size sign steps as
+        large as the init weights — so ANY perturbation grows: the fp32 oracle against itself
+        with the input scaled by (1 + 1e-6 noise) differs by 2e-4 / 6e-4 / 7e-3 after steps
+        1 / 2 / 3, and the bf16 oracle against the fp32 oracle by 7.7e-3 / 0.12 / 0.20 (measured on
+        the CPU).  Steps 1-2 are therefore held to the bf16-vs-fp32 spread (0.15 relative on the
+        log-posteriors) and the loss to 1e-3 relative of both oracles.
+    """
+    from oracle import nets as ON
+    from oracle import run as OR
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config(drop="0.15")
+    B = 128
+    rs = np.random.RandomState(5)
+    X = rs.randn(B * steps, 440).astype(np.float32)
+    lab = np.stack([rs.randint(0, 1928, B * steps), rs.randint(0, 48, B * steps)], 1).astype(np.int32)
+    keeps = {"MLP_layers1.%d" % i: torch.from_numpy((rs.rand(B, 1024) > 0.15).astype(np.uint8))
+             for i in range(5)}
+    nets, opts = build_nets(cfg, C1_DIMS)
+    refs = {}
+    for mode in ("bf16", "fp32"):
+        onets, _ = build_nets(cfg, C1_DIMS, cls=ON.MLP)
+        for a in nets:
+            onets[a].load_state_dict(nets[a].state_dict())
+            onets[a].train()
+            if mode == "bf16":
+                ON.use_bf16_matmuls(onets[a])
+        oopt = {a: ON.make_optimizer(onets[a].parameters(), cfg[s]) for s, a in
+                zip(("architecture1", "architecture2", "architecture3"), nets)}
+        lines = OR.parse_model(cfg["model"]["model"])
+        dm = [keeps["MLP_layers1.%d" % i].float() for i in range(5)]
+        refs[mode] = []
+        for s in range(steps):
+            inp = torch.from_numpy(np.concatenate([X[s * B:(s + 1) * B],
+                                                   lab[s * B:(s + 1) * B].astype(np.float32)], 1))
+            body = onets["MLP_layers1"]
+            f = body.forward
+            body.forward = lambda x, _f=f: _f(x, drop_masks=dm)
+            outs = OR.train_step(lines, onets, oopt, {a: False for a in nets}, {"fmllr": (0, 440)},
+                                 {"lab_cd": 440, "lab_mono": 441}, inp)
+            body.forward = f
+            refs[mode].append((outs["loss_final"].item(), outs["out_dnn2"].detach().clone()))
+    for n in nets.values():
+        n.to(DEV).train()
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                 ["lab_cd", "lab_mono"], batch=B, seed=1, prec=L.PREC_BF16,
+                 drop_keep_in={k: v.to(DEV) for k, v in keeps.items()})
+    eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), B * steps)
+    head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
+    for s in range(steps):
+        eng.train_step()
+        loss, _ = eng.loss_values()
+        post = head.out.view(B, -1).cpu()
+        errs = {}
+        for mode, ref in refs.items():
+            r = ref[s][1]
+            errs[mode] = ((post - r).abs() / r.abs().clamp_min(1e-3)).max().item()
+        print("step %d: posterior max rel err vs bf16 oracle %.3g, vs fp32 oracle %.3g; loss %.6f "
+              "(bf16 oracle %.6f, fp32 oracle %.6f)" % (s, errs["bf16"], errs["fp32"], loss,
+                                                        refs["bf16"][s][0], refs["fp32"][s][0]))
+        if s == 0:
+            assert errs["bf16"] < 1e-4, "vs bf16 oracle %.3g" % errs["bf16"]
+            assert errs["fp32"] < 1e-3, "vs fp32 oracle %.3g" % errs["fp32"]
+        else:
+            assert max(errs.values()) < 0.15, "step %d %s" % (s, errs)
+        np.testing.assert_allclose(loss, refs["bf16"][s][0], rtol=1e-3)
+        np.testing.assert_allclose(loss, refs["fp32"][s][0], rtol=1e-3)
