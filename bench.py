@@ -174,6 +174,113 @@ def batch_sweep(prec, batches=(1024, 4096), steps=30):
     return out
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` started as one process (no WORLD_SIZE): run N ranks through
+    torch.distributed.run as child processes — before this process touches the GPU — and return
+    their exit status (rank 0 prints the line)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def parity_leg(prec, batch, seed=2234):
+    """Posterior error of the measured configuration (BASELINE metric: "posterior max-abs-err vs
+    ref"): the engine's first training step on one batch of the C2 model — same initial weights,
+    same injected dropout masks — against the oracle (the reference's algorithm in fp32 on the
+    CPU).  Part of the CPU-baseline leg: the oracle is the checker here, never the thing timed.
+    Returns max abs / max relative error of the cd head's log-posteriors (the first step: later
+    steps of this model at init are chaotic, tests/test_gpu_mlp.py::test_engine_c2_bf16_vs_oracle)."""
+    from oracle import nets as ON
+    from oracle import run as OR
+    from pkc.engine import Engine, parse_model
+    from pkc.neural_networks import MLP
+    cfg = c1_cfg()
+    torch.manual_seed(seed)
+    nets, onets, opts, oopt = {}, {}, {}, {}
+    for sec, inp in DIMS:
+        o = cfg[sec]
+        a = o["arch_name"]
+        nets[a] = MLP(o, inp)
+        onets[a] = ON.MLP(o, inp)
+        onets[a].load_state_dict(nets[a].state_dict())
+        onets[a].train()
+        nets[a].cuda().train()
+        opts[a] = o
+        oopt[a] = ON.make_optimizer(onets[a].parameters(), o)
+    rs = np.random.RandomState(seed)
+    X = rs.randn(batch, 440).astype(np.float32)
+    lab = np.stack([rs.randint(0, 1928, batch), rs.randint(0, 48, batch)], 1).astype(np.int32)
+    keeps = {"MLP_layers1.%d" % i: torch.from_numpy((rs.rand(batch, 1024) > 0.15).astype(np.uint8))
+             for i in range(5)}
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                 ["lab_cd", "lab_mono"], batch=batch, prec=prec, seed=1,
+                 drop_keep_in={k: v.cuda() for k, v in keeps.items()})
+    eng.bind_chunk(torch.from_numpy(X).cuda(), torch.from_numpy(lab).cuda(), batch)
+    eng.train_step()
+    head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
+    post = head.out.view(batch, -1).cpu().double()
+    inp = torch.from_numpy(np.concatenate([X, lab.astype(np.float32)], 1))
+    body = onets["MLP_layers1"]
+    f = body.forward
+    dm = [keeps["MLP_layers1.%d" % i].float() for i in range(5)]
+    body.forward = lambda x, _f=f: _f(x, drop_masks=dm)
+    outs = OR.train_step(OR.parse_model(cfg["model"]["model"]), onets, oopt,
+                         {a: False for a in onets}, {"fmllr": (0, 440)},
+                         {"lab_cd": 440, "lab_mono": 441}, inp)
+    ref = outs["out_dnn2"].detach().double()
+    d = (post - ref).abs()
+    return {"posterior_max_abs_err": float(d.max()),
+            "posterior_max_rel_err": float((d / ref.abs().clamp_min(1e-3)).max()),
+            "posterior_ref": "oracle fp32 (reference algorithm), first training step, B=%d" % batch}
+
+
+def time_steps(eng, steps, warmup, allreduce=None, world=1):
+    eng.train_steps(warmup, allreduce)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.train_steps(steps, allreduce)        # exactly `steps` batches
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = float(tt.item())
+    return dt
+
+
+def seq_entry(name, steps, warmup, with_cpu, cpu_seconds):
+    """A BASELINE sequence configuration measured like the headline: frames/s over `steps` timed
+    sentence batches, its roofline (max(F_alg / MFMA peak, B_alg / HBM peak) over the
+    measured time, fp32 — the parity precision — and the serial-step figure) and a CPU baseline."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_seq
+    r = bench_seq.run(name, steps=steps, warmup=warmup)
+    achieved = r["alg_tflops_per_s"]
+    peak = MFMA_PEAK_TFLOPS["fp32"]
+    out = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items() if k != "config"}
+    out["dtype"] = "fp32"
+    out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
+                       "unit": "TFLOP/s", "frac": round(achieved / peak, 5),
+                       "note": "algorithmic flops (W, U scaled by mask density, heads; x3 for "
+                               "training) over padded rows / measured step time; the recurrence "
+                               "is serial-latency-bound: see us_per_time_step_per_layer_fwd_bwd"}
+    if with_cpu:
+        out["cpu_baseline"] = bench_seq.cpu_baseline(name, seconds=cpu_seconds)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,6 +291,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-batch-sweep", action="store_true")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 value of the headline")
     ap.add_argument("--no-seq-configs", action="store_true",
                     help="skip the informational C3/C4/C5 sequence-model throughputs")
     ap.add_argument("--pmc-replay", type=int, default=0,
@@ -257,20 +365,7 @@ def main():
         print(json.dumps({"pmc_replay": dom_fn, "launches": nl * args.pmc_replay}), flush=True)
         return
     eng.capture(split_optimizer=world > 1)
-    eng.train_steps(args.warmup, allreduce)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.train_steps(args.steps, allreduce)        # exactly args.steps batches
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], device="cuda")
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = time_steps(eng, args.steps, args.warmup, allreduce, world)
     loss_sum, err_sum = eng.chunk_totals()
     n_done = args.warmup + args.steps
 
@@ -282,19 +377,32 @@ def main():
     per_launch_nb = d["bytes"] / cnt
     avg_ms = dom_us / cnt * 1e-3
     traffic = pmc_traffic(label)
+    del eng
+    torch.cuda.empty_cache()
+    extra = {}
+    if rank == 0 and world == 1 and args.prec == "bf16" and not args.no_fp32:
+        # the same configuration in fp32 (the reference's precision), same step count
+        e32, _, _, _ = build(_lib.PREC_FP32, args.batch, 0, 1)
+        e32.capture()
+        extra["fp32_value"] = round(args.steps * args.batch / time_steps(e32, args.steps,
+                                                                          args.warmup), 1)
+        del e32
+        torch.cuda.empty_cache()
     sweep = {}
     if rank == 0 and world == 1 and not args.no_batch_sweep:
         sweep = batch_sweep(prec)
     seq = {}
     if rank == 0 and world == 1 and not args.no_seq_configs:
-        # BASELINE configs C3-C5 (informational; scripts/bench_seq.py has the details)
-        sys.path.insert(0, os.path.join(ROOT, "scripts"))
-        import bench_seq
-        for c in ("c3", "c4", "c5"):
-            r = bench_seq.run(c, steps=4, warmup=1)
-            seq[c] = {k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()
-                      if k != "config"}
+        # BASELINE configs C3-C5: C3 (the largest single-GPU config) measured like the headline,
+        # C4 / C5 informational
+        seq["c3"] = seq_entry("c3", max(20, args.steps), 3, not args.no_cpu_baseline,
+                              args.cpu_seconds)
+        torch.cuda.empty_cache()
+        for c in ("c4", "c5"):
+            seq[c] = seq_entry(c, 8, 2, False, 0)
             torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        extra.update(parity_leg(prec, args.batch))
     if rank == 0:
         is_gemm = "gemm" in label
         # MFMA-bound only where the launch's arithmetic intensity exceeds the machine balance
@@ -334,10 +442,11 @@ def main():
             "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
                                   sorted(agg.items(), key=lambda kv: -kv[1][1])},
             "batch_sweep_frames_per_s": sweep,
-            "sequence_configs_frames_per_s": seq,
+            "sequence_configs": seq,
             "chunk_prep_s": round(prep_s, 3),
             "mean_loss": round(loss_sum / max(1, n_done), 4),
         }
+        res.update(extra)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.batch, args.cpu_seconds)
         print(json.dumps(res), flush=True)
@@ -346,4 +455,13 @@ def main():
 
 
 if __name__ == "__main__":
+    _a = [a for a in sys.argv[1:]]
+    _n = 1
+    for i, a in enumerate(_a):
+        if a == "--gpus" and i + 1 < len(_a):
+            _n = int(_a[i + 1])
+        elif a.startswith("--gpus="):
+            _n = int(a.split("=", 1)[1])
+    if _n > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(_n))
     main()

@@ -102,6 +102,25 @@ def build(cfg_name, seed=2234):
     return eng, nets, B
 
 
+def alg_flops_per_row(nets):
+    """Algorithmic training flops per padded (T x B x direction) row of a step, SURVEY 8d: the
+    W and U products of every recurrent layer scaled by their HCGS / pattern mask density, the
+    heads' products; x3 for forward + the two backward products.  Returns (flops per row of the
+    first recurrent layer's T*B*dirs rows, flops per frame row of the heads)."""
+    specs = nets["rnn"].layer_specs()
+    per_dir_row = 0.0
+    K = nets["rnn"].input_dim if hasattr(nets["rnn"], "input_dim") else 440
+    for sp in specs:
+        H = sp["H"]
+        G = len(sp["W"])
+        dW = float(sp["Wmask"].float().mean()) if sp.get("Wmask") is not None else 1.0
+        dU = float(sp["Umask"].float().mean()) if sp.get("Umask") is not None else 1.0
+        per_dir_row += 3 * 2 * G * H * (K * dW + H * dU)
+        K = 2 * H if sp["bidir"] else H
+    head = 3 * 2 * (nets["head"].out_dim + nets["mono"].out_dim) * nets["rnn"].out_dim
+    return per_dir_row, head
+
+
 def run(cfg_name, steps, warmup):
     eng, nets, B = build(cfg_name)
     rng = random.Random(7)
@@ -123,11 +142,65 @@ def run(cfg_name, steps, warmup):
         tsteps += int(b[3])
     torch.cuda.synchronize()
     dt = time.time() - t0
-    nl = len(nets["rnn"].layer_specs())
+    specs = nets["rnn"].layer_specs()
+    nl = len(specs)
+    dirs = 2 if specs[0]["bidir"] else 1
+    per_row, head = alg_flops_per_row(nets)
+    flops = tsteps * B * (dirs * per_row + head)          # padded rows, as the reference computes
     return {"config": cfg_name, "batch_sentences": B, "steps": steps,
             "frames_per_s": frames / dt, "ms_per_step": dt * 1e3 / steps,
             "us_per_time_step_per_layer_fwd_bwd": dt * 1e6 / (tsteps * nl),
-            "mean_T": tsteps / steps}
+            "mean_T": tsteps / steps, "alg_tflops_per_s": flops / dt / 1e12,
+            "alg_gflop_per_step": flops / steps / 1e9}
+
+
+def cpu_baseline(cfg_name, seconds=10.0, T=120):
+    """The oracle's eager torch-CPU restatement of the same training step (the reference's
+    per-time-step algorithm, neural_networks.py:1523-1599 / 1077-1097) on the host cores: a
+    bounded sample of sentence batches of length T."""
+    import configparser
+
+    from oracle import nets as ON
+    from oracle import run as OR
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    threads = min(threads, os.cpu_count())
+    torch.set_num_threads(threads)
+    cls, ropts, B = rec_opts(cfg_name)
+    cfg = configparser.ConfigParser()
+    cfg["a1"] = dict(ropts, arch_name="rnn", **OPT)
+    head = dict(dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False", arch_name="head",
+                dnn_lay="1928", dnn_drop="0.0", dnn_use_batchnorm="False", dnn_use_laynorm="False",
+                dnn_act="softmax", **dict(OPT, arch_lr="0.0004"))
+    cfg["a2"] = head
+    cfg["a3"] = dict(head, arch_name="mono", dnn_lay="48")
+    torch.manual_seed(0)
+    np.random.seed(0)
+    rnn = getattr(ON, cls)(cfg["a1"], 440)
+    nets = {"rnn": rnn, "head": ON.MLP(cfg["a2"], rnn.out_dim), "mono": ON.MLP(cfg["a3"], rnn.out_dim)}
+    opts = {k: ON.make_optimizer(nets[k].parameters(), cfg[s]) for k, s in
+            (("rnn", "a1"), ("head", "a2"), ("mono", "a3"))}
+    for n in nets.values():
+        n.train()
+    lines = OR.parse_model("o1=compute(rnn,fea)\no2=compute(head,o1)\no3=compute(mono,o1)\n"
+                           "lm=cost_nll(o3,lab_mono)\nlmw=mult_constant(lm,1.0)\n"
+                           "lc=cost_nll(o2,lab_cd)\nloss_final=sum(lc,lmw)\n"
+                           "err_final=cost_err(o2,lab_cd)")
+    rs = np.random.RandomState(1)
+    inp = torch.from_numpy(np.concatenate([rs.randn(T, B, 440), rs.randint(0, 48, (T, B, 2))],
+                                          2).astype(np.float32))
+    seq = {"rnn": True, "head": False, "mono": False}
+    OR.train_step(lines, nets, opts, seq, {"fea": (0, 440)}, {"lab_cd": 440, "lab_mono": 441},
+                  inp, T, B)
+    n, t0 = 0, time.time()
+    while time.time() - t0 < seconds:
+        OR.train_step(lines, nets, opts, seq, {"fea": (0, 440)}, {"lab_cd": 440, "lab_mono": 441},
+                      inp, T, B)
+        n += 1
+    dt = time.time() - t0
+    return {"value": round(n * T * B / dt, 1), "unit": "frames/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d training steps of %s (B=%d sentences x T=%d frames, oracle restatement, "
+                      "torch-CPU eager, %d threads, %.1f s)" % (n, cfg_name, B, T, threads, dt)}
 
 
 def main():
