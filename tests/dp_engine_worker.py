@@ -1,0 +1,87 @@
+"""Worker of tests/test_gpu_dp.py (not collected by pytest): one rank of a chunk-level
+data-parallel Engine run, launched by torch.distributed.run with the gloo backend (several ranks
+sharing one GPU).  Each rank trains its half of every global batch with Engine(grad_scale=1/R)
+and the bucketed all-reduce of pkc.dist.GradAllReduce (the first bucket overlapping the rest of the
+backward), eagerly or replayed from the split hipGraphs (mode "graph"), and saves its state.
+
+argv: out_dir mode steps B_per_rank
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"), os.path.join(ROOT, "tests"),
+          os.path.join(ROOT, "tests", "golden")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def dp_config():
+    """Body 40 -> 64 (LayerNorm, no BatchNorm: the local batch statistics of BN differ per rank),
+    SGD; cd head 32 (RMSprop), mono head 8 (RMSprop); dropout 0."""
+    from cases import build_mlp_config
+    cfg = build_mlp_config("plain")
+    cfg["architecture1"].update(dnn_lay="64,64", dnn_use_batchnorm="False,False",
+                                dnn_use_laynorm="True,False", dnn_act="relu,tanh")
+    cfg["architecture2"].update(dnn_lay="32")
+    return cfg
+
+
+DIMS = (("architecture1", 40), ("architecture2", 64), ("architecture3", 64))
+
+
+def data(steps, B_total):
+    rs = np.random.RandomState(3)
+    X = rs.randn(steps * B_total, 40).astype(np.float32)
+    lab = np.stack([rs.randint(0, 32, steps * B_total), rs.randint(0, 8, steps * B_total)],
+                   1).astype(np.int32)
+    return X, lab
+
+
+def build(cfg, world, B, X, lab):
+    from pkc.engine import Engine, parse_model
+    from pkc.neural_networks import MLP
+    torch.manual_seed(2234)
+    np.random.seed(2234)
+    nets, opts = {}, {}
+    for sec, inp in DIMS:
+        o = cfg[sec]
+        nets[o["arch_name"]] = MLP(o, inp).cuda().train()
+        opts[o["arch_name"]] = o
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 40)},
+                 ["lab_cd", "lab_mono"], batch=B, seed=1, grad_scale=1.0 / world)
+    eng.bind_chunk(torch.from_numpy(X).cuda(), torch.from_numpy(lab).cuda(), X.shape[0])
+    return eng, nets
+
+
+def main():
+    out, mode, steps, B = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    from pkc import dist as DP
+    dist.init_process_group("gloo")
+    rank, world = DP.world()
+    torch.cuda.set_device(0)
+    X, lab = data(steps, B * world)
+    # rank r's rows of global batch s: [s*B*R + r*B, +B) — laid out so the engine's batch counter
+    # walks them in order
+    rows = np.concatenate([np.arange(s * B * world + rank * B, s * B * world + (rank + 1) * B)
+                           for s in range(steps)])
+    eng, nets = build(dp_config(), world, B, X[rows], lab[rows])
+    ar = DP.GradAllReduce()
+    if mode == "graph":
+        assert eng.capture(split_optimizer=True)
+        assert eng.graph_tail is not None        # bucketed: two backward graphs
+    for _ in range(steps):
+        eng.train_step(ar)
+    torch.cuda.synchronize()
+    loss, err = DP.sum_scalars(eng.chunk_totals())
+    sd = {a + "/" + k: v.detach().cpu().numpy() for a in nets for k, v in nets[a].state_dict().items()}
+    np.savez(os.path.join(out, "rank%d_%s.npz" % (rank, mode)), loss=loss / world, calls=ar.calls,
+             **sd)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

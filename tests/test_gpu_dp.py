@@ -1,0 +1,57 @@
+"""Chunk-level data parallelism through the Engine (SURVEY 8e parity check): 2 ranks (gloo,
+sharing the one GPU; on a node the same code runs over RCCL) each train their half of every
+global batch with Engine(grad_scale = 1/2) and the bucketed, overlapped gradient all-reduce
+(pkc.dist.GradAllReduce) — eagerly and from the split hipGraphs — against one process training
+the full global batch.  No BatchNorm (per-rank batch statistics differ by design), dropout 0.
+
+Checked: the two replicas are bit-identical after every run; they equal the single-process
+full-batch training within fp32 summation-order tolerance; the summed loss equals the full-batch
+loss.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+STEPS, B = 3, 32
+
+
+def full_batch_reference():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dp_engine_worker as W
+    X, lab = W.data(STEPS, 2 * B)
+    eng, nets = W.build(W.dp_config(), 1, 2 * B, X, lab)
+    for _ in range(STEPS):
+        eng.train_step()
+    torch.cuda.synchronize()
+    loss, _ = eng.chunk_totals()
+    return loss, {a + "/" + k: v.detach().cpu().numpy() for a in nets
+                  for k, v in nets[a].state_dict().items()}
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_dp_engine_two_ranks_equal_full_batch(mode, tmp_path):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000 +
+                                                            (7 if mode == "graph" else 0)),
+           os.path.join(ROOT, "tests", "dp_engine_worker.py"), str(tmp_path), mode, str(STEPS),
+           str(B)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    g0 = np.load(os.path.join(tmp_path, "rank0_%s.npz" % mode))
+    g1 = np.load(os.path.join(tmp_path, "rank1_%s.npz" % mode))
+    assert int(g0["calls"]) == 2 * STEPS          # two buckets per step
+    loss, ref = full_batch_reference()
+    for k, v in ref.items():
+        np.testing.assert_array_equal(g0[k], g1[k], err_msg="replicas differ: " + k)
+        if k.endswith("num_batches_tracked"):
+            continue
+        np.testing.assert_allclose(g0[k], v, rtol=1e-4, atol=1e-6, err_msg=k)
+    np.testing.assert_allclose(float(g0["loss"]), loss, rtol=1e-5)

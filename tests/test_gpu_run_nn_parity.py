@@ -176,6 +176,21 @@ def test_run_nn_lifecycle_vs_reference(case, tmp_path):
                 assert float(st[int(pi)][name]) == float(g[key]), key
                 continue
             check(key, st[int(pi)][name].numpy(), g[key])
+        # pkc's checkpoint loads into the torch.optim optimizer the reference builds
+        # (utils.py:1833-1881) and that optimizer steps (every hyperparameter key present)
+        cfg = configparser.ConfigParser()
+        cfg.read(c_tr1)
+        import pkc.neural_networks as NN
+        from pkc.engine import torch_optimizer
+        o = cfg[s]
+        fin = {"architecture1": 200}.get(s, 48 if case == "ligru" else 24 if case != "mlp" else 64)
+        net = getattr(NN, o["arch_class"])(o, fin)
+        net.load_state_dict(got1["model_par"])
+        opt = torch_optimizer(list(net.parameters()), o)
+        opt.load_state_dict(got1["optimizer_par"])
+        for prm in net.parameters():
+            prm.grad = torch.ones_like(prm)
+        opt.step()
     bad = {k: "%.3g" % v[0] for k, v in errs.items() if not v[1]}
     print("worst checkpoint rel err %.3g" % max(v[0] for v in errs.values() if v[1] or True))
     assert not bad, "checkpoint tensors off the reference: %s" % bad
