@@ -6,6 +6,8 @@
   quantize_inp    quantized_modules.py:99-119 (dynamic per-tensor max-abs, ceil grid)
   prune           quantized_modules.py:15-28  (np.percentile over |W|, strict '>')
   apply_patterns  sparsity/sparsity.py:1112-1146 (conv2d score, ties select all, conv_transpose)
+  kmeans_patterns sparsity/sparsity.py:999-1049 (top-k tile candidates, sklearn KMeans, top-k of
+                  each centre); sklearn is the reference's own third-party dependency
 """
 import numpy as np
 import torch
@@ -87,6 +89,33 @@ def prune_mask(w, perc):
     a = np.abs(w.detach().cpu().numpy()).ravel()
     thr = np.percentile(a, perc)
     return (w.detach().abs() > float(thr)).float() if isinstance(w, torch.Tensor) else None
+
+
+def kmeans_patterns(w, pattern_num, pattern_shape, pattern_nnz, random_state=None):
+    """sparsity.py:999-1049 with numpy tiles: per ph x pw tile (row-major tile order, 1018-1020)
+    a {0,1} candidate keeping entries >= its nnz-th largest |w| (1021-1026); KMeans with
+    n_clusters = min(pattern_num, C(ph*pw, nnz)) (1004-1005, 1030) fitted on the candidates as
+    float64 (the reference hands sklearn a list of float32 rows); each centre keeps the last nnz
+    indices of torch's ascending sort (1036-1041: ties among equal centre entries resolve in
+    torch.sort's order, which a numpy stable argsort does not reproduce).  Returns (P, ph, pw)."""
+    import math
+
+    from sklearn.cluster import KMeans
+    ph, pw = pattern_shape
+    a = np.abs(np.asarray(w, dtype=np.float32))
+    nx, ny = (a.shape[0] - ph) // ph + 1, (a.shape[1] - pw) // pw + 1
+    cands = []
+    for i in range(nx):
+        for j in range(ny):
+            t = a[i * ph:(i + 1) * ph, j * pw:(j + 1) * pw].ravel()
+            thr = np.sort(t)[-pattern_nnz]
+            cands.append((t >= thr).astype(np.float64))
+    n = min(pattern_num, math.comb(ph * pw, pattern_nnz))
+    centres = KMeans(n_clusters=n, random_state=random_state).fit(np.array(cands)).cluster_centers_
+    out = np.zeros((n, ph * pw), dtype=np.float32)
+    for p, c in enumerate(centres):
+        out[p, torch.from_numpy(c).sort()[1][-pattern_nnz:].numpy()] = 1.0
+    return out.reshape(n, ph, pw)
 
 
 def apply_patterns(w, patterns):

@@ -89,6 +89,24 @@ class QLinear(nn.Module):
         return y
 
 
+def _pattern_search_opts(net, o):
+    """pattern_num / pattern_nnz / pattern_shape (neural_networks.py:115-124) for the KMeans
+    search; pattern_seed pins sklearn (the reference passes no random_state)."""
+    net.pattern_num = _lst(o, "pattern_num", int) if "pattern_num" in o else []
+    net.pattern_nnz = _lst(o, "pattern_nnz", int) if "pattern_nnz" in o else []
+    net.pattern_shape = _lst(o, "pattern_shape", int) if "pattern_shape" in o else [8, 8]
+    net.pattern_seed = int(o["pattern_seed"]) if "pattern_seed" in o else None
+
+
+def _pattern_set(net, w, i):
+    """The fixed set, or update_patterns' per-weight KMeans search (neural_networks.py:339-348,
+    1162-1172 -> sparsity.py:999-1049) on the weight as it stands at the first layer call."""
+    if net.pattern_kernels is not None:
+        return net.pattern_kernels
+    return M.kmeans_patterns(w, net.pattern_num[i], net.pattern_shape, net.pattern_nnz[i],
+                             random_state=net.pattern_seed)
+
+
 class MLP(nn.Module):
     def __init__(self, o, inp_dim):
         super().__init__()
@@ -147,6 +165,7 @@ class MLP(nn.Module):
             cur = n
         self.out_dim = cur
         self.if_pattern = _b(o["if_pattern"]) if "if_pattern" in o else False
+        _pattern_search_opts(self, o)
         self.pattern_kernels = None
         self.pattern_masks = None
 
@@ -163,9 +182,9 @@ class MLP(nn.Module):
         """neural_networks.py:263-272, 350-361: masks computed once (at the first layer call) from
         |W| of every layer, then every layer's W multiplied by its mask on every layer call."""
         if self.pattern_masks is None:
-            self.pattern_masks = [torch.from_numpy(M.apply_patterns(self.wx[i].weight.data.numpy(),
-                                                                    self.pattern_kernels))
-                                  for i in range(len(self.lay))]
+            ws = [self.wx[i].weight.data.numpy() for i in range(len(self.lay))]
+            self.pattern_masks = [torch.from_numpy(M.apply_patterns(w, _pattern_set(self, w, i)))
+                                  for i, w in enumerate(ws)]
         for i in range(len(self.lay)):
             self.wx[i].weight.data.mul_(self.pattern_masks[i])
 
@@ -501,6 +520,7 @@ class LSTM(_Rec):
         self.quant_inp = _b(o.get("lstm_quant_inp", "False"))
         self.prune = _b(o.get("lstm_prune", "False"))
         self.if_pattern = _b(o["if_pattern"]) if "if_pattern" in o else False
+        _pattern_search_opts(self, o)
         # the reference forces bidir = 0 in forward (:835) and crashes on layer 2 of a bidir cfg;
         # config C4's bidirectional LSTM follows the liGRU convention (shared W/U/BN, cat/flip)
         self.bidir = _b(o.get("lstm_bidir", "False"))
@@ -580,10 +600,10 @@ class LSTM(_Rec):
             self.pattern_masks = {}
             for g in self.GATES:
                 for nm in ("w%sx" % g, "u%sh" % g):
+                    ws = [getattr(self, nm)[i].weight.data.numpy() for i in range(len(self.lay))]
                     self.pattern_masks[nm] = [
-                        torch.from_numpy(M.apply_patterns(getattr(self, nm)[i].weight.data.numpy(),
-                                                          self.pattern_kernels))
-                        for i in range(len(self.lay))]
+                        torch.from_numpy(M.apply_patterns(w, _pattern_set(self, w, i)))
+                        for i, w in enumerate(ws)]
         for g in self.GATES:
             for nm in ("w%sx" % g, "u%sh" % g):
                 for i in range(len(self.lay)):

@@ -106,3 +106,32 @@ def guided_hcgs_mask(out_features, in_features, block_sizes, drop_ratios, w):
     m = np.zeros((out_features, in_features), dtype=np.float32)
     _guided_fill(m, wabs, list(zip(block_sizes, drop_ratios)))
     return m
+
+
+def kmeans_patterns(w, pattern_num, pattern_shape, pattern_nnz, random_state=None):
+    """Pattern-set search of sparsity.find_top_k_by_kmeans (sparsity.py:999-1049), host-side and
+    once per model like the reference: every non-overlapping ph x pw tile of |w| gives a {0,1}
+    candidate keeping its entries >= the tile's pattern_nnz-th largest (ties keep several,
+    1024-1025); sklearn KMeans(n_clusters=min(pattern_num, C(ph*pw, nnz))) clusters the candidates
+    (1030) and each centre's pattern_nnz largest entries (torch.sort order, 1036-1041) become a
+    pattern.  The reference passes no random_state, so its result is not reproducible (parity
+    unpinned); ``random_state`` pins it for tests.  Returns a (P, ph, pw) float32 array."""
+    import math
+
+    import torch
+    from sklearn.cluster import KMeans
+
+    ph, pw = pattern_shape
+    w = torch.as_tensor(w).detach().float().abs().cpu()
+    nx, ny = (w.shape[0] - ph) // ph + 1, (w.shape[1] - pw) // pw + 1
+    n_pat = min(int(pattern_num), math.comb(ph * pw, int(pattern_nnz)))
+    tiles = w[:nx * ph, :ny * pw].reshape(nx, ph, ny, pw).permute(0, 2, 1, 3).reshape(-1, ph * pw)
+    thr = torch.topk(tiles, int(pattern_nnz), dim=1).values[:, -1:]
+    # the reference fits a Python list of float32 rows, which sklearn converts to float64
+    cand = (tiles >= thr).to(torch.float64).numpy()
+    km = KMeans(n_clusters=n_pat, random_state=random_state).fit(cand)
+    out = np.zeros((n_pat, ph * pw), dtype=np.float32)
+    for p, c in enumerate(km.cluster_centers_):
+        idx = torch.from_numpy(c).sort()[1][-int(pattern_nnz):].numpy()
+        out[p, idx] = 1.0
+    return out.reshape(n_pat, ph, pw)

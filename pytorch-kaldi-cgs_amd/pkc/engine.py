@@ -29,6 +29,7 @@ import torch
 
 from . import _lib as L
 from ._lib import call, ptr
+from .cgs import kmeans_patterns
 
 _PAT = re.compile(r"(.*)=(.*)\((.*),(.*)\)")
 # split-K slab budget of a layer output (<= 8: the small-batch dense kernels sum them in
@@ -260,43 +261,57 @@ def pattern_effective_masks(net, s):
     then multiplied into all of them once per layer call (L times per forward; {0,1} except on
     tied tiles).  Masks already held in ``net.pattern_mask`` (carried between chunks by run_nn,
     core.py:129-131, 304-306) are reused, as the reference does; new ones are stored there in the
-    reference's structure.  Returns {id(param): HCGS x pattern^L effective mask}."""
+    reference's structure.  Each weight's pattern set is, in order: the one carried in
+    ``net.pattern``; the shared set (``pattern_kernels`` / ``pattern_from_file``); or a KMeans
+    search of that weight (update_patterns, neural_networks.py:339-348, 1162-1172), stored back
+    into ``net.pattern``.  Returns {id(param): HCGS x pattern^L effective mask}."""
     if not getattr(net, "if_pattern", False):
         return {}
-    pk = net.pattern_kernels
-    if pk is None:
-        raise NotImplementedError("%s: pattern masks need a pattern set" % net.arch_name)
-    P, ph, pw = pk.shape
     dev = next(net.parameters()).device
-    pat = torch.from_numpy(np.ascontiguousarray(pk, dtype=np.float32)).to(dev)
     entries = net.pattern_params()
     nl = 1 + max(e[1] for e in entries)
-    store = net.pattern_mask
+    store, pstore = net.pattern_mask, net.pattern
     have = all(_pm_get(store, key) is not None for key, _, _, _ in entries)
+    shared = net.pattern_kernels
+    if shared is None and not have and not net.can_search_patterns():
+        raise NotImplementedError("%s: pattern masks need a pattern set" % net.arch_name)
     out = {}
     for key, li, p, hmask in entries:
         rows, cols = p.shape
-        if rows % ph or cols % pw:
-            raise NotImplementedError("%s: %dx%d weight not tiled by %dx%d patterns"
-                                      % (net.arch_name, rows, cols, ph, pw))
         if have:
             pm = _pm_get(store, key).to(dev, torch.float32).contiguous()
         else:
             pre = li == 0 and hmask is not None and _is_input_weight(key)
             src = (p * hmask if pre else p).contiguous()
+            pk = _pm_get(pstore, _pattern_key(key))
+            if pk is not None:
+                t = pk.detach().cpu().numpy() if torch.is_tensor(pk) else np.asarray(pk)
+                pk = t.reshape(t.shape[0], t.shape[-2], t.shape[-1]).astype(np.float32)
+            elif shared is not None:
+                pk = shared
+            else:                               # update_patterns: one KMeans search per weight
+                pn, shape, nnz = net.pattern_search_args(li)
+                pk = kmeans_patterns(src, pn, shape, nnz, random_state=net.pattern_seed)
+            P, ph, pw = pk.shape
+            if rows % ph or cols % pw:
+                raise NotImplementedError("%s: %dx%d weight not tiled by %dx%d patterns"
+                                          % (net.arch_name, rows, cols, ph, pw))
+            pat = torch.from_numpy(np.ascontiguousarray(pk, dtype=np.float32)).to(dev)
             pm = torch.empty_like(p)
             call("pkc_pattern_mask", ptr(src), rows, cols, ptr(pat), P, ph, pw, ptr(pm), s)
             _pm_set(store, key, pm)
+            if _pm_get(pstore, _pattern_key(key)) is None:
+                _pm_set(pstore, _pattern_key(key), pat.view(P, 1, ph, pw))
         e = pm.pow(nl) if nl > 1 else pm.clone()
         out[id(p)] = e * hmask if hmask is not None else e
-    if not have:
-        kern = pat.view(P, 1, ph, pw)
-        if isinstance(net.pattern, list):
-            net.pattern[:] = [kern] * nl
-        else:
-            for k in net.pattern:
-                net.pattern[k] = [kern] * nl
     return out
+
+
+def _pattern_key(key):
+    """net.pattern key of a net.pattern_mask key: (None, i) for an MLP layer, ('pattern_wfx', i)
+    for ('pattern_mask_wfx', i) of an LSTM (neural_networks.py:1162-1172)."""
+    name, i = key
+    return (None if name is None else name.replace("pattern_mask_", "pattern_"), i)
 
 
 def _is_input_weight(key):

@@ -71,15 +71,29 @@ def _input_norm_specs(net, ln, bn):
 
 class _PatternSet:
     """Pattern-set plumbing shared by MLP and LSTM (neural_networks.py:115-131, 513-529).
-    The reference searches the set with sklearn KMeans (sparsity.py:999-1049, no random_state:
-    parity unpinned); pkc takes it from ``pattern_from_file`` / ``pattern_file`` (an (P*ph, pw)
-    .npy such as pattern_file/b08b08_k04_n16_pattern.npy), from ``pattern_kernels = ...``, or
-    from the ``patterns`` dict run_nn carries between chunks (core.py:129-131, 304-306)."""
+    A set comes from ``pattern_from_file`` / ``pattern_file`` (an (P*ph, pw) .npy such as
+    pattern_file/b08b08_k04_n16_pattern.npy; a pkc option, shared by every weight), from
+    ``pattern_kernels = ...``, or from the ``patterns`` dict run_nn carries between chunks
+    (core.py:129-131, 304-306).  Without one, each weight's set is searched as the reference does
+    (update_patterns -> sparsity.find_top_k_by_kmeans with pattern_num / pattern_nnz per layer,
+    neural_networks.py:339-348, 1162-1172; ``pkc.cgs.kmeans_patterns``): sklearn KMeans with no
+    random_state, so parity is unpinned unless ``pattern_seed`` is given."""
 
     def _pattern_opts(self, o):
         self.if_pattern = strtobool(o["if_pattern"]) if "if_pattern" in o else False
         self.pattern_shape = _lst(o, "pattern_shape", int) if "pattern_shape" in o else [8, 8]
         self.pattern_from_file = o.get("pattern_from_file", o.get("pattern_file", None))
+        self.pattern_nnz = _lst(o, "pattern_nnz", int) if "pattern_nnz" in o else []
+        self.pattern_num = _lst(o, "pattern_num", int) if "pattern_num" in o else []
+        self.pattern_seed = int(o["pattern_seed"]) if "pattern_seed" in o else None
+
+    def can_search_patterns(self):
+        return bool(self.pattern_nnz) and bool(self.pattern_num)
+
+    def pattern_search_args(self, layer):
+        """(pattern_num, pattern_shape, pattern_nnz) of layer ``layer`` (neural_networks.py:344)."""
+        return (self.pattern_num[min(layer, len(self.pattern_num) - 1)], list(self.pattern_shape),
+                self.pattern_nnz[min(layer, len(self.pattern_nnz) - 1)])
 
     @property
     def pattern_kernels(self):
@@ -258,9 +272,10 @@ class MLP(_PatternSet, nn.Module):
         return _input_norm_specs(self, self.dnn_use_laynorm_inp, self.dnn_use_batchnorm_inp)
 
     def check_supported(self):
-        if self.if_pattern and self.pattern_kernels is None:
+        if self.if_pattern and self.pattern_kernels is None and not self.can_search_patterns():
             raise NotImplementedError("pattern MLP needs a pattern set (pattern_from_file option, "
-                                      "pattern_kernels, or patterns injected by run_nn)")
+                                      "pattern_kernels, patterns injected by run_nn) or "
+                                      "pattern_num / pattern_nnz for the KMeans search")
 
     def forward(self, x):
         """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
@@ -683,9 +698,10 @@ class LSTM(_PatternSet, nn.Module):
         return _input_norm_specs(self, self.lstm_use_laynorm_inp, self.lstm_use_batchnorm_inp)
 
     def check_supported(self):
-        if self.if_pattern and self.pattern_kernels is None:
-            raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option or "
-                                      "patterns injected by run_nn)")
+        if self.if_pattern and self.pattern_kernels is None and not self.can_search_patterns():
+            raise NotImplementedError("pattern LSTM needs a pattern set (pattern_file option, "
+                                      "patterns injected by run_nn) or pattern_num / pattern_nnz "
+                                      "for the KMeans search")
 
     def pattern_params(self):
         """[(store key, layer, W or U, HCGS mask)] in the reference's update_mask order

@@ -206,6 +206,32 @@ def gen_quant():
     np.savez_compressed(os.path.join(OUT, "quant.npz"), **out)
 
 
+def gen_kmeans():
+    """find_top_k_by_kmeans (sparsity.py:999-1049) with sklearn's KMeans given random_state=0
+    (the reference passes none; seeding it is the only way to pin the search), on weights with
+    ties, a ragged edge and a pattern_num above C(ph*pw, nnz)."""
+    import functools
+
+    from sklearn.cluster import KMeans
+    orig = sparsity.KMeans
+    sparsity.KMeans = functools.partial(KMeans, random_state=0)
+    try:
+        out = {}
+        g = torch.Generator().manual_seed(11)
+        cases = [("a", torch.randn(64, 48, generator=g), 16, (8, 8), 4),
+                 ("b", torch.randn(44, 36, generator=g), 8, (8, 8), 2),
+                 ("c", torch.randn(32, 32, generator=g).round(), 16, (8, 8), 6),
+                 ("d", torch.randn(16, 16, generator=g), 12, (2, 2), 1)]
+        for tag, w, num, shape, nnz in cases:
+            k = sparsity.find_top_k_by_kmeans(w.clone(), num, list(shape), nnz, list(shape))
+            out[tag + "_w"] = w.numpy().copy()
+            out[tag + "_args"] = np.array([num, shape[0], shape[1], nnz])
+            out[tag + "_kernel"] = k.numpy()[:, 0]
+    finally:
+        sparsity.KMeans = orig
+    np.savez_compressed(os.path.join(OUT, "kmeans.npz"), **out)
+
+
 # ----------------------------------------------------------------------------------------------
 # guided HCGS masks (guided_hcgs.py:9-77): deterministic functions of |W|
 # ----------------------------------------------------------------------------------------------
@@ -470,12 +496,14 @@ if __name__ == "__main__":
         for a in sys.argv[1:]:
             kind, _, v = a.partition(":")
             {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru(),
-             "cm": lambda _v: gen_cm(), "run_nn": gen_run_nn}[kind](v)
+             "cm": lambda _v: gen_cm(), "run_nn": gen_run_nn,
+             "kmeans": lambda _v: gen_kmeans()}[kind](v)
         sys.exit(0)
     gen_loader()
     gen_hcgs()
     gen_ghcgs()
     gen_quant()
+    gen_kmeans()
     for v in ("plain", "hcgs", "quant", "ln", "l1", "l2", "gl"):
         gen_mlp(v)
     gen_rnn()

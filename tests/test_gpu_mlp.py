@@ -235,14 +235,16 @@ def test_engine_graph_replay_equals_eager():
             torch.testing.assert_close(res[0][1][k], other[1][k], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("variant", ["prune", "pattern", "ghcgs", "inpnorm"])
+@pytest.mark.parametrize("variant", ["prune", "pattern", "pattern_search", "ghcgs", "inpnorm"])
 def test_engine_sparsity_vs_oracle(variant):
     """prune: every forward re-thresholds |W| at np.percentile(prune_perc[i]) and zeroes the rest
     (neural_networks.py:276-278); pattern: 8x8/k4/n16 pattern masks from the pattern_file set,
     computed at the first layer call and multiplied in once per layer call (263-272, 339-361).
     Both on top of HCGS masks on the body; 3 training steps vs the oracle.  inpnorm: ln0 then bn0
     on the body and on the head that reads it (neural_networks.py:246-251): the head's input
-    norms hand their input gradient down to the body."""
+    norms hand their input gradient down to the body.  pattern_search: no pattern set, so every
+    layer's set comes from update_patterns' KMeans search (sparsity.py:999-1049; sklearn seeded
+    through pattern_seed on both sides, the reference itself is unseeded)."""
     from oracle import nets as ON
     from oracle import run as OR
     from oracle.masks import prune_mask
@@ -262,10 +264,13 @@ def test_engine_sparsity_vs_oracle(variant):
     elif variant == "ghcgs":     # guided masks applied (apply_guided_hcgs, :261-262) on the body
         cfg["architecture1"].update(guided_hcgs="True", apply_guided_hcgs="True")
     else:
-        pset = G("quant.npz")["pattern_set"].reshape(16, 8, 8)
+        if variant == "pattern":
+            pset = G("quant.npz")["pattern_set"].reshape(16, 8, 8)
         for sec in ("architecture1", "architecture2"):
             cfg[sec].update(if_pattern="True", pattern_mode="pattern", pattern_shape="8,8",
                             pattern_nnz="4,4", pattern_num="16,16")
+            if variant == "pattern_search":
+                cfg[sec].update(pattern_nnz="4,6", pattern_num="16,8", pattern_seed="0")
     dims = (("architecture1", 40), ("architecture2", 32), ("architecture3", 32))
     nets, opts = build_nets(cfg, dims)
     onets, _ = build_nets(cfg, dims, cls=ON.MLP)
@@ -302,7 +307,7 @@ def test_engine_sparsity_vs_oracle(variant):
         assert rel < 1e-4, "step %d posterior max rel err %.3g" % (s, rel)
     eng.sync_state()
     percs = {"MLP_layers1": (70.0, 55.0), "MLP_layers2": (30.0,)} if variant == "prune" else {}
-    if variant == "pattern":         # the engine stored the reference-structured masks
+    if variant.startswith("pattern"):    # the engine stored the reference-structured masks
         for a in ("MLP_layers1", "MLP_layers2"):
             for pm, opm in zip(nets[a].pattern_mask, onets[a].pattern_masks):
                 np.testing.assert_array_equal(pm.cpu().numpy(), opm.numpy())
@@ -317,7 +322,7 @@ def test_engine_sparsity_vs_oracle(variant):
                     ref = ref * sd_o[mk]
                 if "ghcgs.%d.mask" % i in sd_o:
                     ref = ref * sd_o["ghcgs.%d.mask" % i]
-                if variant == "pattern" and onets[a].if_pattern:
+                if variant.startswith("pattern") and onets[a].if_pattern:
                     ref = ref * onets[a].pattern_masks[i] ** len(onets[a].lay)
                 if a in percs:
                     ref = ref * prune_mask(ref, percs[a][i])

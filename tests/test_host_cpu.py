@@ -235,3 +235,16 @@ def test_product_cm_decode_matches_reference(tmp_path):
         np.testing.assert_array_equal(m, g["mat%d" % i])
     for i, (_, m) in enumerate(D.parse_mat_ark_bytes(ark)):
         np.testing.assert_array_equal(m, g["mat%d" % i])
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c", "d"])
+def test_product_kmeans_pattern_search_matches_reference(tag):
+    """pkc.cgs.kmeans_patterns vs sparsity.find_top_k_by_kmeans (sparsity.py:999-1049), both with
+    sklearn KMeans seeded (random_state=0): candidates with ties (case c), ragged tiles (b) and a
+    pattern_num capped at C(ph*pw, nnz) (d) give the reference's pattern set exactly."""
+    from pkc.cgs import kmeans_patterns
+    g = G("kmeans.npz")
+    num, ph, pw, nnz = (int(v) for v in g[tag + "_args"])
+    k = kmeans_patterns(torch.from_numpy(g[tag + "_w"]), num, [ph, pw], nnz, random_state=0)
+    np.testing.assert_array_equal(k, g[tag + "_kernel"])
+    assert (k.reshape(k.shape[0], -1).sum(1) == nnz).all()
