@@ -15,6 +15,7 @@
 //              weights / activations / gradients the step keeps): half the bytes per workgroup,
 //              one 16-byte load per thread per operand per k-tile.
 // Split-K over blockIdx.z writes deterministic partial slabs (summed by the consumer kernels).
+#include "pkc_gemm_big.h"
 #include "pkc_ops.h"
 #include "pkc_optim.h"
 
@@ -296,13 +297,24 @@ __global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const voi
                                              B, ldb, C, ldc, kchunk, slab_stride);
 }
 
+template <int PREC, bool BIN, bool AKC, bool BKC>
+__global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
+                                                          const void* __restrict__ A, int64_t lda,
+                                                          const void* __restrict__ B, int64_t ldb,
+                                                          float* __restrict__ C, int64_t ldc,
+                                                          int kchunk, int64_t slab_stride) {
+  __shared__ __attribute__((aligned(16))) char lds[big::LDS_BYTES];
+  big::body<PREC, BIN, AKC, BKC>(lds, blockIdx.x, blockIdx.y, blockIdx.z, M, N, K, A, lda, B, ldb,
+                                 C, ldc, kchunk, slab_stride);
+}
+
 // Several independent matmuls in ONE launch (e.g. a layer's dW and dX, both heads' logits):
 // workgroup ranges are assigned to problems in order; each workgroup dispatches on its problem's
 // operand orientation.  One launch boundary instead of one per matmul.
 constexpr int GMAX = 8;
 struct GroupProb {
   int kind;              // PKC_OP_GEMM / PKC_OP_COLSUM / PKC_OP_LOSS
-  int code;              // a_kcontig*4 + b_kcontig*2 + vec
+  int code;              // a_kcontig*4 + b_kcontig*2 + vec (+8: 128x128 tile body)
   int M, N, K, kchunk, tn, tmn, wg0;
   const void* A; int64_t lda; const void* B; int64_t ldb; float* C; int64_t ldc; int64_t slab;
   const void* X1; void* X2; void* X3;
@@ -312,9 +324,11 @@ struct GroupArgs {
   int n;
 };
 
-template <int PREC, bool BIN>
+template <int PREC, bool BIN, bool BIG>
 __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
-  __shared__ Lds<PREC> sm;
+  // BIG: at least one problem takes the 128x128 body; its LDS also holds the 64x64 tiles
+  __shared__ __attribute__((aligned(16))) char lds[BIG ? big::LDS_BYTES : sizeof(Lds<PREC>)];
+  Lds<PREC>& sm = *reinterpret_cast<Lds<PREC>*>(lds);
   int i = 0;
 #pragma unroll
   for (int j = 1; j < GMAX; ++j)
@@ -338,6 +352,21 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
   }
   const int bz = local / p.tmn, rem = local % p.tmn;
   const int by = rem / p.tn, bx = rem % p.tn;
+  if constexpr (BIG) {
+    if (p.code >= 8) {
+#define PKC_BB(AK, BK_)                                                                          \
+  big::body<PREC, BIN, AK, BK_>(lds, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, \
+                                p.kchunk, p.slab)
+      switch (p.code & 6) {
+        case 6: PKC_BB(true, true); break;
+        case 4: PKC_BB(true, false); break;
+        case 2: PKC_BB(false, true); break;
+        default: PKC_BB(false, false); break;
+      }
+#undef PKC_BB
+      return;
+    }
+  }
 #define PKC_GB(AK, BK_, V)                                                                      \
   gemm_body<PREC, AK, BK_, V, 4, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
                                       p.ldc, p.kchunk, p.slab)
@@ -367,6 +396,26 @@ static int launch(int M, int N, int K, const void* A, int64_t lda, const void* B
 }
 
 template <int PREC, bool BIN>
+static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int64_t lda,
+                      const void* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
+                      hipStream_t s) {
+  constexpr int BKB = big::Cfg<PREC, BIN>::BK;
+  int kchunk = (K + splits - 1) / splits;
+  kchunk = ((kchunk + BKB - 1) / BKB) * BKB;
+  dim3 grid((N + big::TN - 1) / big::TN, (M + big::TM - 1) / big::TM, splits);
+#define PKC_L(AK, BK_)                                                                          \
+  hipLaunchKernelGGL((gemm_big_kernel<PREC, BIN, AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, \
+                     lda, B, ldb, C, ldc, kchunk, slab)
+  if (akc && bkc) PKC_L(true, true);
+  else if (akc) PKC_L(true, false);
+  else if (bkc) PKC_L(false, true);
+  else PKC_L(false, false);
+#undef PKC_L
+  PKC_LAUNCH_CHECK("pkc_gemm (128x128)");
+  return PKC_OK;
+}
+
+template <int PREC, bool BIN>
 static int dispatch(int akc, int bkc, bool vec, int M, int N, int K, const void* A, int64_t lda,
                     const void* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
                     hipStream_t s) {
@@ -378,6 +427,17 @@ static int dispatch(int akc, int bkc, bool vec, int M, int N, int K, const void*
   if (vec) PKC_G(false, true, true);
   PKC_G(false, true, false);
 #undef PKC_G
+}
+
+// The 128x128 body takes a matmul with at least this many output tiles (alone: enough to fill the
+// chip; in a grouped launch the other problems fill it).  PKC_GEMM_BIG=0 disables it (A/B runs).
+constexpr int BIG_MIN_TILES = 160, BIG_MIN_TILES_GROUPED = 32;
+static bool big_enabled() {
+  static const int on = [] {
+    const char* v = getenv("PKC_GEMM_BIG");
+    return v ? atoi(v) : 1;
+  }();
+  return on != 0;
 }
 
 }  // namespace pkc
@@ -414,6 +474,16 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
                    ldb % e == 0 && (a_kcontig ? K % e == 0 : M % e == 0) &&
                    (b_kcontig ? K % e == 0 : N % e == 0);
+  if (big_enabled() && big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, BIG_MIN_TILES)) {
+    if (prec == PKC_PREC_FP32)
+      return launch_big<PKC_PREC_FP32, false>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
+                                              splits, slab_stride, S(stream));
+    if (prec == PKC_PREC_BF16IN)
+      return launch_big<PKC_PREC_BF16, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
+                                             splits, slab_stride, S(stream));
+    return launch_big<PKC_PREC_BF16, false>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
+                                            splits, slab_stride, S(stream));
+  }
   if (prec == PKC_PREC_FP32)
     return dispatch<PKC_PREC_FP32, false>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C,
                                           ldc, splits, slab_stride, S(stream));
@@ -432,6 +502,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   GroupArgs g;
   memset(&g, 0, sizeof(g));
   int wg = 0, k = 0;
+  bool any_big = false;
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   for (int i = 0; i < n; ++i) {
     const pkc_gemm_problem& q = probs[i];
@@ -464,29 +535,39 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     int splits = q.splits <= 0 ? pkc_gemm_pick_splits(q.M, q.N, q.K) : q.splits;
     PKC_CHECK_ARG(splits == 1 || q.slab_stride >= (int64_t)q.M * q.ldc,
                   "pkc_gemm_grouped: problem %d slab_stride too small", i);
-    int kchunk = (q.K + splits - 1) / splits;
-    kchunk = ((kchunk + BK - 1) / BK) * BK;
     const bool vec = ((uintptr_t)q.A % 16 == 0) && ((uintptr_t)q.B % 16 == 0) && q.lda % e == 0 &&
                      q.ldb % e == 0 && (q.a_kcontig ? q.K % e == 0 : q.M % e == 0) &&
                      (q.b_kcontig ? q.K % e == 0 : q.N % e == 0);
+    const bool bigp = big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
+                                                     q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED);
+    any_big |= bigp;
+    const int bk = bigp ? (prec == PKC_PREC_FP32 ? 32 : 64) : BK;
+    int kchunk = (q.K + splits - 1) / splits;
+    kchunk = ((kchunk + bk - 1) / bk) * bk;
+    const int tm = bigp ? big::TM : BM, tnn = bigp ? big::TN : BN;
     GroupProb& p = g.p[k++];
     p.kind = PKC_OP_GEMM;
-    p.code = (q.a_kcontig ? 4 : 0) + (q.b_kcontig ? 2 : 0) + (vec ? 1 : 0);
+    p.code = (q.a_kcontig ? 4 : 0) + (q.b_kcontig ? 2 : 0) + (vec ? 1 : 0) + (bigp ? 8 : 0);
     p.M = q.M; p.N = q.N; p.K = q.K; p.kchunk = kchunk;
-    p.tn = (q.N + BN - 1) / BN;
-    p.tmn = p.tn * ((q.M + BM - 1) / BM);
+    p.tn = (q.N + tnn - 1) / tnn;
+    p.tmn = p.tn * ((q.M + tm - 1) / tm);
     p.wg0 = wg;
     p.A = q.A; p.lda = q.lda; p.B = q.B; p.ldb = q.ldb; p.C = q.C; p.ldc = q.ldc; p.slab = q.slab_stride;
     wg += p.tmn * splits;
   }
   g.n = k;
   if (k == 0) return PKC_OK;
-  if (prec == PKC_PREC_FP32)
-    hipLaunchKernelGGL((gemm_grouped_kernel<PKC_PREC_FP32, false>), dim3(wg), dim3(NT), 0, S(stream), g);
-  else if (prec == PKC_PREC_BF16IN)
-    hipLaunchKernelGGL((gemm_grouped_kernel<PKC_PREC_BF16, true>), dim3(wg), dim3(NT), 0, S(stream), g);
-  else
-    hipLaunchKernelGGL((gemm_grouped_kernel<PKC_PREC_BF16, false>), dim3(wg), dim3(NT), 0, S(stream), g);
+#define PKC_GL(P, BIN)                                                                          \
+  do {                                                                                          \
+    if (any_big)                                                                                \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, true>), dim3(wg), dim3(NT), 0, S(stream), g);  \
+    else                                                                                        \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false>), dim3(wg), dim3(NT), 0, S(stream), g); \
+  } while (0)
+  if (prec == PKC_PREC_FP32) PKC_GL(PKC_PREC_FP32, false);
+  else if (prec == PKC_PREC_BF16IN) PKC_GL(PKC_PREC_BF16, true);
+  else PKC_GL(PKC_PREC_BF16, false);
+#undef PKC_GL
   PKC_LAUNCH_CHECK("pkc_gemm_grouped");
   return PKC_OK;
 }

@@ -1,0 +1,327 @@
+// pkc_gemm_big.h — 128x128 MFMA tile body for the large-M matmuls (gfx950 / CDNA4).
+//
+// The 64x64 tile of pkc_gemm.hip is sized for the M = 128-row frame batches of the MLP step,
+// where every matmul is short and latency-bound.  The sequence models' input projections
+// (M = T*B = 2-16 k rows: neural_networks.py:951-954, 1554-1555), their backward, and the MLP at
+// large batches are long contractions: there the 64x64 tile's 2 MFMAs per wave per barrier and
+// 16 flop per staged byte leave the matrix pipe idle.  This body:
+//   * 128x128 output tile per 256-thread workgroup, 4 waves in 2x2, each wave 64x64 = 2x2 blocks
+//     of 32x32 accumulators (64 accumulator registers);
+//   * one LDS row = 128 bytes of k: BK = 64 for bf16 operands (v_mfma_f32_32x32x16_bf16, 16 MFMA
+//     per wave per k-tile), BK = 32 for exact fp32 (v_mfma_f32_32x32x2_f32, 64 MFMA per wave per
+//     k-tile, the parity mode);
+//   * double-buffered LDS (2 x 32 KB) with ONE barrier per k-tile: tile t+1 is written to the
+//     other buffer after the MFMAs of tile t, from registers loaded one (16-byte staging: two)
+//     k-tiles earlier;
+//   * LDS image [row][128 B] with 16-byte chunk c of row r stored at c ^ ((r>>1 ^ r>>4) & 7): the
+//     ds_read_b128 fragment reads of any 16 rows of a 32-row block hit 16 distinct bank groups
+//     (conflict-free), for both operand orientations;
+//   * k-contiguous operands are staged with 16-byte loads and stores; m-contiguous ones (the
+//     transposed operands of dX / dW) with 16-byte loads along m and a transposing store (bf16:
+//     two k-adjacent chunks packed into dwords).
+// Split-K (blockIdx.z-style slice index) writes deterministic partial slabs like pkc_gemm.
+#pragma once
+#include "pkc_common.h"
+
+namespace pkc {
+namespace big {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int TM = 128, TN = 128, NT = 256;
+constexpr int ROWB = 128;                       // bytes of k per LDS row
+constexpr int TILE_BYTES = TM * ROWB;           // one operand tile in LDS (16 KB)
+constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;   // A and B, double-buffered (64 KB)
+
+__device__ __forceinline__ int swz(int r) { return ((r >> 1) ^ (r >> 4)) & 7; }
+
+// Element type in HBM (HE) and in LDS (LE); BK = k per LDS row.
+template <int PREC, bool BIN>
+struct Cfg {
+  using HE = float;
+  using LE = float;
+  static constexpr int BK = 32;
+};
+template <>
+struct Cfg<PKC_PREC_BF16, false> {
+  using HE = float;
+  using LE = __bf16;
+  static constexpr int BK = 64;
+};
+template <>
+struct Cfg<PKC_PREC_BF16, true> {
+  using HE = __bf16;
+  using LE = __bf16;
+  static constexpr int BK = 64;
+};
+
+// One operand tile (128 rows x BK) staged through registers.  HBM chunks are 16 bytes:
+// EPC elements.  KC: row-major [row][k] in HBM; otherwise [k][row].
+template <int PREC, bool BIN, bool KC>
+struct Stage {
+  using C = Cfg<PREC, BIN>;
+  using HE = typename C::HE;
+  using LE = typename C::LE;
+  static constexpr int BK = C::BK;
+  static constexpr int EPC = 16 / sizeof(HE);                  // elements per 16-byte chunk
+  static constexpr int NCH = TM * BK / EPC / NT;               // chunks per thread (4 or 8)
+  static constexpr bool PAIR = !KC && sizeof(LE) == 2;         // pack k, k+1 into dwords
+  float4 v[NCH];
+
+  // chunk i of this thread -> (row, k) of its first element
+  __device__ __forceinline__ void coord(int i, int& r, int& k) const {
+    const int t = threadIdx.x;
+    if (KC) {
+      constexpr int CPR = BK / EPC;                            // chunks per row
+      const int idx = t + NT * i;
+      r = idx / CPR;
+      k = (idx % CPR) * EPC;
+    } else if (PAIR) {
+      // chunk pairs (k, k+1) of the same rows: i even/odd = k even/odd
+      constexpr int CPK = TM / EPC;                            // chunks per k
+      const int idx = t + NT * (i >> 1);
+      r = (idx % CPK) * EPC;
+      k = (idx / CPK) * 2 + (i & 1);
+    } else {
+      constexpr int CPK = TM / EPC;
+      const int idx = t + NT * i;
+      r = (idx % CPK) * EPC;
+      k = idx / CPK;
+    }
+  }
+
+  // Clamped (always valid) addresses, out-of-range elements zeroed by selects afterwards: a load
+  // under a runtime branch makes hipcc drain vmcnt around it (pkc_gemm.hip Stage).
+  __device__ __forceinline__ void load(const HE* __restrict__ P, int64_t ld, int r0, int rmax,
+                                       int k0, int kend) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int r, k;
+      coord(i, r, k);
+      const bool ok = (r0 + r < rmax) && (k0 + k < kend);
+      const int rr = min(r0 + r, rmax - (KC ? 1 : EPC));
+      const int kk = min(k0 + k, kend - (KC ? EPC : 1));
+      const float4 x = KC ? *reinterpret_cast<const float4*>(P + (int64_t)rr * ld + kk)
+                          : *reinterpret_cast<const float4*>(P + (int64_t)kk * ld + rr);
+      v[i] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  // Element access by value only: taking the address of v[] makes the compiler promote the
+  // staging array into extra LDS (16 KB per workgroup), with a round trip per element.
+  __device__ __forceinline__ static uint32_t word(const float4& x, int w) {
+    return __float_as_uint(w == 0 ? x.x : w == 1 ? x.y : w == 2 ? x.z : x.w);
+  }
+  __device__ __forceinline__ static float fl(const float4& x, int w) {
+    return w == 0 ? x.x : w == 1 ? x.y : w == 2 ? x.z : x.w;
+  }
+  __device__ __forceinline__ static uint32_t bf16bits(float f) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f);
+  }
+
+  __device__ __forceinline__ void store(char* __restrict__ s) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int r, k;
+      coord(i, r, k);
+      if (KC) {
+        const int kb = k * (int)sizeof(LE);                    // byte offset of k in the row
+        char* dst = s + r * ROWB + 16 * ((kb >> 4) ^ swz(r)) + (kb & 15);
+        if constexpr (sizeof(HE) == sizeof(LE)) {
+          *reinterpret_cast<float4*>(dst) = v[i];
+        } else {                                               // fp32 -> bf16: 8 bytes
+          uint2 h;
+          h.x = bf16bits(v[i].x) | (bf16bits(v[i].y) << 16);
+          h.y = bf16bits(v[i].z) | (bf16bits(v[i].w) << 16);
+          *reinterpret_cast<uint2*>(dst) = h;
+        }
+      } else if (PAIR) {
+        if (i & 1) continue;                                   // handled with its even partner
+        const int kb = k * 2;
+        const int co = kb & 15;                                // dword-aligned: k even
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) {
+          uint32_t p;
+          if constexpr (sizeof(HE) == 2) {                     // bf16 element j of each chunk
+            const uint32_t a = word(v[i], j >> 1), b = word(v[i + 1], j >> 1);
+            p = (j & 1) ? ((a >> 16) | (b & 0xFFFF0000u)) : ((a & 0xFFFFu) | (b << 16));
+          } else {
+            p = bf16bits(fl(v[i], j)) | (bf16bits(fl(v[i + 1], j)) << 16);
+          }
+          const int rj = r + j;
+          *reinterpret_cast<uint32_t*>(s + rj * ROWB + 16 * ((kb >> 4) ^ swz(rj)) + co) = p;
+        }
+      } else {                                                 // fp32 m-contiguous
+        const int kb = k * 4;
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) {
+          const int rj = r + j;
+          *reinterpret_cast<float*>(s + rj * ROWB + 16 * ((kb >> 4) ^ swz(rj)) + (kb & 15)) =
+              fl(v[i], j);
+        }
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float4 lds16(const char* s, int r, int c) {
+  return *reinterpret_cast<const float4*>(s + r * ROWB + 16 * (c ^ swz(r)));
+}
+
+// MFMAs of one k-tile for this wave's 64x64 sub-tile (rows wm*64 + 32a, cols wn*64 + 32b).
+template <int PREC>
+__device__ __forceinline__ void tile_mfma(const char* __restrict__ sa, const char* __restrict__ sb,
+                                          int wm, int wn, int lane, f32x16 (&acc)[2][2]) {
+  const int r = lane & 31, h = lane >> 5;
+  if constexpr (PREC == PKC_PREC_FP32) {
+    // lane half h takes k = 16h + kk (kk = 0..15), the same permutation of k for A and B
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      float av[16];
+      const int ra = wm * 64 + 32 * a + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = lds16(sa, ra, 4 * h + q);
+        av[4 * q] = x.x; av[4 * q + 1] = x.y; av[4 * q + 2] = x.z; av[4 * q + 3] = x.w;
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float bv[16];
+        const int rb = wn * 64 + 32 * b + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 y = lds16(sb, rb, 4 * h + q);
+          bv[4 * q] = y.x; bv[4 * q + 1] = y.y; bv[4 * q + 2] = y.z; bv[4 * q + 3] = y.w;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc[a][b], 0, 0, 0);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {                     // k = 16t + 8h + j
+      bf16x8 av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const float4 x = lds16(sa, wm * 64 + 32 * a + r, 2 * t + h);
+        av[a] = *reinterpret_cast<const bf16x8*>(&x);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float4 y = lds16(sb, wn * 64 + 32 * b + r, 2 * t + h);
+        bv[b] = *reinterpret_cast<const bf16x8*>(&y);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+  }
+}
+
+// C[bz slab][m0.., n0..] = A[m0.., kbeg..kend) . B[n0.., kbeg..kend)^T for one 128x128 tile.
+// `lds` is LDS_BYTES of workgroup memory.
+template <int PREC, bool BIN, bool AKC, bool BKC>
+__device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int bz, int M, int N,
+                                     int K, const void* __restrict__ Av, int64_t lda,
+                                     const void* __restrict__ Bv, int64_t ldb,
+                                     float* __restrict__ Cp, int64_t ldc, int kchunk,
+                                     int64_t slab_stride) {
+  using Cf = Cfg<PREC, BIN>;
+  using HE = typename Cf::HE;
+  constexpr int BK = Cf::BK;
+  const HE* A = reinterpret_cast<const HE*>(Av);
+  const HE* B = reinterpret_cast<const HE*>(Bv);
+  const int m0 = by * TM, n0 = bx * TN;
+  const int kbeg = bz * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  // Tile t lives in LDS buffer t&1 (A at lds + (t&1)*2*TILE_BYTES, B right after it; computed,
+  // not indexed from a pointer array, which would be promoted into extra LDS).
+  // DEPTH 2 (bf16 and fp32 operands staged as they are stored): two register stages, so a k-tile's
+  // loads are issued two k-tiles before its LDS store; a workgroup alone on its CU (one 128x128
+  // tile per CU) otherwise waits a full HBM/L2 latency every k-tile.  DEPTH 1 for the fp32->bf16
+  // staging, whose stages take twice the registers.
+  constexpr int DEPTH = (sizeof(HE) == sizeof(typename Cf::LE)) ? 2 : 1;
+  Stage<PREC, BIN, AKC> na, nna;      // tile t+1, tile t+2 (DEPTH 2)
+  Stage<PREC, BIN, BKC> nb, nnb;
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;   // uniform
+  if (nk > 0) {
+    na.load(A, lda, m0, M, kbeg, kend);
+    nb.load(B, ldb, n0, N, kbeg, kend);
+    na.store(lds);
+    nb.store(lds + TILE_BYTES);
+    na.load(A, lda, m0, M, kbeg + BK, kend);           // past kend: clamped, zeroed, never stored
+    nb.load(B, ldb, n0, N, kbeg + BK, kend);
+    if constexpr (DEPTH == 2) {
+      nna.load(A, lda, m0, M, kbeg + 2 * BK, kend);
+      nnb.load(B, ldb, n0, N, kbeg + 2 * BK, kend);
+    }
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      char* cur = lds + (t & 1) * 2 * TILE_BYTES;
+      char* nxt = lds + ((t + 1) & 1) * 2 * TILE_BYTES;
+      tile_mfma<PREC>(cur, cur + TILE_BYTES, wm, wn, lane, acc);
+      if (t + 1 < nk) {                               // uniform
+        na.store(nxt);
+        nb.store(nxt + TILE_BYTES);
+        if constexpr (DEPTH == 2) {
+          na = nna;
+          nb = nnb;
+          nna.load(A, lda, m0, M, kbeg + (t + 3) * BK, kend);
+          nnb.load(B, ldb, n0, N, kbeg + (t + 3) * BK, kend);
+        } else {
+          na.load(A, lda, m0, M, kbeg + (t + 2) * BK, kend);
+          nb.load(B, ldb, n0, N, kbeg + (t + 2) * BK, kend);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  float* Cz = Cp + (int64_t)bz * slab_stride;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int col = n0 + wn * 64 + 32 * b + r;
+    if (col >= N) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = m0 + wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < M) Cz[(int64_t)row * ldc + col] = acc[a][b][reg];
+      }
+    }
+  }
+}
+
+// Which problems take this body: 16-byte operand paths (aligned bases and leading dimensions,
+// contiguous extents multiples of a chunk) and enough 128x128 tiles to fill the chip.
+__host__ inline bool eligible(int prec, int akc, int bkc, int M, int N, int K, const void* A,
+                              int64_t lda, const void* B, int64_t ldb, int min_tiles) {
+  const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
+  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
+                   ldb % e == 0 && (akc ? K % e == 0 : M % e == 0) && (bkc ? K % e == 0 : N % e == 0);
+  const int64_t tiles = (int64_t)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  // exact fp32 runs at the vector rate: the 64x64 tile already streams fast enough for it and
+  // balances better over the CUs (C4's projections: 83 vs 73 TF/s, same run); the 128x128 tile
+  // wins only once there are several tiles per CU (4096^3: 118 vs 109 TF/s)
+  if (prec == PKC_PREC_FP32) min_tiles = min_tiles > 1024 ? min_tiles : 1024;
+  return vec && tiles >= min_tiles && K >= 128;
+}
+
+}  // namespace big
+}  // namespace pkc

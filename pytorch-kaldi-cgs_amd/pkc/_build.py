@@ -6,6 +6,7 @@ pytorch-kaldi-cgs_amd/pkc/libpkc.so so it travels with the repository snapshot t
 import concurrent.futures as cf
 import glob
 import os
+import re
 import subprocess
 import sys
 
@@ -23,13 +24,23 @@ def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _deps():
-    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(TOP, "..", "include", "*.h"))
+def _deps(src, seen=None):
+    """Headers `src` includes with "..." (recursively): a kernel file is rebuilt only when one of
+    ITS headers changes (pkc_rnn.hip alone takes minutes)."""
+    seen = set() if seen is None else seen
+    for line in open(src):
+        m = re.match(r'\s*#\s*include\s+"([^"]+)"', line)
+        if m:
+            h = os.path.normpath(os.path.join(os.path.dirname(src), m.group(1)))
+            if os.path.exists(h) and h not in seen:
+                seen.add(h)
+                _deps(h, seen)
+    return seen
 
 
 def _compile(src):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(d) for d in _deps()])
+    newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(d) for d in _deps(src)])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
     cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]

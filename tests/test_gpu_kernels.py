@@ -367,3 +367,71 @@ def test_prune_matches_numpy_percentile(L, shape, perc, zeros):
     torch.cuda.synchronize()
     assert torch.equal(mask.cpu(), ref_mask)
     assert torch.equal(wd.cpu(), w * ref_mask)
+
+
+# shapes that take the 128x128 body (pkc_gemm_big.h: >= 160 output tiles of 128x128, 16-byte
+# operand paths): ragged M / N tails, K tails off the 32/64 k-tile, split-K slabs
+BIG_SHAPES = [(4096, 4096, 256, 1), (2048, 1280, 440, 1), (2056, 1288, 1000, 1), (4096, 1024, 1024, 2), (5280, 1024, 2048, 1),
+              (1032, 2600, 136, 3)]
+
+
+@pytest.mark.parametrize("prec", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K,splits", BIG_SHAPES)
+@pytest.mark.parametrize("orient", ["nt", "nn", "tn", "tt"])
+def test_gemm_big_tile(L, prec, M, N, K, splits, orient):
+    """The large-M matmuls of the sequence models and big-batch MLPs (the 128x128 tile body) vs
+    fp64 products of the same (bf16-rounded for prec 1/2) operands, in every orientation."""
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0), "tt": (0, 1)}[orient]
+    Ast = A if akc else A.t().contiguous()
+    Bst = B if bkc else B.t().contiguous()
+    if prec >= 1:
+        A = A.bfloat16().float()
+        B = B.bfloat16().float()
+    ref = (A.double() @ B.double().t()).float()
+    Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+    if prec == 2:
+        Ad, Bd = Ad.bfloat16().contiguous(), Bd.bfloat16().contiguous()
+    Cd = torch.full((splits, M, N), float("nan"), device=DEV)
+    L.call("pkc_gemm", prec, akc, bkc, M, N, K, L.ptr(Ad), Ast.shape[1], L.ptr(Bd), Bst.shape[1],
+           L.ptr(Cd), N, splits, M * N, _s())
+    out = Cd.sum(0).cpu()
+    tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=tol)
+    if prec == 0 and splits == 1:
+        # exact fp32 MFMA chains: the same sums as the 64x64 tile up to fp32 summation order
+        assert torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("prec", [0, 2])
+def test_gemm_grouped_big(L, prec):
+    """A grouped launch mixing 128x128-tile problems (the B = 4096 MLP backward's dX and dW) with
+    64x64 ones and split-K slabs."""
+    g = torch.Generator().manual_seed(5)
+    specs = [("nn", 4096, 1024, 1024, 1), ("tn", 1024, 1024, 4096, 2), ("nt", 128, 48, 1024, 4),
+             ("nn", 37, 70, 45, 1)]
+    probs, keep, refs = [], [], []
+    for orient, M, N, K, sp in specs:
+        A = torch.randn(M, K, generator=g)
+        B = torch.randn(N, K, generator=g)
+        akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
+        Ast = A if akc else A.t().contiguous()
+        Bst = B if bkc else B.t().contiguous()
+        if prec:
+            A, B = A.bfloat16().float(), B.bfloat16().float()
+        refs.append((A.double() @ B.double().t()).float())
+        Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+        if prec == 2:
+            Ad, Bd = Ad.bfloat16().contiguous(), Bd.bfloat16().contiguous()
+        Cd = torch.full((sp, M, N), float("nan"), device=DEV)
+        keep += [Ad, Bd, Cd]
+        probs.append(L.GemmProblem(a_kcontig=akc, b_kcontig=bkc, M=M, N=N, K=K, splits=sp,
+                                   A=Ad.data_ptr(), lda=Ast.shape[1], B=Bd.data_ptr(),
+                                   ldb=Bst.shape[1], C=Cd.data_ptr(), ldc=N, slab_stride=M * N))
+    arr = (L.GemmProblem * len(probs))(*probs)
+    L.call("pkc_gemm_grouped", prec, arr, len(probs), _s())
+    for (orient, M, N, K, sp), ref, Cd in zip(specs, refs, keep[2::3]):
+        tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
+        torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=tol)
