@@ -58,13 +58,19 @@ int pkc_gemm_pick_splits(int M, int N, int K);
  *   PKC_OP_LOSS  : pkc_loss_finalize(nheads = M, row_loss = A, weights = B, rows = N,
  *                  row_err = X1, out = C, acc = X2, advance_ctr = X3)
  *   PKC_OP_OPTIM : pkc_optim_step(tensors_dev = A, chunk_map_dev = B, nchunks = M) — the update of
- *                  a layer whose gradients are complete rides in a later launch of the backward */
+ *                  a layer whose gradients are complete rides in a later launch of the backward
+ * Block-sparse GEMM (static HCGS masks multiplied into W, HCGS.py:24-28 /
+ * neural_networks.py:258, 858-861): with ktiles != NULL (and splits == 1) the 64-column output
+ * tile j reads only the 32-deep k-tiles ktiles[j * (kmax + 1) + 1 .. + count], count =
+ * ktiles[j * (kmax + 1)]: the k-tiles whose B rows (64 of them) hold a nonzero.  Exact: every
+ * skipped product is a zero weight, so the sums are those of the dense matmul. */
 enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2, PKC_OP_OPTIM = 3 };
 typedef struct {
   int a_kcontig, b_kcontig, M, N, K, splits;
   const void* A; int64_t lda; const void* B; int64_t ldb;
   float* C; int64_t ldc; int64_t slab_stride;
   int kind; const void* X1; void* X2; void* X3;
+  const int32_t* ktiles; int kmax;              /* block-sparse k-tile lists (device), or NULL */
 } pkc_gemm_problem;
 int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream);
 
@@ -347,6 +353,21 @@ int pkc_ark_read_rows(const char* path, int64_t offset, int64_t rows, int64_t co
  * pkc_ark_cm_size -> its byte length; pkc_ark_decode_cm -> rows x cols float32, row-major. */
 int64_t pkc_ark_cm_size(const unsigned char* blob, int64_t nbytes);
 int pkc_ark_decode_cm(const unsigned char* blob, int64_t nbytes, float* out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Chunk-level data parallelism (the reference trains on one GPU, core.py:216-232):
+ * one RCCL all-reduce (SUM) of the flat fp32 gradient buffer per step over xGMI, for hosts that
+ * do not use torch.distributed.  Rank 0: pkc_dp_unique_id (pkc_dp_unique_id_bytes() bytes),
+ * shipped to the other ranks by the host; every rank: pkc_dp_comm_init on its GPU (device < 0:
+ * the current one), then pkc_dp_allreduce(comm, grads, n, stream) between the backward and the
+ * optimizer launches of each step, with the loss gradient pre-scaled by 1/world (or by the
+ * rank's share of the frames) so the sum is the gradient of the global mean loss.
+ * ------------------------------------------------------------------------------------------- */
+int pkc_dp_unique_id_bytes(void);
+int pkc_dp_unique_id(void* id_out);
+int pkc_dp_comm_init(void** comm_out, int world, const void* id, int rank, int device);
+int pkc_dp_allreduce(void* comm, float* buf, int64_t n, void* stream);
+int pkc_dp_comm_destroy(void* comm);
 
 #ifdef __cplusplus
 }

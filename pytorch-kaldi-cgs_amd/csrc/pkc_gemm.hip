@@ -229,21 +229,26 @@ __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, i
 
 // DEPTH k-tiles are in flight in registers at any time: with M = 128-row batches a workgroup's
 // k-range is only a few tiles long, so the whole range is requested up front instead of one
-// HBM/L2 round trip per tile.
+// HBM/L2 round trip per tile.  klist (block-sparse W): this tile's k-tiles are klist[1..klist[0]]
+// instead of the contiguous range; k-tiles past the list load clamped addresses as zeros.
 template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN>
 __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz, int M, int N, int K,
                                           const void* __restrict__ Av, int64_t lda,
                                           const void* __restrict__ Bv, int64_t ldb,
                                           float* __restrict__ C, int64_t ldc, int kchunk,
-                                          int64_t slab_stride) {
+                                          int64_t slab_stride,
+                                          const int32_t* __restrict__ klist = nullptr) {
   using SA = typename StageSel<BIN, AKC, VEC>::T;
   using SB = typename StageSel<BIN, BKC, VEC>::T;
   const auto* A = reinterpret_cast<const typename StageSel<BIN, AKC, VEC>::E*>(Av);
   const auto* B = reinterpret_cast<const typename StageSel<BIN, BKC, VEC>::E*>(Bv);
   constexpr int LD = Lds<PREC>::LD;
   const int n0 = bx * BN, m0 = by * BM;
-  const int kbeg = bz * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  const int kbeg = klist ? 0 : bz * kchunk;
+  const int kend = klist ? K : min(K, kbeg + kchunk);
+  const int nkt = klist ? klist[0] : (kend - kbeg + BK - 1) / BK;     // uniform
+  // first k of the i-th k-tile of this tile (kend: past the range, loads zeros)
+  auto k0_of = [&](int i) { return i < nkt ? (klist ? klist[1 + i] * BK : kbeg + i * BK) : kend; };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int r = lane & 31, h = lane >> 5;
@@ -254,21 +259,22 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
 
   SA sa[DEPTH];
   SB sb[DEPTH];
-  if (kbeg < kend) {   // uniform: an empty trailing split writes zeros
+  if (nkt > 0) {   // uniform: an empty trailing split (or an all-zero sparse tile) writes zeros
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
-      sa[d].load(A, lda, m0, M, kbeg + d * BK, kend);
-      sb[d].load(B, ldb, n0, N, kbeg + d * BK, kend);
+      const int k0 = k0_of(d);
+      sa[d].load(A, lda, m0, M, k0, kend);
+      sb[d].load(B, ldb, n0, N, k0, kend);
     }
-    // whole rounds of DEPTH k-tiles; tiles past kend load clamped addresses and contribute zeros
-    for (int kt = kbeg; kt < kend; kt += DEPTH * BK) {
+    // whole rounds of DEPTH k-tiles; tiles past the last one contribute zeros
+    for (int i0 = 0; i0 < nkt; i0 += DEPTH) {
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d) {
         __syncthreads();
         sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
         sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
         __syncthreads();
-        const int kn = kt + (d + DEPTH) * BK;
+        const int kn = k0_of(i0 + d + DEPTH);
         sa[d].load(A, lda, m0, M, kn, kend);
         sb[d].load(B, ldb, n0, N, kn, kend);
         mfma_tile<PREC, AKC, BKC>(sm, wm, wn, r, h, acc);
@@ -318,6 +324,7 @@ struct GroupProb {
   int M, N, K, kchunk, tn, tmn, wg0;
   const void* A; int64_t lda; const void* B; int64_t ldb; float* C; int64_t ldc; int64_t slab;
   const void* X1; void* X2; void* X3;
+  const int32_t* ktiles; int kmax;
 };
 struct GroupArgs {
   GroupProb p[GMAX];
@@ -367,9 +374,10 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
       return;
     }
   }
+  const int32_t* kl = p.ktiles ? p.ktiles + (int64_t)bx * (p.kmax + 1) : nullptr;
 #define PKC_GB(AK, BK_, V)                                                                      \
   gemm_body<PREC, AK, BK_, V, 4, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
-                                      p.ldc, p.kchunk, p.slab)
+                                      p.ldc, p.kchunk, p.slab, kl)
   switch (p.code) {
     case 7: PKC_GB(true, true, true); break;
     case 6: PKC_GB(true, true, false); break;
@@ -533,12 +541,14 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     if (q.M == 0 || q.N == 0) continue;
     PKC_CHECK_ARG(q.A && q.B && q.C, "pkc_gemm_grouped: problem %d null operand", i);
     int splits = q.splits <= 0 ? pkc_gemm_pick_splits(q.M, q.N, q.K) : q.splits;
+    PKC_CHECK_ARG(!q.ktiles || (splits == 1 && q.kmax >= 0),
+                  "pkc_gemm_grouped: problem %d: k-tile lists need splits == 1", i);
     PKC_CHECK_ARG(splits == 1 || q.slab_stride >= (int64_t)q.M * q.ldc,
                   "pkc_gemm_grouped: problem %d slab_stride too small", i);
     const bool vec = ((uintptr_t)q.A % 16 == 0) && ((uintptr_t)q.B % 16 == 0) && q.lda % e == 0 &&
                      q.ldb % e == 0 && (q.a_kcontig ? q.K % e == 0 : q.M % e == 0) &&
                      (q.b_kcontig ? q.K % e == 0 : q.N % e == 0);
-    const bool bigp = big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
+    const bool bigp = !q.ktiles && big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
                                                      q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED);
     any_big |= bigp;
     const int bk = bigp ? (prec == PKC_PREC_FP32 ? 32 : 64) : BK;
@@ -553,6 +563,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     p.tmn = p.tn * ((q.M + tm - 1) / tm);
     p.wg0 = wg;
     p.A = q.A; p.lda = q.lda; p.B = q.B; p.ldb = q.ldb; p.C = q.C; p.ldc = q.ldc; p.slab = q.slab_stride;
+    p.ktiles = q.ktiles; p.kmax = q.kmax;
     wg += p.tmn * splits;
   }
   g.n = k;

@@ -45,7 +45,8 @@ def _compile(src):
         return obj
     cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-x", "c++", "-c", src, "-o", obj]
+        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-x", "c++", "-c",
+               src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed on %s:\n%s" % (src, r.stderr[-6000:]))
@@ -62,7 +63,9 @@ def build(verbose=False):
     same = os.path.exists(stamp) and open(stamp).read() == listing
     if same and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB
-    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs
+    # RCCL: the pkc_dp_* all-reduce entry points for non-Python hosts
+    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + [
+        "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n%s" % r.stderr[-6000:])

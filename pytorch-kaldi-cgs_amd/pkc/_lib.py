@@ -73,7 +73,7 @@ class GemmProblem(C.Structure):
     _fields_ = [("a_kcontig", C.c_int), ("b_kcontig", C.c_int), ("M", C.c_int), ("N", C.c_int),
                 ("K", C.c_int), ("splits", C.c_int), ("A", vp), ("lda", i64), ("B", vp),
                 ("ldb", i64), ("C", vp), ("ldc", i64), ("slab_stride", i64), ("kind", C.c_int),
-                ("X1", vp), ("X2", vp), ("X3", vp)]
+                ("X1", vp), ("X2", vp), ("X3", vp), ("ktiles", vp), ("kmax", C.c_int)]
 
 
 OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM = 0, 1, 2, 3

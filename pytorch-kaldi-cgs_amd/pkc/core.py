@@ -244,6 +244,8 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
     elif seq_model:
         eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
                      train=(to_do == "train"), max_len=int(lens.max()), grad_scale=1.0 / ws_eff)
+        if ws_eff > 1:                  # frame-weighted sequence DP (pkc.dist.frame_weight)
+            eng.frame_weight = lambda rows: DP.frame_weight(rows, device=eng.dev)
         for net_name in nns:
             pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
             if pt != "none" and to_do == "train":

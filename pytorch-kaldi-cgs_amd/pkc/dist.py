@@ -73,6 +73,18 @@ def agree_min(n, device=None):
     return int(t.item())
 
 
+def frame_weight(rows, device=None):
+    """This rank's share of the rows of the global batch (its loss scale under sequence DP: the
+    padded T_r * B rows differ between ranks, so 1/R would weight a short batch's rows more than a
+    long one's).  One scalar all-reduce per step."""
+    rank, ws = world()
+    if ws == 1:
+        return 1.0
+    t = torch.tensor([float(rows)], dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return float(rows) / float(t.item())
+
+
 def sum_scalars(vals, device=None):
     """Element-wise sum of a list of floats over ranks."""
     rank, ws = world()
@@ -81,6 +93,42 @@ def sum_scalars(vals, device=None):
     t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
     dist.all_reduce(t)
     return [float(v) for v in t.cpu()]
+
+
+class CAbiAllReduce:
+    """The same exchange through libpkc's C ABI (pkc_dp_*: RCCL communicator of its own), as a
+    non-Python host would run it (include/pkc.h).  The unique id travels over the
+    torch.distributed default group (any channel works)."""
+
+    def __init__(self, device=0):
+        import ctypes as C
+
+        from . import _lib as L
+        self.L, self.C = L, C
+        rank, ws = world()
+        nb = L.lib().pkc_dp_unique_id_bytes()
+        idb = (C.c_char * nb)()
+        if rank == 0:
+            L.call("pkc_dp_unique_id", idb)
+        if ws > 1:
+            t = torch.frombuffer(bytearray(idb.raw), dtype=torch.uint8).clone()
+            dist.broadcast(t, 0)
+            C.memmove(idb, bytes(t.tolist()), nb)
+        self.comm = C.c_void_p()
+        L.call("pkc_dp_comm_init", C.byref(self.comm), ws, idb, rank, device)
+        self.calls = 0
+
+    def __call__(self, gflat, async_op=False):
+        self.calls += 1
+        s = torch.cuda.current_stream()
+        self.L.call("pkc_dp_allreduce", self.comm, self.L.ptr(gflat), gflat.numel(),
+                    self.C.c_void_p(s.cuda_stream))
+        return None
+
+    def close(self):
+        if self.comm:
+            self.L.call("pkc_dp_comm_destroy", self.comm)
+            self.comm = self.C.c_void_p()
 
 
 class GradAllReduce:

@@ -156,6 +156,36 @@ class Layer:
 # Block-sparse U in the recurrent step kernels for static HCGS masks: "auto" (when it cuts the
 # contraction), "force" (whenever the tiles fit, used by the parity tests) or "off".
 RNN_SPARSE = os.environ.get("PKC_RNN_SPARSE", "auto")
+# Block-sparse W matmuls (forward and dX) for static masks: "auto" (when at most this fraction of
+# the 64 x 32 weight tiles holds a nonzero), "force" (any saving) or "off".
+W_SPARSE = os.environ.get("PKC_W_SPARSE", "auto")
+W_SPARSE_MAX_FRAC = 0.75
+
+
+def ktile_table(mask, transpose, dev):
+    """k-tile lists of a block-sparse matmul (include/pkc.h pkc_gemm_problem.ktiles) for a static
+    (out, in) weight mask: forward Z = X W^T tiles 64 output units and lists the 32-wide input
+    blocks with a nonzero; dX = dZ W (transpose) tiles 64 inputs and lists the 32-wide output
+    blocks.  Returns (int32 device table [tiles, kmax + 1], kmax, kept fraction) or None."""
+    m = (mask.detach() != 0)
+    if transpose:
+        m = m.t()
+    R, K = m.shape
+    nt, nk = -(-R // 64), -(-K // 32)
+    pm = torch.zeros(nt * 64, nk * 32, dtype=torch.bool, device=m.device)
+    pm[:R, :K] = m
+    blocks = pm.view(nt, 64, nk, 32).any(3).any(1).cpu()          # [tile][k-tile]
+    counts = blocks.sum(1)
+    kmax = int(counts.max().item())
+    frac = float(counts.sum().item()) / (nt * nk)
+    if W_SPARSE == "off" or kmax >= nk or (W_SPARSE != "force" and frac > W_SPARSE_MAX_FRAC):
+        return None
+    tab = torch.full((nt, kmax + 1), -1, dtype=torch.int32)
+    for i in range(nt):
+        idx = torch.nonzero(blocks[i]).flatten()
+        tab[i, 0] = len(idx)
+        tab[i, 1:1 + len(idx)] = idx.to(torch.int32)
+    return tab.to(dev), kmax, frac
 
 
 class NormLayer(Layer):
@@ -355,6 +385,9 @@ class Engine:
         self.train = train
         self.seed = int(seed)
         self.grad_scale = float(grad_scale)    # 1/world_size under data parallelism
+        # sequence DP: callable(rows of this rank's batch) -> this rank's loss scale (set by the
+        # caller, pkc.dist.frame_weight), recomputed every step; None: the fixed grad_scale
+        self.frame_weight = None
         self.prof = None                       # profile mode: list of per-launch events
         self.F = max(c1 for _, c1 in fea_cols.values())
         self.fea_cols = fea_cols
@@ -372,6 +405,7 @@ class Engine:
         self._build_graph()
         self._alloc()
         self._build_masks()
+        self._build_wtiles()
         self._build_kmaps()
         self._build_optim()
         self._build_reg()
@@ -683,6 +717,31 @@ class Engine:
                             n.emask[id(p)] = eff[id(p)]
             elif n.W is not None and id(n.W) in eff:
                 n.mask = eff[id(n.W)]
+
+    def _build_wtiles(self):
+        """Block-sparse W (north_star: HCGS / pattern masks in the matmuls; HCGS.py:24-28,
+        neural_networks.py:258, 858-861): the forward and dX matmuls of a weight with a static
+        mask (no magnitude pruning, whose zeros move) skip the 64 x 32 weight tiles that are all
+        zero.  Masked entries stay exactly zero (masks applied at build and in every optimizer
+        update), so the skipped products are exact zeros and the sums are the dense ones.  dW
+        stays dense: the reference's optimizer also updates (and keeps state for) masked entries."""
+        self.wtiles = {}
+        for n in self.nodes:
+            if n.rec:
+                for li, sp in enumerate(n.layers):
+                    if sp.get("prune") is not None:
+                        continue
+                    for p, key, m in n.params():
+                        if m is not None and key[0] == "dW" and key[1] == li:
+                            self.wtiles[id(p)] = (ktile_table(m, False, self.dev),
+                                                  ktile_table(m, True, self.dev))
+            elif n.W is not None and n.mask is not None and n.spec.get("prune") is None:
+                self.wtiles[id(n.W)] = (ktile_table(n.mask, False, self.dev),
+                                        ktile_table(n.mask, True, self.dev))
+
+    def _wt(self, W, dx):
+        t = self.wtiles.get(id(W))
+        return t[1 if dx else 0] if t is not None else None
 
     def _build_kmaps(self):
         """Block-sparse U for static HCGS masks (liGRU / LSTM; no prune, pattern or quantised h,
@@ -997,20 +1056,24 @@ class Engine:
         """(label, flops, bytes, GemmProblem) of a dense layer's forward matmul Z = X W^T."""
         M = self.M
         a_ptr, lda = self._version(n, n.qv0 + n.reads)
-        sf = _splits(M, n.N, n.K, n.scap)
+        kt = self._wt(n.W, False)
+        sf = 1 if kt is not None else _splits(M, n.N, n.K, n.scap)
         n.sf = sf
         W = n.Wq if n.qbits else n.W
         pr = L.GemmProblem(a_kcontig=1, b_kcontig=1, M=M, N=n.N, K=n.K, splits=sf, A=a_ptr, lda=lda,
                            B=W.data_ptr(), ldb=n.K, C=n.zslab.data_ptr(), ldc=n.N,
                            slab_stride=M * n.N)
-        return ("fwd %dx%dx%d" % (M, n.N, n.K), 2.0 * M * n.N * n.K,
-                4.0 * (M * n.K + n.N * n.K + sf * M * n.N), pr)
+        d = 1.0
+        if kt is not None:
+            pr.ktiles, pr.kmax, d = kt[0].data_ptr(), kt[1], kt[2]
+        return ("fwd %dx%dx%d%s" % (M, n.N, n.K, " sparse %.2f" % d if kt is not None else ""),
+                2.0 * M * n.N * n.K * d, 4.0 * (M * n.K + n.N * n.K * d + sf * M * n.N), pr)
 
     def _gemms(self, probs, s):
         """Launch matmul problems: one pkc_gemm, or pkc_gemm_grouped for several (<= 8 each)."""
         for i in range(0, len(probs), 8):
             part = probs[i:i + 8]
-            if len(part) == 1 and part[0][3].kind == L.OP_GEMM:
+            if len(part) == 1 and part[0][3].kind == L.OP_GEMM and not part[0][3].ktiles:
                 lab, fl, nb, p = part[0]
                 self._k("gemm_" + lab, fl, nb, "pkc_gemm", self.prec, p.a_kcontig, p.b_kcontig,
                         p.M, p.N, p.K, C.c_void_p(p.A), p.lda, C.c_void_p(p.B), p.ldb,
@@ -1147,11 +1210,22 @@ class Engine:
             xin, _ = self._rec_inputs(n, li)
             for g in range(n.G):
                 x_ptr, ldx = xin[g]
-                sf = _splits(M, H, K, MAX_SPLITS)
-                self._k("rnn_gemm_W %dx%dx%d" % (M, H, K), 2.0 * M * H * K,
-                        4.0 * (M * K + H * K + sf * M * H), "pkc_gemm", self.prec, 1, 1, M, H, K,
-                        C.c_void_p(x_ptr), ldx, ptr(n.wq(li, "W", g)), K, ptr(lb["zslab"]), H, sf,
-                        M * H, s)
+                kt = self._wt(sp["W"][g], False)
+                if kt is not None:            # block-sparse W: one problem, k-tile lists
+                    sf = 1
+                    pr = L.GemmProblem(a_kcontig=1, b_kcontig=1, M=M, N=H, K=K, splits=1, A=x_ptr,
+                                       lda=ldx, B=n.wq(li, "W", g).data_ptr(), ldb=K,
+                                       C=lb["zslab"].data_ptr(), ldc=H, slab_stride=M * H,
+                                       ktiles=kt[0].data_ptr(), kmax=kt[1])
+                    self._k("rnn_gemm_W %dx%dx%d sparse %.2f" % (M, H, K, kt[2]),
+                            2.0 * M * H * K * kt[2], 4.0 * (M * K + H * K * kt[2] + M * H),
+                            "pkc_gemm_grouped", self.prec, C.byref(pr), 1, s)
+                else:
+                    sf = _splits(M, H, K, MAX_SPLITS)
+                    self._k("rnn_gemm_W %dx%dx%d" % (M, H, K), 2.0 * M * H * K,
+                            4.0 * (M * K + H * K + sf * M * H), "pkc_gemm", self.prec, 1, 1, M, H, K,
+                            C.c_void_p(x_ptr), ldx, ptr(n.wq(li, "W", g)), K, ptr(lb["zslab"]), H,
+                            sf, M * H, s)
                 bn = sp["bnm"][g]
                 a = L.DenseFwdArgs(
                     M=M, N=H, nslab=sf, zslab=lb["zslab"].data_ptr(), slab_stride=M * H,
@@ -1230,7 +1304,8 @@ class Engine:
         layers read the output (the heads' shared input; the fused small-batch BN backward sums at
         most 8 in registers); the widest consumer gives up splits first."""
         M = self.M
-        want = [1 if c.W is None else _splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
+        want = [1 if (c.W is None or self._wt(c.W, True) is not None)
+                else _splits(M, c.K, c.N, c.sxcap) for c in n.consumers]
         budget = SLAB_BUDGET_MULTI if len(n.consumers) > 1 and not self.cap else MAX_SPLITS
         while sum(want) > budget and max(want) > 1:
             want[want.index(max(want))] -= 1
@@ -1317,12 +1392,16 @@ class Engine:
             P = n.src[1]
             off = P.cons_off[P.consumers.index(n)]
             W = n.Wq if n.qbits else n.W
-            out.append(("dX %dx%dx%d" % (M, n.K, n.N), 2.0 * M * n.N * n.K,
-                        4.0 * (M * n.N + n.N * n.K + n.sx * M * n.K),
-                        L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=n.K, K=n.N, splits=n.sx,
-                                      A=n.dz.data_ptr(), lda=n.N, B=W.data_ptr(), ldb=n.K,
-                                      C=P.gslab.data_ptr() + 4 * off * M * P.N, ldc=n.K,
-                                      slab_stride=M * n.K)))
+            pr = L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=n.K, K=n.N, splits=n.sx,
+                               A=n.dz.data_ptr(), lda=n.N, B=W.data_ptr(), ldb=n.K,
+                               C=P.gslab.data_ptr() + 4 * off * M * P.N, ldc=n.K,
+                               slab_stride=M * n.K)
+            kt, d = self._wt(n.W, True), 1.0
+            if kt is not None:
+                pr.ktiles, pr.kmax, d = kt[0].data_ptr(), kt[1], kt[2]
+            out.append(("dX %dx%dx%d%s" % (M, n.K, n.N, " sparse %.2f" % d if kt is not None else ""),
+                        2.0 * M * n.N * n.K * d, 4.0 * (M * n.N + n.N * n.K * d + n.sx * M * n.K),
+                        pr))
         return out
 
     def _dense_bwd(self, n, s):
@@ -1369,11 +1448,22 @@ class Engine:
                         C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,
                         ptr(usrc), H, ptr(lb["dU"][g]), H, 1, 0, s)
                 if li > 0 or want_dx0:
-                    sx = _splits(M, K, H, MAX_SPLITS)
-                    self._k("rnn_gemm_dX %dx%dx%d" % (M, K, H), 2.0 * M * H * K,
-                            4.0 * (M * H + H * K + sx * M * K), "pkc_gemm", self.prec, 1, 0, M, K, H,
-                            dz, H, ptr(n.wq(li, "W", g)), K,
-                            C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
+                    kt = self._wt(sp["W"][g], True)
+                    if kt is not None:        # block-sparse W^T: one slab per gate
+                        sx = 1
+                        pr = L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=K, K=H, splits=1,
+                                           A=dz.value, lda=H, B=n.wq(li, "W", g).data_ptr(), ldb=K,
+                                           C=lb["dx"].data_ptr() + 4 * nx * M * K, ldc=K,
+                                           slab_stride=M * K, ktiles=kt[0].data_ptr(), kmax=kt[1])
+                        self._k("rnn_gemm_dX %dx%dx%d sparse %.2f" % (M, K, H, kt[2]),
+                                2.0 * M * H * K * kt[2], 4.0 * (M * H + H * K * kt[2] + M * K),
+                                "pkc_gemm_grouped", self.prec, C.byref(pr), 1, s)
+                    else:
+                        sx = _splits(M, K, H, MAX_SPLITS)
+                        self._k("rnn_gemm_dX %dx%dx%d" % (M, K, H), 2.0 * M * H * K,
+                                4.0 * (M * H + H * K + sx * M * K), "pkc_gemm", self.prec, 1, 0, M,
+                                K, H, dz, H, ptr(n.wq(li, "W", g)), K,
+                                C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
                     nx += sx
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
             if li == 0 and n.src[0] == "node":
@@ -1554,6 +1644,11 @@ class Engine:
         if self.seq:
             batch = batch or self.next_seq_batch()
             self._set_rows(batch)
+            if self.frame_weight is not None:
+                # sequence DP: rank r's padded batch has T_r * B rows; scale its mean loss by its
+                # share of all ranks' rows, so the summed gradient is that of the mean over every
+                # row of the global batch, not the mean of unequal batch means
+                self.grad_scale = self.frame_weight(self.M)
             self._train_step_kernels(allreduce, batch)
             self.ctr.add_(1)           # step counter of the dropout RNG streams
         elif self.graph is not None:

@@ -146,3 +146,42 @@ def test_dp_gradient_equals_full_batch():
     g0, g1 = _run(_mlp_grads, 2, 32)
     np.testing.assert_array_equal(g0, g1)        # replicas receive identical gradients
     np.testing.assert_allclose(g0, full, rtol=1e-5, atol=1e-8)
+
+
+def _mlp_grads_uneven(rank, ws, cuts):
+    """Frame-weighted DP (pkc.dist.frame_weight, the sequence-model scaling): rank r holds rows
+    [cuts[r], cuts[r+1]) of one global batch (unequal shares, as unequal padded T_r * B), scales
+    its mean loss by its share of the rows, and the summed gradient is the full-batch gradient."""
+    from oracle import nets as ON
+    from pkc import dist as DP
+    cfg = build_mlp_config("plain")
+    body = dict(cfg["architecture1"])
+    body.update(dnn_use_batchnorm="False,False")
+    cfg["architecture1"] = body
+    torch.manual_seed(5)
+    np.random.seed(5)
+    net1 = ON.MLP(cfg["architecture1"], 40)
+    net2 = ON.MLP(cfg["architecture2"], 32)
+    rs = np.random.RandomState(12)
+    B = cuts[-1]
+    x = torch.from_numpy(rs.normal(size=(B, 40)).astype(np.float32))
+    y = torch.from_numpy(rs.randint(0, 96, size=B).astype(np.int64))
+    r0, r1 = (cuts[rank], cuts[rank + 1]) if ws > 1 else (0, B)
+    w = DP.frame_weight(r1 - r0)
+    logp = net2(net1(x[r0:r1]))
+    loss, _ = ON.nll_err(logp, y[r0:r1])
+    (loss * w).backward()
+    flat = torch.cat([p.grad.reshape(-1) for p in list(net1.parameters()) + list(net2.parameters())
+                      if p.grad is not None])
+    if ws > 1:
+        DP.GradAllReduce()(flat)
+    return w, flat.numpy()
+
+
+def test_dp_frame_weighted_gradient_equals_full_batch():
+    cuts = [0, 30, 40]
+    _, full = _mlp_grads_uneven(0, 1, cuts)
+    (w0, g0), (w1, g1) = _run(_mlp_grads_uneven, 2, cuts)
+    assert (w0, w1) == (0.75, 0.25)
+    np.testing.assert_array_equal(g0, g1)
+    np.testing.assert_allclose(g0, full, rtol=1e-5, atol=1e-8)

@@ -55,3 +55,33 @@ def test_dp_engine_two_ranks_equal_full_batch(mode, tmp_path):
             continue
         np.testing.assert_allclose(g0[k], v, rtol=1e-4, atol=1e-6, err_msg=k)
     np.testing.assert_allclose(float(g0["loss"]), loss, rtol=1e-5)
+
+
+def test_dp_c_abi_allreduce_world1():
+    """The C-ABI data-parallel exchange (include/pkc.h pkc_dp_*: RCCL communicator inside libpkc,
+    for hosts without torch.distributed) on a one-rank world: the all-reduce is the identity, and
+    an Engine step that exchanges its gradients through it equals a step without exchange."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dp_engine_worker as W
+    from pkc import dist as DP
+    ar = DP.CAbiAllReduce(device=0)
+    try:
+        x = torch.randn(1000003, device="cuda")
+        ref = x.clone()
+        ar(x)
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref)
+        X, lab = W.data(STEPS, B)
+        states = []
+        for use in (False, True):
+            eng, nets = W.build(W.dp_config(), 1, B, X, lab)
+            for _ in range(STEPS):
+                eng.train_step(ar if use else None)
+            torch.cuda.synchronize()
+            states.append({a + "/" + k: v.detach().cpu() for a in nets
+                           for k, v in nets[a].state_dict().items()})
+        for k in states[0]:
+            assert torch.equal(states[0][k], states[1][k]), k
+        assert ar.calls >= STEPS + 1
+    finally:
+        ar.close()

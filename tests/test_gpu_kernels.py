@@ -435,3 +435,44 @@ def test_gemm_grouped_big(L, prec):
     for (orient, M, N, K, sp), ref, Cd in zip(specs, refs, keep[2::3]):
         tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
         torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=tol)
+
+
+@pytest.mark.parametrize("prec", [0, 2])
+@pytest.mark.parametrize("M", [128, 2400])
+def test_gemm_block_sparse_matches_dense(L, prec, M):
+    """Block-sparse W (k-tile lists from a static mask, pkc.engine.ktile_table): forward
+    Z = X (W*mask)^T and dX = dZ (W*mask) skip the all-zero 64x32 weight tiles and give exactly
+    the dense matmul's result (the skipped products are zero weights)."""
+    from pkc.engine import ktile_table
+    g = torch.Generator().manual_seed(M)
+    N_out, K_in = 550, 440
+    blk = (torch.rand(-(-N_out // 32), -(-K_in // 32), generator=g) < 0.25).float()
+    mask = blk.repeat_interleave(32, 0).repeat_interleave(32, 1)[:N_out, :K_in]
+    mask = mask * (torch.rand(N_out, K_in, generator=g) < 0.5).float()   # level-2 zeros inside
+    W = torch.randn(N_out, K_in, generator=g) * mask
+    X = torch.randn(M, K_in, generator=g)
+    dZ = torch.randn(M, N_out, generator=g)
+    dt = torch.bfloat16 if prec == 2 else torch.float32
+    Wd, Xd, dZd = W.to(DEV, dt), X.to(DEV, dt), dZ.to(DEV, dt)
+    for transpose in (False, True):
+        kt = ktile_table(mask.to(DEV), transpose, DEV)
+        assert kt is not None and kt[2] < 0.6
+        if not transpose:   # Z[M, N_out] = X W^T
+            shape = dict(a_kcontig=1, b_kcontig=1, M=M, N=N_out, K=K_in, A=Xd.data_ptr(), lda=K_in,
+                         B=Wd.data_ptr(), ldb=K_in)
+            Mo, No = M, N_out
+        else:               # dX[M, K_in] = dZ W
+            shape = dict(a_kcontig=1, b_kcontig=0, M=M, N=K_in, K=N_out, A=dZd.data_ptr(), lda=N_out,
+                         B=Wd.data_ptr(), ldb=K_in)
+            Mo, No = M, K_in
+        outs = []
+        for sparse in (False, True):
+            Cd = torch.full((Mo, No), float("nan"), device=DEV)
+            extra = dict(ktiles=kt[0].data_ptr(), kmax=kt[1]) if sparse else {}
+            pr = L.GemmProblem(splits=1, C=Cd.data_ptr(), ldc=No, slab_stride=Mo * No, **shape, **extra)
+            L.call("pkc_gemm_grouped", prec, C.byref(pr), 1, _s())
+            outs.append(Cd.cpu())
+        torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0)
+        ref = (X.double() @ W.double().t()) if not transpose else (dZ.double() @ W.double())
+        if prec == 0:
+            torch.testing.assert_close(outs[1], ref.float(), rtol=1e-4, atol=1e-3)

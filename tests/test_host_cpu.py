@@ -248,3 +248,26 @@ def test_product_kmeans_pattern_search_matches_reference(tag):
     k = kmeans_patterns(torch.from_numpy(g[tag + "_w"]), num, [ph, pw], nnz, random_state=0)
     np.testing.assert_array_equal(k, g[tag + "_kernel"])
     assert (k.reshape(k.shape[0], -1).sum(1) == nnz).all()
+
+
+def test_dropin_core_module_replaces_run_nn(tmp_path):
+    """pytorch-kaldi-cgs_amd/dropin/core.py ahead of a reference checkout on sys.path: run_exp's
+    `importlib.import_module('core')` (run_exp.py:81-83) gets pkc's run_nn and every other name of
+    the reference's core.py (a stand-in file here, so the test needs no reference)."""
+    import importlib
+    import subprocess
+    import sys
+    ref = tmp_path / "ref"
+    ref.mkdir()
+    (ref / "core.py").write_text("def run_nn(*a):\n    return 'reference'\n"
+                                 "def read_next_chunk_into_shared_list_with_subprocess():\n"
+                                 "    return 'helper'\n")
+    code = ("import importlib, sys; m = importlib.import_module('core'); "
+            "import pkc.core; assert m.run_nn is pkc.core.run_nn; "
+            "assert m.read_next_chunk_into_shared_list_with_subprocess() == 'helper'; print('ok')")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([
+        os.path.join(ROOT, "pytorch-kaldi-cgs_amd", "dropin"), os.path.join(ROOT, "pytorch-kaldi-cgs_amd"),
+        str(ref)]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
