@@ -229,10 +229,69 @@ __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, i
 
 // DEPTH k-tiles are in flight in registers at any time: with M = 128-row batches a workgroup's
 // k-range is only a few tiles long, so the whole range is requested up front instead of one
-// HBM/L2 round trip per tile.  klist (block-sparse W): this tile's k-tiles are klist[1..klist[0]]
-// instead of the contiguous range; k-tiles past the list load clamped addresses as zeros.
+// HBM/L2 round trip per tile.
 template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN>
 __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz, int M, int N, int K,
+                                          const void* __restrict__ Av, int64_t lda,
+                                          const void* __restrict__ Bv, int64_t ldb,
+                                          float* __restrict__ C, int64_t ldc, int kchunk,
+                                          int64_t slab_stride) {
+  using SA = typename StageSel<BIN, AKC, VEC>::T;
+  using SB = typename StageSel<BIN, BKC, VEC>::T;
+  const auto* A = reinterpret_cast<const typename StageSel<BIN, AKC, VEC>::E*>(Av);
+  const auto* B = reinterpret_cast<const typename StageSel<BIN, BKC, VEC>::E*>(Bv);
+  constexpr int LD = Lds<PREC>::LD;
+  const int n0 = bx * BN, m0 = by * BM;
+  const int kbeg = bz * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  SA sa[DEPTH];
+  SB sb[DEPTH];
+  if (kbeg < kend) {   // uniform: an empty trailing split writes zeros
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      sa[d].load(A, lda, m0, M, kbeg + d * BK, kend);
+      sb[d].load(B, ldb, n0, N, kbeg + d * BK, kend);
+    }
+    // whole rounds of DEPTH k-tiles; tiles past kend load clamped addresses and contribute zeros
+    for (int kt = kbeg; kt < kend; kt += DEPTH * BK) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        __syncthreads();
+        sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
+        sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+        __syncthreads();
+        const int kn = kt + (d + DEPTH) * BK;
+        sa[d].load(A, lda, m0, M, kn, kend);
+        sb[d].load(B, ldb, n0, N, kn, kend);
+        mfma_tile<PREC, AKC, BKC>(sm, wm, wn, r, h, acc);
+      }
+    }
+  }
+  // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  const int col = n0 + wn * 32 + r;
+  float* Cz = C + (int64_t)bz * slab_stride;
+  if (col < N) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = m0 + wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < M) Cz[(int64_t)row * ldc + col] = acc[reg];
+    }
+  }
+}
+
+// Block-sparse W (klist): the tile's k-tiles are klist[1..klist[0]] instead of a contiguous
+// range; k-tiles past the list load clamped addresses as zeros.  A body of its own, so the dense
+// body (the latency-bound B = 128 launches) keeps its exact instruction stream.
+template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN, bool SPARSE = true>
+__device__ __forceinline__ void gemm_body_sparse(Lds<PREC>& sm, int bx, int by, int bz, int M, int N, int K,
                                           const void* __restrict__ Av, int64_t lda,
                                           const void* __restrict__ Bv, int64_t ldb,
                                           float* __restrict__ C, int64_t ldc, int kchunk,
@@ -244,11 +303,16 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
   const auto* B = reinterpret_cast<const typename StageSel<BIN, BKC, VEC>::E*>(Bv);
   constexpr int LD = Lds<PREC>::LD;
   const int n0 = bx * BN, m0 = by * BM;
-  const int kbeg = klist ? 0 : bz * kchunk;
-  const int kend = klist ? K : min(K, kbeg + kchunk);
-  const int nkt = klist ? klist[0] : (kend - kbeg + BK - 1) / BK;     // uniform
-  // first k of the i-th k-tile of this tile (kend: past the range, loads zeros)
-  auto k0_of = [&](int i) { return i < nkt ? (klist ? klist[1 + i] * BK : kbeg + i * BK) : kend; };
+  // (the list logic is compiled only into the SPARSE instances: the dense ones stay as lean as
+  // they were, which the latency-bound B = 128 launches notice)
+  const int kbeg = SPARSE ? 0 : bz * kchunk;
+  const int kend = SPARSE ? K : min(K, kbeg + kchunk);
+  const int nkt = SPARSE ? klist[0] : (kend - kbeg + BK - 1) / BK;     // uniform
+  // first k of the i-th k-tile of this tile (dense: past kend loads zeros; sparse: kend)
+  auto k0_of = [&](int i) {
+    if constexpr (SPARSE) return i < nkt ? klist[1 + i] * BK : kend;
+    else return kbeg + i * BK;
+  };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int r = lane & 31, h = lane >> 5;
@@ -331,11 +395,16 @@ struct GroupArgs {
   int n;
 };
 
-template <int PREC, bool BIN, bool BIG>
+template <int PREC, bool BIN, bool BIG, bool SP = false>
 __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
   // BIG: at least one problem takes the 128x128 body; its LDS also holds the 64x64 tiles
-  __shared__ __attribute__((aligned(16))) char lds[BIG ? big::LDS_BYTES : sizeof(Lds<PREC>)];
-  Lds<PREC>& sm = *reinterpret_cast<Lds<PREC>*>(lds);
+  union alignas(16) Shm {
+    Lds<PREC> t;
+    char big[BIG ? big::LDS_BYTES : 16];
+  };
+  __shared__ Shm shm;
+  Lds<PREC>& sm = shm.t;
+  char* lds = shm.big;
   int i = 0;
 #pragma unroll
   for (int j = 1; j < GMAX; ++j)
@@ -374,10 +443,23 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
       return;
     }
   }
-  const int32_t* kl = p.ktiles ? p.ktiles + (int64_t)bx * (p.kmax + 1) : nullptr;
+  if (SP && p.ktiles) {              // block-sparse W: forward (B = W) and dX (B = W^T) forms
+    const int32_t* kl = p.ktiles + (int64_t)bx * (p.kmax + 1);
+#define PKC_GS(AK, BK_, V)                                                                      \
+  gemm_body_sparse<PREC, AK, BK_, V, 4, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B,     \
+                                            p.ldb, p.C, p.ldc, p.kchunk, p.slab, kl)
+    switch (p.code & 7) {
+      case 7: PKC_GS(true, true, true); break;
+      case 6: PKC_GS(true, true, false); break;
+      case 5: PKC_GS(true, false, true); break;
+      default: PKC_GS(true, false, false); break;
+    }
+#undef PKC_GS
+    return;
+  }
 #define PKC_GB(AK, BK_, V)                                                                      \
   gemm_body<PREC, AK, BK_, V, 4, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
-                                      p.ldc, p.kchunk, p.slab, kl)
+                                      p.ldc, p.kchunk, p.slab)
   switch (p.code) {
     case 7: PKC_GB(true, true, true); break;
     case 6: PKC_GB(true, true, false); break;
@@ -438,8 +520,11 @@ static int dispatch(int akc, int bkc, bool vec, int M, int N, int K, const void*
 }
 
 // The 128x128 body takes a matmul with at least this many output tiles (alone: enough to fill the
-// chip; in a grouped launch the other problems fill it).  PKC_GEMM_BIG=0 disables it (A/B runs).
-constexpr int BIG_MIN_TILES = 160, BIG_MIN_TILES_GROUPED = 32;
+// chip; in a grouped launch the other problems fill it).  In a grouped launch it also needs a long
+// contraction: its 64 KB of LDS cuts the residency of every other workgroup of the launch, which
+// the B = 128 step's short dW (K = 128) launches cannot afford (681k -> 627k frames/s when they
+// took it).  PKC_GEMM_BIG=0 disables it (A/B runs).
+constexpr int BIG_MIN_TILES = 160, BIG_MIN_TILES_GROUPED = 32, BIG_MIN_K_GROUPED = 1024;
 static bool big_enabled() {
   static const int on = [] {
     const char* v = getenv("PKC_GEMM_BIG");
@@ -510,7 +595,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   GroupArgs g;
   memset(&g, 0, sizeof(g));
   int wg = 0, k = 0;
-  bool any_big = false;
+  bool any_big = false, any_sparse = false;
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   for (int i = 0; i < n; ++i) {
     const pkc_gemm_problem& q = probs[i];
@@ -541,16 +626,19 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     if (q.M == 0 || q.N == 0) continue;
     PKC_CHECK_ARG(q.A && q.B && q.C, "pkc_gemm_grouped: problem %d null operand", i);
     int splits = q.splits <= 0 ? pkc_gemm_pick_splits(q.M, q.N, q.K) : q.splits;
-    PKC_CHECK_ARG(!q.ktiles || (splits == 1 && q.kmax >= 0),
-                  "pkc_gemm_grouped: problem %d: k-tile lists need splits == 1", i);
+    PKC_CHECK_ARG(!q.ktiles || (splits == 1 && q.kmax >= 0 && q.a_kcontig),
+                  "pkc_gemm_grouped: problem %d: k-tile lists need splits == 1 and a k-contiguous A",
+                  i);
     PKC_CHECK_ARG(splits == 1 || q.slab_stride >= (int64_t)q.M * q.ldc,
                   "pkc_gemm_grouped: problem %d slab_stride too small", i);
     const bool vec = ((uintptr_t)q.A % 16 == 0) && ((uintptr_t)q.B % 16 == 0) && q.lda % e == 0 &&
                      q.ldb % e == 0 && (q.a_kcontig ? q.K % e == 0 : q.M % e == 0) &&
                      (q.b_kcontig ? q.K % e == 0 : q.N % e == 0);
     const bool bigp = !q.ktiles && big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
-                                                     q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED);
+                                                     q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED,
+                                                     BIG_MIN_K_GROUPED);
     any_big |= bigp;
+    any_sparse |= q.ktiles != nullptr;
     const int bk = bigp ? (prec == PKC_PREC_FP32 ? 32 : 64) : BK;
     int kchunk = (q.K + splits - 1) / splits;
     kchunk = ((kchunk + bk - 1) / bk) * bk;
@@ -568,9 +656,14 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   }
   g.n = k;
   if (k == 0) return PKC_OK;
+  // separate instances for launches with 128x128 problems (64 KB of LDS) and with block-sparse
+  // k-tile lists, so the plain launches of the B = 128 step keep their lean code and residency
 #define PKC_GL(P, BIN)                                                                          \
   do {                                                                                          \
-    if (any_big)                                                                                \
+    if (any_sparse)                                                                             \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false, true>), dim3(wg), dim3(NT), 0,      \
+                         S(stream), g);                                                         \
+    else if (any_big)                                                                           \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, true>), dim3(wg), dim3(NT), 0, S(stream), g);  \
     else                                                                                        \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false>), dim3(wg), dim3(NT), 0, S(stream), g); \

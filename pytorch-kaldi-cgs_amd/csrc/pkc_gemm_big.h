@@ -311,7 +311,8 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
 // Which problems take this body: 16-byte operand paths (aligned bases and leading dimensions,
 // contiguous extents multiples of a chunk) and enough 128x128 tiles to fill the chip.
 __host__ inline bool eligible(int prec, int akc, int bkc, int M, int N, int K, const void* A,
-                              int64_t lda, const void* B, int64_t ldb, int min_tiles) {
+                              int64_t lda, const void* B, int64_t ldb, int min_tiles,
+                              int min_k = 128) {
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
                    ldb % e == 0 && (akc ? K % e == 0 : M % e == 0) && (bkc ? K % e == 0 : N % e == 0);
@@ -320,7 +321,7 @@ __host__ inline bool eligible(int prec, int akc, int bkc, int M, int N, int K, c
   // balances better over the CUs (C4's projections: 83 vs 73 TF/s, same run); the 128x128 tile
   // wins only once there are several tiles per CU (4096^3: 118 vs 109 TF/s)
   if (prec == PKC_PREC_FP32) min_tiles = min_tiles > 1024 ? min_tiles : 1024;
-  return vec && tiles >= min_tiles && K >= 128;
+  return vec && tiles >= min_tiles && K >= min_k;
 }
 
 }  // namespace big
