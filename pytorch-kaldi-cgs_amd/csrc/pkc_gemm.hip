@@ -134,6 +134,30 @@ struct Stage {
   }
 };
 
+// [k][row] image of an m-contiguous bf16 64x32 operand tile: 32 k-rows of 64 elements (128 B),
+// 16-byte chunk c of k-row k at chunk c ^ (((k >> 1) & 1) << 2).  A transposed fragment read of one
+// 32-lane half touches 4 consecutive k-rows x 64 contiguous bytes: the XOR moves k-rows k + 2, k + 3
+// to the other 64-byte half, so the four land on 64 distinct banks (conflict-free).
+__device__ __forceinline__ int tr_off_s(int k, int c) { return 128 * k + 16 * (c ^ (((k >> 1) & 1) << 2)); }
+
+// 32x32x16 operand fragment (lane l: row rb + (l & 31), k = kb + 8 (l >> 5) + j) from that image:
+// two ds_read_b64_tr_b16 (lane 4q + p of a 16-lane group addresses k-row k0 + q, rows 4p .. 4p + 3
+// of the group's 16; lane i receives row i of the 4 k-rows).
+__device__ __forceinline__ bf16x8 tr_frag_s(const char* __restrict__ s, int rb, int kb, int lane) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  typedef __attribute__((address_space(3))) v4s lv4s;
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int row = rb + 16 * ((lane >> 4) & 1) + 4 * p;
+  const int k0 = kb + 8 * (lane >> 5) + q;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lv4s*)(s + tr_off_s(k0, row >> 3) + 8 * (p & 1)));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lv4s*)(s + tr_off_s(k0 + 4, row >> 3) + 8 * (p & 1)));
+  const v8s w = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 __device__ __forceinline__ bf16x8 ld8h(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ bf16x8 zero8h() {
   bf16x8 z;
@@ -177,9 +201,10 @@ struct StageH {
       const int r = t >> 2, k = (t & 3) * 8;
       *reinterpret_cast<bf16x8*>(&s[r * LD + k]) = v;
     } else {
+      // m-contiguous: the 8 rows of one k as they lie, into the [k][row] image (tr_off_s), read
+      // back by the transposing fragment read (tr_frag_s) instead of 8 two-byte column writes
       const int k = t >> 3, r = (t & 7) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s[(r + j) * LD + k] = v[j];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(s) + tr_off_s(k, r >> 3)) = v;
     }
   }
 };
@@ -195,7 +220,9 @@ struct StageSel<true, KC, VEC> {
   using E = __bf16;
 };
 
-template <int PREC, bool AKC, bool BKC>
+// ATR / BTR: the operand sits in LDS as a [k][row] image (bf16 m-contiguous operands stored as
+// bf16: StageH) and is read with tr_frag_s
+template <int PREC, bool AKC, bool BKC, bool ATR = false, bool BTR = false>
 __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, int r, int h,
                                           f32x16& acc) {
   constexpr int LD = Lds<PREC>::LD;
@@ -218,10 +245,14 @@ __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, i
     for (int kk = 0; kk < 16; ++kk)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc, 0, 0, 0);
   } else {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      bf16x8 av = *reinterpret_cast<const bf16x8*>(&sm.a[(wm * 32 + r) * LD + 16 * t + 8 * h]);
-      bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sm.b[(wn * 32 + r) * LD + 16 * t + 8 * h]);
+      bf16x8 av, bv;
+      if constexpr (ATR) av = tr_frag_s(reinterpret_cast<const char*>(sm.a), wm * 32, 16 * t, lane);
+      else av = *reinterpret_cast<const bf16x8*>(&sm.a[(wm * 32 + r) * LD + 16 * t + 8 * h]);
+      if constexpr (BTR) bv = tr_frag_s(reinterpret_cast<const char*>(sm.b), wn * 32, 16 * t, lane);
+      else bv = *reinterpret_cast<const bf16x8*>(&sm.b[(wn * 32 + r) * LD + 16 * t + 8 * h]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
     }
   }
@@ -271,7 +302,7 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
         const int kn = kt + (d + DEPTH) * BK;
         sa[d].load(A, lda, m0, M, kn, kend);
         sb[d].load(B, ldb, n0, N, kn, kend);
-        mfma_tile<PREC, AKC, BKC>(sm, wm, wn, r, h, acc);
+        mfma_tile<PREC, AKC, BKC, BIN && !AKC, BIN && !BKC>(sm, wm, wn, r, h, acc);
       }
     }
   }
@@ -341,7 +372,7 @@ __device__ __forceinline__ void gemm_body_sparse(Lds<PREC>& sm, int bx, int by, 
         const int kn = k0_of(i0 + d + DEPTH);
         sa[d].load(A, lda, m0, M, kn, kend);
         sb[d].load(B, ldb, n0, N, kn, kend);
-        mfma_tile<PREC, AKC, BKC>(sm, wm, wn, r, h, acc);
+        mfma_tile<PREC, AKC, BKC, BIN && !AKC, BIN && !BKC>(sm, wm, wn, r, h, acc);
       }
     }
   }

@@ -36,6 +36,33 @@ constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;   // A and B, double-buffered (64 
 
 __device__ __forceinline__ int swz(int r) { return ((r >> 1) ^ (r >> 4)) & 7; }
 
+// [k][row] image of a bf16 m-contiguous operand tile: 64 k-rows of 128 elements (256 B), 16-byte
+// chunk c of k-row k at chunk c ^ xr(k).  The transposed fragment read (tr_frag) of one 32-lane
+// half touches 4 consecutive k-rows x 4 consecutive chunks (c0 % 4 == 0): the XOR puts them on 16
+// distinct chunks = all 64 banks (conflict-free); the 16-byte staging stores fill whole k-rows.
+__device__ __forceinline__ int tr_off(int k, int c) {
+  return 256 * k + 16 * (c ^ (((k & 3) << 2) | ((k >> 2) & 3)));
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// 32x32x16 bf16 operand fragment (lane l: row rb + (l & 31), k = kb + 8 (l >> 5) + j, j = 0..7) from
+// a [k][row] image: two ds_read_b64_tr_b16, each giving a lane 4 consecutive k of its row.  Lane
+// 4q + p of a 16-lane group addresses k-row (k0 + q), rows 4p .. 4p + 3 of the group's 16.
+__device__ __forceinline__ bf16x8 tr_frag(const char* __restrict__ s, int rb, int kb, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int row = rb + 16 * ((lane >> 4) & 1) + 4 * p;
+  const int k0 = kb + 8 * (lane >> 5) + q;
+  typedef __attribute__((address_space(3))) v4s lv4s;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lv4s*)(s + tr_off(k0, row >> 3) + 8 * (p & 1)));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lv4s*)(s + tr_off(k0 + 4, row >> 3) + 8 * (p & 1)));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s w = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 // Element type in HBM (HE) and in LDS (LE); BK = k per LDS row.
 template <int PREC, bool BIN>
 struct Cfg {
@@ -66,7 +93,11 @@ struct Stage {
   static constexpr int BK = C::BK;
   static constexpr int EPC = 16 / sizeof(HE);                  // elements per 16-byte chunk
   static constexpr int NCH = TM * BK / EPC / NT;               // chunks per thread (4 or 8)
-  static constexpr bool PAIR = !KC && sizeof(LE) == 2;         // pack k, k+1 into dwords
+  // bf16 m-contiguous operands stored as bf16 (BIN): staged as they lie, a [k][row] image read
+  // back with the transposing ds_read_b64_tr_b16 (tr_frag); fp32 ones converted to bf16 on the way
+  // (PAIR): two k-adjacent chunks packed into dwords and stored transposed
+  static constexpr bool TR = !KC && sizeof(HE) == 2 && sizeof(LE) == 2;
+  static constexpr bool PAIR = !KC && sizeof(LE) == 2 && !TR;
   float4 v[NCH];
 
   // chunk i of this thread -> (row, k) of its first element
@@ -136,6 +167,8 @@ struct Stage {
           h.y = bf16bits(v[i].z) | (bf16bits(v[i].w) << 16);
           *reinterpret_cast<uint2*>(dst) = h;
         }
+      } else if (TR) {
+        *reinterpret_cast<float4*>(s + tr_off(k, r >> 3)) = v[i];
       } else if (PAIR) {
         if (i & 1) continue;                                   // handled with its even partner
         const int kb = k * 2;
@@ -170,7 +203,7 @@ __device__ __forceinline__ float4 lds16(const char* s, int r, int c) {
 }
 
 // MFMAs of one k-tile for this wave's 64x64 sub-tile (rows wm*64 + 32a, cols wn*64 + 32b).
-template <int PREC>
+template <int PREC, bool ATR = false, bool BTR = false>
 __device__ __forceinline__ void tile_mfma(const char* __restrict__ sa, const char* __restrict__ sb,
                                           int wm, int wn, int lane, f32x16 (&acc)[2][2]) {
   const int r = lane & 31, h = lane >> 5;
@@ -205,13 +238,21 @@ __device__ __forceinline__ void tile_mfma(const char* __restrict__ sa, const cha
       bf16x8 av[2], bv[2];
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        const float4 x = lds16(sa, wm * 64 + 32 * a + r, 2 * t + h);
-        av[a] = *reinterpret_cast<const bf16x8*>(&x);
+        if constexpr (ATR) {
+          av[a] = tr_frag(sa, wm * 64 + 32 * a, 16 * t, lane);
+        } else {
+          const float4 x = lds16(sa, wm * 64 + 32 * a + r, 2 * t + h);
+          av[a] = *reinterpret_cast<const bf16x8*>(&x);
+        }
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const float4 y = lds16(sb, wn * 64 + 32 * b + r, 2 * t + h);
-        bv[b] = *reinterpret_cast<const bf16x8*>(&y);
+        if constexpr (BTR) {
+          bv[b] = tr_frag(sb, wn * 64 + 32 * b, 16 * t, lane);
+        } else {
+          const float4 y = lds16(sb, wn * 64 + 32 * b + r, 2 * t + h);
+          bv[b] = *reinterpret_cast<const bf16x8*>(&y);
+        }
       }
 #pragma unroll
       for (int a = 0; a < 2; ++a)
@@ -273,7 +314,8 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
     for (int t = 0; t < nk; ++t) {
       char* cur = lds + (t & 1) * 2 * TILE_BYTES;
       char* nxt = lds + ((t + 1) & 1) * 2 * TILE_BYTES;
-      tile_mfma<PREC>(cur, cur + TILE_BYTES, wm, wn, lane, acc);
+      tile_mfma<PREC, Stage<PREC, BIN, AKC>::TR, Stage<PREC, BIN, BKC>::TR>(cur, cur + TILE_BYTES,
+                                                                         wm, wn, lane, acc);
       if (t + 1 < nk) {                               // uniform
         na.store(nxt);
         nb.store(nxt + TILE_BYTES);

@@ -50,6 +50,27 @@ def main():
         us = e0.elapsed_time(e1) * 1000.0 / reps
         out[lab] = {"us": round(us, 2), "tflops": round(2.0 * M * N * K / us / 1e6, 1), "splits": splits}
         print(lab, out[lab], flush=True)
+        if "mlp" not in lab:
+            continue
+        # the same matmul as a one-problem grouped launch (the engine's form at large batches:
+        # 128x128 tiles from 32 tiles up), split-K 1 / 2 / 4
+        for sp in (1, 2, 4):
+            Cg = torch.empty(sp, M, N, device="cuda")
+            pr = L.GemmProblem(a_kcontig=akc, b_kcontig=bkc, M=M, N=N, K=K, splits=sp, A=L.ptr(A),
+                               lda=A.shape[1], B=L.ptr(B), ldb=B.shape[1], C=L.ptr(Cg), ldc=N,
+                               slab_stride=M * N)
+            arr = (L.GemmProblem * 1)(pr)
+            for _ in range(3):
+                L.call("pkc_gemm_grouped", prec, arr, 1, L.C.c_void_p(s.cuda_stream))
+            e0.record()
+            for _ in range(reps):
+                L.call("pkc_gemm_grouped", prec, arr, 1, L.C.c_void_p(s.cuda_stream))
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1000.0 / reps
+            key = lab + " grouped s%d" % sp
+            out[key] = {"us": round(us, 2), "tflops": round(2.0 * M * N * K / us / 1e6, 1)}
+            print(key, out[key], flush=True)
     print(json.dumps(out))
 
 
