@@ -397,6 +397,7 @@ __device__ __forceinline__ void tile_blocks(const int32_t* row, int* blk) {
 
 // Sum the four waves' 32x16 partial tiles (MFMA C layout: col = lane & 15, row = 4*(lane>>4)+i)
 // into tile[32][17]; red is [4][32][17] scratch.  Ends with a barrier.
+template <int NW = 4>
 __device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1, float* red,
                                             float* tile) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -408,10 +409,13 @@ __device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1
     rw[(16 + 4 * q + i) * 17 + c] = acc1[i];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 32 * 16; e += RT) {
+  for (int e = threadIdx.x; e < 32 * 16; e += 64 * NW) {
     const int r = e >> 4, cc = e & 15;
     const int o = r * 17 + cc;
-    tile[o] = (red[o] + red[32 * 17 + o]) + (red[2 * 32 * 17 + o] + red[3 * 32 * 17 + o]);
+    float v = (red[o] + red[32 * 17 + o]) + (red[2 * 32 * 17 + o] + red[3 * 32 * 17 + o]);
+    if constexpr (NW == 8)
+      v += (red[4 * 32 * 17 + o] + red[5 * 32 * 17 + o]) + (red[6 * 32 * 17 + o] + red[7 * 32 * 17 + o]);
+    tile[o] = v;
   }
   __syncthreads();
 }
@@ -543,9 +547,13 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 
 // One forward step (PH = 0: the gates that read h_{t-1}; PH = 1: the candidate of a two-phase
 // cell, reading rh).  Tile: rows [32*blockIdx.y, +32) x NG gates of NU = 16/NG units.
-template <int NG, int CELL, int PH, int S, bool QH, bool SP = false>
-__global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
-  __shared__ float red[4 * 32 * 17];
+// NW waves (4: 256 threads, or 8: the contraction in 32 strips of S — half the operand loads per
+// lane and half the MFMA chain per wave, for the long-H layers whose step is load-latency-bound)
+template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
+  static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  constexpr int NTH = 64 * NW;
+  __shared__ float red[NW * 32 * 17];
   __shared__ float tile[32 * 17];
   constexpr int NU = 16 / NG;
   const RnnIdx ix = mkidx(a);
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
   const int gi = c / NU, u = u0 + c % NU;
   const float* pu = a.U[PH == 0 ? gi : cand_gate(CELL)] + (int64_t)(u < H ? u : 0) * H;
   // one epilogue element per thread (LSTM, liGRU, GRU phase 1): its inputs are requested first
-  constexpr bool PF = PH == 0 && 32 * NU <= RT;
+  constexpr bool PF = PH == 0 && 32 * NU <= NTH;
   EpiIn pre;
   if constexpr (PF) {
     const int rl = (int)threadIdx.x / NU, ul = (int)threadIdx.x % NU;
@@ -600,6 +608,7 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
         mx = fmaxf(mx, fmaxf(va[s], vb[s]));
         mn = fminf(mn, fminf(va[s], vb[s]));
       }
+      static_assert(NW == 4 || !QH, "quantised h: 4-wave tiles");
       mx = warp_max(mx);
       mn = -warp_max(-mn);
       if (lane == 0) { qred[w] = mx; qred[4 + w] = mn; }
@@ -626,8 +635,8 @@ __global__ __launch_bounds__(RT) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) 
   } else {
     mfma_chain<S>(va, vb, vu, acc0, acc1);
   }
-  reduce_tile(acc0, acc1, red, tile);
-  for (int p = threadIdx.x; p < 32 * NU; p += RT) {
+  reduce_tile<NW>(acc0, acc1, red, tile);
+  for (int p = threadIdx.x; p < 32 * NU; p += NTH) {
     const int rl = p / NU, ul = p % NU;
     const int r = r0 + rl, j = u0 + ul;
     if (r >= B2 || j >= H) continue;
@@ -701,9 +710,11 @@ __device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, 
 // MODE 0: the product of gate g0 + blockIdx.z into slab blockIdx.z (a.work + (4 + z) n);
 // MODE 1: one-gate product + bwd_step_epi (t = tt + 1); MODE 2: one-gate product + rh_epi.
 // out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
-template <int G, int CELL, int MODE, int S, bool SP = false>
-__global__ __launch_bounds__(RT) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
-  __shared__ float red[4 * 32 * 17];
+template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
+  static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  constexpr int NTH = 64 * NW;
+  __shared__ float red[NW * 32 * 17];
   __shared__ float tile[32 * 17];
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2;
@@ -731,9 +742,9 @@ __global__ __launch_bounds__(RT) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, 
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   mfma_chain<S>(va, vb, vu, acc0, acc1);
-  reduce_tile(acc0, acc1, red, tile);
+  reduce_tile<NW>(acc0, acc1, red, tile);
   const int64_t n = (int64_t)B2 * H;
-  for (int p = threadIdx.x; p < 32 * 16; p += RT) {
+  for (int p = threadIdx.x; p < 32 * 16; p += NTH) {
     const int rl = p >> 4, kl = p & 15;
     const int r = r0 + rl, kk = k0 + kl;
     if (r >= B2 || kk >= H) continue;
@@ -801,6 +812,18 @@ struct SCase {};
 
 static int pick_vw(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
 
+// 8-wave step tiles for the dense one-phase cells at S >= 32 (H > 256): half the operand strip
+// per lane and half the MFMA chain per wave.  Same-run A/B (PKC_RNN_WAVES=4 / 8): C4 89.2k / 90.8k,
+// C5 (8-wave BPTT only; its quantised forward keeps 4) 117.6k / 120.3k frames/s — the step is
+// bound by h_{t-1} arriving from the other XCDs, not by the per-lane load or MFMA work.
+static bool eight_waves(int S) {
+  static const int w = [] {
+    const char* v = getenv("PKC_RNN_WAVES");
+    return v ? atoi(v) : 8;
+  }();
+  return w == 8 && S >= 32;
+}
+
 template <int G, int CELL, int S, bool SP = false>
 static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
@@ -821,6 +844,9 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), g1, dim3(RT), 0, s, *a, t, vw);
       else if (a->qbits > 0)
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
+      else if (eight_waves(S))
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), g1, dim3(2 * RT), 0, s,
+                           *a, t, vw);
       else
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
       if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
@@ -867,6 +893,10 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       if constexpr (G == 1) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
+      } else if (!SP && eight_waves(S)) {
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), dim3(kt, rows, G),
+                           dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
