@@ -55,6 +55,8 @@ int pkc_gemm_pick_splits(int M, int N, int K);
  *   PKC_OP_GEMM  : exactly pkc_gemm(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
  *                  splits, slab_stride)
  *   PKC_OP_COLSUM: C[n] = sum_m A[m*N + n]  (M rows, N columns, fp32)
+ *   PKC_OP_SLABSUM: C[i] = sum_{s<M} A[s*slab_stride + i], i < N, summed in slab order (fp32): the
+ *                  partial slabs of a split-K matmul (e.g. a large-batch dW) into one result
  *   PKC_OP_LOSS  : pkc_loss_finalize(nheads = M, row_loss = A, weights = B, rows = N,
  *                  row_err = X1, out = C, acc = X2, advance_ctr = X3)
  *   PKC_OP_OPTIM : pkc_optim_step(tensors_dev = A, chunk_map_dev = B, nchunks = M) — the update of
@@ -64,7 +66,7 @@ int pkc_gemm_pick_splits(int M, int N, int K);
  * tile j reads only the 32-deep k-tiles ktiles[j * (kmax + 1) + 1 .. + count], count =
  * ktiles[j * (kmax + 1)]: the k-tiles whose B rows (64 of them) hold a nonzero.  Exact: every
  * skipped product is a zero weight, so the sums are those of the dense matmul. */
-enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2, PKC_OP_OPTIM = 3 };
+enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2, PKC_OP_OPTIM = 3, PKC_OP_SLABSUM = 4 };
 typedef struct {
   int a_kcontig, b_kcontig, M, N, K, splits;
   const void* A; int64_t lda; const void* B; int64_t ldb;

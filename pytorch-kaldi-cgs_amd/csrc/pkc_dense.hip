@@ -8,8 +8,8 @@
 //   stats : grid (ceil(N/64), ceil(M/16)), 64 columns x 4 row-threads x 4 rows per workgroup;
 //           sums the split-K slabs (independent loads, fixed order), writes z, and per 16-row block
 //           the column mean / M2 (forward, merged with Chan's formula) or sum(dy) / sum(dy*xhat).
-//   finalize: one workgroup per 64 columns merges each column's partials once (Chan / fixed-order
-//           sums) and writes the BN side outputs / parameter gradients.
+//   finalize: one workgroup per 16 columns (16 row-threads each) merges each column's partials once
+//           (Chan / fixed-order sums) and writes the BN side outputs / parameter gradients.
 //   apply : same grid as stats; normalises / applies the BN backward from the merged statistics.
 #include "pkc_common.h"
 
@@ -80,18 +80,23 @@ __global__ __launch_bounds__(ET) void dense_stats_kernel(pkc_dense_fwd_args a, f
 }
 
 // Chan merge of one column's per-16-row partials, ONCE per column (not once per apply workgroup):
-// 4 row-threads merge every 4th partial in order, then the four in a fixed order (deterministic).
+// a workgroup takes FC_F = 16 columns x FR_F = 16 row-threads; row-thread t merges partials
+// t, t + 16, ... in order, then row-thread 0 merges the 16 states in a fixed order (deterministic).
+// (It used to be 64 columns x 4 row-threads: at M = 4096 that is 64 dependent merges per thread on
+// 16 workgroups, 27 us per BatchNorm; now 16 merges on N / 16 workgroups.)
 // -> part[nrb*2N + c] = mean, part[nrb*2N + N + c] = population variance; the BN training side
 // outputs (save_mean / save_invstd / running statistics) are written here.
+constexpr int FC_F = 16, FR_F = 16;
 __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a, float* part) {
   __shared__ float sn[ET], smu[ET], sm2[ET];
-  const int cl = threadIdx.x % EC, t = threadIdx.x / EC;
-  const int c = blockIdx.x * EC + cl;
+  const int cl = threadIdx.x % FC_F, t = threadIdx.x / FC_F;
+  const int c = blockIdx.x * FC_F + cl;
   const int64_t N = a.N;
   const int nrb = (a.M + ERB - 1) / ERB;
   float n = 0.f, mu = 0.f, M2 = 0.f;
-  if (c < a.N)
-    for (int k = t; k < nrb; k += ER) {
+  if (c < a.N) {
+#pragma unroll 4
+    for (int k = t; k < nrb; k += FR_F) {
       const float nk = (float)min(ERB, a.M - k * ERB);
       const float mk = part[(int64_t)k * 2 * N + c];
       const float M2k = part[(int64_t)k * 2 * N + N + c];
@@ -101,18 +106,19 @@ __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a
       M2 += M2k + d * d * n * nk / nn;
       n = nn;
     }
+  }
   sn[threadIdx.x] = n;
   smu[threadIdx.x] = mu;
   sm2[threadIdx.x] = M2;
   __syncthreads();
   if (t != 0 || c >= a.N) return;
-  for (int j = 1; j < ER; ++j) {
-    const float nk = sn[j * EC + cl];
+  for (int j = 1; j < FR_F; ++j) {
+    const float nk = sn[j * FC_F + cl];
     if (nk == 0.f) continue;
     const float nn = n + nk;
-    const float d = smu[j * EC + cl] - mu;
+    const float d = smu[j * FC_F + cl] - mu;
     mu += d * nk / nn;
-    M2 += sm2[j * EC + cl] + d * d * n * nk / nn;
+    M2 += sm2[j * FC_F + cl] + d * d * n * nk / nn;
     n = nn;
   }
   const float var = M2 / (float)a.M;
@@ -132,22 +138,29 @@ __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a
 // parameter gradients are written here.
 __global__ __launch_bounds__(ET) void dense_bwd_finalize_kernel(pkc_dense_bwd_args a, float* part) {
   __shared__ float s1[ET], s2[ET];
-  const int cl = threadIdx.x % EC, t = threadIdx.x / EC;
-  const int c = blockIdx.x * EC + cl;
+  const int cl = threadIdx.x % FC_F, t = threadIdx.x / FC_F;
+  const int c = blockIdx.x * FC_F + cl;
   const int64_t N = a.N;
   const int nrb = (a.M + ERB - 1) / ERB;
   float tdy = 0.f, tdyx = 0.f;
-  if (c < a.N)
-    for (int k = t; k < nrb; k += ER) {
+  if (c < a.N) {
+#pragma unroll 4
+    for (int k = t; k < nrb; k += FR_F) {
       tdy += part[(int64_t)k * 2 * N + c];
       tdyx += part[(int64_t)k * 2 * N + N + c];
     }
+  }
   s1[threadIdx.x] = tdy;
   s2[threadIdx.x] = tdyx;
   __syncthreads();
   if (t != 0 || c >= a.N) return;
-  tdy = (s1[cl] + s1[EC + cl]) + (s1[2 * EC + cl] + s1[3 * EC + cl]);
-  tdyx = (s2[cl] + s2[EC + cl]) + (s2[2 * EC + cl] + s2[3 * EC + cl]);
+  tdy = 0.f;
+  tdyx = 0.f;
+#pragma unroll
+  for (int j = 0; j < FR_F; j += 4) {
+    tdy += (s1[j * FC_F + cl] + s1[(j + 1) * FC_F + cl]) + (s1[(j + 2) * FC_F + cl] + s1[(j + 3) * FC_F + cl]);
+    tdyx += (s2[j * FC_F + cl] + s2[(j + 1) * FC_F + cl]) + (s2[(j + 2) * FC_F + cl] + s2[(j + 3) * FC_F + cl]);
+  }
   float* fin = part + (int64_t)nrb * 2 * N;
   fin[c] = tdy;
   fin[N + c] = tdyx;
@@ -639,7 +652,8 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   if (a->norm == PKC_NORM_BN_TRAIN) {
     hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
     PKC_LAUNCH_CHECK("pkc_dense_fwd stats");
-    hipLaunchKernelGGL(dense_finalize_kernel, dim3(grid.x), dim3(ET), 0, S(stream), *a, work);
+    hipLaunchKernelGGL(dense_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0, S(stream), *a,
+                       work);
     PKC_LAUNCH_CHECK("pkc_dense_fwd finalize");
   }
   hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
@@ -668,7 +682,8 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd stats");
-  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3(grid.x), dim3(ET), 0, S(stream), *a, work);
+  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0, S(stream),
+                     *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd finalize");
   if (a->norm == PKC_NORM_BN_TRAIN)      // without BN, dz = dy is final after the stats pass
     hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);

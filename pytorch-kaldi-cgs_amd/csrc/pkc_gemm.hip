@@ -414,7 +414,7 @@ __global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
 // operand orientation.  One launch boundary instead of one per matmul.
 constexpr int GMAX = 8;
 struct GroupProb {
-  int kind;              // PKC_OP_GEMM / PKC_OP_COLSUM / PKC_OP_LOSS
+  int kind;              // PKC_OP_GEMM / COLSUM / LOSS / OPTIM / SLABSUM
   int code;              // a_kcontig*4 + b_kcontig*2 + vec (+8: 128x128 tile body)
   int M, N, K, kchunk, tn, tmn, wg0;
   const void* A; int64_t lda; const void* B; int64_t ldb; float* C; int64_t ldc; int64_t slab;
@@ -426,7 +426,10 @@ struct GroupArgs {
   int n;
 };
 
-template <int PREC, bool BIN, bool BIG, bool SP = false>
+// SUM: the launch carries slab-sum operations (large-batch split-K dW); a separate instance,
+// because that body alone raises the kernel's VGPRs from 152 to 191 (occupancy 3 -> 2), which the
+// B = 128 step's lean launches cannot afford
+template <int PREC, bool BIN, bool BIG, bool SP = false, bool SUM = false>
 __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
   // BIG: at least one problem takes the 128x128 body; its LDS also holds the 64x64 tiles
   union alignas(16) Shm {
@@ -445,6 +448,13 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
   if (p.kind == PKC_OP_COLSUM) {
     colsum_body(p.M, p.N, reinterpret_cast<const float*>(p.A), p.C, local * 64);
     return;
+  }
+  if constexpr (SUM) {
+    if (p.kind == PKC_OP_SLABSUM) {
+      slabsum_body(p.M, p.N, reinterpret_cast<const float*>(p.A), p.slab, p.C,
+                   (int64_t)local * 1024, p.code != 0);
+      return;
+    }
   }
   if (p.kind == PKC_OP_OPTIM) {
     optim_wg(reinterpret_cast<const pkc_opt_tensor*>(p.A), reinterpret_cast<const int32_t*>(p.B),
@@ -626,8 +636,10 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   GroupArgs g;
   memset(&g, 0, sizeof(g));
   int wg = 0, k = 0;
-  bool any_big = false, any_sparse = false;
+  bool any_big = false, any_sparse = false, any_sum = false;
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
+  // a launch with block-sparse problems runs the sparse instance, which has no 128x128 body
+  for (int i = 0; i < n; ++i) any_sparse |= probs[i].kind == PKC_OP_GEMM && probs[i].ktiles != nullptr;
   for (int i = 0; i < n; ++i) {
     const pkc_gemm_problem& q = probs[i];
     if (q.kind == PKC_OP_OPTIM) {
@@ -638,6 +650,21 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
       p.A = q.A; p.B = q.B;
       p.wg0 = wg;
       wg += q.M;
+      continue;
+    }
+    if (q.kind == PKC_OP_SLABSUM) {
+      PKC_CHECK_ARG(q.M >= 1 && q.N >= 0 && q.A && q.C && (q.M == 1 || q.slab_stride >= q.N),
+                    "pkc_gemm_grouped: slab-sum op %d arguments", i);
+      if (q.N == 0) continue;
+      GroupProb& p = g.p[k++];
+      memset(&p, 0, sizeof(p));
+      p.kind = q.kind;
+      p.M = q.M; p.N = q.N; p.A = q.A; p.C = q.C; p.slab = q.slab_stride;
+      p.code = ((uintptr_t)q.A % 16 == 0 && (uintptr_t)q.C % 16 == 0 && q.slab_stride % 4 == 0 &&
+                q.N % 4 == 0) ? 1 : 0;
+      p.wg0 = wg;
+      wg += (q.N + 1023) / 1024;
+      any_sum = true;
       continue;
     }
     if (q.kind == PKC_OP_COLSUM || q.kind == PKC_OP_LOSS) {
@@ -665,11 +692,10 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     const bool vec = ((uintptr_t)q.A % 16 == 0) && ((uintptr_t)q.B % 16 == 0) && q.lda % e == 0 &&
                      q.ldb % e == 0 && (q.a_kcontig ? q.K % e == 0 : q.M % e == 0) &&
                      (q.b_kcontig ? q.K % e == 0 : q.N % e == 0);
-    const bool bigp = !q.ktiles && big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
+    const bool bigp = !any_sparse && big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
                                                      q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED,
                                                      BIG_MIN_K_GROUPED);
     any_big |= bigp;
-    any_sparse |= q.ktiles != nullptr;
     const int bk = bigp ? (prec == PKC_PREC_FP32 ? 32 : 64) : BK;
     int kchunk = (q.K + splits - 1) / splits;
     kchunk = ((kchunk + bk - 1) / bk) * bk;
@@ -691,8 +717,14 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   // k-tile lists, so the plain launches of the B = 128 step keep their lean code and residency
 #define PKC_GL(P, BIN)                                                                          \
   do {                                                                                          \
-    if (any_sparse)                                                                             \
+    if (any_sparse && any_sum)                                                                  \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false, true, true>), dim3(wg), dim3(NT), 0, \
+                         S(stream), g);                                                         \
+    else if (any_sparse)                                                                        \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false, true>), dim3(wg), dim3(NT), 0,      \
+                         S(stream), g);                                                         \
+    else if (any_sum)                                                                           \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, true, false, true>), dim3(wg), dim3(NT), 0,  \
                          S(stream), g);                                                         \
     else if (any_big)                                                                           \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, true>), dim3(wg), dim3(NT), 0, S(stream), g);  \

@@ -70,4 +70,27 @@ __device__ __forceinline__ void colsum_body(int M, int N, const float* __restric
   }
 }
 
+// C[i] = sum_{s < ns} A[s * stride + i] for 1024 elements i = i0 .. i0 + 1023 (< n), slab order
+// (deterministic); float4 when vec (16-byte aligned bases, stride and n multiples of 4).
+__device__ __forceinline__ void slabsum_body(int ns, int n, const float* __restrict__ A,
+                                             int64_t stride, float* __restrict__ C, int64_t i0,
+                                             bool vec) {
+  const int64_t i = i0 + 4 * threadIdx.x;
+  if (vec) {
+    if (i >= n) return;
+    float4 acc = *reinterpret_cast<const float4*>(A + i);
+    for (int s = 1; s < ns; ++s) {
+      const float4 x = *reinterpret_cast<const float4*>(A + (int64_t)s * stride + i);
+      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    }
+    *reinterpret_cast<float4*>(C + i) = acc;
+    return;
+  }
+  for (int64_t j = i; j < i + 4 && j < n; ++j) {
+    float acc = A[j];
+    for (int s = 1; s < ns; ++s) acc += A[(int64_t)s * stride + j];
+    C[j] = acc;
+  }
+}
+
 }  // namespace pkc

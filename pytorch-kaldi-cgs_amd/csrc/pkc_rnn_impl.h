@@ -1,4 +1,6 @@
-// pkc_rnn.hip — the serial time loops of the recurrent layers (forward and BPTT).
+// pkc_rnn_impl.h — the serial time loops of the recurrent layers (forward and BPTT).
+// Compiled as two translation units (pkc_rnn_fwd.hip: PKC_RNN_FWD, pkc_rnn_bwd.hip: PKC_RNN_BWD)
+// that build in parallel; each instantiates only its direction's step kernels.
 //
 // Reference: liGRU  neural_networks.py:1573-1584 (z = sig(wz+Uz h); hc = act(wh+Uh h)*drop;
 //                   h = z*h + (1-z)*hc), shared-weight bidirectional rows via cat/flip
@@ -32,6 +34,7 @@
 // their forward step is two launches (gates that read h, then the candidate), their BPTT step two
 // as well (d(rh) = Uh^T da then dr / dz, and dh_{t-1}).  r*h is kept per step (rh, (T, B2, H)):
 // it is the input of the Uh gradient matmul.
+#pragma once
 #include "pkc_common.h"
 
 namespace pkc {
@@ -131,6 +134,7 @@ __device__ __forceinline__ void qin_strips(float* va, float* vb, const QParams& 
 
 
 
+#ifdef PKC_RNN_FWD
 __global__ void rnn_drop_mask_kernel(pkc_rnn_args a, int B2) {
   const int64_t n = (int64_t)B2 * a.H;
   const uint32_t thr = (uint32_t)((double)(1.f - a.drop_p) * 4294967296.0);
@@ -144,6 +148,7 @@ __global__ void rnn_drop_mask_kernel(pkc_rnn_args a, int B2) {
   }
 }
 
+#endif  // PKC_RNN_FWD
 
 // ------------------------------------------------------------------------------- backward
 __device__ __forceinline__ float dy_at(const pkc_rnn_args& a, int64_t i) {
@@ -246,6 +251,7 @@ __global__ void rnn_bwd_init(pkc_rnn_args a) {
 // LayerNorm of the new hidden state (neural_networks.py:1093-1094, 1399-1400, 1581-1582,
 // 1758-1759, 1909-1910): h_t <- gamma (h_t - mean) / (std + eps) + beta per row, std unbiased.
 // One wave per row; saves xhat and (std + eps, std) for the backward.
+#ifdef PKC_RNN_FWD
 __global__ __launch_bounds__(256) void rnn_ln_fwd(pkc_rnn_args a, int t) {
   const RnnIdx ix = mkidx(a);
   const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -275,6 +281,7 @@ __global__ __launch_bounds__(256) void rnn_ln_fwd(pkc_rnn_args a, int t) {
   }
 }
 
+#endif  // PKC_RNN_FWD
 // Backward of that LayerNorm for step tt (row-wise), then the gate gradients of step tt:
 //   gh = g gamma, dh_raw = (gh - mean(gh)) / (std + eps) - xhat sum(gh xhat) / ((H - 1) std)
 template <int G, int CELL>
@@ -310,6 +317,7 @@ __global__ __launch_bounds__(256) void rnn_ln_bwd_gates(pkc_rnn_args a, int tt) 
 }
 
 // dgamma = sum_{t,r} g_post * xhat, dbeta = sum_{t,r} g_post over the T * B2 rows of the layer
+#ifdef PKC_RNN_BWD
 __global__ __launch_bounds__(256) void rnn_ln_param_grads(pkc_rnn_args a) {
   __shared__ float red[2][256];
   const RnnIdx ix = mkidx(a);
@@ -333,6 +341,7 @@ __global__ __launch_bounds__(256) void rnn_ln_param_grads(pkc_rnn_args a) {
   }
 }
 
+#endif  // PKC_RNN_BWD
 
 // ------------------------------------------------------------------------------- MFMA strips
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -770,6 +779,7 @@ __global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt) {
 }
 
 // ut[g][k][j] = U[g][j][k] (the B operand of the backward products), 32 x 32 tiles through LDS
+#ifdef PKC_RNN_BWD
 __global__ __launch_bounds__(256) void rnn_transpose_u(pkc_rnn_args a) {
   __shared__ float tl[32][33];
   const int H = a.H, g = blockIdx.z;
@@ -787,7 +797,10 @@ __global__ __launch_bounds__(256) void rnn_transpose_u(pkc_rnn_args a) {
     if (k < H && j < H) ut[(int64_t)k * H + j] = tl[tx][i];
   }
 }
+
+#endif  // PKC_RNN_BWD
 // fold the per-direction gate gradients (G, T, B2, H) onto the (G, T, B, H) pre-activation rows
+#ifdef PKC_RNN_BWD
 __global__ void rnn_fold_kernel(pkc_rnn_args a, float* dpre) {
   const RnnIdx ix = mkidx(a);
   const int G = cell_gates(a.cell);
@@ -806,6 +819,7 @@ __global__ void rnn_fold_kernel(pkc_rnn_args a, float* dpre) {
   }
 }
 
+#endif  // PKC_RNN_BWD
 
 template <int S>
 struct SCase {};
@@ -824,6 +838,7 @@ static bool eight_waves(int S) {
   return w == 8 && S >= 32;
 }
 
+#ifdef PKC_RNN_FWD
 template <int G, int CELL, int S, bool SP = false>
 static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
@@ -856,6 +871,8 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   return PKC_OK;
 }
 
+#endif  // PKC_RNN_FWD
+#ifdef PKC_RNN_BWD
 template <int G, int CELL, int S, bool SP = false>
 static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
@@ -912,6 +929,7 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   return PKC_OK;
 }
 
+#endif  // PKC_RNN_BWD
 // contraction strip per lane: 16 lane groups x S >= H
 #define PKC_S_DISPATCH(FN, ...)                                      \
   (a->H <= 256 ? FN<G, CELL, 16>(__VA_ARGS__)                        \
@@ -920,6 +938,7 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
    : a->H <= 1024 ? FN<G, CELL, 64>(__VA_ARGS__)                     \
    : FN<G, CELL, 128>(__VA_ARGS__))
 
+#ifdef PKC_RNN_FWD
 template <int G, int CELL>
 static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
@@ -939,6 +958,8 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   return PKC_S_DISPATCH(fwd_impl_s, a, s);
 }
 
+#endif  // PKC_RNN_FWD
+#ifdef PKC_RNN_BWD
 template <int G, int CELL>
 static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   if constexpr (!two_phase(CELL) && G > 1) {
@@ -951,6 +972,7 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   return PKC_S_DISPATCH(bwd_impl_s, a, dpre, s);
 }
 
+#endif  // PKC_RNN_BWD
 static int check(const pkc_rnn_args* a, bool bwd) {
   PKC_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->H > 0 && a->H <= 2048, "pkc_rnn: bad shape (H <= 2048)");
   PKC_CHECK_ARG(a->cell >= PKC_CELL_LIGRU && a->cell <= PKC_CELL_RNN, "pkc_rnn: bad cell %d", a->cell);
@@ -980,6 +1002,7 @@ static int check(const pkc_rnn_args* a, bool bwd) {
 
 }  // namespace pkc
 
+#ifdef PKC_RNN_FWD
 extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
   using namespace pkc;
   int st = check(a, false);
@@ -993,6 +1016,8 @@ extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
   }
 }
 
+#endif  // PKC_RNN_FWD
+#ifdef PKC_RNN_BWD
 extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
   using namespace pkc;
   int st = check(a, true);
@@ -1006,3 +1031,5 @@ extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
     default: return bwd_impl<4, PKC_CELL_LSTM>(a, dpre, S(stream));
   }
 }
+
+#endif  // PKC_RNN_BWD

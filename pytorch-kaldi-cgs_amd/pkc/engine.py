@@ -44,6 +44,11 @@ MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", str(MAX_SPLITS)))   # 
 # that ride in successive backward launches (0: one part).  C2, frames/s: 0 -> 653-657k,
 # 1.2M -> 663k, 700k -> 666-667k, 400k-520k -> 669-671k, 250k -> 644k (the tail launch grows)
 OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "500000"))
+# split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
+# tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
+# 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
+# gradient (0: off)
+DW_SPLIT_ROWS = int(os.environ.get("PKC_DW_SPLIT_ROWS", "1024"))
 
 
 _PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
@@ -602,6 +607,8 @@ class Engine:
             n.save_invstd = _f32(N, dev)
             n.dz = _f32(M * N, dev)
             n.work = _f32(L.lib().pkc_dense_work_size(M, N), dev)
+            n.sdw = self._dw_splits(N, K) if n.W is not None else 1
+            n.dwslab = _f32(n.sdw * N * K, dev) if n.sdw > 1 else None
             if n.qbits:
                 n.Wq = torch.zeros_like(n.W)
             if n.head:
@@ -663,6 +670,15 @@ class Engine:
                                        device=dev)
         if self.seq:
             self.seq_meta = torch.zeros(4 * self.B, dtype=torch.int64, device=dev)
+
+    def _dw_splits(self, N, K):
+        """K-splits of a dense layer's dW = dz^T X (contraction over the M batch rows): enough
+        128x128 tiles x splits for ~256 workgroups at large batches, at most 4, >= 256 rows each."""
+        M = self.Mmax
+        if self.seq or DW_SPLIT_ROWS <= 0 or M < DW_SPLIT_ROWS:
+            return 1
+        tiles = -(-N // 128) * -(-K // 128)
+        return max(1, min(4, -(-256 // tiles), M // 256))
 
     def _alloc_rec(self, n):
         M, dev, B, T = self.Mmax, self.dev, self.B, self.max_len
@@ -1383,11 +1399,13 @@ class Engine:
             out.append(("db %d" % n.N, 0.0, 4.0 * M * n.N,
                         L.GemmProblem(kind=L.OP_COLSUM, M=M, N=n.N, A=n.dz.data_ptr(),
                                       C=n.db.data_ptr())))
-        out += [("dW %dx%dx%d" % (n.N, n.K, M), 2.0 * M * n.N * n.K,
-                4.0 * (M * n.N + M * n.K + n.N * n.K),
-                L.GemmProblem(a_kcontig=0, b_kcontig=0, M=n.N, N=n.K, K=M, splits=1,
-                              A=n.dz.data_ptr(), lda=n.N, B=a_ptr, ldb=lda, C=n.dW.data_ptr(),
-                              ldc=n.K, slab_stride=0))]
+        sdw = getattr(n, "sdw", 1)
+        out += [("dW %dx%dx%d%s" % (n.N, n.K, M, " s%d" % sdw if sdw > 1 else ""),
+                 2.0 * M * n.N * n.K, 4.0 * (M * n.N + M * n.K + sdw * n.N * n.K),
+                 L.GemmProblem(a_kcontig=0, b_kcontig=0, M=n.N, N=n.K, K=M, splits=sdw,
+                               A=n.dz.data_ptr(), lda=n.N, B=a_ptr, ldb=lda,
+                               C=(n.dwslab if sdw > 1 else n.dW).data_ptr(), ldc=n.K,
+                               slab_stride=n.N * n.K if sdw > 1 else 0))]
         if n.src[0] == "node" and self.needs_grad[n.src[1]]:
             P = n.src[1]
             off = P.cons_off[P.consumers.index(n)]
@@ -1403,6 +1421,12 @@ class Engine:
                         2.0 * M * n.N * n.K * d, 4.0 * (M * n.N + n.N * n.K * d + n.sx * M * n.K),
                         pr))
         return out
+
+    def _dw_sum_op(self, n):
+        """The slab sum of a split-K dW into the gradient (an operation of the next launch)."""
+        return ("dW slab-sum %s x%d" % (n.name, n.sdw), 0.0, 4.0 * n.N * n.K * (n.sdw + 1),
+                L.GemmProblem(kind=L.OP_SLABSUM, M=n.sdw, N=n.N * n.K, A=n.dwslab.data_ptr(),
+                              C=n.dW.data_ptr(), slab_stride=n.N * n.K))
 
     def _dense_bwd(self, n, s):
         self._dense_bwd_pre(n, s)
@@ -1520,18 +1544,25 @@ class Engine:
         pend = [loss_op] if loss_op is not None else []
         future = [[], []]       # future[i]: operations riding in the i-th launch from now
         cut_node = self._bucket_cut()[0] if on_cut is not None else None
+        cut_wait = -1           # launches until the cut node's gradient is final
         pend_nodes = []
 
         def flush():
-            nonlocal pend, future, pend_nodes, cut_node
+            nonlocal pend, future, pend_nodes, cut_node, cut_wait
             now = future.pop(0)
             if pend or now:
                 self._gemms(pend + now, s)
             pend = []
             while len(future) < 2:
                 future.append([])
+            if cut_wait > 0:
+                cut_wait -= 1
             if cut_node is not None and cut_node in pend_nodes:
+                # a split-K dW becomes final one launch later (its slab sum)
+                cut_wait = 1 if getattr(cut_node, "sdw", 1) > 1 else 0
                 cut_node = None
+            if cut_wait == 0:
+                cut_wait = -1
                 on_cut()                # the first bucket's gradients are final
             pend_nodes = []
 
@@ -1547,15 +1578,36 @@ class Engine:
             self._dense_bwd_pre(n, s)
             pend += self._bwd_problems(n)
             pend_nodes.append(n)
+            lag = 1
+            if getattr(n, "sdw", 1) > 1 and n.W is not None:
+                future[1].append(self._dw_sum_op(n))    # the launch after the dW's
+                lag = 2                                 # its update one launch later still
             if spread_opt:
                 nparam = sum(self.opt_entries[i]["p"].numel() for i in self.node_opt.get(n, (0, 0, []))[2])
                 parts = -(-nparam // OPT_SPREAD_PARAMS) if OPT_SPREAD_PARAMS > 0 else 1
                 for k, op in enumerate(self._opt_op(n, parts)):
-                    while len(future) <= 1 + k:
+                    while len(future) <= lag + k:
                         future.append([])
-                    future[1 + k].append(op)
+                    future[lag + k].append(op)
         flush()
-        self.spread_tail = [op for f in future for op in f]   # updates still to run
+        # operations still to run, merged into as few launches as the order allows (a layer's
+        # update never shares a launch with the slab sum of its own gradient)
+        self.spread_tail = []
+        cur, summed = [], set()
+        for f in future:
+            if any(op[0].startswith("opt ") and op[0][4:].split(" ")[0] in summed for op in f):
+                self.spread_tail.append(cur)
+                cur, summed = [], set()
+            cur = cur + f
+            summed |= {op[0].split(" ")[2] for op in f if op[0].startswith("dW slab-sum ")}
+        if cur:
+            self.spread_tail.append(cur)
+        if not spread_opt:
+            for f in self.spread_tail:       # slab sums, before the all-reduce / optimizer
+                self._gemms(f, s)
+            self.spread_tail = []
+            if cut_wait >= 0:
+                on_cut()
 
     def _build_reg(self):
         """Device descriptors of the regulariser terms (item lists, block starts, buffers)."""
@@ -1599,7 +1651,8 @@ class Engine:
         spread_opt = spread_opt and not self.reg_terms
         self._reg_grad_kernels(s)
         if spread_opt:
-            self._gemms(self.spread_tail, s)
+            for f in self.spread_tail:
+                self._gemms(f, s)
             self._prune_kernels(s)
             return
         nparam = sum(e["p"].numel() for e in self.opt_entries)

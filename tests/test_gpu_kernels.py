@@ -476,3 +476,44 @@ def test_gemm_block_sparse_matches_dense(L, prec, M):
         ref = (X.double() @ W.double().t()) if not transpose else (dZ.double() @ W.double())
         if prec == 0:
             torch.testing.assert_close(outs[1], ref.float(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("prec", [0, 2])
+def test_gemm_grouped_sparse_big_slabsum(L, prec):
+    """One grouped launch mixing a block-sparse problem, a dense one the 128x128 body would take on
+    its own (it must run the 64x64 body in a sparse launch), and a slab-sum operation (a split-K
+    dW's partial slabs into one gradient, summed in slab order)."""
+    from pkc.engine import ktile_table
+    g = torch.Generator().manual_seed(11)
+    dt = torch.bfloat16 if prec == 2 else torch.float32
+    N_out, K_in, M = 550, 440, 2400
+    blk = (torch.rand(-(-N_out // 32), -(-K_in // 32), generator=g) < 0.25).float()
+    mask = blk.repeat_interleave(32, 0).repeat_interleave(32, 1)[:N_out, :K_in]
+    W = torch.randn(N_out, K_in, generator=g) * mask
+    X = torch.randn(M, K_in, generator=g)
+    kt = ktile_table(mask.to(DEV), False, DEV)
+    A2, B2 = torch.randn(4096, 1024, generator=g), torch.randn(1024, 1024, generator=g)
+    slabs = torch.randn(3, 1000, generator=g)
+    Wd, Xd, A2d, B2d = W.to(DEV, dt), X.to(DEV, dt), A2.to(DEV, dt), B2.to(DEV, dt)
+    C1 = torch.full((M, N_out), float("nan"), device=DEV)
+    C2 = torch.full((4096, 1024), float("nan"), device=DEV)
+    sd, Cs = slabs.to(DEV), torch.full((1000,), float("nan"), device=DEV)
+    probs = [L.GemmProblem(a_kcontig=1, b_kcontig=1, M=M, N=N_out, K=K_in, splits=1, A=Xd.data_ptr(),
+                           lda=K_in, B=Wd.data_ptr(), ldb=K_in, C=C1.data_ptr(), ldc=N_out,
+                           slab_stride=M * N_out, ktiles=kt[0].data_ptr(), kmax=kt[1]),
+             L.GemmProblem(a_kcontig=1, b_kcontig=1, M=4096, N=1024, K=1024, splits=1,
+                           A=A2d.data_ptr(), lda=1024, B=B2d.data_ptr(), ldb=1024, C=C2.data_ptr(),
+                           ldc=1024, slab_stride=0),
+             L.GemmProblem(kind=L.OP_SLABSUM, M=3, N=1000, A=sd.data_ptr(), C=Cs.data_ptr(),
+                           slab_stride=1000)]
+    arr = (L.GemmProblem * 3)(*probs)
+    L.call("pkc_gemm_grouped", prec, arr, 3, _s())
+    torch.cuda.synchronize()
+    if prec == 2:
+        W, X, A2, B2 = (t.bfloat16().float() for t in (W, X, A2, B2))
+    tol = 2e-5 if prec == 0 else 1e-3
+    torch.testing.assert_close(C1.cpu(), (X.double() @ W.double().t()).float(), rtol=1e-4,
+                               atol=tol * K_in ** 0.5)
+    torch.testing.assert_close(C2.cpu(), (A2.double() @ B2.double().t()).float(), rtol=1e-4,
+                               atol=tol * 1024 ** 0.5)
+    assert torch.equal(Cs.cpu(), (slabs[0] + slabs[1]) + slabs[2])

@@ -409,3 +409,53 @@ def test_engine_c2_bf16_vs_oracle(steps):
             assert max(errs.values()) < 0.15, "step %d %s" % (s, errs)
         np.testing.assert_allclose(loss, refs["bf16"][s][0], rtol=1e-3)
         np.testing.assert_allclose(loss, refs["fp32"][s][0], rtol=1e-3)
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph", "dp_graph"])
+def test_engine_split_dw_large_batch(mode):
+    """Large frame batches split each dW = dz^T X over K (the batch rows) into slabs that a slab-sum
+    operation of the NEXT grouped launch adds into the gradient (and the layer's update, one launch
+    later still).  The gradient buffer after a step equals the unsplit run's up to fp32 summation
+    order, in eager, graph-replayed and data-parallel (bucketed, split-optimizer) form."""
+    import pkc.engine as E
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config(drop="0.15")
+    B = 1024
+    grads = []
+
+    def no_op_allreduce(t, async_op=False):
+        return None
+
+    old = E.DW_SPLIT_ROWS
+    try:
+        for rows in (0, 1024):
+            E.DW_SPLIT_ROWS = rows
+            nets, opts = build_nets(cfg, C1_DIMS)
+            for n in nets.values():
+                n.to(DEV).train()
+            rs = np.random.RandomState(4)
+            X = torch.from_numpy(rs.randn(2 * B, 440).astype(np.float32)).to(DEV)
+            lab = torch.from_numpy(np.stack([rs.randint(0, 1928, 2 * B), rs.randint(0, 48, 2 * B)], 1)
+                                   .astype(np.int32)).to(DEV)
+            eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                         ["lab_cd", "lab_mono"], batch=B, seed=3)
+            eng.bind_chunk(X, lab, 2 * B)
+            split = [n for n in eng.nodes if getattr(n, "sdw", 1) > 1]
+            assert bool(split) == (rows > 0)
+            if mode == "graph":
+                assert eng.capture(steps_per_graph=1)
+                eng.ctr.zero_()
+                eng.loss_acc.zero_()
+            if mode == "dp_graph":
+                assert eng.capture(split_optimizer=True)
+                eng.ctr.zero_()
+                eng.loss_acc.zero_()
+            eng.train_step(no_op_allreduce if mode == "dp_graph" else None)
+            torch.cuda.synchronize()
+            grads.append((eng.gflat.detach().cpu().double(), eng.chunk_totals()))
+    finally:
+        E.DW_SPLIT_ROWS = old
+    (g0, t0), (g1, t1) = grads
+    assert t0 == pytest.approx(t1, rel=1e-6)
+    err = (g1 - g0).abs().max().item()
+    assert err <= 1e-5 * g0.abs().max().item(), "split-K dW gradient max abs diff %.3g" % err
