@@ -398,6 +398,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const voi
                                              B, ldb, C, ldc, kchunk, slab_stride);
 }
 
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(big::NT) void gemm_glds_kernel(int M, int N, int K,
+                                                           const void* __restrict__ A, int64_t lda,
+                                                           const void* __restrict__ B, int64_t ldb,
+                                                           float* __restrict__ C, int64_t ldc,
+                                                           int kchunk, int64_t slab_stride) {
+  __shared__ __attribute__((aligned(16))) char lds[big::GL_LDS_BYTES];
+  big::body_glds<AKC, BKC>(lds, blockIdx.x, blockIdx.y, blockIdx.z, M, N, K, A, lda, B, ldb, C,
+                           ldc, kchunk, slab_stride);
+}
+
 template <int PREC, bool BIN, bool AKC, bool BKC>
 __global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
                                                           const void* __restrict__ A, int64_t lda,
@@ -526,6 +537,14 @@ static int launch(int M, int N, int K, const void* A, int64_t lda, const void* B
   return PKC_OK;
 }
 
+static bool glds_enabled() {                   // PKC_GEMM_GLDS=0: register-staged body (A/B)
+  static const int on = [] {
+    const char* v = getenv("PKC_GEMM_GLDS");
+    return v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
+
 template <int PREC, bool BIN>
 static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
@@ -534,6 +553,22 @@ static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int6
   int kchunk = (K + splits - 1) / splits;
   kchunk = ((kchunk + BKB - 1) / BKB) * BKB;
   dim3 grid((N + big::TN - 1) / big::TN, (M + big::TM - 1) / big::TM, splits);
+  // LDS-DMA ring (bf16 operands, whole k-tiles) when the grid is one workgroup per CU at most:
+  // 4096x1024x1024 27.8 -> 21.8 us (forward) / 27.7 -> 20.3 (dX); with several tiles per CU its
+  // 96 KB of LDS (one workgroup per CU) loses to the register body (4096x1928x1024 31.6 -> 35.3,
+  // 8192^3 755 -> 656 TF/s), same run
+  if (BIN && K % 64 == 0 && (int64_t)grid.x * grid.y * grid.z <= 256 && glds_enabled()) {
+#define PKC_L(AK, BK_)                                                                          \
+  hipLaunchKernelGGL((gemm_glds_kernel<AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, lda, B,   \
+                     ldb, C, ldc, kchunk, slab)
+    if (akc && bkc) PKC_L(true, true);
+    else if (akc) PKC_L(true, false);
+    else if (bkc) PKC_L(false, true);
+    else PKC_L(false, false);
+#undef PKC_L
+    PKC_LAUNCH_CHECK("pkc_gemm (128x128 LDS-DMA)");
+    return PKC_OK;
+  }
 #define PKC_L(AK, BK_)                                                                          \
   hipLaunchKernelGGL((gemm_big_kernel<PREC, BIN, AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, \
                      lda, B, ldb, C, ldc, kchunk, slab)

@@ -40,9 +40,8 @@ __device__ __forceinline__ int swz(int r) { return ((r >> 1) ^ (r >> 4)) & 7; }
 // chunk c of k-row k at chunk c ^ xr(k).  The transposed fragment read (tr_frag) of one 32-lane
 // half touches 4 consecutive k-rows x 4 consecutive chunks (c0 % 4 == 0): the XOR puts them on 16
 // distinct chunks = all 64 banks (conflict-free); the 16-byte staging stores fill whole k-rows.
-__device__ __forceinline__ int tr_off(int k, int c) {
-  return 256 * k + 16 * (c ^ (((k & 3) << 2) | ((k >> 2) & 3)));
-}
+__device__ __forceinline__ int xr(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+__device__ __forceinline__ int tr_off(int k, int c) { return 256 * k + 16 * (c ^ xr(k)); }
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
@@ -333,6 +332,103 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
     }
   }
   // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  float* Cz = Cp + (int64_t)bz * slab_stride;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int col = n0 + wn * 64 + 32 * b + r;
+    if (col >= N) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = m0 + wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < M) Cz[(int64_t)row * ldc + col] = acc[a][b][reg];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS-DMA form of the bf16 body (operands stored as bf16, k-range a multiple of 64): one workgroup
+// per CU holds a 128x128 tile, so a k-tile whose loads are issued only two k-tiles ahead through
+// registers waits most of a memory round trip (the 4096x1024x1024 forward: 27 us = 12 % of the
+// CUs' MFMA rate).  Here global_load_lds writes the operand images straight into a ring of 3 LDS
+// buffers (96 KB): two k-tiles stay in flight across each barrier (counted vmcnt, raw s_barrier:
+// __syncthreads() would drain the DMA), no staging registers, no ds_write pass.  The DMA writes
+// each wave-instruction's 64 x 16 bytes linearly, so the swizzles of the register path's images
+// (swz for row images, xr for the [k][row] images) go on the per-lane SOURCE addresses instead.
+constexpr int GL_BUFS = 3;
+constexpr int GL_LDS_BYTES = GL_BUFS * 2 * TILE_BYTES;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glb_void;
+
+// one 16 KB operand image of k-tile [k0, k0 + 64): 16 wave-instructions of 1 KB, 4 per wave
+template <bool KC>
+__device__ __forceinline__ void glds_tile(const __bf16* __restrict__ P, int64_t ld, int r0, int rmax,
+                                          int k0, char* dst) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * i + w;                  // 1 KB piece j of the image
+    const __bf16* src;
+    if constexpr (KC) {                       // rows 8j .. 8j+7 of 128 B: slot (lane & 7)
+      const int r = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ swz(r);
+      src = P + (int64_t)min(r0 + r, rmax - 1) * ld + k0 + 8 * c;
+    } else {                                  // k-rows 4j .. 4j+3 of 256 B: slot (lane & 15)
+      const int k = 4 * j + (lane >> 4);
+      const int c = (lane & 15) ^ xr(k);
+      src = P + (int64_t)(k0 + k) * ld + min(r0 + 8 * c, rmax - 8);
+    }
+    __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(dst + 1024 * j), 16, 0, 0);
+  }
+}
+
+template <bool AKC, bool BKC>
+__device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by, int bz, int M,
+                                          int N, int K, const void* __restrict__ Av, int64_t lda,
+                                          const void* __restrict__ Bv, int64_t ldb,
+                                          float* __restrict__ Cp, int64_t ldc, int kchunk,
+                                          int64_t slab_stride) {
+  const __bf16* A = reinterpret_cast<const __bf16*>(Av);
+  const __bf16* B = reinterpret_cast<const __bf16*>(Bv);
+  const int m0 = by * TM, n0 = bx * TN;
+  const int kbeg = bz * kchunk, kend = min(K, kbeg + kchunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+  const int nk = kbeg < kend ? (kend - kbeg) / 64 : 0;      // uniform; k-range % 64 == 0
+  auto buf = [&](int t) { return lds + (t % GL_BUFS) * 2 * TILE_BYTES; };
+  auto issue = [&](int t) {
+    glds_tile<AKC>(A, lda, m0, M, kbeg + 64 * t, buf(t));
+    glds_tile<BKC>(B, ldb, n0, N, kbeg + 64 * t, buf(t) + TILE_BYTES);
+  };
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  for (int t = 0; t < nk; ++t) {
+    // tile t + 2 refills the buffer of tile t - 1, released by the barrier ending iteration t - 1
+    if (t + 2 < nk) issue(t + 2);
+    // this thread's DMAs of tile t are done once at most the later tiles' 8 each are in flight
+    if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();             // ... and every thread's
+    asm volatile("" ::: "memory");
+    const char* cur = buf(t);
+    tile_mfma<PKC_PREC_BF16, !AKC, !BKC>(cur, cur + TILE_BYTES, wm, wn, lane, acc);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();             // every wave has read buffer t % 3
+    asm volatile("" ::: "memory");
+  }
   float* Cz = Cp + (int64_t)bz * slab_stride;
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
