@@ -130,9 +130,15 @@ def cpu_baseline(batch, seconds=12.0):
         OR.train_step(lines, nets, opts, seq, fc, lc, inp)
         n += 1
     dt = time.time() - t0
-    return {"value": round(n * batch / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": "%d training steps of the C1 MLP at B=%d (oracle restatement, torch-CPU eager, "
-                      "%d threads, %.1f s)" % (n, batch, threads, dt)}
+    out = {"value": round(n * batch / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": "%d training steps of the C1 MLP at B=%d (oracle restatement, torch-CPU eager, "
+                     "%d threads, %.1f s)" % (n, batch, threads, dt)}
+    try:   # the restatement's speed relative to the reference itself (scripts/cpu_calibrate.py)
+        cal = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))["results"]
+        out["calibration_port_over_reference"] = {k: v["oracle_over_reference"] for k, v in cal.items()}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def pmc_traffic(label):

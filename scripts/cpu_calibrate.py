@@ -1,0 +1,114 @@
+"""Calibrate the CPU baseline: the oracle restatement that bench.py times on the GPU
+box's host cores against the REFERENCE itself (imported from /root/reference, build container
+only) on the same cores and the same C1 MLP training step (TIMIT_MLP_fmllr.cfg shape, B = 128),
+with all 8 threads and with 1.  Writes profiles/r02_cpu_calibration.json.  The reference never
+travels to the GPU box; only this ratio does.
+
+Shims (this process only): torch.Tensor.cuda -> identity (the reference hard-codes .cuda()).
+Usage: PYTHONDONTWRITEBYTECODE=1 python scripts/cpu_calibrate.py
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def steps_per_s(step, seconds):
+    for _ in range(2):
+        step()
+    n, t0 = 0, time.time()
+    while time.time() - t0 < seconds:
+        step()
+        n += 1
+    return n / (time.time() - t0)
+
+
+def oracle_step(B):
+    from oracle import nets as ON
+    from oracle import run as OR
+    cfg = bench.c1_cfg()
+    torch.manual_seed(0)
+    nets, opts = {}, {}
+    for sec, inp in bench.DIMS:
+        o = cfg[sec]
+        nets[o["arch_name"]] = ON.MLP(o, inp).train()
+        opts[o["arch_name"]] = ON.make_optimizer(nets[o["arch_name"]].parameters(), o)
+    lines = OR.parse_model(cfg["model"]["model"])
+    rs = np.random.RandomState(1)
+    inp = torch.from_numpy(np.concatenate([rs.randn(B, 440), rs.randint(0, 48, (B, 2))],
+                                          1).astype(np.float32))
+    seq = {k: False for k in nets}
+    fc, lc = {"fmllr": (0, 440)}, {"lab_cd": 440, "lab_mono": 441}
+    return lambda: OR.train_step(lines, nets, opts, seq, fc, lc, inp)
+
+
+def reference_step(B):
+    if not os.path.isdir(REF):
+        raise SystemExit("the reference is only present in the build container")
+    torch.Tensor.cuda = lambda t, *a, **k: t      # noqa: E731
+    sys.path.insert(0, REF)
+    import utils
+    cfg = bench.c1_cfg()
+    cfg["exp"] = {"use_cuda": "False", "to_do": "train", "seed": "2234"}
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from cases import MLP_DEF               # the reference MLP's remaining option keys
+    for sec, _ in bench.DIMS:                 # the reference's plug-in keys (utils.py:1768-1779)
+        nl = len(cfg[sec]["dnn_lay"].split(","))
+        for k, v in MLP_DEF.items():
+            if k not in cfg[sec]:
+                cfg[sec][k] = ",".join([v.split(",")[0]] * nl) if k in ("param_quant", "mlp_prune_perc") else v
+        cfg[sec].update(arch_library="neural_networks", arch_class="MLP", arch_seq_model="False",
+                        arch_pretrain_file="none", use_cuda="False")
+    arch_dict = {"MLP_layers1": ["architecture1", "MLP_layers1", 0],
+                 "MLP_layers2": ["architecture2", "MLP_layers2", 0],
+                 "MLP_layers3": ["architecture3", "MLP_layers3", 0]}
+    fea_dict = {"fmllr": ["fmllr", "x.scp", "", "5", "5", 0, 440, 440]}
+    lab_dict = {"lab_cd": ["lab_cd", "a", "ali-to-pdf", 440], "lab_mono": ["lab_mono", "a", "p", 441]}
+    model = cfg["model"]["model"].split("\n")
+    torch.manual_seed(0)
+    inp_out = dict(fea_dict)
+    nns, costs = utils.model_init(inp_out, model, cfg, arch_dict, False, False, "train")
+    opts = utils.optimizer_init(nns, cfg, arch_dict)
+    rs = np.random.RandomState(1)
+    inp = torch.from_numpy(np.concatenate([rs.randn(B, 440), rs.randint(0, 48, (B, 2))],
+                                          1).astype(np.float32))
+
+    def step():            # core.py:216-232
+        outs = utils.forward_model(fea_dict, lab_dict, arch_dict, model, nns, costs, inp, inp_out,
+                                   0, B, "train", [])
+        for o in opts.values():
+            o.zero_grad()
+        outs["loss_final"].backward()
+        for o in opts.values():
+            o.step()
+    return step
+
+
+def main():
+    B, seconds = 128, float(os.environ.get("CAL_SECONDS", "10"))
+    out = {"workload": "C1/C2 MLP training step 440-5x1024-{1928,48}, B=128, fp32, torch-CPU eager",
+           "container_cpus": os.cpu_count(), "results": {}}
+    for threads in (os.cpu_count(), 1):
+        torch.set_num_threads(threads)
+        r_ref = steps_per_s(reference_step(B), seconds) * B
+        r_orc = steps_per_s(oracle_step(B), seconds) * B
+        out["results"][str(threads)] = {"reference_frames_per_s": round(r_ref, 1),
+                                        "oracle_frames_per_s": round(r_orc, 1),
+                                        "oracle_over_reference": round(r_orc / r_ref, 3)}
+        print(threads, out["results"][str(threads)], flush=True)
+    json.dump(out, open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
