@@ -398,15 +398,37 @@ __global__ __launch_bounds__(NT) void gemm_kernel(int M, int N, int K, const voi
                                              B, ldb, C, ldc, kchunk, slab_stride);
 }
 
+// XCD-aware tile order for the standalone 128x128 launches of at most 256 workgroups (PKC_GEMM_XCD,
+// default on; B = 4096 step 3.94-3.96 M -> 4.05-4.06 M frames/s, same run): workgroup
+// w runs on XCD w % 8 (round-robin dispatch), so the linear id is remapped (bijectively, for any
+// grid size) to give each XCD a contiguous run of tiles in (N-tile fastest, M-tile, split) order:
+// the N-tiles of one A row-block share an XCD and its L2, and an XCD reads 1/8 of A instead of
+// all of it.  Speed only: any placement computes the same tiles.
+__device__ __forceinline__ void xcd_tile(int remap, int& bx, int& by, int& bz) {
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int nwg = nx * ny * gridDim.z;
+  int id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  if (remap && nwg >= 16 && nwg <= 256) {     // one workgroup per CU at most (several tiles per
+                                              // CU measured slower: 8192^3 750 -> 685 TF/s)
+    const int xcd = id % 8, q = nwg / 8, r = nwg % 8;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+  }
+  bx = id % nx;
+  by = (id / nx) % ny;
+  bz = id / (nx * ny);
+}
+
 template <bool AKC, bool BKC>
 __global__ __launch_bounds__(big::NT) void gemm_glds_kernel(int M, int N, int K,
                                                            const void* __restrict__ A, int64_t lda,
                                                            const void* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc,
-                                                           int kchunk, int64_t slab_stride) {
+                                                           int kchunk, int64_t slab_stride,
+                                                           int remap) {
   __shared__ __attribute__((aligned(16))) char lds[big::GL_LDS_BYTES];
-  big::body_glds<AKC, BKC>(lds, blockIdx.x, blockIdx.y, blockIdx.z, M, N, K, A, lda, B, ldb, C,
-                           ldc, kchunk, slab_stride);
+  int bx, by, bz;
+  xcd_tile(remap, bx, by, bz);
+  big::body_glds<AKC, BKC>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk, slab_stride);
 }
 
 template <int PREC, bool BIN, bool AKC, bool BKC>
@@ -414,10 +436,13 @@ __global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
                                                           const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,
                                                           float* __restrict__ C, int64_t ldc,
-                                                          int kchunk, int64_t slab_stride) {
+                                                          int kchunk, int64_t slab_stride,
+                                                          int remap) {
   __shared__ __attribute__((aligned(16))) char lds[big::LDS_BYTES];
-  big::body<PREC, BIN, AKC, BKC>(lds, blockIdx.x, blockIdx.y, blockIdx.z, M, N, K, A, lda, B, ldb,
-                                 C, ldc, kchunk, slab_stride);
+  int bx, by, bz;
+  xcd_tile(remap, bx, by, bz);
+  big::body<PREC, BIN, AKC, BKC>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk,
+                                 slab_stride);
 }
 
 // Several independent matmuls in ONE launch (e.g. a layer's dW and dX, both heads' logits):
@@ -537,6 +562,14 @@ static int launch(int M, int N, int K, const void* A, int64_t lda, const void* B
   return PKC_OK;
 }
 
+static int xcd_remap() {                      // PKC_GEMM_XCD=0: launch order (A/B)
+  static const int on = [] {
+    const char* v = getenv("PKC_GEMM_XCD");
+    return v ? atoi(v) : 1;
+  }();
+  return on;
+}
+
 static bool glds_enabled() {                   // PKC_GEMM_GLDS=0: register-staged body (A/B)
   static const int on = [] {
     const char* v = getenv("PKC_GEMM_GLDS");
@@ -560,7 +593,7 @@ static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int6
   if (BIN && K % 64 == 0 && (int64_t)grid.x * grid.y * grid.z <= 256 && glds_enabled()) {
 #define PKC_L(AK, BK_)                                                                          \
   hipLaunchKernelGGL((gemm_glds_kernel<AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, lda, B,   \
-                     ldb, C, ldc, kchunk, slab)
+                     ldb, C, ldc, kchunk, slab, xcd_remap())
     if (akc && bkc) PKC_L(true, true);
     else if (akc) PKC_L(true, false);
     else if (bkc) PKC_L(false, true);
@@ -571,7 +604,7 @@ static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int6
   }
 #define PKC_L(AK, BK_)                                                                          \
   hipLaunchKernelGGL((gemm_big_kernel<PREC, BIN, AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, \
-                     lda, B, ldb, C, ldc, kchunk, slab)
+                     lda, B, ldb, C, ldc, kchunk, slab, xcd_remap())
   if (akc && bkc) PKC_L(true, true);
   else if (akc) PKC_L(true, false);
   else if (bkc) PKC_L(false, true);
