@@ -119,6 +119,25 @@ typedef struct {
   float* dz; float* dgamma; float* dbeta; float* dbias;
 } pkc_dense_bwd_args;
 int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* stream);
+/* SyncBN (cross-rank BatchNorm statistics): the training-mode BatchNorm of
+ * pkc_dense_fwd / pkc_dense_bwd split around a collective the caller runs (sync_bn of the
+ * reference recipe; the reference itself has no multi-GPU training).
+ *   pkc_dense_fwd_stats: this rank's column state (n, mean, M2) -> state[3N] (floats: N counts,
+ *     N means, N M2).  The caller gathers the R ranks' states into states[R][3N] (e.g. an
+ *     all-reduce SUM of a zero-filled buffer that rank r writes at row r);
+ *   pkc_dense_fwd_sync_apply: merges them in rank order (Chan), writes save_mean / save_invstd /
+ *     running statistics (unbiased over the global count) and applies BN / act / dropout to this
+ *     rank's rows.
+ *   pkc_dense_bwd_stats: this rank's column sums (sum dy, sum dy * xhat) -> sums[2N] and the LOCAL
+ *     dgamma / dbeta (the gradient all-reduce sums them); after an all-reduce SUM of sums[2N],
+ *   pkc_dense_bwd_sync_apply applies the BatchNorm backward with the global sums over total_rows.
+ * work: pkc_dense_work_size(M, N) floats, the same buffer for both halves of a direction. */
+int pkc_dense_fwd_stats(const pkc_dense_fwd_args* a, float* work, float* state, void* stream);
+int pkc_dense_fwd_sync_apply(const pkc_dense_fwd_args* a, float* work, const float* states,
+                             int nranks, void* stream);
+int pkc_dense_bwd_stats(const pkc_dense_bwd_args* a, float* work, float* sums, void* stream);
+int pkc_dense_bwd_sync_apply(const pkc_dense_bwd_args* a, float* work, const float* sums,
+                             int total_rows, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused LogSoftmax + NLLLoss(mean) + error rate + d(loss)/d(logits) for one output head

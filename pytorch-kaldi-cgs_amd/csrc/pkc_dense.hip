@@ -87,7 +87,10 @@ __global__ __launch_bounds__(ET) void dense_stats_kernel(pkc_dense_fwd_args a, f
 // -> part[nrb*2N + c] = mean, part[nrb*2N + N + c] = population variance; the BN training side
 // outputs (save_mean / save_invstd / running statistics) are written here.
 constexpr int FC_F = 16, FR_F = 16;
-__global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a, float* part) {
+// STATE: write this rank's (n, mean, M2) per column to state[3N] instead (SyncBN, no side outputs)
+template <bool STATE = false>
+__global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a, float* part,
+                                                            float* state = nullptr) {
   __shared__ float sn[ET], smu[ET], sm2[ET];
   const int cl = threadIdx.x % FC_F, t = threadIdx.x / FC_F;
   const int c = blockIdx.x * FC_F + cl;
@@ -120,6 +123,12 @@ __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a
     mu += d * nk / nn;
     M2 += sm2[j * FC_F + cl] + d * d * n * nk / nn;
     n = nn;
+  }
+  if constexpr (STATE) {
+    state[c] = n;
+    state[N + c] = mu;
+    state[2 * N + c] = M2;
+    return;
   }
   const float var = M2 / (float)a.M;
   float* fin = part + (int64_t)nrb * 2 * N;
@@ -172,6 +181,36 @@ __global__ __launch_bounds__(ET) void dense_bwd_finalize_kernel(pkc_dense_bwd_ar
   } else if (a.dbias) {
     a.dbias[c] = tdy;
   }
+}
+
+// SyncBN: the ranks' (n, mean, M2) column states merged in rank order (Chan), then the same
+// outputs as dense_finalize_kernel from the global statistics (running_var unbiased over the
+// global row count).  One thread per column.
+__global__ void dense_sync_merge_kernel(pkc_dense_fwd_args a, float* part, const float* states,
+                                        int nranks) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.N) return;
+  const int64_t N = a.N;
+  float n = 0.f, mu = 0.f, M2 = 0.f;
+  for (int r = 0; r < nranks; ++r) {
+    const float* st = states + (int64_t)r * 3 * N;
+    const float nk = st[c];
+    if (nk == 0.f) continue;
+    const float nn = n + nk;
+    const float d = st[N + c] - mu;
+    mu += d * nk / nn;
+    M2 += st[2 * N + c] + d * d * n * nk / nn;
+    n = nn;
+  }
+  const float var = n > 0.f ? M2 / n : 0.f;
+  float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+  fin[c] = mu;
+  fin[N + c] = var;
+  a.save_mean[c] = mu;
+  a.save_invstd[c] = 1.f / sqrtf(var + a.eps);
+  const float unb = n > 1.f ? var * n / (n - 1.f) : var;
+  a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
+  a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
 }
 
 __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, const float* part) {
@@ -261,7 +300,9 @@ __global__ __launch_bounds__(ET) void dense_bwd_stats_kernel(pkc_dense_bwd_args 
   }
 }
 
-__global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args a, const float* part) {
+// invM: 1 / the row count the column sums are over (this rank's M, or the global count: SyncBN)
+__global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args a, const float* part,
+                                                             float invM) {
   const int c = blockIdx.x * EC + threadIdx.x % EC;
   const int t = threadIdx.x / EC;
   const int r0 = blockIdx.y * ERB;
@@ -271,7 +312,6 @@ __global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args 
   const float tdy = fin[c], tdyx = fin[N + c];
   const bool bn = a.norm == PKC_NORM_BN_TRAIN;
   if (!bn) return;
-  const float invM = 1.f / (float)a.M;
   const float k = a.gamma[c] * a.save_invstd[c];
   const float mdy = tdy * invM, mdyx = tdyx * invM;
 #pragma unroll
@@ -652,8 +692,8 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   if (a->norm == PKC_NORM_BN_TRAIN) {
     hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
     PKC_LAUNCH_CHECK("pkc_dense_fwd stats");
-    hipLaunchKernelGGL(dense_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0, S(stream), *a,
-                       work);
+    hipLaunchKernelGGL(dense_finalize_kernel<false>, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
+                       S(stream), *a, work, nullptr);
     PKC_LAUNCH_CHECK("pkc_dense_fwd finalize");
   }
   hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
@@ -686,8 +726,88 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
                      *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd finalize");
   if (a->norm == PKC_NORM_BN_TRAIN)      // without BN, dz = dy is final after the stats pass
-    hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+    hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work,
+                       1.f / (float)a->M);
   PKC_LAUNCH_CHECK("pkc_dense_bwd apply");
+  return PKC_OK;
+}
+
+// ------------------------------------------------------------------ SyncBN
+static int sync_fwd_check(const pkc_dense_fwd_args* a, const float* work) {
+  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab >= 1 && a->zslab && a->out &&
+                    a->norm == PKC_NORM_BN_TRAIN && a->gamma && a->beta && a->running_mean &&
+                    a->running_var && a->save_mean && a->save_invstd && a->xhat && work,
+                "pkc_dense_fwd sync: BN training arguments");
+  PKC_CHECK_ARG(a->nslab == 1 || a->slab_stride >= (int64_t)a->M * a->N,
+                "pkc_dense_fwd sync: slab_stride too small");
+  PKC_CHECK_ARG(a->drop_p >= 0.f && a->drop_p < 1.f, "pkc_dense_fwd sync: drop_p out of range");
+  return PKC_OK;
+}
+
+extern "C" int pkc_dense_fwd_stats(const pkc_dense_fwd_args* a, float* work, float* state,
+                                   void* stream) {
+  using namespace pkc;
+  int st = sync_fwd_check(a, work);
+  if (st) return st;
+  PKC_CHECK_ARG(state, "pkc_dense_fwd_stats: null state");
+  dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  hipLaunchKernelGGL(dense_finalize_kernel<true>, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
+                     S(stream), *a, work, state);
+  PKC_LAUNCH_CHECK("pkc_dense_fwd_stats");
+  return PKC_OK;
+}
+
+extern "C" int pkc_dense_fwd_sync_apply(const pkc_dense_fwd_args* a, float* work,
+                                        const float* states, int nranks, void* stream) {
+  using namespace pkc;
+  int st = sync_fwd_check(a, work);
+  if (st) return st;
+  PKC_CHECK_ARG(states && nranks >= 1, "pkc_dense_fwd_sync_apply: states / nranks");
+  hipLaunchKernelGGL(dense_sync_merge_kernel, dim3((a->N + 255) / 256), dim3(256), 0, S(stream), *a,
+                     work, states, nranks);
+  dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  PKC_LAUNCH_CHECK("pkc_dense_fwd_sync_apply");
+  return PKC_OK;
+}
+
+static int sync_bwd_check(const pkc_dense_bwd_args* a, const float* work) {
+  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab >= 1 && a->gslab && a->xhat && a->dz && work &&
+                    a->norm == PKC_NORM_BN_TRAIN && a->gamma && a->beta && a->save_invstd,
+                "pkc_dense_bwd sync: BN training arguments");
+  PKC_CHECK_ARG(a->drop_p == 0.f || a->keep, "pkc_dense_bwd sync: dropout needs the keep mask");
+  return PKC_OK;
+}
+
+extern "C" int pkc_dense_bwd_stats(const pkc_dense_bwd_args* a, float* work, float* sums,
+                                   void* stream) {
+  using namespace pkc;
+  int st = sync_bwd_check(a, work);
+  if (st) return st;
+  PKC_CHECK_ARG(sums, "pkc_dense_bwd_stats: null sums");
+  dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
+                     S(stream), *a, work);
+  const float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
+  hipMemcpyAsync(sums, fin, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice, S(stream));
+  PKC_LAUNCH_CHECK("pkc_dense_bwd_stats");
+  return PKC_OK;
+}
+
+extern "C" int pkc_dense_bwd_sync_apply(const pkc_dense_bwd_args* a, float* work, const float* sums,
+                                        int total_rows, void* stream) {
+  using namespace pkc;
+  int st = sync_bwd_check(a, work);
+  if (st) return st;
+  PKC_CHECK_ARG(sums && total_rows >= a->M, "pkc_dense_bwd_sync_apply: sums / total_rows");
+  float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
+  hipMemcpyAsync(fin, sums, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice, S(stream));
+  dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work,
+                     1.f / (float)total_rows);
+  PKC_LAUNCH_CHECK("pkc_dense_bwd_sync_apply");
   return PKC_OK;
 }
 

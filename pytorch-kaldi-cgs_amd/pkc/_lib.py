@@ -114,6 +114,10 @@ _SIGS = {
     "pkc_dense_fwd": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp]),
     "pkc_dense_bwd": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp]),
     "pkc_dense_work_size": (i64, [C.c_int, C.c_int]),
+    "pkc_dense_fwd_stats": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp, vp]),
+    "pkc_dense_fwd_sync_apply": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp, C.c_int, vp]),
+    "pkc_dense_bwd_stats": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp, vp]),
+    "pkc_dense_bwd_sync_apply": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp, C.c_int, vp]),
     "pkc_nll_fused": (C.c_int, [C.POINTER(NllArgs), vp]),
     "pkc_loss_finalize": (C.c_int, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp]),
     "pkc_nll_fused_multi": (C.c_int, [vp, C.c_int, vp]),

@@ -283,8 +283,14 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         if to_do == "train":
             eng.sync_state()
     elif to_do in ("train", "valid"):
+        # SyncBN (pkc extension): [exp] sync_bn = True synchronises the MLP layers'
+        # BatchNorm statistics over the ranks (default: per-rank statistics, as each reference
+        # batch is normalised by its own)
+        sbn = None
+        if ws_eff > 1 and to_do == "train" and config["exp"].get("sync_bn", "False") == "True":
+            sbn = DP.SyncBatchNorm()
         eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
-                     train=(to_do == "train"), grad_scale=1.0 / ws_eff)
+                     train=(to_do == "train"), grad_scale=1.0 / ws_eff, sync_bn=sbn)
         for net_name in nns:
             pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
             if pt != "none" and to_do == "train":

@@ -147,6 +147,25 @@ class GradAllReduce:
         return dist.all_reduce(gflat, group=self.group, async_op=async_op)
 
 
+class SyncBatchNorm:
+    """Engine(sync_bn=SyncBatchNorm()): the MLP layers' training-mode BatchNorm statistics over
+    the GLOBAL batch of all ranks (SURVEY 8e's optional SyncBN; its DP parity recipe: R ranks on a
+    split global batch equal one process on the whole batch).  Per BatchNorm layer and direction
+    one small all-reduce: the ranks' (n, mean, M2) column states (forward, merged in rank order by
+    pkc_dense_fwd_sync_apply) and the column sums of dy, dy * xhat (backward).  Eager steps only
+    (Engine.capture returns False with it)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank, self.world = world()
+        self.calls = 0
+
+    def __call__(self, t):
+        self.calls += 1
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+
+
 def average_buffers(modules, device=None):
     """Average BatchNorm running_mean / running_var over ranks (one all-reduce per chunk)."""
     rank, ws = world()

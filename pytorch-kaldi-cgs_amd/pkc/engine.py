@@ -382,7 +382,7 @@ class Engine:
 
     def __init__(self, nets, arch_opts, lines, fea_cols, lab_names, batch, prec=L.PREC_FP32,
                  device="cuda", seed=0, train=True, drop_keep_in=None, grad_scale=1.0, max_len=None,
-                 rnn_drop_in=None):
+                 rnn_drop_in=None, sync_bn=None):
         self.dev = torch.device(device)
         self.nets, self.arch_opts, self.lines = nets, arch_opts, lines
         self.B = int(batch)
@@ -393,6 +393,8 @@ class Engine:
         # sequence DP: callable(rows of this rank's batch) -> this rank's loss scale (set by the
         # caller, pkc.dist.frame_weight), recomputed every step; None: the fixed grad_scale
         self.frame_weight = None
+        # SyncBN (pkc.dist.SyncBatchNorm): the MLP layers' BatchNorm statistics over all ranks
+        self.sync_bn = sync_bn
         self.prof = None                       # profile mode: list of per-launch events
         self.F = max(c1 for _, c1 in fea_cols.values())
         self.fea_cols = fea_cols
@@ -607,6 +609,9 @@ class Engine:
             n.save_invstd = _f32(N, dev)
             n.dz = _f32(M * N, dev)
             n.work = _f32(L.lib().pkc_dense_work_size(M, N), dev)
+            if self.sync_bn is not None and n.bn and not n.head and n.W is not None:
+                n.bn_states = _f32(self.sync_bn.world * 3 * N, dev)     # ranks' (n, mean, M2)
+                n.bn_sums = _f32(2 * N, dev)                           # sum dy, sum dy * xhat
             n.sdw = self._dw_splits(N, K) if n.W is not None else 1
             n.dwslab = _f32(n.sdw * N * K, dev) if n.sdw > 1 else None
             if n.qbits:
@@ -1153,6 +1158,17 @@ class Engine:
             keep_in=keep_in.data_ptr() if keep_in is not None else None,
             keep_out=n.keep.data_ptr() if (n.keep is not None and train) else None,
             xhat=n.xhat.data_ptr(), out=n.out.data_ptr(), count_n=0)
+        if train and n.bn and getattr(n, "bn_states", None) is not None:
+            # SyncBN: this rank's column state into its row of bn_states, all-reduce (gather),
+            # merge + apply
+            R, r = self.sync_bn.world, self.sync_bn.rank
+            n.bn_states.zero_()
+            self._k("dense_fwd_stats N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 1), "pkc_dense_fwd_stats",
+                    C.byref(a), ptr(n.work), C.c_void_p(n.bn_states.data_ptr() + 4 * r * 3 * n.N), s)
+            self.sync_bn(n.bn_states)
+            self._k("dense_fwd_sync_apply N=%d" % n.N, 0, 4.0 * M * n.N * 3,
+                    "pkc_dense_fwd_sync_apply", C.byref(a), ptr(n.work), ptr(n.bn_states), R, s)
+            return
         self._k("dense_fwd N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_dense_fwd",
                 C.byref(a), ptr(n.work), s)
 
@@ -1365,8 +1381,17 @@ class Engine:
                            dgamma=n.dgamma.data_ptr() if n.bn else None,
                            dbeta=n.dbeta.data_ptr() if n.bn else None,
                            dbias=n.db.data_ptr() if (n.b is not None and not n.ln) else None)
-        self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 3), "pkc_dense_bwd",
-                C.byref(a), ptr(n.work), s)
+        if n.bn and getattr(n, "bn_sums", None) is not None:
+            # SyncBN: local column sums (and local dgamma / dbeta), all-reduce, global apply
+            self._k("dense_bwd_stats N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 2), "pkc_dense_bwd_stats",
+                    C.byref(a), ptr(n.work), ptr(n.bn_sums), s)
+            self.sync_bn(n.bn_sums)
+            self._k("dense_bwd_sync_apply N=%d" % n.N, 0, 4.0 * M * n.N * 3,
+                    "pkc_dense_bwd_sync_apply", C.byref(a), ptr(n.work), ptr(n.bn_sums),
+                    M * self.sync_bn.world, s)
+        else:
+            self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 3), "pkc_dense_bwd",
+                    C.byref(a), ptr(n.work), s)
         if n.ln:
             # the Linear's bias sits in front of the LayerNorm (per-row statistics): its gradient
             # is the column sum of the LayerNorm's input gradient
@@ -1823,8 +1848,8 @@ class Engine:
         Without the split, a second graph holds steps_per_graph consecutive steps (the batch
         counter lives on the device), so train_steps() pays one graph launch per that many
         batches instead of one per batch."""
-        if not self.static_opt or self.seq:
-            return False
+        if not self.static_opt or self.seq or self.sync_bn is not None:
+            return False             # SyncBN: collectives inside the forward / backward, eager
         self._set_rows(None)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

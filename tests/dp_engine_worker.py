@@ -4,7 +4,7 @@ sharing one GPU).  Each rank trains its half of every global batch with Engine(g
 and the bucketed all-reduce of pkc.dist.GradAllReduce (the first bucket overlapping the rest of the
 backward), eagerly or replayed from the split hipGraphs (mode "graph"), and saves its state.
 
-argv: out_dir mode steps B_per_rank
+argv: out_dir mode (eager | graph | syncbn) steps B_per_rank
 """
 import os
 import sys
@@ -19,13 +19,18 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
-def dp_config():
-    """Body 40 -> 64 (LayerNorm, no BatchNorm: the local batch statistics of BN differ per rank),
-    SGD; cd head 32 (RMSprop), mono head 8 (RMSprop); dropout 0."""
+def dp_config(bn=False):
+    """Body 40 -> 64 (LayerNorm, no BatchNorm: the local batch statistics of BN differ per rank;
+    bn=True: BatchNorm on both layers, for the SyncBN runs), SGD; cd head 32 (RMSprop), mono head 8
+    (RMSprop); dropout 0."""
     from cases import build_mlp_config
     cfg = build_mlp_config("plain")
-    cfg["architecture1"].update(dnn_lay="64,64", dnn_use_batchnorm="False,False",
-                                dnn_use_laynorm="True,False", dnn_act="relu,tanh")
+    if bn:
+        cfg["architecture1"].update(dnn_lay="64,64", dnn_use_batchnorm="True,True",
+                                    dnn_use_laynorm="False,False", dnn_act="relu,tanh")
+    else:
+        cfg["architecture1"].update(dnn_lay="64,64", dnn_use_batchnorm="False,False",
+                                    dnn_use_laynorm="True,False", dnn_act="relu,tanh")
     cfg["architecture2"].update(dnn_lay="32")
     return cfg
 
@@ -41,7 +46,7 @@ def data(steps, B_total):
     return X, lab
 
 
-def build(cfg, world, B, X, lab):
+def build(cfg, world, B, X, lab, sync_bn=None):
     from pkc.engine import Engine, parse_model
     from pkc.neural_networks import MLP
     torch.manual_seed(2234)
@@ -52,7 +57,7 @@ def build(cfg, world, B, X, lab):
         nets[o["arch_name"]] = MLP(o, inp).cuda().train()
         opts[o["arch_name"]] = o
     eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 40)},
-                 ["lab_cd", "lab_mono"], batch=B, seed=1, grad_scale=1.0 / world)
+                 ["lab_cd", "lab_mono"], batch=B, seed=1, grad_scale=1.0 / world, sync_bn=sync_bn)
     eng.bind_chunk(torch.from_numpy(X).cuda(), torch.from_numpy(lab).cuda(), X.shape[0])
     return eng, nets
 
@@ -68,7 +73,8 @@ def main():
     # walks them in order
     rows = np.concatenate([np.arange(s * B * world + rank * B, s * B * world + (rank + 1) * B)
                            for s in range(steps)])
-    eng, nets = build(dp_config(), world, B, X[rows], lab[rows])
+    sbn = DP.SyncBatchNorm() if mode == "syncbn" else None
+    eng, nets = build(dp_config(bn=mode == "syncbn"), world, B, X[rows], lab[rows], sync_bn=sbn)
     ar = DP.GradAllReduce()
     if mode == "graph":
         assert eng.capture(split_optimizer=True)

@@ -22,11 +22,11 @@ pytestmark = pytest.mark.gpu
 STEPS, B = 3, 32
 
 
-def full_batch_reference():
+def full_batch_reference(bn=False):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import dp_engine_worker as W
     X, lab = W.data(STEPS, 2 * B)
-    eng, nets = W.build(W.dp_config(), 1, 2 * B, X, lab)
+    eng, nets = W.build(W.dp_config(bn=bn), 1, 2 * B, X, lab)
     for _ in range(STEPS):
         eng.train_step()
     torch.cuda.synchronize()
@@ -35,12 +35,15 @@ def full_batch_reference():
                   for k, v in nets[a].state_dict().items()}
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph"])
+@pytest.mark.parametrize("mode", ["eager", "graph", "syncbn"])
 def test_dp_engine_two_ranks_equal_full_batch(mode, tmp_path):
+    """syncbn: the body layers carry BatchNorm, its statistics synchronised over the ranks
+    (pkc.dist.SyncBatchNorm, SURVEY 8e's DP parity recipe): then the split global batch still
+    equals the one-process full batch, running statistics included."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000 +
-                                                            (7 if mode == "graph" else 0)),
+                                                            {"graph": 7, "syncbn": 13}.get(mode, 0)),
            os.path.join(ROOT, "tests", "dp_engine_worker.py"), str(tmp_path), mode, str(STEPS),
            str(B)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
@@ -48,7 +51,7 @@ def test_dp_engine_two_ranks_equal_full_batch(mode, tmp_path):
     g0 = np.load(os.path.join(tmp_path, "rank0_%s.npz" % mode))
     g1 = np.load(os.path.join(tmp_path, "rank1_%s.npz" % mode))
     assert int(g0["calls"]) == 2 * STEPS          # two buckets per step
-    loss, ref = full_batch_reference()
+    loss, ref = full_batch_reference(bn=mode == "syncbn")
     for k, v in ref.items():
         np.testing.assert_array_equal(g0[k], g1[k], err_msg="replicas differ: " + k)
         if k.endswith("num_batches_tracked"):
