@@ -170,6 +170,27 @@ def test_engine_c1_full_size_vs_oracle():
         ref = outs["out_dnn2"].detach()
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
         assert rel < 1e-4, "step %d posterior max rel err %.3g" % (s, rel)
+        if s == 0:
+            # the first step's gradients, every parameter, before any optimizer drift: the
+            # engine's flat gradient buffer vs the oracle's autograd .grad
+            gview = {id(p): getattr(n, key) for n in eng.nodes for (p, key, _m) in n.params()
+                     if isinstance(key, str)}
+            checked = 0
+            for a in nets:
+                mine = dict(nets[a].named_parameters())
+                for name, op in onets[a].named_parameters():
+                    if op.grad is None or id(mine[name]) not in gview:
+                        continue
+                    g = gview[id(mine[name])].detach().cpu().double().reshape(op.grad.shape)
+                    r = op.grad.double()
+                    d = (g - r).norm().item()
+                    # (a Linear bias in front of BatchNorm has an exactly zero gradient, which
+                    # pkc writes; autograd leaves rounding residue of ~1e-8 there)
+                    assert d <= 1e-4 * r.norm().item() + 1e-6 * r.numel() ** 0.5, \
+                        "%s %s grad rel frob err %.3g" % (
+                        a, name, d / max(r.norm().item(), 1e-30))
+                    checked += 1
+            assert checked >= 20
         np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-5)
         np.testing.assert_allclose(err, outs["err_final"].item())
     # Parameters after 3 steps: a pre-activation within rounding of 0 can take the other ReLU
