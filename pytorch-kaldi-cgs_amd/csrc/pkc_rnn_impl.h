@@ -429,13 +429,14 @@ __device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1
   __syncthreads();
 }
 
-template <int S>
+// R16: the tile has only its first 16 rows (2B <= 16: C3, C5), the second chain is skipped
+template <int S, bool R16 = false>
 __device__ __forceinline__ void mfma_chain(const float* va, const float* vb, const float* vu,
                                            f32x4& acc0, f32x4& acc1) {
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s], vu[s], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[s], vu[s], acc1, 0, 0, 0);
+    if constexpr (!R16) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[s], vu[s], acc1, 0, 0, 0);
   }
 }
 
@@ -558,7 +559,7 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 // cell, reading rh).  Tile: rows [32*blockIdx.y, +32) x NG gates of NU = 16/NG units.
 // NW waves (4: 256 threads, or 8: the contraction in 32 strips of S — half the operand loads per
 // lane and half the MFMA chain per wave, for the long-H layers whose step is load-latency-bound)
-template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4>
+template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4, bool R16 = false>
 __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
   constexpr int NTH = 64 * NW;
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   const int H = a.H, B2 = ix.B2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, q = lane >> 4;
-  const int u0 = blockIdx.x * NU, r0 = blockIdx.y * 32;
+  const int u0 = blockIdx.x * NU, r0 = blockIdx.y * (R16 ? 16 : 32);
   const float* src = (PH == 0 ? a.hs : a.rh) + (int64_t)t * B2 * H;
   const int ra = r0 + c, rb = r0 + 16 + c;
   const int gi = c / NU, u = u0 + c % NU;
@@ -588,13 +589,17 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     int blk[S / 16];
     tile_blocks<S>(a.kmap_fwd + (int64_t)blockIdx.x * S, blk);
     load_blocks<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
-    load_blocks<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
+    if constexpr (!R16) load_blocks<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
     load_blocks<S>(pu, u < H, blk, H, vw, vu);
   } else {
     const int kb = (w * 4 + q) * S;
     load_strip<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
-    load_strip<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
+    if constexpr (!R16) load_strip<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
     load_strip<S>(pu, u < H, kb, H, vw, vu);
+  }
+  if constexpr (R16) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) vb[s] = 0.f;
   }
   float vars[4] = {0.f, 0.f, 0.f, 0.f};
   const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
@@ -639,16 +644,16 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
       float vg[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) vg[s] = gi == g ? vu[s] : 0.f;
-      mfma_chain<S>(va, vb, vg, acc0, acc1);
+      mfma_chain<S, R16>(va, vb, vg, acc0, acc1);
     }
   } else {
-    mfma_chain<S>(va, vb, vu, acc0, acc1);
+    mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
   }
   reduce_tile<NW>(acc0, acc1, red, tile);
   for (int p = threadIdx.x; p < 32 * NU; p += NTH) {
     const int rl = p / NU, ul = p % NU;
     const int r = r0 + rl, j = u0 + ul;
-    if (r >= B2 || j >= H) continue;
+    if ((R16 && rl >= 16) || r >= B2 || j >= H) continue;
     if constexpr (PH == 1) {
       cand_epi<cand_gate(CELL)>(a, ix, t, r, j, tile[rl * 17 + ul]);
     } else {
@@ -719,7 +724,7 @@ __device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, 
 // MODE 0: the product of gate g0 + blockIdx.z into slab blockIdx.z (a.work + (4 + z) n);
 // MODE 1: one-gate product + bwd_step_epi (t = tt + 1); MODE 2: one-gate product + rh_epi.
 // out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
-template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4>
+template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4, bool R16 = false>
 __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
   constexpr int NTH = 64 * NW;
@@ -729,7 +734,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   const int H = a.H, B2 = ix.B2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, q = lane >> 4;
-  const int k0 = blockIdx.x * 16, r0 = blockIdx.y * 32;
+  const int k0 = blockIdx.x * 16, r0 = blockIdx.y * (R16 ? 16 : 32);
   const int g = g0 + blockIdx.z;
   const int64_t TB2H = (int64_t)a.T * B2 * H;
   const float* dg = a.dgates + g * TB2H + (int64_t)t * B2 * H;
@@ -741,22 +746,22 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
     int blk[S / 16];
     tile_blocks<S>(a.kmap_bwd + ((int64_t)g * gridDim.x + blockIdx.x) * S, blk);
     load_blocks<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
-    load_blocks<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
+    if constexpr (!R16) load_blocks<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
     load_blocks<S>(pu, k < H, blk, H, vw, vu);
   } else {
     const int kb = (w * 4 + q) * S;
     load_strip<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
-    load_strip<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
+    if constexpr (!R16) load_strip<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
     load_strip<S>(pu, k < H, kb, H, vw, vu);
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  mfma_chain<S>(va, vb, vu, acc0, acc1);
+  mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
   reduce_tile<NW>(acc0, acc1, red, tile);
   const int64_t n = (int64_t)B2 * H;
   for (int p = threadIdx.x; p < 32 * 16; p += NTH) {
     const int rl = p >> 4, kl = p & 15;
     const int r = r0 + rl, kk = k0 + kl;
-    if (r >= B2 || kk >= H) continue;
+    if ((R16 && rl >= 16) || r >= B2 || kk >= H) continue;
     const float v = tile[rl * 17 + kl];
     if constexpr (MODE == 0) a.work[(4 + blockIdx.z) * n + (int64_t)r * H + kk] = v;
     else if constexpr (MODE == 1) bwd_step_epi<G, CELL>(a, ix, t - 1, r, kk, v);
@@ -826,6 +831,15 @@ struct SCase {};
 
 static int pick_vw(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
 
+// 16-row step tiles when 2B <= 16 (PKC_RNN_ROWS16=0: the 32-row tiles, A/B)
+static bool rows16() {
+  static const int on = [] {
+    const char* v = getenv("PKC_RNN_ROWS16");
+    return v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
+
 // 8-wave step tiles for the dense one-phase cells at S >= 32 (H > 256): half the operand strip
 // per lane and half the MFMA chain per wave.  Same-run A/B (PKC_RNN_WAVES=4 / 8): C4 89.2k / 90.8k,
 // C5 (8-wave BPTT only; its quantised forward keeps 4) 117.6k / 120.3k frames/s — the step is
@@ -854,8 +868,24 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     }
   } else {
     dim3 g1((a->H + 16 / G - 1) / (16 / G), rows);
+    // 2B <= 16 rows (C3, C5): 16-row tiles, no second MFMA chain or operand strip
+    const bool r16 = B2 <= 16 && rows16();
+    const dim3 g16(g1.x, 1);
     for (int t = 0; t < a->T; ++t) {
-      if constexpr (SP)
+      if (r16) {
+        if constexpr (SP)
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), g16, dim3(RT), 0, s,
+                             *a, t, vw);
+        else if (a->qbits > 0)
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), g16, dim3(RT), 0, s,
+                             *a, t, vw);
+        else if (eight_waves(S))
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true>), g16,
+                             dim3(2 * RT), 0, s, *a, t, vw);
+        else
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true>), g16, dim3(RT), 0,
+                             s, *a, t, vw);
+      } else if constexpr (SP)
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), g1, dim3(RT), 0, s, *a, t, vw);
       else if (a->qbits > 0)
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
@@ -910,6 +940,14 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       if constexpr (G == 1) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
+      } else if (B2 <= 16 && rows16()) {            // 16-row tiles (C3, C5)
+        if (!SP && eight_waves(S))
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>), dim3(kt, 1, G),
+                             dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
+        else
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), dim3(kt, 1, G), dim3(RT), 0,
+                             s, *a, tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else if (!SP && eight_waves(S)) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), dim3(kt, rows, G),
                            dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
