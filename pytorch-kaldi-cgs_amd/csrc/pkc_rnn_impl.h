@@ -831,13 +831,13 @@ struct SCase {};
 
 static int pick_vw(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
 
-// 16-row step tiles when 2B <= 16 (PKC_RNN_ROWS16=0: the 32-row tiles, A/B)
-static bool rows16() {
-  static const int on = [] {
+// 16-row step tiles up to 2B <= PKC_RNN_ROWS16 rows (default 16; 0: always the 32-row tiles)
+static bool rows16(int B2) {
+  static const int lim = [] {
     const char* v = getenv("PKC_RNN_ROWS16");
-    return v ? atoi(v) : 1;
+    return v ? atoi(v) : 16;
   }();
-  return on != 0;
+  return B2 <= lim;
 }
 
 // 8-wave step tiles for the dense one-phase cells at S >= 32 (H > 256): half the operand strip
@@ -857,20 +857,29 @@ template <int G, int CELL, int S, bool SP = false>
 static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
   const int vw = pick_vw(a->H);
-  const unsigned rows = (unsigned)((B2 + 31) / 32);
+  const unsigned rows = (unsigned)((B2 + 31) / 32), rows_16 = (unsigned)((B2 + 15) / 16);
   if constexpr (two_phase(CELL)) {
     constexpr int NG = G - 1;                        // gates that read h_{t-1}
     dim3 g1((a->H + 16 / NG - 1) / (16 / NG), rows), g2((a->H + 15) / 16, rows);
+    const bool r16 = rows16(B2);
+    const dim3 g1r(g1.x, rows_16), g2r(g2.x, rows_16);
     for (int t = 0; t < a->T; ++t) {
-      hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
-      hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), g2, dim3(RT), 0, s, *a, t, vw);
+      if (r16) {
+        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false, false, 4, true>), g1r, dim3(RT), 0, s,
+                           *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false, false, 4, true>), g2r, dim3(RT), 0, s,
+                           *a, t, vw);
+      } else {
+        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), g2, dim3(RT), 0, s, *a, t, vw);
+      }
       if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
   } else {
     dim3 g1((a->H + 16 / G - 1) / (16 / G), rows);
     // 2B <= 16 rows (C3, C5): 16-row tiles, no second MFMA chain or operand strip
-    const bool r16 = B2 <= 16 && rows16();
-    const dim3 g16(g1.x, 1);
+    const bool r16 = rows16(B2);
+    const dim3 g16(g1.x, rows_16);
     for (int t = 0; t < a->T; ++t) {
       if (r16) {
         if constexpr (SP)
@@ -907,7 +916,8 @@ template <int G, int CELL, int S, bool SP = false>
 static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
   const int vw = pick_vw(a->H);
-  const unsigned rows = (unsigned)((B2 + 31) / 32);
+  const unsigned rows = (unsigned)((B2 + 31) / 32), rows_16 = (unsigned)((B2 + 15) / 16);
+  const bool r16 = rows16(B2);
   const int64_t n = (int64_t)B2 * a->H;
   const unsigned eb = (unsigned)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024);
   const dim3 tg((a->H + 31) / 32, (a->H + 31) / 32, G);
@@ -920,33 +930,52 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
   const unsigned kt = (unsigned)((a->H + 15) / 16);
   if constexpr (two_phase(CELL)) {
     constexpr int HG = cand_gate(CELL);
-    hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
-                       a->T - 1, HG, vw);
+    // the candidate gate's U^T product (MODE 2) and the gates' sum (MODE 0 / 1)
+    auto mm2 = [&](int t) {
+      if (r16)
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S, false, 4, true>), dim3(kt, rows_16, 1),
+                           dim3(RT), 0, s, *a, t, HG, vw);
+      else
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a, t,
+                           HG, vw);
+    };
+    mm2(a->T - 1);
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (CELL == PKC_CELL_GRU) {           // Uz^T dz + Ur^T dr: two gate slabs
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, 2), dim3(RT), 0, s, *a,
-                           tt + 1, 0, vw);
+        if (r16)
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true>), dim3(kt, rows_16, 2),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
+        else
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, 2), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw);
         hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, 2>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else {                                        // minimalGRU: Uz^T dz, one gate
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
-                           tt + 1, 0, vw);
+        if (r16)
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), dim3(kt, rows_16, 1),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
+        else
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw);
       }
       if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
-      hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a, tt,
-                         HG, vw);
+      mm2(tt);
     }
   } else {
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (G == 1) {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
-                           tt + 1, 0, vw);
-      } else if (B2 <= 16 && rows16()) {            // 16-row tiles (C3, C5)
-        if (!SP && eight_waves(S))
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>), dim3(kt, 1, G),
-                             dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
+        if (r16)
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), dim3(kt, rows_16, 1),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), dim3(kt, 1, G), dim3(RT), 0,
-                             s, *a, tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw);
+      } else if (r16) {                               // 16-row tiles (C3, C5)
+        if (!SP && eight_waves(S))
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>),
+                             dim3(kt, rows_16, G), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
+        else
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), dim3(kt, rows_16, G),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
         hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else if (!SP && eight_waves(S)) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), dim3(kt, rows, G),
