@@ -101,6 +101,7 @@ typedef struct {
   float* out;                                 /* M x N */
   int64_t count_n;   /* rows BatchNorm1d sees for the unbiased running_var (0 -> M); a shared-
                         weight bidirectional layer normalises 2x duplicated rows (2*M) */
+  void* out_bf16;    /* optional bf16 copy of out (M x N): the next layer's PKC_PREC_BF16IN operand */
 } pkc_dense_fwd_args;
 int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream);
 /* floats of device workspace pkc_dense_fwd / pkc_dense_bwd need (per-16-row column partials) */
@@ -117,6 +118,7 @@ typedef struct {
   const float* gamma; const float* beta; const float* save_invstd;
   const float* xhat; const uint8_t* keep; float drop_p;
   float* dz; float* dgamma; float* dbeta; float* dbias;
+  void* dz_bf16;     /* optional bf16 copy of dz (M x N): the dW / dX PKC_PREC_BF16IN operand */
 } pkc_dense_bwd_args;
 int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* stream);
 /* SyncBN (cross-rank BatchNorm statistics): the training-mode BatchNorm of

@@ -213,6 +213,18 @@ __global__ void dense_sync_merge_kernel(pkc_dense_fwd_args a, float* part, const
   a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unb;
 }
 
+// bf16 copies of the outputs (operands of the next PKC_PREC_BF16IN matmuls): round-to-nearest-even,
+// the same rounding the PKC_PREC_BF16 matmuls apply to the fp32 values when they stage them
+__device__ __forceinline__ void st_h1(void* p, int64_t i, float v) {
+  reinterpret_cast<__bf16*>(p)[i] = (__bf16)v;
+}
+__device__ __forceinline__ void st_h4(void* p, int64_t i, float4 v) {   // i % 4 == 0
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  bf16x4 h;
+  h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+  *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(p) + i) = h;
+}
+
 __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, const float* part) {
   const int c = blockIdx.x * EC + threadIdx.x % EC;
   const int t = threadIdx.x / EC;
@@ -260,6 +272,7 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
     }
     if (a.xhat) a.xhat[idx] = xh;
     a.out[idx] = o;
+    if (a.out_bf16) st_h1(a.out_bf16, idx, o);
   }
 }
 
@@ -288,6 +301,7 @@ __global__ __launch_bounds__(ET) void dense_bwd_stats_kernel(pkc_dense_bwd_args 
       const float y = bn ? xh * gam + bet : xh;
       const float dy = g * act_bwd(a.act, y, act_fwd(a.act, y));
       a.dz[idx] = dy;
+      if (!bn && a.dz_bf16) st_h1(a.dz_bf16, idx, dy);    // final without BN
       sdy += dy;
       sdyx += dy * xh;
     }
@@ -319,7 +333,9 @@ __global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args 
     const int r = r0 + t + ER * i;
     if (r >= a.M) break;
     const int64_t idx = r * N + c;
-    a.dz[idx] = k * (a.dz[idx] - mdy - a.xhat[idx] * mdyx);
+    const float d = k * (a.dz[idx] - mdy - a.xhat[idx] * mdyx);
+    a.dz[idx] = d;
+    if (a.dz_bf16) st_h1(a.dz_bf16, idx, d);
   }
 }
 
@@ -546,6 +562,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
     if (drop && a.keep_out) *reinterpret_cast<uint32_t*>(a.keep_out + idx) = kw;
     if (a.xhat) *reinterpret_cast<float4*>(a.xhat + idx) = xh;
     *reinterpret_cast<float4*>(a.out + idx) = o;
+    if (a.out_bf16) st_h4(a.out_bf16, idx, o);
   }
 }
 
@@ -631,6 +648,7 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
       f4set(o, j, bn ? f4get(k, j) * (d - f4get(mdy, j) - f4get(xh[i], j) * f4get(mdyx, j)) : d);
     }
     *reinterpret_cast<float4*>(a.dz + (int64_t)row * N + c) = o;
+    if (a.dz_bf16) st_h4(a.dz_bf16, (int64_t)row * N + c, o);
   }
 }
 
@@ -678,7 +696,7 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   PKC_CHECK_ARG(a->nslab == 1 || a->slab_stride >= (int64_t)a->M * a->N,
                 "pkc_dense_fwd: slab_stride too small");
   if (small_ok(a->M, a->N, a->nslab, a->zslab, a->out, a->slab_stride) &&
-      (uintptr_t)a->xhat % 16 == 0 && (!a->bias || (uintptr_t)a->bias % 16 == 0) &&
+      (uintptr_t)a->xhat % 16 == 0 && (uintptr_t)a->out_bf16 % 8 == 0 && (!a->bias || (uintptr_t)a->bias % 16 == 0) &&
       (a->norm == PKC_NORM_NONE || ((uintptr_t)a->gamma % 16 == 0 && (uintptr_t)a->beta % 16 == 0 &&
                                     (uintptr_t)a->running_mean % 16 == 0 &&
                                     (uintptr_t)a->running_var % 16 == 0)) &&
@@ -710,7 +728,7 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
   PKC_CHECK_ARG(a->norm != PKC_NORM_BN_EVAL, "pkc_dense_bwd: backward through eval BN unsupported");
   PKC_CHECK_ARG(a->drop_p == 0.f || a->keep, "pkc_dense_bwd: dropout needs the keep mask");
   if (small_ok(a->M, a->N, a->nslab, a->gslab, a->dz, a->slab_stride) &&
-      (uintptr_t)a->xhat % 16 == 0 && (!a->dbias || (uintptr_t)a->dbias % 16 == 0) &&
+      (uintptr_t)a->xhat % 16 == 0 && (uintptr_t)a->dz_bf16 % 8 == 0 && (!a->dbias || (uintptr_t)a->dbias % 16 == 0) &&
       (a->norm == PKC_NORM_NONE ||
        ((uintptr_t)a->gamma % 16 == 0 && (uintptr_t)a->beta % 16 == 0 &&
         (uintptr_t)a->save_invstd % 16 == 0 && (!a->dgamma || (uintptr_t)a->dgamma % 16 == 0) &&

@@ -28,14 +28,15 @@ class DenseFwdArgs(C.Structure):
                 ("save_mean", vp), ("save_invstd", vp),
                 ("act", C.c_int), ("drop_p", C.c_float), ("seed", C.c_uint64), ("step_ctr", vp),
                 ("stream_id", i64), ("keep_in", vp), ("keep_out", vp), ("xhat", vp), ("out", vp),
-                ("count_n", i64)]
+                ("count_n", i64), ("out_bf16", vp)]
 
 
 class DenseBwdArgs(C.Structure):
     _fields_ = [("M", C.c_int), ("N", C.c_int), ("nslab", C.c_int),
                 ("gslab", vp), ("slab_stride", i64), ("norm", C.c_int), ("act", C.c_int),
                 ("gamma", vp), ("beta", vp), ("save_invstd", vp), ("xhat", vp), ("keep", vp),
-                ("drop_p", C.c_float), ("dz", vp), ("dgamma", vp), ("dbeta", vp), ("dbias", vp)]
+                ("drop_p", C.c_float), ("dz", vp), ("dgamma", vp), ("dbeta", vp), ("dbias", vp),
+                ("dz_bf16", vp)]
 
 
 class NllArgs(C.Structure):

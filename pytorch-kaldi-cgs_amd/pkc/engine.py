@@ -382,7 +382,7 @@ class Engine:
 
     def __init__(self, nets, arch_opts, lines, fea_cols, lab_names, batch, prec=L.PREC_FP32,
                  device="cuda", seed=0, train=True, drop_keep_in=None, grad_scale=1.0, max_len=None,
-                 rnn_drop_in=None, sync_bn=None):
+                 rnn_drop_in=None, sync_bn=None, bf16_store=None):
         self.dev = torch.device(device)
         self.nets, self.arch_opts, self.lines = nets, arch_opts, lines
         self.B = int(batch)
@@ -416,6 +416,7 @@ class Engine:
         self._build_kmaps()
         self._build_optim()
         self._build_reg()
+        self._build_h16(bf16_store)
         self.graph = None
         self.graph_opt = None
         self.graph_multi, self.steps_per_graph = None, 1
@@ -685,6 +686,50 @@ class Engine:
         tiles = -(-N // 128) * -(-K // 128)
         return max(1, min(4, -(-256 // tiles), M // 256))
 
+    def _build_h16(self, want):
+        """bf16 storage of the MLP matmul operands (PKC_PREC_BF16IN): the producers write a bf16
+        copy beside each fp32 tensor a matmul reads — the gathered batch (pkc_batch_gather), a
+        layer's output (pkc_dense_fwd out_bf16), its gradient dz (pkc_dense_bwd dz_bf16, the heads'
+        dlogits_bf16) and W (the optimizer's bout) — rounded exactly as the PREC_BF16 matmuls round
+        the fp32 values when they stage them, so the results are the same while every workgroup
+        pulls half the operand bytes.  bf16_store=None: on unless PKC_BF16_STORE=0 (A/B).  Only
+        for bf16 MLP steps without in-place weight pruning or input fake-quantisation (their
+        operands change outside the producers above)."""
+        if want is None:
+            want = os.environ.get("PKC_BF16_STORE", "1") != "0"
+        self.h16 = (bool(want) and self.prec == L.PREC_BF16 and not self.seq and not self.prune_list
+                    and not any(ent["Q"] for ent in self.qsrc.values()))
+        self.x_h = None
+        for n in self.nodes:
+            n.W_h = n.out_h = n.dz_h = None
+        if not self.h16:
+            return
+        M, dev, bf = self.Mmax, self.dev, torch.bfloat16
+        mm = [n for n in self.nodes if not n.rec and n.W is not None and not n.qbits]
+        if any(n.src[0] == "fea" for n in mm):
+            self.x_h = torch.zeros(M * self.F, dtype=bf, device=dev)
+        for n in mm:
+            n.W_h = torch.zeros(n.W.numel(), dtype=bf, device=dev)
+            if not n.head and any(c in mm for c in n.consumers):
+                n.out_h = torch.zeros(M * n.N, dtype=bf, device=dev)
+            if self.needs_grad[n] and not n.ln:
+                n.dz_h = torch.zeros(M * n.N, dtype=bf, device=dev)
+        for e in self.opt_entries:
+            nd = e["node"]
+            if nd is not None and getattr(nd, "W_h", None) is not None and e["p"] is nd.W:
+                e["bout"] = nd.W_h
+        if self.opt_entries:
+            self._upload_opt_desc(step_inc=1)
+        self.refresh_bf16()
+
+    def refresh_bf16(self):
+        """Re-cast the bf16 weight copies from the fp32 weights (after the weights changed outside
+        the optimizer, which keeps them current itself)."""
+        s = self._stream()
+        for n in self.nodes:
+            if getattr(n, "W_h", None) is not None:
+                call("pkc_cast_bf16", ptr(n.W), ptr(n.W_h), n.W.numel(), s)
+
     def _alloc_rec(self, n):
         M, dev, B, T = self.Mmax, self.dev, self.B, self.max_len
         G = n.G
@@ -953,6 +998,7 @@ class Engine:
             t.clampv = 1.0 if e["qbits"] else 0.0
             t.qout = e["q"].data_ptr() if e["qbits"] else None
             t.qbits = e["qbits"]
+            t.bout = e["bout"].data_ptr() if e.get("bout") is not None else None
             t.step = e["step"] + step_inc
             if kind == "sgd" and e.get("has_buf"):
                 t.step = max(t.step, 2)   # torch SGD starts buf = g only when it has no buffer
@@ -1026,6 +1072,24 @@ class Engine:
             return self.x.data_ptr() + 4 * n.src[1], self.F
         return n.src[1].out.data_ptr(), n.src[1].N
 
+    def _src_h(self, n):
+        """bf16 copy of n's (unquantised) matmul input, same leading dimension as _src, or None."""
+        if not self.h16:
+            return None
+        if n.src[0] == "fea":
+            return None if self.x_h is None else self.x_h.data_ptr() + 2 * n.src[1]
+        P = n.src[1]
+        return None if getattr(P, "out_h", None) is None else P.out_h.data_ptr()
+
+    @staticmethod
+    def _h_variant(pr, A, B):
+        """The same problem with bf16 operand pointers (PKC_PREC_BF16IN), or None."""
+        if A is None or B is None:
+            return None
+        q = L.GemmProblem.from_buffer_copy(pr)
+        q.A, q.B = A, B
+        return q
+
     def _version(self, n, v):
         """(pointer, ld) of version v of n's input tensor (0: as produced, k: after k in-place
         input quantisations)."""
@@ -1057,7 +1121,7 @@ class Engine:
             self._k("batch_gather", 0, 8.0 * M * self.F, "pkc_batch_gather", ptr(self.chunk_feats),
                     self.chunk_feats.stride(0), self.F, ptr(self.chunk_labels), self.nlab, self.B,
                     self.n_batches, ptr(self.ctr), ptr(self.x), ptr(self.labs),
-                    0 if self.loss_heads else 1, ptr(getattr(self, "x_bf16", None)), s)
+                    0 if self.loss_heads else 1, ptr(self.x_h), s)
             return
         begs, lens, lefts, T = batch
         # [B x int64 begin rows][B x int32 lengths][B x int32 left pads]
@@ -1087,23 +1151,36 @@ class Engine:
         d = 1.0
         if kt is not None:
             pr.ktiles, pr.kmax, d = kt[0].data_ptr(), kt[1], kt[2]
+        prh = self._h_variant(pr, self._src_h(n) if not (n.qv0 + n.reads) else None,
+                              n.W_h.data_ptr() if n.W_h is not None else None)
         return ("fwd %dx%dx%d%s" % (M, n.N, n.K, " sparse %.2f" % d if kt is not None else ""),
-                2.0 * M * n.N * n.K * d, 4.0 * (M * n.K + n.N * n.K * d + sf * M * n.N), pr)
+                2.0 * M * n.N * n.K * d, 4.0 * (M * n.K + n.N * n.K * d + sf * M * n.N), pr,
+                None if prh is None else (2.0 * (M * n.K + n.N * n.K * d) + 4.0 * sf * M * n.N, prh))
 
     def _gemms(self, probs, s):
-        """Launch matmul problems: one pkc_gemm, or pkc_gemm_grouped for several (<= 8 each)."""
+        """Launch matmul problems: one pkc_gemm, or pkc_gemm_grouped for several (<= 8 each).
+        A launch whose matmuls all have bf16 operand copies (a 5th tuple item: (bytes, problem))
+        runs on them (PKC_PREC_BF16IN); its other operations are precision-neutral."""
         for i in range(0, len(probs), 8):
             part = probs[i:i + 8]
+            gem = [q for q in part if q[3].kind == L.OP_GEMM]
+            prec = self.prec
+            if gem and all(len(q) > 4 and q[4] is not None for q in gem):
+                prec = L.PREC_BF16IN
+                part = [(q[0], q[1]) + tuple(q[4]) if len(q) > 4 and q[4] is not None else q[:4]
+                        for q in part]
+            else:
+                part = [q[:4] for q in part]
             if len(part) == 1 and part[0][3].kind == L.OP_GEMM and not part[0][3].ktiles:
                 lab, fl, nb, p = part[0]
-                self._k("gemm_" + lab, fl, nb, "pkc_gemm", self.prec, p.a_kcontig, p.b_kcontig,
+                self._k("gemm_" + lab, fl, nb, "pkc_gemm", prec, p.a_kcontig, p.b_kcontig,
                         p.M, p.N, p.K, C.c_void_p(p.A), p.lda, C.c_void_p(p.B), p.ldb,
                         C.c_void_p(p.C), p.ldc, p.splits, p.slab_stride, s)
             else:
                 arr = (L.GemmProblem * len(part))(*[q[3] for q in part])
                 self._k("gemm_group[" + ", ".join(q[0] for q in part) + "]",
                         sum(q[1] for q in part), sum(q[2] for q in part), "pkc_gemm_grouped",
-                        self.prec, arr, len(part), s)
+                        prec, arr, len(part), s)
 
     def _dense_fwd(self, n, s, train):
         self._quant_chain(n, s)
@@ -1138,7 +1215,9 @@ class Engine:
                           logp=n.out.data_ptr(), log_prior=None,
                           dlogits=(n.dz_ln if n.ln else n.dz).data_ptr() if (train and has_lab)
                           else None,
-                          row_loss=n.row_loss.data_ptr(), row_err=n.row_err.data_ptr())
+                          row_loss=n.row_loss.data_ptr(), row_err=n.row_err.data_ptr(),
+                          dlogits_bf16=n.dz_h.data_ptr() if (train and has_lab and n.dz_h is not None)
+                          else None)
             if out is not None:
                 C.memmove(C.byref(out), C.byref(a), C.sizeof(a))
                 return
@@ -1157,7 +1236,8 @@ class Engine:
             step_ctr=self.ctr.data_ptr(), stream_id=zlib.crc32(n.name.encode()),
             keep_in=keep_in.data_ptr() if keep_in is not None else None,
             keep_out=n.keep.data_ptr() if (n.keep is not None and train) else None,
-            xhat=n.xhat.data_ptr(), out=n.out.data_ptr(), count_n=0)
+            xhat=n.xhat.data_ptr(), out=n.out.data_ptr(), count_n=0,
+            out_bf16=n.out_h.data_ptr() if n.out_h is not None else None)
         if train and n.bn and getattr(n, "bn_states", None) is not None:
             # SyncBN: this rank's column state into its row of bn_states, all-reduce (gather),
             # merge + apply
@@ -1380,7 +1460,9 @@ class Engine:
                            dz=(n.dz_ln if n.ln else self._norm_dx(n) if n.W is None else n.dz).data_ptr(),
                            dgamma=n.dgamma.data_ptr() if n.bn else None,
                            dbeta=n.dbeta.data_ptr() if n.bn else None,
-                           dbias=n.db.data_ptr() if (n.b is not None and not n.ln) else None)
+                           dbias=n.db.data_ptr() if (n.b is not None and not n.ln) else None,
+                           dz_bf16=n.dz_h.data_ptr() if (n.W is not None and n.dz_h is not None)
+                           else None)
         if n.bn and getattr(n, "bn_sums", None) is not None:
             # SyncBN: local column sums (and local dgamma / dbeta), all-reduce, global apply
             self._k("dense_bwd_stats N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 2), "pkc_dense_bwd_stats",
@@ -1425,12 +1507,15 @@ class Engine:
                         L.GemmProblem(kind=L.OP_COLSUM, M=M, N=n.N, A=n.dz.data_ptr(),
                                       C=n.db.data_ptr())))
         sdw = getattr(n, "sdw", 1)
+        dzh = n.dz_h.data_ptr() if getattr(n, "dz_h", None) is not None else None
+        pr = L.GemmProblem(a_kcontig=0, b_kcontig=0, M=n.N, N=n.K, K=M, splits=sdw,
+                           A=n.dz.data_ptr(), lda=n.N, B=a_ptr, ldb=lda,
+                           C=(n.dwslab if sdw > 1 else n.dW).data_ptr(), ldc=n.K,
+                           slab_stride=n.N * n.K if sdw > 1 else 0)
+        prh = self._h_variant(pr, dzh, None if self.qsrc[n.qkey]["Q"] else self._src_h(n))
         out += [("dW %dx%dx%d%s" % (n.N, n.K, M, " s%d" % sdw if sdw > 1 else ""),
-                 2.0 * M * n.N * n.K, 4.0 * (M * n.N + M * n.K + sdw * n.N * n.K),
-                 L.GemmProblem(a_kcontig=0, b_kcontig=0, M=n.N, N=n.K, K=M, splits=sdw,
-                               A=n.dz.data_ptr(), lda=n.N, B=a_ptr, ldb=lda,
-                               C=(n.dwslab if sdw > 1 else n.dW).data_ptr(), ldc=n.K,
-                               slab_stride=n.N * n.K if sdw > 1 else 0))]
+                 2.0 * M * n.N * n.K, 4.0 * (M * n.N + M * n.K + sdw * n.N * n.K), pr,
+                 None if prh is None else (2.0 * (M * n.N + M * n.K) + 4.0 * sdw * n.N * n.K, prh))]
         if n.src[0] == "node" and self.needs_grad[n.src[1]]:
             P = n.src[1]
             off = P.cons_off[P.consumers.index(n)]
@@ -1442,9 +1527,11 @@ class Engine:
             kt, d = self._wt(n.W, True), 1.0
             if kt is not None:
                 pr.ktiles, pr.kmax, d = kt[0].data_ptr(), kt[1], kt[2]
+            prh = self._h_variant(pr, dzh, n.W_h.data_ptr() if n.W_h is not None else None)
             out.append(("dX %dx%dx%d%s" % (M, n.K, n.N, " sparse %.2f" % d if kt is not None else ""),
                         2.0 * M * n.N * n.K * d, 4.0 * (M * n.N + n.N * n.K * d + n.sx * M * n.K),
-                        pr))
+                        pr, None if prh is None else
+                        (2.0 * (M * n.N + n.N * n.K * d) + 4.0 * n.sx * M * n.K, prh)))
         return out
 
     def _dw_sum_op(self, n):
@@ -1525,12 +1612,14 @@ class Engine:
             return []
         nch, cmap, idx = self.node_opt[n]
         nparam = sum(self.opt_entries[i]["p"].numel() for i in idx)
+        nbout = sum(self.opt_entries[i]["p"].numel() for i in idx
+                    if self.opt_entries[i].get("bout") is not None)
         parts = max(1, min(parts, nch))
         ops, b = [], 0
         for k in range(parts):
             e = (nch * (k + 1)) // parts
             ops.append(("opt %s%s" % (n.name, "" if parts == 1 else " [%d/%d]" % (k + 1, parts)), 0.0,
-                        20.0 * nparam * (e - b) / nch,
+                        (20.0 * nparam + 2.0 * nbout) * (e - b) / nch,
                         L.GemmProblem(kind=L.OP_OPTIM, M=e - b, A=self.opt_desc.data_ptr(),
                                       B=cmap.data_ptr() + 8 * b)))
             b = e

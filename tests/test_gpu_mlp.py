@@ -480,3 +480,55 @@ def test_engine_split_dw_large_batch(mode):
     assert t0 == pytest.approx(t1, rel=1e-6)
     err = (g1 - g0).abs().max().item()
     assert err <= 1e-5 * g0.abs().max().item(), "split-K dW gradient max abs diff %.3g" % err
+
+
+@pytest.mark.parametrize("B,mode", [(128, "eager"), (128, "graph"), (1024, "eager")])
+def test_engine_bf16_store_matches_bf16_staging(B, mode):
+    """bf16 operand storage (the producers write bf16 copies that the matmuls read as
+    PKC_PREC_BF16IN) rounds exactly what PREC_BF16 rounds when it stages the fp32 tensors, so both
+    forms give the same step.  B = 128 (64x64 bodies, both forms accumulate k in the same order):
+    bit-identical gradients, posteriors, weights and loss over 3 steps; B = 1024 (128x128 and
+    LDS-DMA bodies for the bf16 form): the first step's gradients within 1e-5 of their scale."""
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config(drop="0.15")
+    steps = 3 if B == 128 else 1
+    rs = np.random.RandomState(9)
+    X = torch.from_numpy(rs.randn(B * steps, 440).astype(np.float32)).to(DEV)
+    lab = torch.from_numpy(np.stack([rs.randint(0, 1928, B * steps), rs.randint(0, 48, B * steps)],
+                                    1).astype(np.int32)).to(DEV)
+    runs = []
+    for store in (False, True):
+        nets, opts = build_nets(cfg, C1_DIMS)
+        for n in nets.values():
+            n.to(DEV).train()
+        eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                     ["lab_cd", "lab_mono"], batch=B, seed=7, prec=L.PREC_BF16, bf16_store=store)
+        assert eng.h16 == store
+        eng.bind_chunk(X, lab, B * steps)
+        if mode == "graph":
+            assert eng.capture(steps_per_graph=1)
+            eng.ctr.zero_()
+            eng.loss_acc.zero_()
+        grads, posts = [], []
+        head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
+        for _ in range(steps):
+            eng.train_step()
+            torch.cuda.synchronize()
+            grads.append(eng.gflat.detach().cpu().clone())
+            posts.append(head.out.view(B, -1).cpu().clone())
+        sd = {a + "/" + k: v.detach().cpu().clone() for a in nets for k, v in nets[a].state_dict().items()}
+        runs.append((grads, posts, sd, eng.chunk_totals()))
+    (g0, p0, s0, t0), (g1, p1, s1, t1) = runs
+    if B == 128:
+        for s in range(steps):
+            assert torch.equal(g0[s], g1[s]), "step %d gradients differ: %.3g" % (
+                s, (g0[s] - g1[s]).abs().max().item())
+            assert torch.equal(p0[s], p1[s]), "step %d posteriors differ" % s
+        for k in s0:
+            assert torch.equal(s0[k], s1[k]), k
+        assert t0 == t1
+    else:
+        err = (g1[0] - g0[0]).abs().max().item()
+        assert err <= 1e-5 * g0[0].abs().max().item(), "gradient max abs diff %.3g" % err
+        assert t0 == pytest.approx(t1, rel=1e-5)
