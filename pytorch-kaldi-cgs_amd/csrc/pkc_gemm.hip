@@ -465,7 +465,7 @@ struct GroupArgs {
 // SUM: the launch carries slab-sum operations (large-batch split-K dW); a separate instance,
 // because that body alone raises the kernel's VGPRs from 152 to 191 (occupancy 3 -> 2), which the
 // B = 128 step's lean launches cannot afford
-template <int PREC, bool BIN, bool BIG, bool SP = false, bool SUM = false>
+template <int PREC, bool BIN, bool BIG, bool SP = false, bool SUM = false, int GD = 4>
 __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
   // BIG: at least one problem takes the 128x128 body; its LDS also holds the 64x64 tiles
   union alignas(16) Shm {
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
     return;
   }
 #define PKC_GB(AK, BK_, V)                                                                      \
-  gemm_body<PREC, AK, BK_, V, 4, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
+  gemm_body<PREC, AK, BK_, V, GD, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
                                       p.ldc, p.kchunk, p.slab)
   switch (p.code) {
     case 7: PKC_GB(true, true, true); break;
@@ -550,14 +550,34 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
 #undef PKC_GB
 }
 
+// k-tiles in flight per workgroup for bf16-stored operands: a stage is one 16-byte register per
+// operand, so depth 8 costs 32 VGPRs more and puts a B = 128 split's whole k-range in flight at
+// once.  Standalone launches (PKC_GEMM_DEPTH, default 8): C2 706k -> 720k, B = 1024 1.97M ->
+// 2.06M frames/s; grouped launches (PKC_GEMM_DEPTH_G, default 4): 8 measured 664-669k, the
+// extra VGPRs cost their optimizer / dW work items residency (same runs)
+static int bin_depth(bool grouped = false) {
+  static const int d[2] = {[] {
+    const char* v = getenv("PKC_GEMM_DEPTH");
+    return v && atoi(v) == 4 ? 4 : 8;
+  }(), [] {
+    const char* v = getenv("PKC_GEMM_DEPTH_G");
+    return v && atoi(v) == 8 ? 8 : 4;
+  }()};
+  return d[grouped ? 1 : 0];
+}
+
 template <int PREC, bool AKC, bool BKC, bool VEC, bool BIN>
 static int launch(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb,
                   float* C, int64_t ldc, int splits, int64_t slab, hipStream_t s) {
   int kchunk = (K + splits - 1) / splits;
   kchunk = ((kchunk + BK - 1) / BK) * BK;
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((gemm_kernel<PREC, AKC, BKC, VEC, 4, BIN>), grid, dim3(NT), 0, s, M, N, K, A,
-                     lda, B, ldb, C, ldc, kchunk, slab);
+  if (BIN && bin_depth() == 8)
+    hipLaunchKernelGGL((gemm_kernel<PREC, AKC, BKC, VEC, 8, BIN>), grid, dim3(NT), 0, s, M, N, K, A,
+                       lda, B, ldb, C, ldc, kchunk, slab);
+  else
+    hipLaunchKernelGGL((gemm_kernel<PREC, AKC, BKC, VEC, 4, BIN>), grid, dim3(NT), 0, s, M, N, K, A,
+                       lda, B, ldb, C, ldc, kchunk, slab);
   PKC_LAUNCH_CHECK("pkc_gemm");
   return PKC_OK;
 }
@@ -796,6 +816,9 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
                          S(stream), g);                                                         \
     else if (any_big)                                                                           \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, true>), dim3(wg), dim3(NT), 0, S(stream), g);  \
+    else if (BIN && bin_depth(true) == 8)                                                       \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false, false, false, 8>), dim3(wg), dim3(NT), \
+                         0, S(stream), g);                                                      \
     else                                                                                        \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false>), dim3(wg), dim3(NT), 0, S(stream), g); \
   } while (0)
