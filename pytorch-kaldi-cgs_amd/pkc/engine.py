@@ -49,6 +49,8 @@ OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "500000"))
 # 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
 # gradient (0: off)
 DW_SPLIT_ROWS = int(os.environ.get("PKC_DW_SPLIT_ROWS", "1024"))
+# recurrent layers' dW / dU split-K cap (1: unsplit, A/B)
+REC_DW_SPLITS = int(os.environ.get("PKC_REC_DW_SPLITS", "4"))
 
 
 _PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
@@ -765,8 +767,16 @@ class Engine:
                 for g in range(G):
                     for p in (sp["W"][g], sp["U"][g]):
                         n.qw[id(p)] = (torch.zeros_like(p), sp["qbits"])
+            # split-K of the weight gradients dW = dz^T x (H x K over the T*B rows) and dU (H x H
+            # over the T*2B rows): their 64x64 tiles alone leave most CUs idle (C3: 81 tiles of
+            # dU), so the contraction is split into slabs that a slab-sum launch adds up
+            lb["sw"] = _splits(H, K, M, REC_DW_SPLITS)
+            lb["su"] = _splits(H, H, T * B2, REC_DW_SPLITS)
             n.lbuf.append(lb)
             K = D
+        need = max(max(lb["sw"] * lb["H"] * lb["K"] if lb["sw"] > 1 else 0,
+                       lb["su"] * lb["H"] * lb["H"] if lb["su"] > 1 else 0) for lb in n.lbuf)
+        n.rslab = _f32(need, dev) if need else None
         n.out = n.lbuf[-1]["y"]
 
     def _build_masks(self):
@@ -1573,16 +1583,24 @@ class Engine:
                 self._k("rnn_bn_bwd H=%d" % H, 0, 4.0 * M * H * 4, "pkc_dense_bwd", C.byref(a),
                         ptr(lb["work"]), s)
                 dz = C.c_void_p(lb["dz"].data_ptr() + 4 * g * M * H)
-                self._k("rnn_gemm_dW %dx%dx%d" % (H, K, M), 2.0 * M * H * K,
-                        4.0 * (M * H + M * K + H * K), "pkc_gemm", self.prec, 0, 0, H, K, M, dz, H,
-                        C.c_void_p(x_ptr), ldx, ptr(lb["dW"][g]), K, 1, 0, s)
+                sw, su = lb["sw"], lb["su"]
+                self._k("rnn_gemm_dW %dx%dx%d%s" % (H, K, M, " s%d" % sw if sw > 1 else ""),
+                        2.0 * M * H * K, 4.0 * (M * H + M * K + sw * H * K), "pkc_gemm", self.prec,
+                        0, 0, H, K, M, dz, H, C.c_void_p(x_ptr), ldx,
+                        ptr(n.rslab if sw > 1 else lb["dW"][g]), K, sw, H * K if sw > 1 else 0, s)
+                if sw > 1:
+                    self._rec_slab_sum(n.rslab, sw, H * K, lb["dW"][g], s)
                 # dU = sum_t dgates[t]^T h_{t-1}: K = T*B2 rows of hs[0:T] (GRU Uh: r*h_{t-1})
                 R2 = T * lb["B2"]
                 usrc = lb["rh"] if g == n.cand else hsrc
-                self._k("rnn_gemm_dU %dx%dx%d" % (H, H, R2), 2.0 * R2 * H * H,
-                        4.0 * (2 * R2 * H + H * H), "pkc_gemm", self.prec, 0, 0, H, H, R2,
+                self._k("rnn_gemm_dU %dx%dx%d%s" % (H, H, R2, " s%d" % su if su > 1 else ""),
+                        2.0 * R2 * H * H, 4.0 * (2 * R2 * H + su * H * H), "pkc_gemm", self.prec,
+                        0, 0, H, H, R2,
                         C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,
-                        ptr(usrc), H, ptr(lb["dU"][g]), H, 1, 0, s)
+                        ptr(usrc), H, ptr(n.rslab if su > 1 else lb["dU"][g]), H, su,
+                        H * H if su > 1 else 0, s)
+                if su > 1:
+                    self._rec_slab_sum(n.rslab, su, H * H, lb["dU"][g], s)
                 if li > 0 or want_dx0:
                     kt = self._wt(sp["W"][g], True)
                     if kt is not None:        # block-sparse W^T: one slab per gate
@@ -1604,6 +1622,12 @@ class Engine:
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
             if li == 0 and n.src[0] == "node":
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
+
+    def _rec_slab_sum(self, slab, ns, numel, out, s):
+        """out = sum of ns split-K slabs of a recurrent weight gradient (one grouped launch)."""
+        self._gemms([("rnn slab-sum x%d" % ns, 0.0, 4.0 * numel * (ns + 1),
+                      L.GemmProblem(kind=L.OP_SLABSUM, M=ns, N=numel, A=slab.data_ptr(),
+                                    C=out.data_ptr(), slab_stride=numel))], s)
 
     def _opt_op(self, n, parts=1):
         """The optimizer update of node n's parameters as operations of grouped launches: `parts`
