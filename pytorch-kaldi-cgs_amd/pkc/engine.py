@@ -51,6 +51,8 @@ OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "500000"))
 DW_SPLIT_ROWS = int(os.environ.get("PKC_DW_SPLIT_ROWS", "1024"))
 # recurrent layers' dW / dU split-K cap (1: unsplit, A/B)
 REC_DW_SPLITS = int(os.environ.get("PKC_REC_DW_SPLITS", "4"))
+# recurrent layers: sum the output-gradient slabs before the BPTT loop (0: per step, A/B)
+REC_DY_PRESUM = os.environ.get("PKC_REC_DY_PRESUM", "1") != "0"
 
 
 _PAT3 = re.compile(r"(.*)=(.*)\((.*),(.*),(.*)\)")
@@ -777,6 +779,9 @@ class Engine:
         need = max(max(lb["sw"] * lb["H"] * lb["K"] if lb["sw"] > 1 else 0,
                        lb["su"] * lb["H"] * lb["H"] if lb["su"] > 1 else 0) for lb in n.lbuf)
         n.rslab = _f32(need, dev) if need else None
+        # dL/dy of a layer summed over its producers' slabs once, before the serial BPTT loop
+        # (whose per-step epilogue would otherwise read every slab at every step)
+        n.dysum = _f32(M * max(lb["D"] for lb in n.lbuf), dev) if REC_DY_PRESUM else None
         n.out = n.lbuf[-1]["y"]
 
     def _build_masks(self):
@@ -1562,6 +1567,9 @@ class Engine:
             sp, lb = n.layers[li], n.lbuf[li]
             H, K = lb["H"], lb["K"]
             ra = self._rnn_args(n, li, True, T)
+            if dy_ns > 1 and n.dysum is not None:
+                self._rec_slab_sum_ptr(dy_ptr, dy_ns, M * lb["D"], dy_stride, n.dysum, s)
+                dy_ptr, dy_ns, dy_stride = n.dysum.data_ptr(), 1, M * lb["D"]
             ra.dy, ra.dy_nslab, ra.dy_slab_stride = dy_ptr, dy_ns, dy_stride
             self._k("rnn_bwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_bwd", C.byref(ra), ptr(lb["dpre"]), s)
@@ -1625,9 +1633,12 @@ class Engine:
 
     def _rec_slab_sum(self, slab, ns, numel, out, s):
         """out = sum of ns split-K slabs of a recurrent weight gradient (one grouped launch)."""
+        self._rec_slab_sum_ptr(slab.data_ptr(), ns, numel, numel, out, s)
+
+    def _rec_slab_sum_ptr(self, a_ptr, ns, numel, stride, out, s):
         self._gemms([("rnn slab-sum x%d" % ns, 0.0, 4.0 * numel * (ns + 1),
-                      L.GemmProblem(kind=L.OP_SLABSUM, M=ns, N=numel, A=slab.data_ptr(),
-                                    C=out.data_ptr(), slab_stride=numel))], s)
+                      L.GemmProblem(kind=L.OP_SLABSUM, M=ns, N=numel, A=a_ptr,
+                                    C=out.data_ptr(), slab_stride=stride))], s)
 
     def _opt_op(self, n, parts=1):
         """The optimizer update of node n's parameters as operations of grouped launches: `parts`
