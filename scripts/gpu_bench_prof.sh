@@ -10,5 +10,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/b
 T=$(find /tmp/bprof -name 'bench_kernel_trace.csv' -print -quit)
 S=$(find /tmp/bprof -name 'bench_kernel_stats.csv' -print -quit)
 cp "$S" gpurun_out/bprof/bench_kernel_stats.csv
-python3 scripts/trace_gaps.py "$T" > gpurun_out/bprof/timeline.txt
+python3 scripts/trace_gaps.py "$T" batch_gather "gemm_grouped_kernel<1, true" > gpurun_out/bprof/timeline.txt
 tail -3 gpurun_out/bprof/timeline.txt

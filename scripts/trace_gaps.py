@@ -8,6 +8,9 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 first = sys.argv[2] if len(sys.argv) > 2 else "batch_gather"
+# optional: keep only steps with a kernel whose name contains this (e.g. the bf16 instances, so
+# the fp32 leg of the same bench command is not the one summarised)
+need = sys.argv[3] if len(sys.argv) > 3 else None
 starts = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
 # the bench's own steps: the most common launch count between consecutive gathers (other
 # workloads in the same trace — batch sweep, sequence configs — have other shapes)
@@ -15,6 +18,11 @@ pairs = list(zip(starts, starts[1:]))
 lens = defaultdict(int)
 for a, b in pairs:
     lens[b - a] += 1
+if need:
+    pairs = [(a, b) for a, b in pairs if any(need in r["Kernel_Name"] for r in rows[a:b])]
+    lens = defaultdict(int)
+    for a, b in pairs:
+        lens[b - a] += 1
 L = max(lens, key=lens.get)
 steps = [rows[a:b] for a, b in pairs if b - a == L][-200:]
 agg = defaultdict(lambda: [0.0, 0.0, 0])
