@@ -30,6 +30,16 @@ void set_error(const char* fmt, ...);
     }                                                                              \
   } while (0)
 
+// a HIP runtime call's status into the library error (returns PKC_ERR_HIP from the caller)
+#define PKC_HIP_CHECK(call, where)                                                 \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      ::pkc::set_error("%s: %s", where, hipGetErrorString(e_));                    \
+      return PKC_ERR_HIP;                                                          \
+    }                                                                              \
+  } while (0)
+
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ------------------------------------------------------------------ device helpers

@@ -376,12 +376,16 @@ __global__ __launch_bounds__(ET) void colsum_kernel(int M, int N, int nslab, con
 }
 
 // ------------------------------------------------------------- small-batch fused forms (M <= 512)
-// A workgroup owns 16 columns x ALL rows of the batch, so the BatchNorm column statistics are a
+// A workgroup owns 8 columns x ALL rows of the batch, so the BatchNorm column statistics are a
 // workgroup reduction (wave shuffles + 4-entry LDS merge) and the layer epilogue is ONE launch
 // with every load issued up front: split-K slabs are summed in registers (NS = power-of-two bound
 // on the slab count, loads clamped to the last slab instead of branched, so none is serialised).
+// PKC_DENSE_FG float4 column groups per workgroup: 2 (8 columns, 128 workgroups at N = 1024, one
+// row per thread at M = 128) measured 720k -> 761k frames/s for C2 against 4 (16 columns, 64
+// workgroups): the step's ten BatchNorm launches are latency-bound and half the bytes per
+// workgroup over twice the CUs is what they need
 #ifndef PKC_DENSE_FG
-#define PKC_DENSE_FG 4
+#define PKC_DENSE_FG 2
 #endif
 constexpr int FG = PKC_DENSE_FG, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
 
@@ -809,7 +813,8 @@ extern "C" int pkc_dense_bwd_stats(const pkc_dense_bwd_args* a, float* work, flo
   hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
                      S(stream), *a, work);
   const float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
-  hipMemcpyAsync(sums, fin, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice, S(stream));
+  PKC_HIP_CHECK(hipMemcpyAsync(sums, fin, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice,
+                               S(stream)), "pkc_dense_bwd_stats copy");
   PKC_LAUNCH_CHECK("pkc_dense_bwd_stats");
   return PKC_OK;
 }
@@ -821,7 +826,8 @@ extern "C" int pkc_dense_bwd_sync_apply(const pkc_dense_bwd_args* a, float* work
   if (st) return st;
   PKC_CHECK_ARG(sums && total_rows >= a->M, "pkc_dense_bwd_sync_apply: sums / total_rows");
   float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
-  hipMemcpyAsync(fin, sums, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice, S(stream));
+  PKC_HIP_CHECK(hipMemcpyAsync(fin, sums, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice,
+                               S(stream)), "pkc_dense_bwd_sync_apply copy");
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work,
                      1.f / (float)total_rows);

@@ -1009,8 +1009,10 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
 template <int G, int CELL>
 static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
-  hipMemsetAsync(a->hs, 0, sizeof(float) * (size_t)B2 * a->H, s);            // h_init = 0
-  if constexpr (CELL == PKC_CELL_LSTM) hipMemsetAsync(a->cs, 0, sizeof(float) * (size_t)B2 * a->H, s);
+  PKC_HIP_CHECK(hipMemsetAsync(a->hs, 0, sizeof(float) * (size_t)B2 * a->H, s),   // h_init = 0
+                "pkc_rnn_fwd h_init");
+  if constexpr (CELL == PKC_CELL_LSTM)
+    PKC_HIP_CHECK(hipMemsetAsync(a->cs, 0, sizeof(float) * (size_t)B2 * a->H, s), "pkc_rnn_fwd c_init");
   if (a->train && a->drop_p > 0.f) {
     hipLaunchKernelGGL(rnn_drop_mask_kernel, dim3(64), dim3(256), 0, s, *a, B2);
     PKC_LAUNCH_CHECK("pkc_rnn_fwd drop mask");
