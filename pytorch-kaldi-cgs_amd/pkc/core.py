@@ -27,6 +27,7 @@ import torch
 from . import data_io as D
 from . import dist as DP
 from . import frontend as FE
+from . import _lib as L
 from . import neural_networks as NN
 from .engine import Engine, ForwardRunner, parse_model
 from .neural_networks import strtobool
@@ -201,6 +202,12 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
     require_dec = list(map(strtobool, config["forward"]["require_decoding"].split(",")))
     batch_size = {"train": int(config["batches"]["batch_size_train"]),
                   "valid": int(config["batches"]["batch_size_valid"])}.get(to_do, 1)
+    # [exp] pkc_prec = bf16 (a pkc key): bf16 matmul operands with fp32 accumulation, master
+    # weights, BatchNorm, loss and optimizer; default fp32, the reference's arithmetic
+    prec = {"fp32": L.PREC_FP32, "bf16": L.PREC_BF16}.get(
+        config["exp"].get("pkc_prec", "fp32").strip().lower())
+    if prec is None:
+        raise ValueError("[exp] pkc_prec must be fp32 or bf16, not %r" % config["exp"]["pkc_prec"])
 
     if processed_first:
         shared = []
@@ -243,7 +250,8 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         pass
     elif seq_model:
         eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
-                     train=(to_do == "train"), max_len=int(lens.max()), grad_scale=1.0 / ws_eff)
+                     train=(to_do == "train"), max_len=int(lens.max()), grad_scale=1.0 / ws_eff,
+                     prec=prec)
         if ws_eff > 1:                  # frame-weighted sequence DP (pkc.dist.frame_weight)
             eng.frame_weight = lambda rows: DP.frame_weight(rows, device=eng.dev)
         for net_name in nns:
@@ -290,7 +298,7 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         if ws_eff > 1 and to_do == "train" and config["exp"].get("sync_bn", "False") == "True":
             sbn = DP.SyncBatchNorm()
         eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
-                     train=(to_do == "train"), grad_scale=1.0 / ws_eff, sync_bn=sbn)
+                     train=(to_do == "train"), grad_scale=1.0 / ws_eff, sync_bn=sbn, prec=prec)
         for net_name in nns:
             pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
             if pt != "none" and to_do == "train":

@@ -267,3 +267,39 @@ def test_read_lab_fea_six_items_vs_reference(seq, tmp_path):
     ref = g["rlf_%s_data" % tag]
     np.testing.assert_array_equal(arr[:, -2:].astype(np.float32), ref[:, -2:])
     np.testing.assert_allclose(arr[:, :-2].astype(np.float32), ref[:, :-2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("case", ["mlp", "ligru"])
+def test_run_nn_bf16_key(case, tmp_path):
+    """[exp] pkc_prec = bf16 (a pkc key) trains the same chunk with bf16 matmul operands: the
+    chunk's .info loss within 2e-2 relative of the fp32 run (bf16 rounding over ~20 steps of
+    training from scratch), finite checkpoints with the same keys; an unknown value is refused."""
+    from pkc.core import run_nn
+    src = os.path.join(GOLDEN, "run_nn_" + case)
+    g = np.load(os.path.join(src, "expected.npz"), allow_pickle=False)
+    d = str(tmp_path)
+    scp0 = write_chunk(d, "ck0", g)
+    out = {}
+    for prec in ("fp32", "bf16", "fp8"):
+        name = "train_" + prec
+        c = run_nn_cfg(d, name, "train", scp0, case)
+        cfg = configparser.ConfigParser()
+        cfg.read(c)
+        cfg["exp"]["pkc_prec"] = prec
+        with open(c, "w") as f:
+            cfg.write(f)
+        if prec == "fp8":
+            with pytest.raises(ValueError):
+                run_nn(None, None, None, None, None, None, c, True, c)
+            continue
+        run_nn(None, None, None, None, None, None, c, True, c)
+        out[prec] = (read_info(os.path.join(d, name + ".info")),
+                     {s: torch.load(os.path.join(d, "%s_%s.pkl" % (name, s)), weights_only=True,
+                                    map_location="cpu") for s in SECS})
+    (l32, _), ck32 = out["fp32"]
+    (l16, _), ck16 = out["bf16"]
+    assert abs(l16 - l32) <= 2e-2 * abs(l32), (l16, l32)
+    for s in SECS:
+        assert set(ck16[s]["model_par"]) == set(ck32[s]["model_par"])
+        for k, v in ck16[s]["model_par"].items():
+            assert torch.isfinite(v.float()).all(), (s, k)
