@@ -376,18 +376,19 @@ __global__ __launch_bounds__(ET) void colsum_kernel(int M, int N, int nslab, con
 }
 
 // ------------------------------------------------------------- small-batch fused forms (M <= 512)
-// A workgroup owns 8 columns x ALL rows of the batch, so the BatchNorm column statistics are a
+// A workgroup owns 4G columns x ALL rows of the batch, so the BatchNorm column statistics are a
 // workgroup reduction (wave shuffles + 4-entry LDS merge) and the layer epilogue is ONE launch
 // with every load issued up front: split-K slabs are summed in registers (NS = power-of-two bound
 // on the slab count, loads clamped to the last slab instead of branched, so none is serialised).
-// PKC_DENSE_FG float4 column groups per workgroup: 2 (8 columns, 128 workgroups at N = 1024, one
-// row per thread at M = 128) measured 720k -> 761k frames/s for C2 against 4 (16 columns, 64
-// workgroups): the step's ten BatchNorm launches are latency-bound and half the bytes per
-// workgroup over twice the CUs is what they need
-#ifndef PKC_DENSE_FG
-#define PKC_DENSE_FG 2
-#endif
-constexpr int FG = PKC_DENSE_FG, FC = 4 * FG, FT = 256, RG = FT / FG;  // float4 groups, cols, threads, row groups
+// G float4 column groups per workgroup (FT / G row groups of threads).  Layers of N >= 512
+// columns take G = 2 (8 columns: 128 workgroups at N = 1024, one row per thread at M = 128),
+// measured 720k -> 761k frames/s for C2 against G = 4 (16 columns, 64 workgroups; G = 1: 743-748k):
+// the step's ten BatchNorm launches are latency-bound, and half the bytes per workgroup over twice
+// the CUs is what they need.  Narrower layers keep G = 4 and its summation order, to which the
+// recurrent run_nn lifecycle tests are pinned (with G = 2 their from-scratch chunk's BatchNorm
+// betas, whose RMSprop steps follow the sign of near-zero gradients, land 3e-2 off the reference's
+// instead of 3e-5; test_dense_bn_fwd_bwd holds both forms to torch)
+constexpr int FT = 256;
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
@@ -418,28 +419,29 @@ __device__ __forceinline__ void f4set(float4& v, int j, float x) {
 }
 
 // column-sum of a float4 (4 columns) over the 64 row-groups of the workgroup; all threads get it
+template <int G>
 __device__ __forceinline__ float4 colsum_rows(float4 v, float4* red) {
 #pragma unroll
-  for (int o = FG; o < 64; o <<= 1) {
+  for (int o = G; o < 64; o <<= 1) {
     v.x += __shfl_xor(v.x, o, 64);
     v.y += __shfl_xor(v.y, o, 64);
     v.z += __shfl_xor(v.z, o, 64);
     v.w += __shfl_xor(v.w, o, 64);
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c4 = threadIdx.x % FG;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c4 = threadIdx.x % G;
   __syncthreads();
-  if (lane < FG) red[wave * FG + lane] = v;
+  if (lane < G) red[wave * G + lane] = v;
   __syncthreads();
-  return f4add(f4add(red[c4], red[FG + c4]), f4add(red[2 * FG + c4], red[3 * FG + c4]));
+  return f4add(f4add(red[c4], red[G + c4]), f4add(red[2 * G + c4], red[3 * G + c4]));
 }
 
-template <int NS, int RI>
+template <int NS, int RI, int G>
 __device__ __forceinline__ void load_slabs(const float* __restrict__ base, int64_t stride, int ns,
                                            int rg, int M, int64_t N, int c, bool cok, float4* z) {
   float4 v[RI][NS];
 #pragma unroll
   for (int i = 0; i < RI; ++i) {
-    const int row = rg + RG * i;
+    const int row = rg + (FT / G) * i;
     const bool ok = cok && row < M;
     const float* p = base + (ok ? (int64_t)row * N + c : 0);
 #pragma unroll
@@ -453,15 +455,16 @@ __device__ __forceinline__ void load_slabs(const float* __restrict__ base, int64
     float4 acc = v[i][0];
 #pragma unroll
     for (int q = 1; q < NS; ++q) acc = f4add(acc, f4sel(q < ns, v[i][q]));
-    const int row = rg + RG * i;
+    const int row = rg + (FT / G) * i;
     z[i] = f4sel(cok && row < M, acc);
   }
 }
 
-template <int NS, int RI>
+template <int NS, int RI, int G>
 __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args a) {
-  __shared__ float4 red[4 * FG];
-  const int c4 = threadIdx.x % FG, rg = threadIdx.x / FG;
+  constexpr int FC = 4 * G, RG = FT / G;
+  __shared__ float4 red[4 * G];
+  const int c4 = threadIdx.x % G, rg = threadIdx.x / G;
   const int c = col_group(blockIdx.x, gridDim.x) * FC + c4 * 4;
   const bool cok = c < a.N;
   const int64_t N = a.N;
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
   const float4 rv0 = ld4(bnp ? a.running_var + cc : dummy);
   const int64_t step0 = *(a.step_ctr ? a.step_ctr : reinterpret_cast<const int64_t*>(dummy));
   float4 z[RI];
-  load_slabs<NS, RI>(a.zslab, a.slab_stride, a.nslab, rg, M, N, c, cok, z);
+  load_slabs<NS, RI, G>(a.zslab, a.slab_stride, a.nslab, rg, M, N, c, cok, z);
   const float4 b = hb ? b0 : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int i = 0; i < RI; ++i) z[i] = f4sel(cok && rg + RG * i < M, f4add(z[i], b));
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
     float4 sum = z[0];
 #pragma unroll
     for (int i = 1; i < RI; ++i) sum = f4add(sum, z[i]);
-    sum = colsum_rows(sum, red);
+    sum = colsum_rows<G>(sum, red);
     const float inv = 1.f / (float)M;
     mean = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
     float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
         m2 = f4add(m2, make_float4(dx * dx, dy * dy, dz * dz, dw * dw));
       }
     }
-    m2 = colsum_rows(m2, red);
+    m2 = colsum_rows<G>(m2, red);
     const float4 var = make_float4(m2.x * inv, m2.y * inv, m2.z * inv, m2.w * inv);
     invstd = make_float4(1.f / sqrtf(var.x + a.eps), 1.f / sqrtf(var.y + a.eps),
                          1.f / sqrtf(var.z + a.eps), 1.f / sqrtf(var.w + a.eps));
@@ -570,10 +573,11 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
   }
 }
 
-template <int NS, int RI>
+template <int NS, int RI, int G>
 __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args a) {
-  __shared__ float4 red[4 * FG];
-  const int c4 = threadIdx.x % FG, rg = threadIdx.x / FG;
+  constexpr int FC = 4 * G, RG = FT / G;
+  __shared__ float4 red[4 * G];
+  const int c4 = threadIdx.x % G, rg = threadIdx.x / G;
   const int c = col_group(blockIdx.x, gridDim.x) * FC + c4 * 4;
   const bool cok = c < a.N;
   const int64_t N = a.N;
@@ -587,7 +591,7 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
   const float4 is0 = ld4(bn ? a.save_invstd + cc : dummy);
   float4 g[RI], xh[RI];
   uint32_t kp[RI];
-  load_slabs<NS, RI>(a.gslab, a.slab_stride, a.nslab, rg, M, N, c, cok, g);
+  load_slabs<NS, RI, G>(a.gslab, a.slab_stride, a.nslab, rg, M, N, c, cok, g);
   const bool drop = a.drop_p > 0.f;
   const uint8_t* kb = drop ? a.keep : reinterpret_cast<const uint8_t*>(a.xhat);
 #pragma unroll
@@ -620,8 +624,8 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
     sdyx = f4add(sdyx, make_float4(dy[i].x * xh[i].x, dy[i].y * xh[i].y, dy[i].z * xh[i].z,
                                    dy[i].w * xh[i].w));
   }
-  sdy = colsum_rows(sdy, red);
-  sdyx = colsum_rows(sdyx, red);
+  sdy = colsum_rows<G>(sdy, red);
+  sdyx = colsum_rows<G>(sdyx, red);
   if (!cok) return;
   if (rg == 0) {
     if (bn) {
@@ -656,27 +660,37 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
   }
 }
 
+// at most 128 rows (the MLP batch): larger row counts (a recurrent layer's T * 2B rows) keep the
+// stats / finalize / apply form and its summation order, which the recurrent run_nn lifecycle
+// tests are pinned to (the 8-column form at M = 129..256 moves the from-scratch chunk's weights
+// by up to 3e-2 of the reference's: a chaotic 20-step training, not a kernel error —
+// test_dense_bn_fwd_bwd holds both forms to torch at those shapes)
 static bool small_ok(int M, int N, int nslab, const void* p0, const void* p1, int64_t stride) {
-  return M <= 2 * RG && N % 4 == 0 && nslab <= 8 && ((uintptr_t)p0 % 16 == 0) &&
+  return M <= 128 && N % 4 == 0 && nslab <= 8 && ((uintptr_t)p0 % 16 == 0) &&
          ((uintptr_t)p1 % 16 == 0) && (nslab == 1 || stride % 4 == 0);
 }
 
-#define PKC_SMALL_LAUNCH(KERN, args, M, nslab, stream)                                          \
+#define PKC_SMALL_LAUNCH_G(KERN, G, args, M, nslab, stream)                                     \
   do {                                                                                         \
-    dim3 grid_((args).N / FC + ((args).N % FC ? 1 : 0));                                       \
-    const int ri_ = (M) <= RG ? 1 : 2;                                                         \
+    dim3 grid_((args).N / (4 * G) + ((args).N % (4 * G) ? 1 : 0));                             \
+    const int ri_ = (M) <= FT / G ? 1 : 2;                                                     \
     const int ns_ = (nslab) <= 1 ? 1 : ((nslab) <= 2 ? 2 : ((nslab) <= 4 ? 4 : 8));            \
     if (ri_ == 1) {                                                                            \
-      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 1>), grid_, dim3(FT), 0, stream, args);       \
-      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 1>), grid_, dim3(FT), 0, stream, args);  \
-      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 1>), grid_, dim3(FT), 0, stream, args);  \
-      else hipLaunchKernelGGL((KERN<8, 1>), grid_, dim3(FT), 0, stream, args);                \
+      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 1, G>), grid_, dim3(FT), 0, stream, args);    \
+      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 1, G>), grid_, dim3(FT), 0, stream, args); \
+      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 1, G>), grid_, dim3(FT), 0, stream, args); \
+      else hipLaunchKernelGGL((KERN<8, 1, G>), grid_, dim3(FT), 0, stream, args);             \
     } else {                                                                                   \
-      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 2>), grid_, dim3(FT), 0, stream, args);       \
-      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 2>), grid_, dim3(FT), 0, stream, args);  \
-      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 2>), grid_, dim3(FT), 0, stream, args);  \
-      else hipLaunchKernelGGL((KERN<8, 2>), grid_, dim3(FT), 0, stream, args);                \
+      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 2, G>), grid_, dim3(FT), 0, stream, args);    \
+      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 2, G>), grid_, dim3(FT), 0, stream, args); \
+      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 2, G>), grid_, dim3(FT), 0, stream, args); \
+      else hipLaunchKernelGGL((KERN<8, 2, G>), grid_, dim3(FT), 0, stream, args);             \
     }                                                                                          \
+  } while (0)
+#define PKC_SMALL_LAUNCH(KERN, args, M, nslab, stream)                                          \
+  do {                                                                                         \
+    if ((args).N >= 512) PKC_SMALL_LAUNCH_G(KERN, 2, args, M, nslab, stream);                  \
+    else PKC_SMALL_LAUNCH_G(KERN, 4, args, M, nslab, stream);                                  \
   } while (0)
 
 }  // namespace pkc
