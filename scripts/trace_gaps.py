@@ -24,7 +24,12 @@ if need:
     for a, b in pairs:
         lens[b - a] += 1
 L = max(lens, key=lens.get)
-steps = [rows[a:b] for a, b in pairs if b - a == L][-200:]
+# the graph-replayed steps of the timed region: of the steps with the common shape, the 200
+# shortest from first launch start to last launch end (eager steps of the same command — the
+# parity leg, per-launch cost probes — carry host launch gaps)
+cand = [rows[a:b] for a, b in pairs if b - a == L]
+cand.sort(key=lambda st: int(st[-1]["End_Timestamp"]) - int(st[0]["Start_Timestamp"]))
+steps = sorted(cand[:200], key=lambda st: int(st[0]["Start_Timestamp"]))
 agg = defaultdict(lambda: [0.0, 0.0, 0])
 order = []
 tot = []
