@@ -195,10 +195,134 @@ __device__ __forceinline__ void nll_reg_body(const pkc_nll_args& a, int block, N
   }
 }
 
+// The same with 16-byte accesses (N % 4 == 0, aligned rows): each thread owns two float4 column
+// chunks (j = 4 (tr + T q) + e), so a row takes 2 NS load instructions per thread instead of 8 NS
+template <int WPR, int NS>
+__device__ __forceinline__ void nll_vec_body(const pkc_nll_args& a, int block, NllShared& sh) {
+  constexpr int RPB = LW / WPR;
+  constexpr int T = 64 * WPR;
+  constexpr int NQ = 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rl = wave / WPR;
+  const int tr = threadIdx.x - rl * T;
+  const int r = block * RPB + rl;
+  const bool rok = r < a.M;
+  const int64_t N = a.N;
+  const int rr = rok ? r : a.M - 1;
+  const float* zb = a.zslab + (int64_t)rr * N;
+  const int y_ = *(a.labels ? a.labels + (int64_t)rr * a.label_stride
+                            : reinterpret_cast<const int32_t*>(a.zslab));
+  float4 v[NQ][NS];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int j0 = min(4 * (tr + T * q), a.N - 4);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int st = t < a.nslab ? t : a.nslab - 1;
+      v[q][t] = *reinterpret_cast<const float4*>(zb + (int64_t)st * a.slab_stride + j0);
+    }
+  }
+  float z[NQ][4];
+  float mx = -INFINITY;
+  int arg = 0x7fffffff;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int j0 = 4 * (tr + T * q);
+    float4 acc = v[q][0];
+#pragma unroll
+    for (int t = 1; t < NS; ++t) {
+      if (t < a.nslab) {
+        acc.x += v[q][t].x; acc.y += v[q][t].y; acc.z += v[q][t].z; acc.w += v[q][t].w;
+      }
+    }
+    if (a.bias) {
+      const float4 b = *reinterpret_cast<const float4*>(a.bias + min(j0, a.N - 4));
+      acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+    }
+    z[q][0] = acc.x; z[q][1] = acc.y; z[q][2] = acc.z; z[q][3] = acc.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)      // ascending j: first max per thread
+      if (j0 < a.N && z[q][e] > mx) { mx = z[q][e]; arg = j0 + e; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
+  if (WPR > 1) {
+    if (lane == 0) { sh.m[wave] = mx; sh.a[wave] = arg; }
+    __syncthreads();
+    for (int w = rl * WPR; w < rl * WPR + WPR; ++w) {
+      const float om = sh.m[w];
+      const int oa = sh.a[w];
+      if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    if (4 * (tr + T * q) < a.N) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) se += expf(z[q][e] - mx);
+    }
+  se = warp_sum(se);
+  if (WPR > 1) {
+    if (lane == 0) sh.s[wave] = se;
+    __syncthreads();
+    se = 0.f;
+    for (int w = rl * WPR; w < rl * WPR + WPR; ++w) se += sh.s[w];
+  }
+  if (!rok) return;
+  const float lse = mx + logf(se);
+  const int y = a.labels ? y_ : -1;
+  const float gscale = a.weight / (float)a.M;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int j0 = 4 * (tr + T * q);
+    if (j0 >= a.N) break;
+    const int64_t o = (int64_t)r * N + j0;
+    float lp[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lp[e] = z[q][e] - lse;
+    if (a.dlogits) {
+      float d[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float p = expf(lp[e]);
+        d[e] = gscale * (j0 + e == y ? p - 1.f : p);
+      }
+      *reinterpret_cast<float4*>(a.dlogits + o) = make_float4(d[0], d[1], d[2], d[3]);
+      if (a.dlogits_bf16) {
+        bf16x4 h;
+        h[0] = (__bf16)d[0]; h[1] = (__bf16)d[1]; h[2] = (__bf16)d[2]; h[3] = (__bf16)d[3];
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.dlogits_bf16) + o) = h;
+      }
+    }
+    float4 w = make_float4(lp[0], lp[1], lp[2], lp[3]);
+    if (a.log_prior) {
+      const float4 pr = *reinterpret_cast<const float4*>(a.log_prior + j0);
+      w.x -= pr.x; w.y -= pr.y; w.z -= pr.z; w.w -= pr.w;
+    }
+    *reinterpret_cast<float4*>(a.logp + o) = w;
+    if (y >= j0 && y < j0 + 4) {   // exactly one thread of the row owns the label column
+      if (a.row_loss) a.row_loss[r] = -lp[y - j0];
+      if (a.row_err) a.row_err[r] = (arg != y) ? 1.f : 0.f;
+    }
+  }
+}
+
 template <int WPR, int NS>
 __global__ __launch_bounds__(64 * LW) void nll_reg_kernel(pkc_nll_args a) {
   __shared__ NllShared sh;
   nll_reg_body<WPR, NS>(a, blockIdx.x, sh);
+}
+
+template <int WPR, int NS>
+__global__ __launch_bounds__(64 * LW) void nll_vec_kernel(pkc_nll_args a) {
+  __shared__ NllShared sh;
+  nll_vec_body<WPR, NS>(a, blockIdx.x, sh);
 }
 
 // several heads' LogSoftmax/NLL in one launch (workgroup ranges per head)
@@ -206,7 +330,7 @@ constexpr int NLL_MAX = 4;
 struct NllMulti {
   pkc_nll_args a[NLL_MAX];
   int wg0[NLL_MAX];
-  int code[NLL_MAX];   // 4 * (wide) + log2(NS)
+  int code[NLL_MAX];   // 8 * (16-byte form) + 4 * (wide) + log2(NS)
   int n;
 };
 
@@ -218,6 +342,14 @@ __global__ __launch_bounds__(64 * LW) void nll_multi_kernel(NllMulti g) {
     if (j < g.n && (int)blockIdx.x >= g.wg0[j]) i = j;
   const int b = blockIdx.x - g.wg0[i];
   switch (g.code[i]) {
+    case 8: nll_vec_body<1, 1>(g.a[i], b, sh); break;
+    case 9: nll_vec_body<1, 2>(g.a[i], b, sh); break;
+    case 10: nll_vec_body<1, 4>(g.a[i], b, sh); break;
+    case 11: nll_vec_body<1, 8>(g.a[i], b, sh); break;
+    case 12: nll_vec_body<4, 1>(g.a[i], b, sh); break;
+    case 13: nll_vec_body<4, 2>(g.a[i], b, sh); break;
+    case 14: nll_vec_body<4, 4>(g.a[i], b, sh); break;
+    case 15: nll_vec_body<4, 8>(g.a[i], b, sh); break;
     case 0: nll_reg_body<1, 1>(g.a[i], b, sh); break;
     case 1: nll_reg_body<1, 2>(g.a[i], b, sh); break;
     case 2: nll_reg_body<1, 4>(g.a[i], b, sh); break;
@@ -238,6 +370,18 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(int nheads, const fl
 
 }  // namespace pkc
 
+// the 16-byte form: whole float4 column chunks, aligned rows (PKC_NLL_VEC=0: scalar form, A/B)
+static bool nll_vec_ok(const pkc_nll_args* a) {
+  static const int on = [] {
+    const char* v = getenv("PKC_NLL_VEC");
+    return v ? atoi(v) : 1;
+  }();
+  auto al = [](const void* p, int b) { return ((uintptr_t)p % b) == 0; };
+  return on && a->N % 4 == 0 && a->N >= 4 && (a->nslab == 1 || a->slab_stride % 4 == 0) &&
+         al(a->zslab, 16) && al(a->logp, 16) && al(a->dlogits, 16) && al(a->bias, 16) &&
+         al(a->log_prior, 16) && al(a->dlogits_bf16, 8);
+}
+
 extern "C" int pkc_nll_fused(const pkc_nll_args* a, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab >= 1 && a->zslab && a->logp,
@@ -247,14 +391,19 @@ extern "C" int pkc_nll_fused(const pkc_nll_args* a, void* stream) {
   const bool wide = a->N >= 512;
   if (a->nslab <= 8 && a->N <= (wide ? 2048 : 512)) {
     const dim3 grid(wide ? a->M : (a->M + LW - 1) / LW), blk(64 * LW);
-#define PKC_NLL(W)                                                                    \
+#define PKC_NLL(K, W)                                                                 \
     switch (ns) {                                                                     \
-      case 1: hipLaunchKernelGGL((nll_reg_kernel<W, 1>), grid, blk, 0, S(stream), *a); break; \
-      case 2: hipLaunchKernelGGL((nll_reg_kernel<W, 2>), grid, blk, 0, S(stream), *a); break; \
-      case 4: hipLaunchKernelGGL((nll_reg_kernel<W, 4>), grid, blk, 0, S(stream), *a); break; \
-      default: hipLaunchKernelGGL((nll_reg_kernel<W, 8>), grid, blk, 0, S(stream), *a); break; \
+      case 1: hipLaunchKernelGGL((K<W, 1>), grid, blk, 0, S(stream), *a); break;     \
+      case 2: hipLaunchKernelGGL((K<W, 2>), grid, blk, 0, S(stream), *a); break;     \
+      case 4: hipLaunchKernelGGL((K<W, 4>), grid, blk, 0, S(stream), *a); break;     \
+      default: hipLaunchKernelGGL((K<W, 8>), grid, blk, 0, S(stream), *a); break;    \
     }
-    if (wide) { PKC_NLL(4) } else { PKC_NLL(1) }
+    const bool v4 = nll_vec_ok(a);
+    if (wide) {
+      if (v4) { PKC_NLL(nll_vec_kernel, 4) } else { PKC_NLL(nll_reg_kernel, 4) }
+    } else {
+      if (v4) { PKC_NLL(nll_vec_kernel, 1) } else { PKC_NLL(nll_reg_kernel, 1) }
+    }
 #undef PKC_NLL
   } else if (wide) {
     hipLaunchKernelGGL(nll_kernel<4>, dim3(a->M), dim3(64 * LW), 0, S(stream), *a);
@@ -270,7 +419,7 @@ static bool nll_reg_code(const pkc_nll_args* a, int* code, int* nwg) {
   const int ns = a->nslab <= 1 ? 0 : (a->nslab <= 2 ? 1 : (a->nslab <= 4 ? 2 : 3));
   const bool wide = a->N >= 512;
   if (a->nslab > 8 || a->N > (wide ? 2048 : 512)) return false;
-  *code = (wide ? 4 : 0) + ns;
+  *code = (nll_vec_ok(a) ? 8 : 0) + (wide ? 4 : 0) + ns;
   *nwg = wide ? a->M : (a->M + LW - 1) / LW;
   return true;
 }
