@@ -660,6 +660,245 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
   }
 }
 
+// ------------------------------------------------ 16-byte forms of the large-M (M > 128) kernels
+// Same row split as the scalar kernels — row-thread t of a 16-row block takes rows t, t + 4, t + 8,
+// t + 12 and the block's partials are reduced over the 4 row-threads in the same order — with each
+// thread owning 4 adjacent columns (a block spans 256 columns): every column's arithmetic is the
+// scalar kernels' operation for operation, in one 16-byte access instead of four 4-byte ones.
+constexpr int EC4 = 64;   // float4 column groups per block
+
+__device__ __forceinline__ float4 z4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float4 slab_sum_v4(const float* __restrict__ p, int64_t stride, int nslab) {
+  float4 a0 = z4(), a1 = z4(), a2 = z4(), a3 = z4();
+  int s = 0;
+  for (; s + 4 <= nslab; s += 4) {
+    a0 = f4add(a0, ld4(p + (int64_t)s * stride));
+    a1 = f4add(a1, ld4(p + (int64_t)(s + 1) * stride));
+    a2 = f4add(a2, ld4(p + (int64_t)(s + 2) * stride));
+    a3 = f4add(a3, ld4(p + (int64_t)(s + 3) * stride));
+  }
+  for (; s < nslab; ++s) a0 = f4add(a0, ld4(p + (int64_t)s * stride));
+  return f4add(f4add(a0, a1), f4add(a2, a3));
+}
+
+__device__ __forceinline__ float4 colsum4_v4(float4 v, float4* red) {
+  const int c = threadIdx.x % EC4, t = threadIdx.x / EC4;
+  __syncthreads();
+  red[t * EC4 + c] = v;
+  __syncthreads();
+  return f4add(f4add(red[c], red[EC4 + c]), f4add(red[2 * EC4 + c], red[3 * EC4 + c]));
+}
+
+__global__ __launch_bounds__(ET) void dense_stats_v4_kernel(pkc_dense_fwd_args a, float* part) {
+  __shared__ float4 red[ET];
+  const int c = (blockIdx.x * EC4 + threadIdx.x % EC4) * 4;
+  const int t = threadIdx.x / EC4;
+  const int r0 = blockIdx.y * ERB;
+  const bool cok = c < a.N;
+  const int64_t N = a.N;
+  const float4 b = (cok && a.bias) ? ld4(a.bias + c) : z4();
+  float4 z[RPT];
+  float4 s = z4();
+  int nb = 0;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + t + ER * i;
+    z[i] = z4();
+    if (cok && r < a.M) {
+      z[i] = f4add(slab_sum_v4(a.zslab + r * N + c, a.slab_stride, a.nslab), b);
+      st4(a.xhat + r * N + c, z[i]);
+      s = f4add(s, z[i]);
+      ++nb;
+    }
+  }
+  const float nrows = (float)min(ERB, a.M - r0);
+  const float4 sm = colsum4_v4(s, red);
+  const float4 mean_b = make_float4(sm.x / nrows, sm.y / nrows, sm.z / nrows, sm.w / nrows);
+  float4 m2 = z4();
+#pragma unroll
+  for (int i = 0; i < RPT; ++i)
+    if (i < nb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = f4get(z[i], j) - f4get(mean_b, j);
+        f4set(m2, j, f4get(m2, j) + d * d);
+      }
+    }
+  m2 = colsum4_v4(m2, red);
+  if (cok && t == 0) {
+    st4(part + (int64_t)blockIdx.y * 2 * N + c, mean_b);
+    st4(part + (int64_t)blockIdx.y * 2 * N + N + c, m2);
+  }
+}
+
+__global__ __launch_bounds__(ET) void dense_apply_v4_kernel(pkc_dense_fwd_args a, const float* part) {
+  const int c = (blockIdx.x * EC4 + threadIdx.x % EC4) * 4;
+  const int t = threadIdx.x / EC4;
+  const int r0 = blockIdx.y * ERB;
+  if (c >= a.N) return;
+  const int64_t N = a.N;
+  float mean[4] = {0.f, 0.f, 0.f, 0.f}, invstd[4] = {1.f, 1.f, 1.f, 1.f};
+  float gam[4] = {1.f, 1.f, 1.f, 1.f}, bet[4] = {0.f, 0.f, 0.f, 0.f};
+  if (a.norm == PKC_NORM_BN_TRAIN) {
+    const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mean[j] = fin[c + j];
+      invstd[j] = 1.f / sqrtf(fin[N + c + j] + a.eps);
+      gam[j] = a.gamma[c + j];
+      bet[j] = a.beta[c + j];
+    }
+  } else if (a.norm == PKC_NORM_BN_EVAL) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mean[j] = a.running_mean[c + j];
+      invstd[j] = 1.f / sqrtf(a.running_var[c + j] + a.eps);
+      gam[j] = a.gamma[c + j];
+      bet[j] = a.beta[c + j];
+    }
+  }
+  const bool drop = a.drop_p > 0.f;
+  const float scale = drop ? 1.f / (1.f - a.drop_p) : 1.f;
+  const uint32_t thr = drop ? (uint32_t)((double)(1.f - a.drop_p) * 4294967296.0) : 0u;
+  const int64_t step = a.step_ctr ? *a.step_ctr : 0;
+  const float4 b = a.bias ? ld4(a.bias + c) : z4();
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + t + ER * i;
+    if (r >= a.M) break;
+    const int64_t idx = r * N + c;
+    const float4 zz = (a.norm == PKC_NORM_BN_TRAIN) ? ld4(a.xhat + idx)
+                                                    : f4add(slab_sum_v4(a.zslab + idx, a.slab_stride, a.nslab), b);
+    float4 xh, o;
+    uint32_t kw = 0;
+    uchar4 kin = make_uchar4(1, 1, 1, 1);
+    if (drop && a.keep_in) kin = *reinterpret_cast<const uchar4*>(a.keep_in + idx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float z = f4get(zz, j);
+      const float x = (a.norm == PKC_NORM_NONE) ? z : (z - mean[j]) * invstd[j];
+      const float y = (a.norm == PKC_NORM_NONE) ? z : x * gam[j] + bet[j];
+      float v = act_fwd(a.act, y);
+      if (drop) {
+        uint32_t k;
+        if (a.keep_in) k = j == 0 ? kin.x : (j == 1 ? kin.y : (j == 2 ? kin.z : kin.w));
+        else k = hash_drop(hash_seed(a.seed, (uint64_t)a.stream_id, (uint64_t)step), (uint32_t)(idx + j)) < thr;
+        kw |= (k ? 1u : 0u) << (8 * j);
+        v = k ? v * scale : 0.f;
+      }
+      f4set(xh, j, x);
+      f4set(o, j, v);
+    }
+    if (drop && a.keep_out) *reinterpret_cast<uint32_t*>(a.keep_out + idx) = kw;
+    if (a.xhat) st4(a.xhat + idx, xh);
+    st4(a.out + idx, o);
+    if (a.out_bf16) st_h4(a.out_bf16, idx, o);
+  }
+}
+
+__global__ __launch_bounds__(ET) void dense_bwd_stats_v4_kernel(pkc_dense_bwd_args a, float* part) {
+  __shared__ float4 red[ET];
+  const int c = (blockIdx.x * EC4 + threadIdx.x % EC4) * 4;
+  const int t = threadIdx.x / EC4;
+  const int r0 = blockIdx.y * ERB;
+  const bool cok = c < a.N;
+  const int64_t N = a.N;
+  const bool bn = a.norm == PKC_NORM_BN_TRAIN;
+  const float4 gam = (cok && bn) ? ld4(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 bet = (cok && bn) ? ld4(a.beta + c) : z4();
+  const bool drop = a.drop_p > 0.f;
+  const float scale = drop ? 1.f / (1.f - a.drop_p) : 1.f;
+  float4 sdy = z4(), sdyx = z4();
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + t + ER * i;
+    if (cok && r < a.M) {
+      const int64_t idx = r * N + c;
+      const float4 g4 = slab_sum_v4(a.gslab + idx, a.slab_stride, a.nslab);
+      const float4 xh4 = ld4(a.xhat + idx);
+      const uchar4 kp = drop ? *reinterpret_cast<const uchar4*>(a.keep + idx) : make_uchar4(1, 1, 1, 1);
+      float4 d4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float g = f4get(g4, j);
+        const uint8_t kj = j == 0 ? kp.x : (j == 1 ? kp.y : (j == 2 ? kp.z : kp.w));
+        if (drop) g = kj ? g * scale : 0.f;
+        const float xh = f4get(xh4, j);
+        const float y = bn ? xh * f4get(gam, j) + f4get(bet, j) : xh;
+        const float dy = g * act_bwd(a.act, y, act_fwd(a.act, y));
+        f4set(d4, j, dy);
+        f4set(sdy, j, f4get(sdy, j) + dy);
+        f4set(sdyx, j, f4get(sdyx, j) + dy * xh);
+      }
+      st4(a.dz + idx, d4);
+      if (!bn && a.dz_bf16) st_h4(a.dz_bf16, idx, d4);    // final without BN
+    }
+  }
+  sdy = colsum4_v4(sdy, red);
+  sdyx = colsum4_v4(sdyx, red);
+  if (cok && t == 0) {
+    st4(part + (int64_t)blockIdx.y * 2 * N + c, sdy);
+    st4(part + (int64_t)blockIdx.y * 2 * N + N + c, sdyx);
+  }
+}
+
+__global__ __launch_bounds__(ET) void dense_bwd_apply_v4_kernel(pkc_dense_bwd_args a, const float* part,
+                                                                float invM) {
+  const int c = (blockIdx.x * EC4 + threadIdx.x % EC4) * 4;
+  const int t = threadIdx.x / EC4;
+  const int r0 = blockIdx.y * ERB;
+  if (c >= a.N || a.norm != PKC_NORM_BN_TRAIN) return;
+  const int64_t N = a.N;
+  const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+  float k[4], mdy[4], mdyx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    k[j] = a.gamma[c + j] * a.save_invstd[c + j];
+    mdy[j] = fin[c + j] * invM;
+    mdyx[j] = fin[N + c + j] * invM;
+  }
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = r0 + t + ER * i;
+    if (r >= a.M) break;
+    const int64_t idx = r * N + c;
+    const float4 dz = ld4(a.dz + idx), xh = ld4(a.xhat + idx);
+    float4 d;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f4set(d, j, k[j] * (f4get(dz, j) - mdy[j] - f4get(xh, j) * mdyx[j]));
+    st4(a.dz + idx, d);
+    if (a.dz_bf16) st_h4(a.dz_bf16, idx, d);
+  }
+}
+
+static inline bool al16(const void* p) { return (uintptr_t)p % 16 == 0; }
+// the 16-byte forms cover 4x the columns per workgroup: only for grids that still have this many
+// workgroups (B = 4096: 4.74M -> 4.96M frames/s; at B = 1024, 256 workgroups instead of 1024 ran
+// 2.06M -> 2.00M, the small-grid loss the latency-bound BatchNorm kernels show everywhere)
+constexpr int64_t V4_MIN_WG = 1024;
+// the 16-byte large-M forms (PKC_DENSE_V4=0: scalar forms, A/B)
+static bool dense_v4_enabled() {
+  static const int on = [] {
+    const char* v = getenv("PKC_DENSE_V4");
+    return v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
+static bool v4_fwd(const pkc_dense_fwd_args* a) {
+  return dense_v4_enabled() && a->N % 4 == 0 && (a->nslab == 1 || a->slab_stride % 4 == 0) &&
+         al16(a->zslab) && al16(a->xhat) && al16(a->out) && al16(a->bias) && al16(a->gamma) &&
+         al16(a->beta) && al16(a->running_mean) && al16(a->running_var) &&
+         (uintptr_t)a->keep_in % 4 == 0 && (uintptr_t)a->keep_out % 4 == 0 &&
+         (uintptr_t)a->out_bf16 % 8 == 0;
+}
+static bool v4_bwd(const pkc_dense_bwd_args* a) {
+  return dense_v4_enabled() && a->N % 4 == 0 && (a->nslab == 1 || a->slab_stride % 4 == 0) &&
+         al16(a->gslab) && al16(a->xhat) && al16(a->dz) && al16(a->gamma) && al16(a->beta) &&
+         al16(a->save_invstd) && (uintptr_t)a->keep % 4 == 0 && (uintptr_t)a->dz_bf16 % 8 == 0;
+}
+
 // at most 128 rows (the MLP batch): larger row counts (a recurrent layer's T * 2B rows) keep the
 // stats / finalize / apply form and its summation order, which the recurrent run_nn lifecycle
 // tests are pinned to (the 8-column form at M = 129..256 moves the from-scratch chunk's weights
@@ -725,14 +964,16 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
     return PKC_OK;
   }
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
   if (a->norm == PKC_NORM_BN_TRAIN) {
-    hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+    { if (v4) hipLaunchKernelGGL(dense_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
     PKC_LAUNCH_CHECK("pkc_dense_fwd stats");
     hipLaunchKernelGGL(dense_finalize_kernel<false>, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
                        S(stream), *a, work, nullptr);
     PKC_LAUNCH_CHECK("pkc_dense_fwd finalize");
   }
-  hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  { if (v4) hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   PKC_LAUNCH_CHECK("pkc_dense_fwd apply");
   return PKC_OK;
 }
@@ -756,14 +997,15 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
     return PKC_OK;
   }
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
-  hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  { if (v4) hipLaunchKernelGGL(dense_bwd_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd stats");
   hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0, S(stream),
                      *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd finalize");
   if (a->norm == PKC_NORM_BN_TRAIN)      // without BN, dz = dy is final after the stats pass
-    hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work,
-                       1.f / (float)a->M);
+    { if (v4) hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, 1.f / (float)a->M); else hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, 1.f / (float)a->M); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd apply");
   return PKC_OK;
 }
@@ -787,7 +1029,9 @@ extern "C" int pkc_dense_fwd_stats(const pkc_dense_fwd_args* a, float* work, flo
   if (st) return st;
   PKC_CHECK_ARG(state, "pkc_dense_fwd_stats: null state");
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
-  hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  { if (v4) hipLaunchKernelGGL(dense_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   hipLaunchKernelGGL(dense_finalize_kernel<true>, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
                      S(stream), *a, work, state);
   PKC_LAUNCH_CHECK("pkc_dense_fwd_stats");
@@ -803,7 +1047,9 @@ extern "C" int pkc_dense_fwd_sync_apply(const pkc_dense_fwd_args* a, float* work
   hipLaunchKernelGGL(dense_sync_merge_kernel, dim3((a->N + 255) / 256), dim3(256), 0, S(stream), *a,
                      work, states, nranks);
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
-  hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  { if (v4) hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   PKC_LAUNCH_CHECK("pkc_dense_fwd_sync_apply");
   return PKC_OK;
 }
@@ -823,7 +1069,9 @@ extern "C" int pkc_dense_bwd_stats(const pkc_dense_bwd_args* a, float* work, flo
   if (st) return st;
   PKC_CHECK_ARG(sums, "pkc_dense_bwd_stats: null sums");
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
-  hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  { if (v4) hipLaunchKernelGGL(dense_bwd_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
                      S(stream), *a, work);
   const float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
@@ -843,8 +1091,9 @@ extern "C" int pkc_dense_bwd_sync_apply(const pkc_dense_bwd_args* a, float* work
   PKC_HIP_CHECK(hipMemcpyAsync(fin, sums, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice,
                                S(stream)), "pkc_dense_bwd_sync_apply copy");
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
-  hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work,
-                     1.f / (float)total_rows);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  { if (v4) hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, 1.f / (float)total_rows); else hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, 1.f / (float)total_rows); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd_sync_apply");
   return PKC_OK;
 }
