@@ -86,7 +86,13 @@ __global__ __launch_bounds__(ET) void dense_stats_kernel(pkc_dense_fwd_args a, f
 // 16 workgroups, 27 us per BatchNorm; now 16 merges on N / 16 workgroups.)
 // -> part[nrb*2N + c] = mean, part[nrb*2N + N + c] = population variance; the BN training side
 // outputs (save_mean / save_invstd / running statistics) are written here.
-constexpr int FC_F = 16, FR_F = 16;
+// PKC_FIN_COLS columns per finalize workgroup of FC_F x FR_F threads: each column's merge order
+// depends on FR_F only, so any width gives the same bits; 4 columns (N / 4 workgroups of 64
+// threads) measured no faster than 16 (B = 4096: 4.87-4.90M vs 4.92-4.94M frames/s, same box)
+#ifndef PKC_FIN_COLS
+#define PKC_FIN_COLS 16
+#endif
+constexpr int FC_F = PKC_FIN_COLS, FR_F = 16;
 // STATE: write this rank's (n, mean, M2) per column to state[3N] instead (SyncBN, no side outputs)
 template <bool STATE = false>
 __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a, float* part,
@@ -969,7 +975,7 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   if (a->norm == PKC_NORM_BN_TRAIN) {
     { if (v4) hipLaunchKernelGGL(dense_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
     PKC_LAUNCH_CHECK("pkc_dense_fwd stats");
-    hipLaunchKernelGGL(dense_finalize_kernel<false>, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
+    hipLaunchKernelGGL(dense_finalize_kernel<false>, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0,
                        S(stream), *a, work, nullptr);
     PKC_LAUNCH_CHECK("pkc_dense_fwd finalize");
   }
@@ -1001,7 +1007,7 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
   const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
   { if (v4) hipLaunchKernelGGL(dense_bwd_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd stats");
-  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0, S(stream),
+  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0, S(stream),
                      *a, work);
   PKC_LAUNCH_CHECK("pkc_dense_bwd finalize");
   if (a->norm == PKC_NORM_BN_TRAIN)      // without BN, dz = dy is final after the stats pass
@@ -1032,7 +1038,7 @@ extern "C" int pkc_dense_fwd_stats(const pkc_dense_fwd_args* a, float* work, flo
   const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
   const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
   { if (v4) hipLaunchKernelGGL(dense_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
-  hipLaunchKernelGGL(dense_finalize_kernel<true>, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
+  hipLaunchKernelGGL(dense_finalize_kernel<true>, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0,
                      S(stream), *a, work, state);
   PKC_LAUNCH_CHECK("pkc_dense_fwd_stats");
   return PKC_OK;
@@ -1072,7 +1078,7 @@ extern "C" int pkc_dense_bwd_stats(const pkc_dense_bwd_args* a, float* work, flo
   const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
   const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
   { if (v4) hipLaunchKernelGGL(dense_bwd_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
-  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(ET), 0,
+  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0,
                      S(stream), *a, work);
   const float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
   PKC_HIP_CHECK(hipMemcpyAsync(sums, fin, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice,
