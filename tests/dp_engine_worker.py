@@ -4,7 +4,7 @@ sharing one GPU).  Each rank trains its half of every global batch with Engine(g
 and the bucketed all-reduce of pkc.dist.GradAllReduce (the first bucket overlapping the rest of the
 backward), eagerly or replayed from the split hipGraphs (mode "graph"), and saves its state.
 
-argv: out_dir mode (eager | graph | syncbn) steps B_per_rank
+argv: out_dir mode (eager | graph | syncbn | bf16graph) steps B_per_rank
 """
 import os
 import sys
@@ -46,7 +46,8 @@ def data(steps, B_total):
     return X, lab
 
 
-def build(cfg, world, B, X, lab, sync_bn=None):
+def build(cfg, world, B, X, lab, sync_bn=None, prec=None):
+    from pkc import _lib as L
     from pkc.engine import Engine, parse_model
     from pkc.neural_networks import MLP
     torch.manual_seed(2234)
@@ -57,7 +58,8 @@ def build(cfg, world, B, X, lab, sync_bn=None):
         nets[o["arch_name"]] = MLP(o, inp).cuda().train()
         opts[o["arch_name"]] = o
     eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 40)},
-                 ["lab_cd", "lab_mono"], batch=B, seed=1, grad_scale=1.0 / world, sync_bn=sync_bn)
+                 ["lab_cd", "lab_mono"], batch=B, seed=1, grad_scale=1.0 / world, sync_bn=sync_bn,
+                 prec=L.PREC_FP32 if prec is None else prec)
     eng.bind_chunk(torch.from_numpy(X).cuda(), torch.from_numpy(lab).cuda(), X.shape[0])
     return eng, nets
 
@@ -74,9 +76,11 @@ def main():
     rows = np.concatenate([np.arange(s * B * world + rank * B, s * B * world + (rank + 1) * B)
                            for s in range(steps)])
     sbn = DP.SyncBatchNorm() if mode == "syncbn" else None
-    eng, nets = build(dp_config(bn=mode == "syncbn"), world, B, X[rows], lab[rows], sync_bn=sbn)
+    from pkc import _lib as L
+    eng, nets = build(dp_config(bn=mode == "syncbn"), world, B, X[rows], lab[rows], sync_bn=sbn,
+                      prec=L.PREC_BF16 if mode == "bf16graph" else None)
     ar = DP.GradAllReduce()
-    if mode == "graph":
+    if mode in ("graph", "bf16graph"):
         assert eng.capture(split_optimizer=True)
         assert eng.graph_tail is not None        # bucketed: two backward graphs
     for _ in range(steps):

@@ -22,11 +22,11 @@ pytestmark = pytest.mark.gpu
 STEPS, B = 3, 32
 
 
-def full_batch_reference(bn=False):
+def full_batch_reference(bn=False, prec=None):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import dp_engine_worker as W
     X, lab = W.data(STEPS, 2 * B)
-    eng, nets = W.build(W.dp_config(bn=bn), 1, 2 * B, X, lab)
+    eng, nets = W.build(W.dp_config(bn=bn), 1, 2 * B, X, lab, prec=prec)
     for _ in range(STEPS):
         eng.train_step()
     torch.cuda.synchronize()
@@ -35,15 +35,20 @@ def full_batch_reference(bn=False):
                   for k, v in nets[a].state_dict().items()}
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph", "syncbn"])
+@pytest.mark.parametrize("mode", ["eager", "graph", "syncbn", "bf16graph"])
 def test_dp_engine_two_ranks_equal_full_batch(mode, tmp_path):
     """syncbn: the body layers carry BatchNorm, its statistics synchronised over the ranks
     (pkc.dist.SyncBatchNorm, SURVEY 8e's DP parity recipe): then the split global batch still
-    equals the one-process full batch, running statistics included."""
+    equals the one-process full batch, running statistics included.  bf16graph: the bench's
+    precision (bf16-stored operands, the optimizer refreshing the bf16 weight copies after the
+    all-reduce) from the split graphs: replicas bit-identical; against the one-process bf16 run
+    the fp32 sums differ in order, which can flip a weight's bf16 rounding: 1e-2 / 1e-3 on the
+    weights and 1e-3 on the loss (a stale bf16 copy moves the loss by far more)."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000 +
-                                                            {"graph": 7, "syncbn": 13}.get(mode, 0)),
+                                                            {"graph": 7, "syncbn": 13,
+                                                             "bf16graph": 19}.get(mode, 0)),
            os.path.join(ROOT, "tests", "dp_engine_worker.py"), str(tmp_path), mode, str(STEPS),
            str(B)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
@@ -51,13 +56,16 @@ def test_dp_engine_two_ranks_equal_full_batch(mode, tmp_path):
     g0 = np.load(os.path.join(tmp_path, "rank0_%s.npz" % mode))
     g1 = np.load(os.path.join(tmp_path, "rank1_%s.npz" % mode))
     assert int(g0["calls"]) == 2 * STEPS          # two buckets per step
-    loss, ref = full_batch_reference(bn=mode == "syncbn")
+    from pkc import _lib as L
+    bf = mode == "bf16graph"
+    loss, ref = full_batch_reference(bn=mode == "syncbn", prec=L.PREC_BF16 if bf else None)
     for k, v in ref.items():
         np.testing.assert_array_equal(g0[k], g1[k], err_msg="replicas differ: " + k)
         if k.endswith("num_batches_tracked"):
             continue
-        np.testing.assert_allclose(g0[k], v, rtol=1e-4, atol=1e-6, err_msg=k)
-    np.testing.assert_allclose(float(g0["loss"]), loss, rtol=1e-5)
+        np.testing.assert_allclose(g0[k], v, rtol=1e-2 if bf else 1e-4, atol=1e-3 if bf else 1e-6,
+                                   err_msg=k)
+    np.testing.assert_allclose(float(g0["loss"]), loss, rtol=1e-3 if bf else 1e-5)
 
 
 def test_dp_c_abi_allreduce_world1():
