@@ -143,7 +143,7 @@ def cpu_baseline(batch, seconds=12.0):
 
 def pmc_traffic(label):
     """HBM bytes per launch of `label` from the committed rocprofv3 PMC summary
-    (scripts/gpu_pmc.sh -> profiles/*pmc_traffic.json): (2 x FETCH_SIZE + WRITE_SIZE) KiB, the
+    (scripts/gpu.sh pmc -> profiles/*pmc_traffic.json): (2 x FETCH_SIZE + WRITE_SIZE) KiB, the
     gfx950 FETCH_SIZE half-count correction applied as MI355X_MICROARCH.md's HBM section
     prescribes (it is exact for 128-byte coalesced reads; for 64-byte row segments it can
     over-count the reads up to 2x — the summary keeps the raw counters).  None when the summary
@@ -287,48 +287,11 @@ def seq_entry(name, steps, warmup, with_cpu, cpu_seconds):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=128)
-    ap.add_argument("--prec", choices=["bf16", "fp32"], default="bf16")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-batch-sweep", action="store_true")
-    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 value of the headline")
-    ap.add_argument("--no-seq-configs", action="store_true",
-                    help="skip the informational C3/C4/C5 sequence-model throughputs")
-    ap.add_argument("--pmc-replay", type=int, default=0,
-                    help="only replay the dominant launch N times (for rocprofv3 --pmc passes)")
-    ap.add_argument("--pmc-kernel", default="",
-                    help="entry point to replay with --pmc-replay (default: pick the dominant one)")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # PKC_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
-    backend = os.environ.get("PKC_DIST_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % torch.cuda.device_count()
-    torch.cuda.set_device(local)
-    allreduce = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-
-        def allreduce(t, async_op=False):
-            return dist.all_reduce(t, async_op=async_op)
+def measure_mlp(prec, args, rank, world, allreduce):
+    """The C2 step at `prec`: live per-launch profile -> dominant entry point, the captured
+    step's timed region (exactly args.steps batches), the dominant launch's roofline."""
     from pkc import _lib
-    prec = _lib.PREC_BF16 if args.prec == "bf16" else _lib.PREC_FP32
     eng, chunk, prep_s, nets = build(prec, args.batch, rank, world)
-
     # per-launch device times of warm eager steps -> dominant kernel + its roofline inputs
     for _ in range(3):
         eng.train_step(allreduce)
@@ -365,35 +328,152 @@ def main():
         return fn, costs[fn]
 
     if args.pmc_replay:
-        # counter runs (scripts/gpu_pmc.sh): the dominant kernel's launches, N rounds, last
+        # counter runs (scripts/gpu.sh pmc): the dominant kernel's launches, N rounds, last
         dom_fn = args.pmc_kernel or pick_dominant()[0]
         nl = eng.replay_launches(dom_fn, args.pmc_replay)
-        print(json.dumps({"pmc_replay": dom_fn, "launches": nl * args.pmc_replay}), flush=True)
-        return
+        tag = dom_fn + ("@fp32" if prec == _lib.PREC_FP32 else "")
+        print(json.dumps({"pmc_replay": tag, "launches": nl * args.pmc_replay}), flush=True)
+        sys.exit(0)
     eng.capture(split_optimizer=world > 1)
     dt = time_steps(eng, args.steps, args.warmup, allreduce, world)
     loss_sum, err_sum = eng.chunk_totals()
     n_done = args.warmup + args.steps
-
     dom_fn, dom_us = pick_dominant()
     d = by_fn[dom_fn]
-    label = dom_fn
     cnt = d["launches"]
     per_launch_fl = d["flops"] / cnt
     per_launch_nb = d["bytes"] / cnt
     avg_ms = dom_us / cnt * 1e-3
-    traffic = pmc_traffic(label)
+    pname = "bf16" if prec == _lib.PREC_BF16 else "fp32"
+    traffic = pmc_traffic(dom_fn if pname == "bf16" else dom_fn + "@fp32")
     del eng
     torch.cuda.empty_cache()
+    # MFMA-bound only where the launch's arithmetic intensity exceeds the machine balance
+    balance = MFMA_PEAK_TFLOPS[pname] * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if "gemm" in dom_fn and per_launch_fl / max(per_launch_nb, 1.0) > balance:
+        bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS[pname], "TFLOP/s"
+        achieved = per_launch_fl / (avg_ms * 1e-3) / 1e12
+    else:
+        bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
+        achieved = per_launch_nb / (avg_ms * 1e-3) / 1e9
+    frames = args.steps * args.batch * world
+    return {"value": round(frames / dt, 1), "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "dtype": pname,
+            "roofline": {"kernel": dom_fn, "labels": sorted(d["labels"]), "bound": bound,
+                         "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "avg_launch_us": round(avg_ms * 1e3, 3), "launches_per_step": cnt,
+                         "algorithmic_bytes_per_launch": per_launch_nb,
+                         "algorithmic_flops_per_launch": per_launch_fl,
+                         "mfma_tflops_per_launch": round(per_launch_fl / (avg_ms * 1e-3) / 1e12, 2)},
+            "launches_per_step": len(prof),
+            "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
+                                  sorted(agg.items(), key=lambda kv: -kv[1][1])},
+            "chunk_frames_per_rank": chunk.n_rows, "chunk_prep_s": round(prep_s, 3),
+            "mean_loss": round(loss_sum / max(1, n_done), 4)}
+
+
+WORKLOADS = {
+    "c2": "TIMIT_baselines MLP 440-5x1024-{1928,48} (TIMIT_MLP_fmllr.cfg), batch_size_train=128, "
+          "dropout 0.15, SGD body + RMSprop heads",
+    "c3": "TIMIT_CGS liGRU 4x550 bidirectional + HCGS [32,2]/[75,75] on W and U, B=8 sentences, "
+          "heads 1928 cd + 48 mono",
+    "c4": "Librispeech_baselines LSTM 4x1024 bidirectional, B=16 sentences per rank, T<=450, "
+          "heads 1928 cd + 48 mono, chunk DP (frame-weighted all-reduce)",
+    "c5": "LibriSpeech_CGS LSTM 3x512 + Pattern b08b08_k04_n16 + 8-bit weight / 16-bit input "
+          "fake-quant, B=12 sentences per rank, T<=200, chunk DP (frame-weighted all-reduce)",
+}
+
+
+def seq_main(args, rank, world, allreduce):
+    """`--config c3|c4|c5`: the sequence configuration measured as THE line (one rank per GPU,
+    every rank its own synthetic chunk, B sentences per rank and step: weak scaling)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_seq
+    r = bench_seq.run(args.config, steps=args.steps, warmup=args.warmup, allreduce=allreduce,
+                      rank=rank, world=world)
+    if rank != 0:
+        return
+    peak = MFMA_PEAK_TFLOPS["fp32"]
+    res = {"metric": "acoustic frames/sec (train)", "value": round(r["frames_per_s"], 1),
+           "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(r["ms_per_step"], 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic TIMIT-shaped chunk per rank (64 x B length-sorted sentences, "
+                   "440-dim features), random-init weights",
+           "config": {"workload": WORKLOADS[args.config],
+                      "global_batch": r["batch_sentences"] * world,
+                      "parallelism": "dp%d" % world},
+           "roofline": {"bound": "mfma", "achieved": round(r["alg_tflops_per_s"], 3),
+                        "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(r["alg_tflops_per_s"] / peak, 5), "traffic": None,
+                        "note": "whole step: algorithmic flops (W, U scaled by mask density, "
+                                "heads; x3 for training) over padded rows / measured time; the "
+                                "recurrence is serial-latency-bound (us_per_time_step...)"},
+           "us_per_time_step_per_layer_fwd_bwd": round(r["us_per_time_step_per_layer_fwd_bwd"], 3),
+           "mean_T": round(r["mean_T"], 1)}
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = bench_seq.cpu_baseline(args.config, seconds=args.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: the headline MLP (default); c3/c4/c5: a sequence configuration "
+                         "as the line (with --gpus N: N data-parallel ranks of it)")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--prec", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-batch-sweep", action="store_true")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 value of the headline")
+    ap.add_argument("--no-seq-configs", action="store_true",
+                    help="skip the informational C3/C4/C5 sequence-model throughputs")
+    ap.add_argument("--pmc-replay", type=int, default=0,
+                    help="only replay the dominant launch N times (for rocprofv3 --pmc passes)")
+    ap.add_argument("--pmc-kernel", default="",
+                    help="entry point to replay with --pmc-replay (default: pick the dominant one)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PKC_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU
+    backend = os.environ.get("PKC_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    allreduce = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+
+        def allreduce(t, async_op=False):
+            return dist.all_reduce(t, async_op=async_op)
+    if args.config != "c2":
+        seq_main(args, rank, world, allreduce)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    from pkc import _lib
+    prec = _lib.PREC_BF16 if args.prec == "bf16" else _lib.PREC_FP32
+    head = measure_mlp(prec, args, rank, world, allreduce)
     extra = {}
     if rank == 0 and world == 1 and args.prec == "bf16" and not args.no_fp32:
-        # the same configuration in fp32 (the reference's precision), same step count
-        e32, _, _, _ = build(_lib.PREC_FP32, args.batch, 0, 1)
-        e32.capture()
-        extra["fp32_value"] = round(args.steps * args.batch / time_steps(e32, args.steps,
-                                                                          args.warmup), 1)
-        del e32
-        torch.cuda.empty_cache()
+        # the same configuration in fp32 (the reference's precision: the entry whose posteriors
+        # meet north_star's 1e-4), measured the same way, with its own roofline and timeline
+        extra["fp32_entry"] = measure_mlp(_lib.PREC_FP32, args, 0, 1, None)
+        extra["fp32_value"] = extra["fp32_entry"]["value"]
+        if not args.no_cpu_baseline:
+            extra["fp32_entry"].update(parity_leg(_lib.PREC_FP32, args.batch))
     sweep = {}
     if rank == 0 and world == 1 and not args.no_batch_sweep:
         sweep = batch_sweep(prec)
@@ -410,47 +490,30 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         extra.update(parity_leg(prec, args.batch))
     if rank == 0:
-        is_gemm = "gemm" in label
-        # MFMA-bound only where the launch's arithmetic intensity exceeds the machine balance
-        balance = MFMA_PEAK_TFLOPS[args.prec] * 1e12 / (HBM_PEAK_GBS * 1e9)
-        if is_gemm and per_launch_fl / max(per_launch_nb, 1.0) > balance:
-            bound, peak, unit = "mfma", MFMA_PEAK_TFLOPS[args.prec], "TFLOP/s"
-            achieved = per_launch_fl / (avg_ms * 1e-3) / 1e12
-        else:
-            bound, peak, unit = "hbm", HBM_PEAK_GBS, "GB/s"
-            achieved = per_launch_nb / (avg_ms * 1e-3) / 1e9
-        frames = args.steps * args.batch * world
         res = {
             "metric": "acoustic frames/sec (train)",
-            "value": round(frames / dt, 1),
+            "value": head["value"],
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.prec,
             "data": "synthetic TIMIT-shaped fMLLR chunk (740 utts x U[150,450] frames x 40 dims, "
                     "context +-5, GPU-prepared), random-init weights",
-            "config": {"workload": "TIMIT_baselines MLP 440-5x1024-{1928,48} (TIMIT_MLP_fmllr.cfg), "
-                                   "batch_size_train=128, dropout 0.15, SGD body + RMSprop heads",
+            "config": {"workload": WORKLOADS["c2"],
                        "global_batch": args.batch * world, "parallelism": "dp%d" % world,
-                       "chunk_frames_per_rank": chunk.n_rows},
-            "roofline": {"kernel": label, "labels": sorted(d["labels"]), "bound": bound,
-                         "achieved": round(achieved, 2),
-                         "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-                         "traffic": traffic, "avg_launch_us": round(avg_ms * 1e3, 3),
-                         "launches_per_step": cnt,
-                         "algorithmic_bytes_per_launch": per_launch_nb,
-                         "algorithmic_flops_per_launch": per_launch_fl},
-            "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
-                                  sorted(agg.items(), key=lambda kv: -kv[1][1])},
+                       "chunk_frames_per_rank": head["chunk_frames_per_rank"]},
+            "roofline": head["roofline"],
+            "launches_per_step": head["launches_per_step"],
+            "step_breakdown_us": head["step_breakdown_us"],
             "batch_sweep_frames_per_s": sweep,
             "sequence_configs": seq,
-            "chunk_prep_s": round(prep_s, 3),
-            "mean_loss": round(loss_sum / max(1, n_done), 4),
+            "chunk_prep_s": head["chunk_prep_s"],
+            "mean_loss": head["mean_loss"],
         }
         res.update(extra)
         if not args.no_cpu_baseline and world == 1:

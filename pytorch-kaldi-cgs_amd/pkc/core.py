@@ -94,7 +94,8 @@ def _read_features(fea_scp, fea_opts, output_folder):
 
 def _read_labels(lab_folder, lab_opts, output_folder):
     """``gunzip -c ali*.gz | <lab_opts> final.mdl ark:- ark:-|`` (data_io.py:19-21); a
-    pre-converted ``<lab_folder>/<lab_opts-tag>.ark`` binary int-vector ark is read directly."""
+    pre-converted ``<lab_folder>/<lab_opts-tag>.ark`` int-vector ark (binary or text) is read
+    directly."""
     tag = "pdf" if "pdf" in lab_opts else "phones"
     pre = os.path.join(lab_folder, "ali_%s.ark" % tag)
     if os.path.exists(pre):
@@ -252,8 +253,6 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         eng = Engine(nns, arch_opts, lines, fea_cols, lab_names, batch=batch_size, seed=eseed,
                      train=(to_do == "train"), max_len=int(lens.max()), grad_scale=1.0 / ws_eff,
                      prec=prec)
-        if ws_eff > 1:                  # frame-weighted sequence DP (pkc.dist.frame_weight)
-            eng.frame_weight = lambda rows: DP.frame_weight(rows, device=eng.dev)
         for net_name in nns:
             pt = config[arch_dict[net_name][0]]["arch_pretrain_file"]
             if pt != "none" and to_do == "train":
@@ -264,6 +263,9 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
                        sentences=DP.shard_sentences(chunk.end_index, rank, ws_eff))
         if ws_eff > 1:
             eng.n_batches = DP.agree_min(eng.n_batches, device=eng.dev)
+            if to_do == "train":        # frame-weighted sequence DP: the chunk's loss scales
+                eng.frame_scales = DP.frame_weights(eng.sent_len, eng.B, eng.n_batches,
+                                                    device=eng.dev)
         post_files, priors = {}, {}
         if to_do == "forward":
             for oi, out in enumerate(forward_outs):

@@ -24,7 +24,7 @@ def write_mat_path(path, m, key="", append=False):
 
 
 def read_mat_ark_path(path):
-    """Binary FM/DM/CM ark -> generator of (key, float32 matrix) (data_io.py:645-766)."""
+    """Binary FM/DM/CM or text ark -> generator of (key, float32 matrix) (data_io.py:645-766)."""
     lib = L.lib()
     n = lib.pkc_ark_index(path.encode(), None, None, None, 0, None, 0)
     if n == L.PKC_ERR_UNSUPPORTED:         # compressed matrices: parse the bytes (pkc_ark_decode_cm)
@@ -46,15 +46,50 @@ def read_mat_ark_path(path):
         yield keys[i].decode("latin1"), out
 
 
+def _readline(buf, pos):
+    """The bytes of buf from pos through the next newline (file.readline), and the new position."""
+    nl = buf.find(b"\n", pos)
+    end = len(buf) if nl < 0 else nl + 1
+    return buf[pos:end], end
+
+
+def _read_mat_ascii(buf, pos):
+    """Text matrix body after its " [" (data_io.py:714-726, reached from read_mat :680-681): the
+    rest of the "[" line is skipped, then one row per line until a line whose last token is "]";
+    tokens parsed as float32 (numpy's str -> float32, as there).  Returns (matrix, new pos)."""
+    _, pos = _readline(buf, pos)
+    rows = []
+    while True:
+        line, pos = _readline(buf, pos)
+        if not line:
+            raise ValueError("text matrix ends before its ']'")
+        arr = line.decode().strip().split()
+        if not arr:
+            continue
+        if arr[-1] != "]":
+            rows.append(np.array(arr, dtype=np.float32))
+        else:
+            rows.append(np.array(arr[:-1], dtype=np.float32))
+            return np.vstack(rows), pos
+
+
 def parse_mat_ark_bytes(buf):
-    """Binary FM/DM ark held in memory (e.g. a Kaldi pipe's stdout) -> [(key, float32 matrix)]."""
+    """FM / DM / CM binary or text (`ark,t:`) matrix ark held in memory (e.g. a Kaldi pipe's
+    stdout) -> [(key, float32 matrix)]; text and binary entries may alternate (read_mat decides per
+    entry, data_io.py:669-684)."""
     out, pos = [], 0
     while pos < len(buf):
+        if not buf[pos:].strip():            # read_key: an empty key ends the ark (:399)
+            break
         sp = buf.index(b" ", pos)
         key = buf[pos:sp].decode("latin1").strip()
         pos = sp + 1
+        if buf[pos:pos + 2] == b" [":
+            m, pos = _read_mat_ascii(buf, pos + 2)
+            out.append((key, m))
+            continue
         if buf[pos:pos + 2] != b"\0B":
-            raise ValueError("only binary matrices are supported")
+            raise ValueError("%s: neither a binary matrix nor a text one (' [')" % key)
         hdr = buf[pos + 2:pos + 5]
         if hdr == b"CM ":
             out.append((key, decode_cm(buf, pos + 5)))
@@ -93,20 +128,33 @@ def decode_cm(buf, off):
 
 
 def read_vec_int_ark_path(path):
-    """Binary int32-vector ark (alignments after ali-to-pdf) -> generator (data_io.py:412-455)."""
+    """Binary or text int32-vector ark (alignments after ali-to-pdf) -> generator
+    (data_io.py:412-455)."""
     with open(path, "rb") as f:
         buf = f.read()
     return parse_vec_int_ark_bytes(buf)
 
 
 def parse_vec_int_ark_bytes(buf):
+    """Binary or text int-vector ark -> generator of (key, int32 vector) (read_vec_int,
+    data_io.py:431-455: the text form is the rest of the line, optional "[" / "]" tokens removed)."""
     pos = 0
     while pos < len(buf):
+        if not buf[pos:].strip():
+            break
         sp = buf.index(b" ", pos)
         key = buf[pos:sp].decode("latin1").strip()
         pos = sp + 1
         if buf[pos:pos + 2] != b"\0B":
-            raise ValueError("only binary int vectors are supported")
+            line, pos = _readline(buf, pos)
+            arr = line.decode().strip().split()
+            try:                              # :448-452 (a missing "[" leaves a "]" in place)
+                arr.remove("[")
+                arr.remove("]")
+            except ValueError:
+                pass
+            yield key, np.array(arr, dtype=np.int64).astype(np.int32)
+            continue
         n = struct.unpack("<i", buf[pos + 3:pos + 7])[0]
         pos += 7
         rec = np.frombuffer(buf[pos:pos + 5 * n], dtype=[("size", "i1"), ("value", "<i4")])

@@ -76,13 +76,31 @@ def agree_min(n, device=None):
 def frame_weight(rows, device=None):
     """This rank's share of the rows of the global batch (its loss scale under sequence DP: the
     padded T_r * B rows differ between ranks, so 1/R would weight a short batch's rows more than a
-    long one's).  One scalar all-reduce per step."""
+    long one's).  One scalar all-reduce; the engine takes a whole chunk's scales at once
+    (frame_weights)."""
     rank, ws = world()
     if ws == 1:
         return 1.0
     t = torch.tensor([float(rows)], dtype=torch.float64, device=device)
     dist.all_reduce(t)
     return float(rows) / float(t.item())
+
+
+def frame_weights(sent_len, B, n_batches, device=None):
+    """Every batch's loss scale for this rank over a whole chunk of sequence DP: batch i of rank r
+    is padded to T_r[i] = the longest of its B sentences, so its rows are T_r[i] * B and its share
+    of the global batch i is T_r[i] / sum_r' T_r'[i] (see frame_weight).  The T's follow from the
+    sentence lengths alone (the random left padding does not change them), so ONE all-reduce per
+    chunk replaces the per-step scalar all-reduce and its host sync.  Returns float64 (n_batches,)."""
+    lens = np.asarray(sent_len, dtype=np.int64)[:n_batches * B].reshape(n_batches, B)
+    T = lens.max(1).astype(np.float64)
+    rank, ws = world()
+    if ws == 1:
+        return np.ones(n_batches)
+    t = torch.zeros((ws, n_batches), dtype=torch.float64, device=device)
+    t[rank] = torch.from_numpy(T).to(t.device)
+    dist.all_reduce(t)
+    return T / t.sum(0).cpu().numpy()
 
 
 def sum_scalars(vals, device=None):

@@ -397,9 +397,10 @@ class Engine:
         self.train = train
         self.seed = int(seed)
         self.grad_scale = float(grad_scale)    # 1/world_size under data parallelism
-        # sequence DP: callable(rows of this rank's batch) -> this rank's loss scale (set by the
-        # caller, pkc.dist.frame_weight), recomputed every step; None: the fixed grad_scale
-        self.frame_weight = None
+        # sequence DP: this rank's loss scale of every batch of the bound chunk (its share of the
+        # global batch's rows, pkc.dist.frame_weights: one collective per chunk, none per step),
+        # indexed by batch; None: the fixed grad_scale
+        self.frame_scales = None
         # SyncBN (pkc.dist.SyncBatchNorm): the MLP layers' BatchNorm statistics over all ranks
         self.sync_bn = sync_bn
         self.prof = None                       # profile mode: list of per-launch events
@@ -1063,6 +1064,7 @@ class Engine:
         if T > self.max_len:
             raise ValueError("batch of %d frames exceeds max_len %d" % (T, self.max_len))
         lefts = np.array([rng.randint(0, T - int(l)) for l in lens], dtype=np.int64)
+        self.batch_i = i0 // self.B
         self.snt += self.B
         return begs.astype(np.int64), lens.astype(np.int64), lefts, T
 
@@ -1710,8 +1712,11 @@ class Engine:
             if cut_wait > 0:
                 cut_wait -= 1
             if cut_node is not None and cut_node in pend_nodes:
-                # a split-K dW becomes final one launch later (its slab sum)
-                cut_wait = 1 if getattr(cut_node, "sdw", 1) > 1 else 0
+                # a split-K dW becomes final one launch later (its slab sum).  Output heads do not
+                # flush, so sibling heads can share the cut node's launch: wait for the slowest of
+                # them (an unsplit cut head beside a split one would otherwise ship the split
+                # head's stale dW in the first bucket)
+                cut_wait = 1 if any(getattr(p, "sdw", 1) > 1 for p in pend_nodes) else 0
                 cut_node = None
             if cut_wait == 0:
                 cut_wait = -1
@@ -1849,11 +1854,11 @@ class Engine:
         if self.seq:
             batch = batch or self.next_seq_batch()
             self._set_rows(batch)
-            if self.frame_weight is not None:
+            if self.frame_scales is not None:
                 # sequence DP: rank r's padded batch has T_r * B rows; scale its mean loss by its
                 # share of all ranks' rows, so the summed gradient is that of the mean over every
                 # row of the global batch, not the mean of unequal batch means
-                self.grad_scale = self.frame_weight(self.M)
+                self.grad_scale = float(self.frame_scales[self.batch_i])
             self._train_step_kernels(allreduce, batch)
             self.ctr.add_(1)           # step counter of the dropout RNG streams
         elif self.graph is not None:

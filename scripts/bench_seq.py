@@ -62,7 +62,11 @@ def rec_opts(cfg_name):
     return "LSTM", d, (16 if cfg_name == "c4" else 12)
 
 
-def build(cfg_name, seed=2234):
+def build(cfg_name, seed=2234, rank=0, world=1):
+    """Engine + nets of `cfg_name` bound to a synthetic length-sorted chunk of 64 * B sentences.
+    Data parallelism (world > 1): every rank builds the same model from the same seeds and draws
+    its OWN chunk (weak scaling: B sentences per rank and step), its loss scaled per batch by its
+    share of the global batch's padded rows (pkc.dist.frame_weights, one collective per chunk)."""
     import pkc.neural_networks as NN
     from pkc.engine import Engine, parse_model
     cls, ropts, B = rec_opts(cfg_name)
@@ -87,18 +91,30 @@ def build(cfg_name, seed=2234):
     for n in nets.values():
         n.cuda().train()
     opts = {"rnn": cfg["a1"], "head": cfg["a2"], "mono": cfg["a3"]}
-    rs = np.random.RandomState(seed)
+    rs = np.random.RandomState(seed + 1000 * rank)
     lo, hi = (100, 200) if cfg_name == "c5" else (150, 450)
     n_utt = 64 * B
     lens = np.sort(rs.randint(lo, hi + 1, size=n_utt))          # length-sorted, as the loader
     end = np.cumsum(lens)
     N = int(end[-1])
-    feats = torch.randn(N, 440, device="cuda")
-    labs = torch.stack([torch.randint(0, 1928, (N,), device="cuda"),
-                        torch.randint(0, 48, (N,), device="cuda")], 1).to(torch.int32).contiguous()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed + 1000 * rank)
+    feats = torch.randn(N, 440, device="cuda", generator=g)
+    labs = torch.stack([torch.randint(0, 1928, (N,), device="cuda", generator=g),
+                        torch.randint(0, 48, (N,), device="cuda", generator=g)],
+                       1).to(torch.int32).contiguous()
+    # the chunk's longest sentence over all ranks sizes the buffers (the same on every rank)
+    max_len = int(lens.max())
+    if world > 1:
+        from pkc import dist as DP
+        max_len = -DP.agree_min(-max_len, device="cuda")
     eng = Engine(nets, opts, parse_model(model), {"fea": (0, 440)}, ["lab_cd", "lab_mono"],
-                 batch=B, max_len=int(lens.max()), seed=seed)
+                 batch=B, max_len=max_len, seed=seed + rank, grad_scale=1.0 / world)
     eng.bind_chunk(feats, labs, N, end_index=end)
+    if world > 1:
+        from pkc import dist as DP
+        eng.n_batches = DP.agree_min(eng.n_batches, device="cuda")
+        eng.frame_scales = DP.frame_weights(eng.sent_len, eng.B, eng.n_batches, device="cuda")
     return eng, nets, B
 
 
@@ -121,8 +137,11 @@ def alg_flops_per_row(nets):
     return per_dir_row, head
 
 
-def run(cfg_name, steps, warmup):
-    eng, nets, B = build(cfg_name)
+def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1):
+    """Times `steps` sentence batches after `warmup` (barrier + synchronize on both sides of the
+    timed region; the max over ranks).  frames_per_s is the whole job's: every rank's real frames
+    over that time."""
+    eng, nets, B = build(cfg_name, rank=rank, world=world)
     rng = random.Random(7)
     # sample the batches across the length-sorted chunk (short and long sentences alike)
     nb = eng.n_batches
@@ -131,23 +150,36 @@ def run(cfg_name, steps, warmup):
     for i in order:
         eng.snt = i * B
         batches.append(eng.next_seq_batch(rng))
-    for b in batches[:warmup]:
-        eng.train_step(batch=b)
-    torch.cuda.synchronize()
+    for i, b in zip(order[:warmup], batches[:warmup]):
+        eng.batch_i = i                   # the frame weight of batch i (data parallelism)
+        eng.train_step(allreduce, batch=b)
     frames, tsteps = 0, 0
-    t0 = time.time()
-    for b in batches[warmup:]:
-        eng.train_step(batch=b)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i, b in zip(order[warmup:], batches[warmup:]):
+        eng.batch_i = i
+        eng.train_step(allreduce, batch=b)
         frames += int(b[1].sum())
         tsteps += int(b[3])
     torch.cuda.synchronize()
-    dt = time.time() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        from pkc import dist as DP
+        t = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+        frames, tsteps = DP.sum_scalars([frames, tsteps], device="cuda")
+        frames, tsteps = int(frames), tsteps / world   # padded lengths vary: the mean over ranks
     specs = nets["rnn"].layer_specs()
     nl = len(specs)
     dirs = 2 if specs[0]["bidir"] else 1
     per_row, head = alg_flops_per_row(nets)
-    flops = tsteps * B * (dirs * per_row + head)          # padded rows, as the reference computes
-    return {"config": cfg_name, "batch_sentences": B, "steps": steps,
+    flops = world * tsteps * B * (dirs * per_row + head)  # padded rows, as the reference computes
+    return {"config": cfg_name, "batch_sentences": B, "steps": steps, "n_ranks": world,
             "frames_per_s": frames / dt, "ms_per_step": dt * 1e3 / steps,
             "us_per_time_step_per_layer_fwd_bwd": dt * 1e6 / (tsteps * nl),
             "mean_T": tsteps / steps, "alg_tflops_per_s": flops / dt / 1e12,

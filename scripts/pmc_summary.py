@@ -1,4 +1,4 @@
-"""Summarise the two PMC passes of scripts/gpu_pmc.sh: the last N dispatches of each pass are
+"""Summarise the two PMC passes of scripts/gpu.sh pmc: the last N dispatches of each pass are
 the replayed dominant launch; traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB per dispatch (gfx950
 FETCH_SIZE counts half of a wide coalesced read, MI355X_MICROARCH.md HBM section)."""
 import csv

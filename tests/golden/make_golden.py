@@ -390,6 +390,50 @@ def gen_cm():
     np.savez_compressed(os.path.join(OUT, "cm.npz"), **out)
 
 
+def text_ark_inputs():
+    """Kaldi text-form arks (`ark,t:` — copy-feats / copy-int-vector output, kaldi-matrix.cc
+    Matrix::Write text branch): float matrices as "key  [\n  v v v \n  v v v ]\n", int vectors as
+    "key v v v \n", a bracketed int vector, formats %g-style with exponents and negative zero; plus a
+    mixed ark (text entries between binary FM / DM ones)."""
+    import struct
+    rs = np.random.RandomState(23)
+    mats = []
+    txt = b""
+    for i, (r, c) in enumerate([(3, 4), (1, 6), (5, 2)]):
+        m = (rs.randn(r, c) * 10.0 ** rs.randint(-6, 4, size=(r, c))).astype(np.float32)
+        m[0, 0] = -0.0
+        rows = ["  " + " ".join(("%g" if (j + k) % 2 else "%.7g") % v for k, v in enumerate(row))
+                for j, row in enumerate(m)]
+        txt += ("utt%d  [\n" % i + " \n".join(rows) + " ]\n").encode()
+        mats.append(m)
+    vtxt = b"".join(("a%d " % i + " ".join(str(v) for v in rs.randint(0, 1928, size=n)) + " \n")
+                    .encode() for i, n in enumerate((5, 1, 9)))
+    vtxt += b"b0 [ 3 1 4 1 5 ]\n"
+    fm = rs.randn(2, 3).astype(np.float32)
+    dm = rs.randn(3, 2)
+    mixed = (b"bin0 \0BFM \x04" + struct.pack("<i", 2) + b"\x04" + struct.pack("<i", 3) + fm.tobytes()
+             + b"txt0  [\n  1.5 -2 3e-07 \n  4 5 6 ]\n"
+             + b"bin1 \0BDM \x04" + struct.pack("<i", 3) + b"\x04" + struct.pack("<i", 2) + dm.tobytes())
+    return txt, vtxt, mixed
+
+
+def gen_text_ark():
+    """Text-form arks read by the reference's read_mat_ark / read_vec_int_ark (data_io.py:645-726,
+    412-455): the input bytes and the reference's decoded matrices / vectors."""
+    out = {}
+    for tag, blob in zip(("mat", "vec", "mixed"), text_ark_inputs()):
+        path = os.path.join(_TMP, "text_%s.ark" % tag)
+        with open(path, "wb") as f:
+            f.write(blob)
+        out[tag + "_bytes"] = np.frombuffer(blob, dtype=np.uint8).copy()
+        reader = data_io.read_vec_int_ark if tag == "vec" else data_io.read_mat_ark
+        items = list(reader("ark:" + path, _TMP))
+        out[tag + "_keys"] = np.array([k for k, _ in items])
+        for i, (k, v) in enumerate(items):
+            out["%s_%d" % (tag, i)] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, "text_ark.npz"), **out)
+
+
 def gen_gru():
     from cases import GRU_CASES
     out = {}
@@ -497,7 +541,7 @@ if __name__ == "__main__":
             kind, _, v = a.partition(":")
             {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru(),
              "cm": lambda _v: gen_cm(), "run_nn": gen_run_nn,
-             "kmeans": lambda _v: gen_kmeans()}[kind](v)
+             "kmeans": lambda _v: gen_kmeans(), "text_ark": lambda _v: gen_text_ark()}[kind](v)
         sys.exit(0)
     gen_loader()
     gen_hcgs()
@@ -510,6 +554,7 @@ if __name__ == "__main__":
     gen_gru()
     gen_cm()
     gen_ark()
+    gen_text_ark()
     for c in RUN_NN_CASES:
         gen_run_nn(c)
     total = sum(os.path.getsize(os.path.join(OUT, f)) for f in os.listdir(OUT))

@@ -185,3 +185,19 @@ def test_dp_frame_weighted_gradient_equals_full_batch():
     assert (w0, w1) == (0.75, 0.25)
     np.testing.assert_array_equal(g0, g1)
     np.testing.assert_allclose(g0, full, rtol=1e-5, atol=1e-8)
+
+
+def _frame_weights(rank, ws, lens, B):
+    from pkc import dist as DP
+    return DP.frame_weights(lens[rank], B, 2).tolist()
+
+
+def test_frame_weights_one_collective_per_chunk():
+    """pkc.dist.frame_weights: every batch's loss scale of a chunk from the sentence lengths
+    alone (T_r[i] = the longest of rank r's i-th B sentences; scale T_r[i] / sum_r T_r[i]), in one
+    all-reduce at bind time instead of one host-blocking scalar all-reduce per step."""
+    lens = [[5, 9, 3, 3, 7, 2, 30], [4, 4, 10, 1, 1, 1, 1]]       # B = 3: T = [9, 7] and [10, 1]
+    w0, w1 = _run(_frame_weights, 2, lens, 3)
+    np.testing.assert_allclose(w0, [9 / 19, 7 / 8], rtol=1e-15)
+    np.testing.assert_allclose(w1, [10 / 19, 1 / 8], rtol=1e-15)
+    assert _frame_weights(0, 1, lens, 3) == [1.0, 1.0]

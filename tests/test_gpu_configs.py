@@ -28,14 +28,18 @@ DEV = "cuda"
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
-def build_pair(name, seed=2234):
-    """pkc nets + oracle nets (same state dict) for bench_seq config `name`."""
+def build_pair(name, seed=2234, drop=None):
+    """pkc nets + oracle nets (same state dict) for bench_seq config `name` (drop: override the
+    recurrent dropout rate of every layer)."""
     import configparser
 
     import bench_seq as BS
     import pkc.neural_networks as NN
     from oracle import nets as ON
     cls, ropts, B = BS.rec_opts(name)
+    if drop is not None:
+        ropts = {k: (",".join([drop] * len(v.split(","))) if k.endswith("_drop") else v)
+                 for k, v in ropts.items()}
     cfg = configparser.ConfigParser()
     cfg["a1"] = dict(ropts, arch_name="rnn", **BS.OPT)
     head = dict(dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False", arch_name="head",

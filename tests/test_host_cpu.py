@@ -237,6 +237,35 @@ def test_product_cm_decode_matches_reference(tmp_path):
         np.testing.assert_array_equal(m, g["mat%d" % i])
 
 
+@pytest.mark.parametrize("tag", ["mat", "vec", "mixed"])
+def test_product_text_ark_matches_reference(tag, tmp_path):
+    """Text-form (`ark,t:`) Kaldi arks (data_io.py:680-681 + 714-726 for matrices, 446-453 for int
+    vectors), and a mixed ark whose text entries sit between binary FM / DM ones: the pkc readers
+    (file path and pipe bytes) return exactly what the reference's read_mat_ark /
+    read_vec_int_ark returned on the same bytes (golden text_ark.npz, float32 values bit-equal)."""
+    from pkc import data_io as D
+    g = G("text_ark.npz")
+    blob = g[tag + "_bytes"].tobytes()
+    keys = list(g[tag + "_keys"])
+    path = str(tmp_path / "t.ark")
+    open(path, "wb").write(blob)
+    if tag == "vec":
+        runs = [list(D.read_vec_int_ark_path(path)), list(D.parse_vec_int_ark_bytes(blob))]
+    else:
+        runs = [list(D.read_mat_ark_path(path)), D.parse_mat_ark_bytes(blob)]
+    for got in runs:
+        assert [k for k, _ in got] == keys
+        for i, (_, v) in enumerate(got):
+            ref = g["%s_%d" % (tag, i)]
+            if tag == "vec":
+                assert v.dtype == np.int32
+                np.testing.assert_array_equal(v, ref)
+            else:
+                assert v.dtype == np.float32
+                np.testing.assert_array_equal(v, ref.astype(np.float32))
+                assert np.signbit(v).tolist() == np.signbit(ref.astype(np.float32)).tolist()
+
+
 @pytest.mark.parametrize("tag", ["a", "b", "c", "d"])
 def test_product_kmeans_pattern_search_matches_reference(tag):
     """pkc.cgs.kmeans_patterns vs sparsity.find_top_k_by_kmeans (sparsity.py:999-1049), both with
