@@ -27,12 +27,15 @@ import torch.distributed as dist  # noqa: E402
 
 
 def chunk(name, steps, world):
-    """A length-sorted chunk of world * steps * B short sentences (T in [8, 20]), 440-dim
+    """A length-sorted chunk of world * steps * B short sentences (T in [8, 22]), 440-dim
     features, cd / mono labels; the same on every rank."""
     import bench_seq as BS
     B = BS.rec_opts(name)[2]
     rs = np.random.RandomState(29)
     lens = np.sort(rs.randint(8, 21, size=world * steps * B))
+    # the last sentence of every global batch (rank world-1's) 2 frames longer: unequal padded
+    # T per rank in every step, whatever the draw
+    lens[world * B - 1::world * B] += 2
     end = np.cumsum(lens)
     X = rs.randn(end[-1], 440).astype(np.float32)
     lab = np.stack([rs.randint(0, 1928, end[-1]), rs.randint(0, 48, end[-1])], 1).astype(np.int32)
