@@ -104,38 +104,50 @@ def build(prec, batch, rank, world, seed=2234):
 
 
 def cpu_baseline(batch, seconds=12.0):
-    """The oracle (reference algorithm restated in PyTorch-CPU eager) on the host cores."""
+    """The oracle (reference algorithm restated in PyTorch-CPU eager) on the host cores, and on
+    one core (cores_1)."""
     from oracle import nets as ON
     from oracle import run as OR
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     threads = min(threads, os.cpu_count())
-    torch.set_num_threads(threads)
     cfg = c1_cfg()
-    torch.manual_seed(0)
-    nets, opts = {}, {}
-    for sec, inp in DIMS:
-        o = cfg[sec]
-        nets[o["arch_name"]] = ON.MLP(o, inp).train()
-        opts[o["arch_name"]] = ON.make_optimizer(nets[o["arch_name"]].parameters(), o)
     lines = OR.parse_model(cfg["model"]["model"])
     rs = np.random.RandomState(1)
     inp = torch.from_numpy(np.concatenate([rs.randn(batch, 440), rs.randint(0, 48, (batch, 2))],
                                           1).astype(np.float32))
-    seq = {k: False for k in nets}
     fc, lc = {"fmllr": (0, 440)}, {"lab_cd": 440, "lab_mono": 441}
-    for _ in range(2):
-        OR.train_step(lines, nets, opts, seq, fc, lc, inp)
-    n, t0 = 0, time.time()
-    while time.time() - t0 < seconds:
-        OR.train_step(lines, nets, opts, seq, fc, lc, inp)
-        n += 1
-    dt = time.time() - t0
-    out = {"value": round(n * batch / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+
+    def rate(nthreads, secs):
+        torch.set_num_threads(nthreads)
+        torch.manual_seed(0)
+        nets, opts = {}, {}
+        for sec, inp_dim in DIMS:
+            o = cfg[sec]
+            nets[o["arch_name"]] = ON.MLP(o, inp_dim).train()
+            opts[o["arch_name"]] = ON.make_optimizer(nets[o["arch_name"]].parameters(), o)
+        seq = {k: False for k in nets}
+        for _ in range(2):
+            OR.train_step(lines, nets, opts, seq, fc, lc, inp)
+        n, t0 = 0, time.time()
+        while n == 0 or time.time() - t0 < secs:
+            OR.train_step(lines, nets, opts, seq, fc, lc, inp)
+            n += 1
+        dt = time.time() - t0
+        return n * batch / dt, n, dt
+
+    v, n, dt = rate(threads, seconds)
+    v1, n1, dt1 = rate(1, seconds / 2)
+    torch.set_num_threads(threads)
+    out = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
            "sample": "%d training steps of the C1 MLP at B=%d (oracle restatement, torch-CPU eager, "
-                     "%d threads, %.1f s)" % (n, batch, threads, dt)}
+                     "%d threads, %.1f s)" % (n, batch, threads, dt),
+           "cores_1": {"value": round(v1, 1), "unit": "frames/s", "cores": 1,
+                       "sample": "%d training steps at B=%d, 1 thread, %.1f s" % (n1, batch, dt1)}}
     try:   # the restatement's speed relative to the reference itself (scripts/cpu_calibrate.py)
-        cal = json.load(open(os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")))["results"]
-        out["calibration_port_over_reference"] = {k: v["oracle_over_reference"] for k, v in cal.items()}
+        cal = json.load(open(os.path.join(ROOT, "profiles", "r03_cpu_calibration.json")))
+        out["calibration_port_over_reference"] = {
+            "mlp": {k: v["oracle_over_reference"] for k, v in cal["results"].items()},
+            "ligru_seq": {k: v["oracle_over_reference"] for k, v in cal["sequence"]["results"].items()}}
     except (OSError, ValueError, KeyError):
         pass
     return out
@@ -481,8 +493,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_seq_configs:
         # BASELINE configs C3-C5: C3 (the largest single-GPU config) measured like the headline,
         # C4 / C5 informational
-        seq["c3"] = seq_entry("c3", max(20, args.steps), 3, not args.no_cpu_baseline,
-                              args.cpu_seconds)
+        seq["c3"] = seq_entry("c3", max(20, args.steps), 3, False, 0)
         torch.cuda.empty_cache()
         for c in ("c4", "c5"):
             seq[c] = seq_entry(c, 8, 2, False, 0)
@@ -518,6 +529,10 @@ def main():
         res.update(extra)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.batch, args.cpu_seconds)
+            sys.path.insert(0, os.path.join(ROOT, "scripts"))
+            import bench_seq
+            for c, e in seq.items():          # after every timed region: CPU legs last
+                e["cpu_baseline"] = bench_seq.cpu_baseline(c, seconds=args.cpu_seconds)
         print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -831,11 +831,14 @@ struct SCase {};
 
 static int pick_vw(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
 
-// 16-row step tiles up to 2B <= PKC_RNN_ROWS16 rows (default 16; 0: always the 32-row tiles)
+// 16-row step tiles up to 2B <= PKC_RNN_ROWS16 rows (default 16; 0: always the 32-row tiles).
+// Clamped to 16: a 16-row tile holds rows [16 y, 16 y + 16) only, so with more rows the grid would
+// have two row tiles — and the quantised-h step takes var (max |h_{t-1}|) from ONE tile's registers.
 static bool rows16(int B2) {
   static const int lim = [] {
     const char* v = getenv("PKC_RNN_ROWS16");
-    return v ? atoi(v) : 16;
+    const int l = v ? atoi(v) : 16;
+    return l < 16 ? l : 16;
   }();
   return B2 <= lim;
 }

@@ -403,6 +403,18 @@ class Engine:
         self.frame_scales = None
         # SyncBN (pkc.dist.SyncBatchNorm): the MLP layers' BatchNorm statistics over all ranks
         self.sync_bn = sync_bn
+        if sync_bn is not None:
+            # SyncBN covers the BatchNorm of the MLP layers (the DP parity recipe);
+            # input-normalisation BatchNorms and the recurrent layers' gate BatchNorms keep
+            # per-rank statistics: refuse a model whose parity would silently not hold
+            for a, net in nets.items():
+                if getattr(net, "seq_model", False) and any(
+                        sp.get("bn") for sp in net.layer_specs()):
+                    raise NotImplementedError("sync_bn: %s is recurrent with BatchNorm (its gate "
+                                              "statistics are per rank)" % a)
+                if any(sp.get("kind") == "bn" for sp in (net.input_norm_specs() if hasattr(net, "input_norm_specs") else [])):
+                    raise NotImplementedError("sync_bn: %s has an input BatchNorm (per-rank "
+                                              "statistics)" % a)
         self.prof = None                       # profile mode: list of per-launch events
         self.F = max(c1 for _, c1 in fea_cols.values())
         self.fea_cols = fea_cols

@@ -186,16 +186,22 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1):
             "alg_gflop_per_step": flops / steps / 1e9}
 
 
-def cpu_baseline(cfg_name, seconds=10.0, T=120):
-    """The oracle's eager torch-CPU restatement of the same training step (the reference's
-    per-time-step algorithm, neural_networks.py:1523-1599 / 1077-1097) on the host cores: a
-    bounded sample of sentence batches of length T."""
+def gpu_like_T(cfg_name, seed=5):
+    """A padded batch length drawn like the GPU's: the longest of B sentence lengths from the
+    config's distribution (U[150, 450]; C5 U[100, 200])."""
+    _, _, B = rec_opts(cfg_name)
+    lo, hi = (100, 200) if cfg_name == "c5" else (150, 450)
+    return int(np.random.RandomState(seed).randint(lo, hi + 1, size=B).max())
+
+
+def _cpu_rate(cfg_name, T, threads, seconds):
+    """(frames/s, steps, seconds) of the oracle's eager torch-CPU restatement of the training step
+    (the reference's per-time-step algorithm, neural_networks.py:1523-1599 / 1077-1097) on one
+    padded batch of B sentences x T frames; at least one timed step."""
     import configparser
 
     from oracle import nets as ON
     from oracle import run as OR
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    threads = min(threads, os.cpu_count())
     torch.set_num_threads(threads)
     cls, ropts, B = rec_opts(cfg_name)
     cfg = configparser.ConfigParser()
@@ -208,6 +214,10 @@ def cpu_baseline(cfg_name, seconds=10.0, T=120):
     torch.manual_seed(0)
     np.random.seed(0)
     rnn = getattr(ON, cls)(cfg["a1"], 440)
+    if cfg_name == "c5":
+        pset = np.load(os.path.join(ROOT, "tests", "golden", "quant.npz"),
+                       allow_pickle=False)["pattern_set"]
+        rnn.pattern_kernels = pset.reshape(16, 8, 8)
     nets = {"rnn": rnn, "head": ON.MLP(cfg["a2"], rnn.out_dim), "mono": ON.MLP(cfg["a3"], rnn.out_dim)}
     opts = {k: ON.make_optimizer(nets[k].parameters(), cfg[s]) for k, s in
             (("rnn", "a1"), ("head", "a2"), ("mono", "a3"))}
@@ -221,18 +231,48 @@ def cpu_baseline(cfg_name, seconds=10.0, T=120):
     inp = torch.from_numpy(np.concatenate([rs.randn(T, B, 440), rs.randint(0, 48, (T, B, 2))],
                                           2).astype(np.float32))
     seq = {"rnn": True, "head": False, "mono": False}
-    OR.train_step(lines, nets, opts, seq, {"fea": (0, 440)}, {"lab_cd": 440, "lab_mono": 441},
-                  inp, T, B)
-    n, t0 = 0, time.time()
-    while time.time() - t0 < seconds:
+
+    def step():
         OR.train_step(lines, nets, opts, seq, {"fea": (0, 440)}, {"lab_cd": 440, "lab_mono": 441},
                       inp, T, B)
+
+    step()                                   # warm-up (allocations, pattern masks)
+    n, t0 = 0, time.time()
+    while n == 0 or time.time() - t0 < seconds:
+        step()
         n += 1
     dt = time.time() - t0
-    return {"value": round(n * T * B / dt, 1), "unit": "frames/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d training steps of %s (B=%d sentences x T=%d frames, oracle restatement, "
-                      "torch-CPU eager, %d threads, %.1f s)" % (n, cfg_name, B, T, threads, dt)}
+    return n * T * B / dt, n, dt
+
+
+# all-core sample length cap: C4's eager step at the GPU-like T = 381 takes 105 s on 8 threads
+# (its per-frame cost GROWS with T: 58 frames/s there against 122 on ONE thread at T = 24 — every
+# time step's U-gradient accumulation streams the 4 x 1024 x 1024 fp32 U matrices through DRAM), so
+# the bench's bounded sample runs C4 at T = 96; profiles/r03_cpu_seq_baselines.json holds the
+# full-T figures measured in the build container
+T_CAP = {"c4": 96}
+
+
+def cpu_baseline(cfg_name, seconds=10.0, T=None, T1=24):
+    """CPU baseline of a sequence configuration on the host cores: the oracle restatement (kind
+    "port"; its speed against the reference itself: profiles/r03_cpu_calibration.json) on all
+    cores at a padded length drawn like the GPU's (gpu_like_T, capped by T_CAP), and on ONE core
+    (cores_1) at a short batch T1 (one core at T ~ 300 takes minutes per step)."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    threads = min(threads, os.cpu_count())
+    _, _, B = rec_opts(cfg_name)
+    T = T or min(gpu_like_T(cfg_name), T_CAP.get(cfg_name, 10 ** 9))
+    v, n, dt = _cpu_rate(cfg_name, T, threads, seconds)
+    v1, n1, dt1 = _cpu_rate(cfg_name, T1, 1, seconds / 2)
+    torch.set_num_threads(threads)
+    return {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": "%d training steps of %s (B=%d sentences x T=%d frames, T drawn like the "
+                      "GPU's%s, oracle restatement, torch-CPU eager, %d threads, %.1f s)"
+                      % (n, cfg_name, B, T, " and capped" if cfg_name in T_CAP else "", threads,
+                         dt),
+            "cores_1": {"value": round(v1, 1), "unit": "frames/s", "cores": 1,
+                        "sample": "%d training steps (B=%d x T=%d, 1 thread, %.1f s)"
+                                  % (n1, B, T1, dt1)}}
 
 
 def main():

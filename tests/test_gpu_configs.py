@@ -22,6 +22,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN, ROOT
+from quantcheck import assert_few_flips
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -133,6 +134,7 @@ def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta
     eng.sync_state()
     sd_o = onets["rnn"].state_dict()
     wworst = 0.0
+    flips = {}
     for k in nets:
         osd = onets[k].state_dict()
         for pname, v in nets[k].state_dict().items():
@@ -146,6 +148,10 @@ def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta
             if k == "rnn" and name == "c5" and pname.endswith("weight") and len(parts[0]) == 3:
                 # pattern^L: every layer call multiplies all layers' masks in (:876-884, 1226-1237)
                 r = r * onets["rnn"].pattern_masks[parts[0]][int(parts[1])].double() ** len(specs)
+            if quant_beta_bound and pname.endswith("weight") and v.dim() == 2:
+                # 8-bit weights: at most 0.2 % of a matrix on another grid point, one quantum each
+                nf = assert_few_flips(v.cpu().numpy(), r.numpy(), "%s %s" % (name, pname), 2e-3)
+                flips[pname] = nf
             d = (v.cpu().double() - r).norm().item()
             e = d / max(r.norm().item(), 1e-30)
             if quant_beta_bound and ".bias" in pname and pname.startswith("bn"):
@@ -158,8 +164,8 @@ def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta
                 continue
             wworst = max(wworst, e)
             assert d <= w_tol * r.norm().item() + 1e-6, "%s %s %s rel err %.3g" % (name, k, pname, e)
-    print("%s (sparse=%s): posterior max rel err %.3g, weights max rel err %.3g" % (
-        name, sparse, worst, wworst))
+    print("%s (sparse=%s): posterior max rel err %.3g, weights max rel err %.3g, 8-bit grid flips "
+          "%s" % (name, sparse, worst, wworst, flips))
     return eng
 
 

@@ -437,7 +437,8 @@ def test_engine_split_dw_large_batch(mode):
     """Large frame batches split each dW = dz^T X over K (the batch rows) into slabs that a slab-sum
     operation of the NEXT grouped launch adds into the gradient (and the layer's update, one launch
     later still).  The gradient buffer after a step equals the unsplit run's up to fp32 summation
-    order, in eager, graph-replayed and data-parallel (bucketed, split-optimizer) form."""
+    order, and so do all parameters after two steps, in eager, graph-replayed and data-parallel
+    (bucketed, split-optimizer) form."""
     import pkc.engine as E
     from pkc.engine import Engine, parse_model
     cfg = c1_config(drop="0.15")
@@ -473,13 +474,26 @@ def test_engine_split_dw_large_batch(mode):
                 eng.loss_acc.zero_()
             eng.train_step(no_op_allreduce if mode == "dp_graph" else None)
             torch.cuda.synchronize()
-            grads.append((eng.gflat.detach().cpu().double(), eng.chunk_totals()))
+            g_first = eng.gflat.detach().cpu().double()
+            # a second step: its weights prove each update used the SUMMED gradient and ran after
+            # its slab sum (lag 2; the spread tail never merges a layer's update into the launch
+            # of its own slab sum) — a wrong order leaves gflat right and the weights wrong
+            eng.train_step(no_op_allreduce if mode == "dp_graph" else None)
+            torch.cuda.synchronize()
+            eng.sync_state()
+            sd = {a + "/" + k: v.detach().cpu().double() for a in nets
+                  for k, v in nets[a].state_dict().items() if not k.endswith("num_batches_tracked")}
+            grads.append((g_first, eng.chunk_totals(), sd))
     finally:
         E.DW_SPLIT_ROWS = old
-    (g0, t0), (g1, t1) = grads
+    (g0, t0, s0), (g1, t1, s1) = grads
     assert t0 == pytest.approx(t1, rel=1e-6)
     err = (g1 - g0).abs().max().item()
     assert err <= 1e-5 * g0.abs().max().item(), "split-K dW gradient max abs diff %.3g" % err
+    for k in s0:
+        d = (s1[k] - s0[k]).norm().item()
+        assert d <= 1e-4 * s0[k].norm().item() + 1e-7, "%s after 2 steps: rel diff %.3g" % (
+            k, d / max(s0[k].norm().item(), 1e-30))
 
 
 @pytest.mark.parametrize("B,mode", [(128, "eager"), (128, "graph"), (1024, "eager")])

@@ -27,6 +27,7 @@ import torch
 
 from cases import RUN_NN_CASES, run_nn_cfg
 from conftest import GOLDEN
+from quantcheck import assert_few_flips
 
 pytestmark = pytest.mark.gpu
 SECS = ("architecture1", "architecture2", "architecture3")
@@ -141,8 +142,13 @@ def test_run_nn_lifecycle_vs_reference(case, tmp_path):
     tol = 5e-3 if "quant" in case else 1e-4
     errs = {}
 
+    flips = {}
+
     def check(tag, got, ref):
         got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+        if "quant" in case and tag.endswith("weight") and ref.ndim == 2 and " opt" not in tag:
+            # the 2e-2 / 5e-3 tolerances below hold only with few 8-bit grid flips (quantcheck)
+            flips[tag] = assert_few_flips(got, ref, tag, 2e-3)
         d = np.linalg.norm(got - ref)
         t = 2e-2 if ("quant" in case and tag.startswith("ck0")) else tol
         bound = t * np.linalg.norm(ref) + 1e-6 * np.sqrt(ref.size)
@@ -192,7 +198,8 @@ def test_run_nn_lifecycle_vs_reference(case, tmp_path):
             prm.grad = torch.ones_like(prm)
         opt.step()
     bad = {k: "%.3g" % v[0] for k, v in errs.items() if not v[1]}
-    print("worst checkpoint rel err %.3g" % max(v[0] for v in errs.values() if v[1] or True))
+    print("worst checkpoint rel err %.3g; 8-bit grid flips %s" % (
+        max(v[0] for v in errs.values() if v[1] or True), flips))
     assert not bad, "checkpoint tensors off the reference: %s" % bad
 
     # forward-mode posteriors

@@ -300,3 +300,42 @@ def test_dropin_core_module_replaces_run_nn(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        cwd=str(tmp_path))
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
+
+
+def test_sync_bn_refuses_per_rank_batchnorm():
+    """[exp] sync_bn synchronises the MLP layers' BatchNorm only: an input BatchNorm
+    (dnn_use_batchnorm_inp) would keep per-rank statistics, so the engine refuses it instead of
+    silently breaking the R-ranks-equal-one-process recipe."""
+    from pkc.engine import Engine, parse_model
+    from pkc.neural_networks import MLP
+    cfg = build_mlp_config("plain")
+    cfg["architecture1"]["dnn_use_batchnorm_inp"] = "True"
+    torch.manual_seed(0)
+    nets = {cfg[s]["arch_name"]: MLP(cfg[s], k) for s, k in
+            (("architecture1", 40), ("architecture2", 32), ("architecture3", 32))}
+    opts = {cfg[s]["arch_name"]: cfg[s] for s in ("architecture1", "architecture2", "architecture3")}
+
+    class Sync:
+        world, rank = 2, 0
+
+    with pytest.raises(NotImplementedError, match="input BatchNorm"):
+        Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 40)},
+               ["lab_cd", "lab_mono"], batch=8, device="cpu", sync_bn=Sync())
+
+
+def test_quantcheck_flip_bound():
+    """The flip-count helper of the quantised-config GPU tests: summation-order noise near a grid
+    boundary moves few weights by one quantum; an off-by-one quantiser moves most of them."""
+    from quantcheck import grid_index, quantum_flips
+    rs = np.random.RandomState(0)
+    w = rs.uniform(-0.99, 0.99, size=(64, 64)).astype(np.float32)
+    assert quantum_flips(w, w) == (0, 0.0)
+    k = grid_index(w)
+    near = np.clip(w, -1, 1) * 128
+    e = w.copy()
+    e[0, 0] = np.float32(np.sign(w[0, 0]) * (np.floor(abs(near[0, 0])) / 128))   # onto the boundary
+    assert quantum_flips(e, w)[1] <= 1.0
+    shifted = (np.sign(w) * (np.abs(np.clip(w, -1, 1)) + 1.0 / 128)).astype(np.float32)
+    n, dmax = quantum_flips(shifted, w)
+    assert n > 0.9 * w.size and dmax == 1.0
+    assert (np.abs(k) <= 128).all()
