@@ -347,6 +347,7 @@ def measure_mlp(prec, args, rank, world, allreduce):
         print(json.dumps({"pmc_replay": tag, "launches": nl * args.pmc_replay}), flush=True)
         sys.exit(0)
     eng.capture(split_optimizer=world > 1)
+    graph_lps = eng.graph_launches_per_step
     dt = time_steps(eng, args.steps, args.warmup, allreduce, world)
     loss_sum, err_sum = eng.chunk_totals()
     n_done = args.warmup + args.steps
@@ -379,6 +380,7 @@ def measure_mlp(prec, args, rank, world, allreduce):
                          "algorithmic_flops_per_launch": per_launch_fl,
                          "mfma_tflops_per_launch": round(per_launch_fl / (avg_ms * 1e-3) / 1e12, 2)},
             "launches_per_step": len(prof),
+            "graph_launches_per_step": graph_lps,
             "step_breakdown_us": {k: round(v[1] * 1e3, 2) for k, v in
                                   sorted(agg.items(), key=lambda kv: -kv[1][1])},
             "chunk_frames_per_rank": chunk.n_rows, "chunk_prep_s": round(prep_s, 3),
@@ -520,6 +522,7 @@ def main():
                        "chunk_frames_per_rank": head["chunk_frames_per_rank"]},
             "roofline": head["roofline"],
             "launches_per_step": head["launches_per_step"],
+            "graph_launches_per_step": head["graph_launches_per_step"],
             "step_breakdown_us": head["step_breakdown_us"],
             "batch_sweep_frames_per_s": sweep,
             "sequence_configs": seq,

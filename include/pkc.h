@@ -61,12 +61,17 @@ int pkc_gemm_pick_splits(int M, int N, int K);
  *                  row_err = X1, out = C, acc = X2, advance_ctr = X3)
  *   PKC_OP_OPTIM : pkc_optim_step(tensors_dev = A, chunk_map_dev = B, nchunks = M) — the update of
  *                  a layer whose gradients are complete rides in a later launch of the backward
+ *   PKC_OP_GATHER: pkc_batch_gather(feats = A, ld_feats = lda, F = N, labels = B, nlab = ldb,
+ *                  B = M rows, n_batches = slab_stride, step_ctr = X1, x_out = C, lab_out = X2,
+ *                  advance = 0, x_bf16 = X3) — the next batch's gather sharing a launch with the
+ *                  previous step's last weight update (neither reads what the other writes)
  * Block-sparse GEMM (static HCGS masks multiplied into W, HCGS.py:24-28 /
  * neural_networks.py:258, 858-861): with ktiles != NULL (and splits == 1) the 64-column output
  * tile j reads only the 32-deep k-tiles ktiles[j * (kmax + 1) + 1 .. + count], count =
  * ktiles[j * (kmax + 1)]: the k-tiles whose B rows (64 of them) hold a nonzero.  Exact: every
  * skipped product is a zero weight, so the sums are those of the dense matmul. */
-enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2, PKC_OP_OPTIM = 3, PKC_OP_SLABSUM = 4 };
+enum { PKC_OP_GEMM = 0, PKC_OP_COLSUM = 1, PKC_OP_LOSS = 2, PKC_OP_OPTIM = 3, PKC_OP_SLABSUM = 4,
+       PKC_OP_GATHER = 5 };
 typedef struct {
   int a_kcontig, b_kcontig, M, N, K, splits;
   const void* A; int64_t lda; const void* B; int64_t ldb;

@@ -398,18 +398,28 @@ constexpr int FT = 256;
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// Column group of a workgroup (PKC_DENSE_XCD, measured 0.1976 -> 0.1957 ms per C2 step): workgroup
-// w runs on XCD w % 8 (round-robin
-// dispatch), so give each XCD a contiguous run of groups — the two 64-byte halves of a slab's
-// 128-byte line are then read through one L2 instead of two.
-#ifndef PKC_DENSE_XCD
-#define PKC_DENSE_XCD 1
-#endif
-__device__ __forceinline__ int col_group(int b, int nb) {
-  if (!PKC_DENSE_XCD) return b;
-  const int per = nb >> 3;
-  if (b >= per * 8) return b;
-  return (b & 7) * per + (b >> 3);
+// Column group of a workgroup.  Workgroup w runs on XCD w % 8 (round-robin dispatch, observed;
+// speed only — any placement computes the same columns).
+//   XM = 1 (PKC_DENSE_XCD=1, round 1: 0.1976 -> 0.1957 ms per C2 step against launch order): each
+//          XCD takes a contiguous run of groups, so the two 64-byte halves of a slab's 128-byte line
+//          are read through one L2 instead of two;
+//   XM = 2 (default since round 3): each XCD takes the 64-column tiles j == XCD (mod 8) — the
+//          tiles its own workgroups PRODUCED: the split-K matmuls that write these slabs (the
+//          standalone forward matmul's grid (N / 64, M / 64, splits) and the dX problems, which
+//          lead their grouped launches at 8-aligned offsets) run tile j on XCD j % 8, so the
+//          slabs are read from the consumer's own L2 instead of another XCD's.  Needs N / 64 % 8 == 0
+//          (else XM = 1).
+template <int XM>
+__device__ __forceinline__ int col_group(int b, int nb, int fc) {
+  if constexpr (XM == 2) {
+    const int gpt = 64 / fc;                       // groups per 64-column tile
+    const int x = b & 7, i = b >> 3;
+    return (x + 8 * (i / gpt)) * gpt + i % gpt;
+  } else {
+    const int per = nb >> 3;
+    if (b >= per * 8) return b;
+    return (b & 7) * per + (b >> 3);
+  }
 }
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -466,12 +476,12 @@ __device__ __forceinline__ void load_slabs(const float* __restrict__ base, int64
   }
 }
 
-template <int NS, int RI, int G>
+template <int NS, int RI, int G, int XM>
 __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args a) {
   constexpr int FC = 4 * G, RG = FT / G;
   __shared__ float4 red[4 * G];
   const int c4 = threadIdx.x % G, rg = threadIdx.x / G;
-  const int c = col_group(blockIdx.x, gridDim.x) * FC + c4 * 4;
+  const int c = col_group<XM>(blockIdx.x, gridDim.x, FC) * FC + c4 * 4;
   const bool cok = c < a.N;
   const int64_t N = a.N;
   const int M = a.M;
@@ -579,12 +589,12 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
   }
 }
 
-template <int NS, int RI, int G>
+template <int NS, int RI, int G, int XM>
 __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args a) {
   constexpr int FC = 4 * G, RG = FT / G;
   __shared__ float4 red[4 * G];
   const int c4 = threadIdx.x % G, rg = threadIdx.x / G;
-  const int c = col_group(blockIdx.x, gridDim.x) * FC + c4 * 4;
+  const int c = col_group<XM>(blockIdx.x, gridDim.x, FC) * FC + c4 * 4;
   const bool cok = c < a.N;
   const int64_t N = a.N;
   const int M = a.M;
@@ -915,22 +925,38 @@ static bool small_ok(int M, int N, int nslab, const void* p0, const void* p1, in
          ((uintptr_t)p1 % 16 == 0) && (nslab == 1 || stride % 4 == 0);
 }
 
-#define PKC_SMALL_LAUNCH_G(KERN, G, args, M, nslab, stream)                                     \
+static int dense_xcd() {                        // PKC_DENSE_XCD=1: the round-1 mapping (A/B)
+  static const int m = [] {
+    const char* v = getenv("PKC_DENSE_XCD");
+    return v ? atoi(v) : 2;
+  }();
+  return m;
+}
+
+#define PKC_SMALL_LAUNCH_X(KERN, G, XM, args, M, nslab, stream)                                  \
   do {                                                                                         \
     dim3 grid_((args).N / (4 * G) + ((args).N % (4 * G) ? 1 : 0));                             \
     const int ri_ = (M) <= FT / G ? 1 : 2;                                                     \
     const int ns_ = (nslab) <= 1 ? 1 : ((nslab) <= 2 ? 2 : ((nslab) <= 4 ? 4 : 8));            \
     if (ri_ == 1) {                                                                            \
-      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 1, G>), grid_, dim3(FT), 0, stream, args);    \
-      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 1, G>), grid_, dim3(FT), 0, stream, args); \
-      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 1, G>), grid_, dim3(FT), 0, stream, args); \
-      else hipLaunchKernelGGL((KERN<8, 1, G>), grid_, dim3(FT), 0, stream, args);             \
+      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 1, G, XM>), grid_, dim3(FT), 0, stream, args); \
+      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 1, G, XM>), grid_, dim3(FT), 0, stream, args); \
+      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 1, G, XM>), grid_, dim3(FT), 0, stream, args); \
+      else hipLaunchKernelGGL((KERN<8, 1, G, XM>), grid_, dim3(FT), 0, stream, args);          \
     } else {                                                                                   \
-      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 2, G>), grid_, dim3(FT), 0, stream, args);    \
-      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 2, G>), grid_, dim3(FT), 0, stream, args); \
-      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 2, G>), grid_, dim3(FT), 0, stream, args); \
-      else hipLaunchKernelGGL((KERN<8, 2, G>), grid_, dim3(FT), 0, stream, args);             \
+      if (ns_ == 1) hipLaunchKernelGGL((KERN<1, 2, G, XM>), grid_, dim3(FT), 0, stream, args); \
+      else if (ns_ == 2) hipLaunchKernelGGL((KERN<2, 2, G, XM>), grid_, dim3(FT), 0, stream, args); \
+      else if (ns_ == 4) hipLaunchKernelGGL((KERN<4, 2, G, XM>), grid_, dim3(FT), 0, stream, args); \
+      else hipLaunchKernelGGL((KERN<8, 2, G, XM>), grid_, dim3(FT), 0, stream, args);          \
     }                                                                                          \
+  } while (0)
+// the producer-aligned mapping needs whole 64-column tiles, 8 of them per XCD round
+#define PKC_SMALL_LAUNCH_G(KERN, G, args, M, nslab, stream)                                     \
+  do {                                                                                         \
+    if (dense_xcd() == 2 && (args).N % 512 == 0)                                               \
+      PKC_SMALL_LAUNCH_X(KERN, G, 2, args, M, nslab, stream);                                  \
+    else                                                                                       \
+      PKC_SMALL_LAUNCH_X(KERN, G, 1, args, M, nslab, stream);                                  \
   } while (0)
 #define PKC_SMALL_LAUNCH(KERN, args, M, nslab, stream)                                          \
   do {                                                                                         \

@@ -450,7 +450,7 @@ __global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
 // operand orientation.  One launch boundary instead of one per matmul.
 constexpr int GMAX = 8;
 struct GroupProb {
-  int kind;              // PKC_OP_GEMM / COLSUM / LOSS / OPTIM / SLABSUM
+  int kind;              // PKC_OP_GEMM / COLSUM / LOSS / OPTIM / SLABSUM / GATHER
   int code;              // a_kcontig*4 + b_kcontig*2 + vec (+8: 128x128 tile body)
   int M, N, K, kchunk, tn, tmn, wg0;
   const void* A; int64_t lda; const void* B; int64_t ldb; float* C; int64_t ldc; int64_t slab;
@@ -495,6 +495,13 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
   if (p.kind == PKC_OP_OPTIM) {
     optim_wg(reinterpret_cast<const pkc_opt_tensor*>(p.A), reinterpret_cast<const int32_t*>(p.B),
              local);
+    return;
+  }
+  if (p.kind == PKC_OP_GATHER) {
+    gather_row_body(reinterpret_cast<const float*>(p.A), p.lda, p.N,
+                    reinterpret_cast<const int32_t*>(p.B), (int)p.ldb, p.M, p.slab,
+                    reinterpret_cast<const int64_t*>(p.X1), p.C, reinterpret_cast<int32_t*>(p.X2),
+                    reinterpret_cast<__bf16*>(p.X3), p.code != 0, local);
     return;
   }
   if (p.kind == PKC_OP_LOSS) {
@@ -753,6 +760,21 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
       p.wg0 = wg;
       wg += (q.N + 1023) / 1024;
       any_sum = true;
+      continue;
+    }
+    if (q.kind == PKC_OP_GATHER) {
+      PKC_CHECK_ARG(q.M > 0 && q.N > 0 && q.A && q.B && q.C && q.X1 && q.X2 && q.slab_stride > 0 &&
+                        q.ldb >= 0 && q.ldb <= 256 && q.lda >= q.N,
+                    "pkc_gemm_grouped: gather op %d arguments", i);
+      GroupProb& p = g.p[k++];
+      memset(&p, 0, sizeof(p));
+      p.kind = q.kind;
+      p.M = q.M; p.N = q.N; p.A = q.A; p.lda = q.lda; p.B = q.B; p.ldb = q.ldb; p.C = q.C;
+      p.slab = q.slab_stride; p.X1 = q.X1; p.X2 = q.X2; p.X3 = q.X3;
+      p.code = (q.N % 4 == 0 && q.lda % 4 == 0 && (uintptr_t)q.A % 16 == 0 &&
+                (uintptr_t)q.C % 16 == 0 && (uintptr_t)q.X3 % 8 == 0) ? 1 : 0;
+      p.wg0 = wg;
+      wg += q.M;
       continue;
     }
     if (q.kind == PKC_OP_COLSUM || q.kind == PKC_OP_LOSS) {

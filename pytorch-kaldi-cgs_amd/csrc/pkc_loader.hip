@@ -6,6 +6,7 @@
 // (np.roll order: block b of row r is raw[(r + 2L - b) mod N]), the column statistics (fp64,
 // population std as np.std) and the row permutation of the shuffle are applied on the device.
 #include "pkc_common.h"
+#include "pkc_ops.h"
 
 namespace pkc {
 
@@ -75,29 +76,8 @@ __global__ __launch_bounds__(256) void batch_gather_kernel(const float* feats, i
                                                            float* x_out, int32_t* lab_out,
                                                            int advance, unsigned* done,
                                                            __bf16* xb, bool vec) {
-  const int64_t i = *ctr % n_batches;
-  const int64_t row0 = i * B;
-  const int r = blockIdx.x;
-  const float* src = feats + (row0 + r) * ld;
-  if (vec) {   // 16-byte rows (F % 4 == 0, aligned): one load per thread for a 440-wide row
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-    for (int c = 4 * threadIdx.x; c < F; c += 1024) {
-      const float4 v = *reinterpret_cast<const float4*>(src + c);
-      *reinterpret_cast<float4*>(x_out + (int64_t)r * F + c) = v;
-      if (xb) {
-        bf16x4 h;
-        h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
-        *reinterpret_cast<bf16x4*>(xb + (int64_t)r * F + c) = h;
-      }
-    }
-  } else {
-    for (int c = threadIdx.x; c < F; c += 256) {
-      const float v = src[c];
-      x_out[(int64_t)r * F + c] = v;
-      if (xb) xb[(int64_t)r * F + c] = (__bf16)v;
-    }
-  }
-  if (threadIdx.x < nlab) lab_out[r * nlab + threadIdx.x] = labels[(row0 + r) * nlab + threadIdx.x];
+  gather_row_body(feats, ld, F, labels, nlab, B, n_batches, ctr, x_out, lab_out, xb, vec,
+                  blockIdx.x);
   if (advance) {
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -93,4 +93,37 @@ __device__ __forceinline__ void slabsum_body(int ns, int n, const float* __restr
   }
 }
 
+// One row r of the batch gather (pkc_batch_gather, include/pkc.h): row i*B + r of the chunk's
+// feature matrix (i = *ctr % n_batches, the device batch counter) into x_out (+ its bf16 copy) and
+// its label columns into lab_out; 256 threads.  Shared by batch_gather_kernel and the grouped
+// launch's PKC_OP_GATHER.
+__device__ __forceinline__ void gather_row_body(const float* feats, int64_t ld, int F,
+                                                const int32_t* labels, int nlab, int B,
+                                                int64_t n_batches, const int64_t* ctr,
+                                                float* x_out, int32_t* lab_out, __bf16* xb,
+                                                bool vec, int r) {
+  const int64_t i = *ctr % n_batches;
+  const int64_t row0 = i * B;
+  const float* src = feats + (row0 + r) * ld;
+  if (vec) {   // 16-byte rows (F % 4 == 0, aligned): one load per thread for a 440-wide row
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    for (int c = 4 * threadIdx.x; c < F; c += 1024) {
+      const float4 v = *reinterpret_cast<const float4*>(src + c);
+      *reinterpret_cast<float4*>(x_out + (int64_t)r * F + c) = v;
+      if (xb) {
+        bf16x4 h;
+        h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+        *reinterpret_cast<bf16x4*>(xb + (int64_t)r * F + c) = h;
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < F; c += 256) {
+      const float v = src[c];
+      x_out[(int64_t)r * F + c] = v;
+      if (xb) xb[(int64_t)r * F + c] = (__bf16)v;
+    }
+  }
+  if (threadIdx.x < nlab) lab_out[r * nlab + threadIdx.x] = labels[(row0 + r) * nlab + threadIdx.x];
+}
+
 }  // namespace pkc

@@ -77,7 +77,7 @@ class GemmProblem(C.Structure):
                 ("X1", vp), ("X2", vp), ("X3", vp), ("ktiles", vp), ("kmax", C.c_int)]
 
 
-OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM, OP_SLABSUM = 0, 1, 2, 3, 4
+OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM, OP_SLABSUM, OP_GATHER = 0, 1, 2, 3, 4, 5
 
 REG_L1, REG_L2 = 1, 2
 

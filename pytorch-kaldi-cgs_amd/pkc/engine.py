@@ -52,6 +52,10 @@ OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "2500000"))
 # 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
 # gradient (0: off)
 DW_SPLIT_ROWS = int(os.environ.get("PKC_DW_SPLIT_ROWS", "1024"))
+# multi-step graphs: the last launch of a step (the first layer's weight update, which needs the
+# dW of the step's last matmul launch) rides in the NEXT step's first launch, beside that step's
+# batch gather (PKC_OP_GATHER): one launch per step fewer; 0: off (A/B)
+DEFER_TAIL = os.environ.get("PKC_DEFER_TAIL", "1") != "0"
 # recurrent layers' dW / dU split-K cap (1: unsplit, A/B)
 REC_DW_SPLITS = int(os.environ.get("PKC_REC_DW_SPLITS", "4"))
 # recurrent layers: sum the output-gradient slabs before the BPTT loop (0: per step, A/B)
@@ -443,6 +447,8 @@ class Engine:
         self.graph_tail = None
         self.steps_done = 0
         self.skip_labels = set()
+        self.n_launches = 0                    # libpkc launches issued (or captured) so far
+        self.graph_launches_per_step = None    # of the multi-step graph (capture)
 
     # ------------------------------------------------------------------ graph construction
     def _build_graph(self):
@@ -1089,6 +1095,7 @@ class Engine:
         """Launch one libpkc entry point; in profile mode bracket it with events."""
         if label in self.skip_labels:     # measurement only (step_cost_of)
             return
+        self.n_launches += 1
         if self.prof is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -1169,6 +1176,16 @@ class Engine:
                 C.c_void_p(mp), C.c_void_p(mp + 8 * self.B), C.c_void_p(mp + 8 * self.B + 4 * self.B),
                 self.B, T, ptr(self.x), ptr(self.labs), s)
 
+    def _gather_op(self):
+        """The frame batch gather as an operation of a grouped launch (PKC_OP_GATHER)."""
+        M = self.M
+        p = L.GemmProblem(kind=L.OP_GATHER, M=self.B, N=self.F, A=self.chunk_feats.data_ptr(),
+                          lda=self.chunk_feats.stride(0), B=self.chunk_labels.data_ptr(),
+                          ldb=self.nlab, C=self.x.data_ptr(), slab_stride=self.n_batches,
+                          X1=self.ctr.data_ptr(), X2=self.labs.data_ptr(),
+                          X3=self.x_h.data_ptr() if self.x_h is not None else None)
+        return ("gather", 0.0, 8.0 * M * self.F, p)
+
     def _fwd_problem(self, n):
         """(label, flops, bytes, GemmProblem) of a dense layer's forward matmul Z = X W^T."""
         M = self.M
@@ -1194,7 +1211,11 @@ class Engine:
         A launch whose matmuls all have bf16 operand copies (a 5th tuple item: (bytes, problem))
         runs on them (PKC_PREC_BF16IN); its other operations are precision-neutral."""
         for i in range(0, len(probs), 8):
-            part = probs[i:i + 8]
+            # dX problems lead the launch: at a workgroup offset that is a multiple of 8 (the
+            # preceding dX grids have 16k-wide tile rows), tile j of a 1024-column dX runs on XCD
+            # j % 8 — the XCD whose BatchNorm-backward workgroups read that tile's slabs
+            # (pkc_dense.hip col_group<2>)
+            part = sorted(probs[i:i + 8], key=lambda q: 0 if q[0].startswith("dX") else 1)
             gem = [q for q in part if q[3].kind == L.OP_GEMM]
             prec = self.prec
             if gem and all(len(q) > 4 and q[4] is not None for q in gem):
@@ -1389,8 +1410,13 @@ class Engine:
             self._k("rnn_fwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_fwd", C.byref(ra), s)
 
-    def _forward_kernels(self, s, train, batch=None, defer_loss=False):
-        self._gather(s, batch)
+    def _forward_kernels(self, s, train, batch=None, defer_loss=False, pending=None):
+        """pending: the previous step's deferred last launch (see _optim_kernels), run together
+        with this step's gather."""
+        if pending:
+            self._gemms([self._gather_op()] + list(pending), s)
+        else:
+            self._gather(s, batch)
         if self.reg_terms and self.loss_heads:
             self._reg_loss_kernels(s)
         nodes, i = self.nodes, 0
@@ -1814,16 +1840,25 @@ class Engine:
             self._k("reg_grad", 0, 12.0 * t.nparam, "pkc_reg_grad", t.kind, ptr(t.items_dev),
                     t.nitems, ptr(t.coef), s)
 
-    def _optim_kernels(self, s, spread_opt=False):
+    def _optim_kernels(self, s, spread_opt=False, defer=False):
+        """defer (spread mode): when the step's last launch holds weight updates only, return its
+        operations instead of launching them — the next step's first launch (its batch gather,
+        which reads neither) carries them (multi-step graphs; the graph's last step flushes)."""
         if not self.opt_entries:
-            return
+            return None
         spread_opt = spread_opt and not self.reg_terms
         self._reg_grad_kernels(s)
         if spread_opt:
-            for f in self.spread_tail:
+            tail, pend = self.spread_tail, None
+            if (defer and DEFER_TAIL and tail and not self.prune_list and not self.seq
+                    and self.loss_heads and len(tail[-1]) < 8
+                    and all(op[3].kind == L.OP_OPTIM for op in tail[-1])):
+                tail, pend = tail[:-1], tail[-1]
+            for f in tail:
                 self._gemms(f, s)
-            self._prune_kernels(s)
-            return
+            if pend is None:
+                self._prune_kernels(s)
+            return pend
         nparam = sum(e["p"].numel() for e in self.opt_entries)
         self._k("optim_step", 0, 4.0 * nparam * 5, "pkc_optim_step", ptr(self.opt_desc),
                 len(self.opt_entries), ptr(self.opt_map), self.opt_nchunks, s)
@@ -1998,13 +2033,14 @@ class Engine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
 
-        def one_step(st):
+        def one_step(st, pending=None, defer_tail=False):
             defer = bool(self.loss_heads)
-            self._forward_kernels(st, True, defer_loss=defer)
+            self._forward_kernels(st, True, defer_loss=defer, pending=pending)
             self._backward_kernels(st, self._loss_op() if defer else None,
                                    spread_opt=not split_optimizer)
             if not split_optimizer:
-                self._optim_kernels(st, spread_opt=True)
+                return self._optim_kernels(st, spread_opt=True, defer=defer_tail)
+            return None
 
         self.graph_tail = None
         if split_optimizer and self._bucket_cut()[0] is not None:
@@ -2033,9 +2069,12 @@ class Engine:
         self.graph_multi, self.steps_per_graph = None, 1
         if not split_optimizer and steps_per_graph > 1:
             gm = torch.cuda.CUDAGraph()
+            n0 = self.n_launches
             with torch.cuda.graph(gm, stream=s):
-                for _ in range(steps_per_graph):
-                    one_step(self._stream())
+                pend = None
+                for k in range(steps_per_graph):
+                    pend = one_step(self._stream(), pend, defer_tail=k < steps_per_graph - 1)
+            self.graph_launches_per_step = (self.n_launches - n0) / steps_per_graph
             self.graph_multi, self.steps_per_graph = gm, steps_per_graph
         self.graph_opt = None
         if split_optimizer:
