@@ -62,7 +62,9 @@ r_bench_prof() {
   T=$(find /tmp/bprof -name 'bench_kernel_trace.csv' -print -quit)
   S=$(find /tmp/bprof -name 'bench_kernel_stats.csv' -print -quit)
   cp "$S" gpurun_out/bprof/bench_kernel_stats.csv
-  python3 scripts/trace_gaps.py "$T" batch_gather "gemm_grouped_kernel<1, true" > gpurun_out/bprof/timeline.txt
+  # anchor: the heads' NLL launch (once per step; with the deferred tail the gather rides in a
+  # grouped launch inside the multi-step graphs): the listing starts there, one whole step long
+  python3 scripts/trace_gaps.py "$T" nll_multi_kernel "gemm_grouped_kernel<1, true" > gpurun_out/bprof/timeline.txt
   tail -3 gpurun_out/bprof/timeline.txt
 }
 

@@ -27,7 +27,7 @@ import torch
 
 from cases import RUN_NN_CASES, run_nn_cfg
 from conftest import GOLDEN
-from quantcheck import assert_few_flips
+from quantcheck import assert_few_flips, rmsprop_quanta
 
 pytestmark = pytest.mark.gpu
 SECS = ("architecture1", "architecture2", "architecture3")
@@ -146,9 +146,12 @@ def test_run_nn_lifecycle_vs_reference(case, tmp_path):
 
     def check(tag, got, ref):
         got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
-        if "quant" in case and tag.endswith("weight") and ref.ndim == 2 and " opt" not in tag:
+        if ("quant" in case and " architecture1 " in tag and tag.endswith("weight")
+                and ref.ndim == 2):
             # the 2e-2 / 5e-3 tolerances below hold only with few 8-bit grid flips (quantcheck)
-            flips[tag] = assert_few_flips(got, ref, tag, 2e-3)
+            # 3 RMSprop steps (lr 1.6e-3) per chunk: sign steps of near-zero gradients
+            flips[tag] = assert_few_flips(got, ref, tag, 5e-2,
+                                          max_quanta=rmsprop_quanta(1.6e-3, 3) + 1)
         d = np.linalg.norm(got - ref)
         t = 2e-2 if ("quant" in case and tag.startswith("ck0")) else tol
         bound = t * np.linalg.norm(ref) + 1e-6 * np.sqrt(ref.size)
