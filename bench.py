@@ -278,6 +278,25 @@ def time_steps(eng, steps, warmup, allreduce=None, world=1):
     return dt
 
 
+def mfma_profile(name):
+    """MFMA utilisation of a configuration from its committed rocprofv3 counter pass
+    (scripts/gpu.sh mfma -> profiles/r*_mfma_<name>.json, scripts/mfma_summary.py: busy cycles over
+    the SIMD cycles the kernels had), MFMA-flop weighted over the kernels; None without one."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_%s.json" % name)), reverse=True):
+        try:
+            rows = json.load(open(f))
+            fl = sum(r["mfma_gflop"] for r in rows if r.get("mfma_util_pct") is not None)
+            if fl <= 0:
+                continue
+            u = sum(r["mfma_util_pct"] * r["mfma_gflop"] for r in rows
+                    if r.get("mfma_util_pct") is not None) / fl
+            return {"mfma_util_pct": round(u, 2), "source": os.path.relpath(f, ROOT)}
+        except (OSError, ValueError, KeyError, TypeError):
+            continue
+    return None
+
+
 def seq_entry(name, steps, warmup, with_cpu, cpu_seconds):
     """A BASELINE sequence configuration measured like the headline: frames/s over `steps` timed
     sentence batches, its roofline (max(F_alg / MFMA peak, B_alg / HBM peak) over the
@@ -294,6 +313,9 @@ def seq_entry(name, steps, warmup, with_cpu, cpu_seconds):
                        "note": "algorithmic flops (W, U scaled by mask density, heads; x3 for "
                                "training) over padded rows / measured step time; the recurrence "
                                "is serial-latency-bound: see us_per_time_step_per_layer_fwd_bwd"}
+    prof = mfma_profile(name)
+    if prof:
+        out["roofline"]["mfma_util"] = prof
     if with_cpu:
         out["cpu_baseline"] = bench_seq.cpu_baseline(name, seconds=cpu_seconds)
     return out
@@ -426,6 +448,9 @@ def seq_main(args, rank, world, allreduce):
                                 "recurrence is serial-latency-bound (us_per_time_step...)"},
            "us_per_time_step_per_layer_fwd_bwd": round(r["us_per_time_step_per_layer_fwd_bwd"], 3),
            "mean_T": round(r["mean_T"], 1)}
+    prof = mfma_profile(args.config)
+    if prof:
+        res["roofline"]["mfma_util"] = prof
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = bench_seq.cpu_baseline(args.config, seconds=args.cpu_seconds)
     print(json.dumps(res), flush=True)

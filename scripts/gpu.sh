@@ -13,7 +13,7 @@
 #   pmc         HBM traffic of the dominant launch: FETCH_SIZE and WRITE_SIZE passes
 #               (PMC_PREC=fp32 PMC_OUT=pmc_traffic_fp32.json for the fp32 entry)
 #                                                             -> gpurun_out/pmc_traffic*.json
-#   mfma        MFMA counters of the C2 step (B=128, B=4096) and the C4 step -> gpurun_out/mfma/
+#   mfma        MFMA counters of the C2 step (B=128, B=4096) and the C3/C4/C5 steps -> gpurun_out/mfma/
 #   seq         scripts/bench_seq.py (C3/C4/C5/GRU)           -> gpurun_out/seq.log
 #   seq_prof    bench_seq under rocprofv3 --kernel-trace --stats -> gpurun_out/prof_seq/
 #   b4k_prof    the B=4096 step under rocprofv3 + timeline     -> gpurun_out/b4k/
@@ -93,10 +93,12 @@ r_mfma() {
     --batch 4096 --steps 10 --warmup 3 --no-cpu-baseline --no-batch-sweep --no-fp32 --no-seq-configs > gpurun_out/mfma/b4096.log 2>&1
   ok $? mfma_b4096
   python3 scripts/mfma_summary.py /tmp/mfma4k > gpurun_out/mfma/b4096.json
-  timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d /tmp/mfmac4 -o p -- python3 scripts/bench_seq.py \
-    --configs c4 --steps 2 --warmup 1 > gpurun_out/mfma/c4.log 2>&1
-  ok $? mfma_c4
-  python3 scripts/mfma_summary.py /tmp/mfmac4 > gpurun_out/mfma/c4.json
+  for c in c3 c4 c5; do
+    timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d /tmp/mfma$c -o p -- python3 scripts/bench_seq.py \
+      --configs $c --steps 2 --warmup 1 > gpurun_out/mfma/$c.log 2>&1
+    ok $? mfma_$c
+    python3 scripts/mfma_summary.py /tmp/mfma$c > gpurun_out/mfma/$c.json
+  done
   head -c 1500 gpurun_out/mfma/b4096.json
 }
 
