@@ -418,17 +418,17 @@ __device__ __forceinline__ void xcd_tile(int remap, int& bx, int& by, int& bz) {
   bz = id / (nx * ny);
 }
 
-template <bool AKC, bool BKC>
+template <int NB, bool AKC, bool BKC>
 __global__ __launch_bounds__(big::NT) void gemm_glds_kernel(int M, int N, int K,
                                                            const void* __restrict__ A, int64_t lda,
                                                            const void* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc,
                                                            int kchunk, int64_t slab_stride,
                                                            int remap) {
-  __shared__ __attribute__((aligned(16))) char lds[big::GL_LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[big::gl_lds_bytes<NB>()];
   int bx, by, bz;
   xcd_tile(remap, bx, by, bz);
-  big::body_glds<AKC, BKC>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk, slab_stride);
+  big::body_glds<NB, AKC, BKC>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk, slab_stride);
 }
 
 template <int PREC, bool BIN, bool AKC, bool BKC>
@@ -605,6 +605,15 @@ static bool glds_enabled() {                   // PKC_GEMM_GLDS=0: register-stag
   return on != 0;
 }
 
+static int glds_bufs() {                      // PKC_GLDS_BUFS: LDS-DMA ring depth (3, 4, 5)
+  static const int nb = [] {
+    const char* v = getenv("PKC_GLDS_BUFS");
+    const int n = v ? atoi(v) : 3;
+    return n < 3 ? 3 : n > 5 ? 5 : n;
+  }();
+  return nb;
+}
+
 template <int PREC, bool BIN>
 static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
@@ -618,13 +627,19 @@ static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int6
   // 96 KB of LDS (one workgroup per CU) loses to the register body (4096x1928x1024 31.6 -> 35.3,
   // 8192^3 755 -> 656 TF/s), same run
   if (BIN && K % 64 == 0 && (int64_t)grid.x * grid.y * grid.z <= 256 && glds_enabled()) {
-#define PKC_L(AK, BK_)                                                                          \
-  hipLaunchKernelGGL((gemm_glds_kernel<AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, lda, B,   \
-                     ldb, C, ldc, kchunk, slab, xcd_remap())
-    if (akc && bkc) PKC_L(true, true);
-    else if (akc) PKC_L(true, false);
-    else if (bkc) PKC_L(false, true);
-    else PKC_L(false, false);
+#define PKC_L(NB, AK, BK_)                                                                      \
+  hipLaunchKernelGGL((gemm_glds_kernel<NB, AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, lda,  \
+                     B, ldb, C, ldc, kchunk, slab, xcd_remap())
+#define PKC_LN(NB)                                                                              \
+  if (akc && bkc) PKC_L(NB, true, true);                                                        \
+  else if (akc) PKC_L(NB, true, false);                                                         \
+  else if (bkc) PKC_L(NB, false, true);                                                         \
+  else PKC_L(NB, false, false)
+    const int nb = glds_bufs();
+    if (nb == 5) { PKC_LN(5); }
+    else if (nb == 4) { PKC_LN(4); }
+    else { PKC_LN(3); }
+#undef PKC_LN
 #undef PKC_L
     PKC_LAUNCH_CHECK("pkc_gemm (128x128 LDS-DMA)");
     return PKC_OK;

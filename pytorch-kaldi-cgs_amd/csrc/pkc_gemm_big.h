@@ -353,13 +353,16 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
 // LDS-DMA form of the bf16 body (operands stored as bf16, k-range a multiple of 64): one workgroup
 // per CU holds a 128x128 tile, so a k-tile whose loads are issued only two k-tiles ahead through
 // registers waits most of a memory round trip (the 4096x1024x1024 forward: 27 us = 12 % of the
-// CUs' MFMA rate).  Here global_load_lds writes the operand images straight into a ring of 3 LDS
-// buffers (96 KB): two k-tiles stay in flight across each barrier (counted vmcnt, raw s_barrier:
+// CUs' MFMA rate).  Here global_load_lds writes the operand images straight into a ring of NB LDS
+// buffers (32 KB each): NB - 1 k-tiles stay in flight across each barrier (counted vmcnt, raw s_barrier:
 // __syncthreads() would drain the DMA), no staging registers, no ds_write pass.  The DMA writes
 // each wave-instruction's 64 x 16 bytes linearly, so the swizzles of the register path's images
 // (swz for row images, xr for the [k][row] images) go on the per-lane SOURCE addresses instead.
-constexpr int GL_BUFS = 3;
-constexpr int GL_LDS_BYTES = GL_BUFS * 2 * TILE_BYTES;
+// NB buffers in the ring, NB - 1 k-tiles in flight: a lone workgroup per CU keeps only
+// (NB - 1) x 32 KB of operand requests outstanding, so its k-tile rate is that over the load
+// latency under full-chip traffic (PKC_GLDS_BUFS selects NB = 3, 4 or 5; 5 = all 160 KB of LDS).
+template <int NB>
+constexpr int gl_lds_bytes() { return NB * 2 * TILE_BYTES; }
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void glb_void;
@@ -387,7 +390,18 @@ __device__ __forceinline__ void glds_tile(const __bf16* __restrict__ P, int64_t 
   }
 }
 
-template <bool AKC, bool BKC>
+// s_waitcnt vmcnt(8 n): 8 glds per thread per k-tile, n later k-tiles left in flight
+__device__ __forceinline__ void wait_tiles(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+  }
+}
+
+template <int NB, bool AKC, bool BKC>
 __device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by, int bz, int M,
                                           int N, int K, const void* __restrict__ Av, int64_t lda,
                                           const void* __restrict__ Bv, int64_t ldb,
@@ -407,20 +421,21 @@ __device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
   const int nk = kbeg < kend ? (kend - kbeg) / 64 : 0;      // uniform; k-range % 64 == 0
-  auto buf = [&](int t) { return lds + (t % GL_BUFS) * 2 * TILE_BYTES; };
+  static_assert(NB >= 3 && NB <= 5, "body_glds: 3..5 ring buffers");
+  auto buf = [&](int t) { return lds + (t % NB) * 2 * TILE_BYTES; };
   auto issue = [&](int t) {
     glds_tile<AKC>(A, lda, m0, M, kbeg + 64 * t, buf(t));
     glds_tile<BKC>(B, ldb, n0, N, kbeg + 64 * t, buf(t) + TILE_BYTES);
   };
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
+#pragma unroll
+  for (int t = 0; t < NB - 1; ++t)
+    if (t < nk) issue(t);
   for (int t = 0; t < nk; ++t) {
-    // tile t + 2 refills the buffer of tile t - 1, released by the barrier ending iteration t - 1
-    if (t + 2 < nk) issue(t + 2);
+    // tile t + NB - 1 refills the buffer of tile t - 1, released by the barrier ending iteration
+    // t - 1
+    if (t + NB - 1 < nk) issue(t + NB - 1);
     // this thread's DMAs of tile t are done once at most the later tiles' 8 each are in flight
-    if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_tiles(min(NB - 1, nk - 1 - t));
     __builtin_amdgcn_s_barrier();             // ... and every thread's
     asm volatile("" ::: "memory");
     const char* cur = buf(t);

@@ -129,8 +129,8 @@ def alg_flops_per_row(nets):
     for sp in specs:
         H = sp["H"]
         G = len(sp["W"])
-        dW = float(sp["Wmask"].float().mean()) if sp.get("Wmask") is not None else 1.0
-        dU = float(sp["Umask"].float().mean()) if sp.get("Umask") is not None else 1.0
+        dW = float(sp["Wmask"].detach().float().mean()) if sp.get("Wmask") is not None else 1.0
+        dU = float(sp["Umask"].detach().float().mean()) if sp.get("Umask") is not None else 1.0
         per_dir_row += 3 * 2 * G * H * (K * dW + H * dU)
         K = 2 * H if sp["bidir"] else H
     head = 3 * 2 * (nets["head"].out_dim + nets["mono"].out_dim) * nets["rnn"].out_dim

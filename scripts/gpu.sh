@@ -20,6 +20,9 @@
 #   dp2         bench.py --gpus 2 on one GPU over gloo (C2)    -> gpurun_out/dp2.log
 #   seq_dp2     bench.py --gpus 2 --config c4 / c5 on one GPU over gloo -> gpurun_out/seq_dp2.log
 #   kprof       scripts/kbench.py plain and under rocprofv3    -> gpurun_out/kprof/
+#   ab          same-run A/B of one environment knob: AB_VAR over AB_VALUES (space-separated), two
+#               alternating rounds of `python AB_CMD` (e.g. "bench.py --batch 4096 ...")
+#                                                             -> gpurun_out/ab.txt
 #   round       tests smoke bench bench_prof pmc
 #
 # Extra arguments for a recipe's python command: PKC_ARGS="..." (bench, seq, kprof).
@@ -150,6 +153,16 @@ r_kprof() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kprof -o k \
     -- python3 scripts/kbench.py $A > gpurun_out/kprof.log 2>&1
   ok $? kprof
+}
+
+r_ab() {
+  : > gpurun_out/ab.txt
+  for i in 1 2; do for v in $AB_VALUES; do
+    env "$AB_VAR=$v" timeout -k 10 300 python -u $AB_CMD > gpurun_out/ab_run.log 2>&1
+    ok $? "ab $AB_VAR=$v"
+    grep -E '^\{|^ *[a-z0-9].*(TF/s|us)' gpurun_out/ab_run.log | sed "s/^/$AB_VAR=$v  /" | cut -c1-400 >> gpurun_out/ab.txt
+  done; done
+  cat gpurun_out/ab.txt
 }
 
 [ $# -gt 0 ] || { sed -n 2,30p "$0"; exit 2; }

@@ -373,7 +373,10 @@ def test_prune_matches_numpy_percentile(L, shape, perc, zeros):
 # shapes that take the 128x128 body (pkc_gemm_big.h: >= 160 output tiles of 128x128, 16-byte
 # operand paths): ragged M / N tails, K tails off the 32/64 k-tile, split-K slabs
 BIG_SHAPES = [(4096, 4096, 256, 1), (2048, 1280, 440, 1), (2056, 1288, 1000, 1), (4096, 1024, 1024, 2), (5280, 1024, 2048, 1),
-              (1032, 2600, 136, 3)]
+              (1032, 2600, 136, 3),
+              # <= 256 tiles, K % 64 == 0: the LDS-DMA ring body for bf16-stored operands (prec 2),
+              # ragged M / N tails, 3 to 32 k-tiles per workgroup
+              (4096, 1024, 1024, 1), (2056, 1288, 1024, 1), (2048, 1280, 2048, 1), (1280, 2048, 192, 1)]
 
 
 @pytest.mark.parametrize("prec", [0, 1, 2])
