@@ -80,6 +80,18 @@ typedef struct {
   const int32_t* ktiles; int kmax;              /* block-sparse k-tile lists (device), or NULL */
 } pkc_gemm_problem;
 int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream);
+/* Large-batch forward matmul of a BatchNorm'd layer (neural_networks.py:306-311: BN(wx(x)) over
+ * the batch) with the BatchNorm column statistics in the matmul's epilogue: one slab
+ * C = A B^T (as pkc_gemm, splits = 1) and, per 128-row block b of C, the block's column mean of
+ * C + bias and M2 = sum (C - mean)^2 into part[b*2N + n], part[b*2N + N + n] — the partials
+ * pkc_dense_fwd_pre(part_rows = 128) merges, so no separate statistics pass reads C.  Only for
+ * shapes that take the 128x128 tile body: pkc_gemm_colstats_ok says which (1 / 0); bias may be
+ * NULL; part holds 2 N ceil(M / 128) floats (a pkc_dense_work_size(M, N) buffer does). */
+int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                         const void* A, int64_t lda, const void* B, int64_t ldb);
+int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                      const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
+                      int64_t ldc, const float* bias, float* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Dense layer epilogue, forward (neural_networks.py:306-317: drop(act(BN(z)))) where
@@ -109,6 +121,11 @@ typedef struct {
   void* out_bf16;    /* optional bf16 copy of out (M x N): the next layer's PKC_PREC_BF16IN operand */
 } pkc_dense_fwd_args;
 int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream);
+/* pkc_dense_fwd in BatchNorm training mode (norm == PKC_NORM_BN_TRAIN, nslab == 1) whose column
+ * partials the producing matmul already wrote into work at part_rows rows per block
+ * (pkc_gemm_colstats: 128): merges them (Chan, fixed order) and applies — the same outputs with
+ * the statistics summed in that blocking. */
+int pkc_dense_fwd_pre(const pkc_dense_fwd_args* a, float* work, int part_rows, void* stream);
 /* floats of device workspace pkc_dense_fwd / pkc_dense_bwd need (per-16-row column partials) */
 int64_t pkc_dense_work_size(int M, int N);
 

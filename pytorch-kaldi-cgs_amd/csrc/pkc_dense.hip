@@ -94,19 +94,20 @@ __global__ __launch_bounds__(ET) void dense_stats_kernel(pkc_dense_fwd_args a, f
 #endif
 constexpr int FC_F = PKC_FIN_COLS, FR_F = 16;
 // STATE: write this rank's (n, mean, M2) per column to state[3N] instead (SyncBN, no side outputs)
+// rb: rows per partial block (ERB from the stats pass; 128 from pkc_gemm_colstats' tiles)
 template <bool STATE = false>
 __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a, float* part,
-                                                            float* state = nullptr) {
+                                                            float* state = nullptr, int rb = ERB) {
   __shared__ float sn[ET], smu[ET], sm2[ET];
   const int cl = threadIdx.x % FC_F, t = threadIdx.x / FC_F;
   const int c = blockIdx.x * FC_F + cl;
   const int64_t N = a.N;
-  const int nrb = (a.M + ERB - 1) / ERB;
+  const int nrb = (a.M + rb - 1) / rb;
   float n = 0.f, mu = 0.f, M2 = 0.f;
   if (c < a.N) {
 #pragma unroll 4
     for (int k = t; k < nrb; k += FR_F) {
-      const float nk = (float)min(ERB, a.M - k * ERB);
+      const float nk = (float)min(rb, a.M - k * rb);
       const float mk = part[(int64_t)k * 2 * N + c];
       const float M2k = part[(int64_t)k * 2 * N + N + c];
       const float nn = n + nk;
@@ -231,7 +232,11 @@ __device__ __forceinline__ void st_h4(void* p, int64_t i, float4 v) {   // i % 4
   *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(p) + i) = h;
 }
 
-__global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, const float* part) {
+// staged: BN training reads z from xhat (the stats pass staged the slab sum there); otherwise z is
+// the one slab + bias (pkc_dense_fwd_pre).  rb: rows per partial block of `part` (its merged
+// statistics follow the ceil(M / rb) partial blocks).
+__global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, const float* part,
+                                                         int rb = ERB, bool staged = true) {
   const int c = blockIdx.x * EC + threadIdx.x % EC;
   const int t = threadIdx.x / EC;
   const int r0 = blockIdx.y * ERB;
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
   float mean = 0.f, invstd = 1.f, gam = 1.f, bet = 0.f;
   if (a.norm == PKC_NORM_BN_TRAIN) {
     if (cok) {   // the column statistics, merged once per column by dense_finalize_kernel
-      const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+      const float* fin = part + (int64_t)((a.M + rb - 1) / rb) * 2 * N;
       mean = fin[c];
       invstd = 1.f / sqrtf(fin[N + c] + a.eps);
       gam = a.gamma[c];
@@ -264,8 +269,9 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
     if (r >= a.M) break;
     const int64_t idx = r * N + c;
     // BN training: z was staged in xhat by the stats pass; otherwise sum the slabs here
-    const float z = (a.norm == PKC_NORM_BN_TRAIN) ? a.xhat[idx]
-                                                 : slab_sum(a.zslab + idx, a.slab_stride, a.nslab) + b;
+    const float z = (a.norm == PKC_NORM_BN_TRAIN && staged)
+                        ? a.xhat[idx]
+                        : slab_sum(a.zslab + idx, a.slab_stride, a.nslab) + b;
     const float xh = (a.norm == PKC_NORM_NONE) ? z : (z - mean) * invstd;
     const float y = (a.norm == PKC_NORM_NONE) ? z : xh * gam + bet;
     float o = act_fwd(a.act, y);
@@ -749,7 +755,8 @@ __global__ __launch_bounds__(ET) void dense_stats_v4_kernel(pkc_dense_fwd_args a
   }
 }
 
-__global__ __launch_bounds__(ET) void dense_apply_v4_kernel(pkc_dense_fwd_args a, const float* part) {
+__global__ __launch_bounds__(ET) void dense_apply_v4_kernel(pkc_dense_fwd_args a, const float* part,
+                                                            int rb = ERB, bool staged = true) {
   const int c = (blockIdx.x * EC4 + threadIdx.x % EC4) * 4;
   const int t = threadIdx.x / EC4;
   const int r0 = blockIdx.y * ERB;
@@ -758,7 +765,7 @@ __global__ __launch_bounds__(ET) void dense_apply_v4_kernel(pkc_dense_fwd_args a
   float mean[4] = {0.f, 0.f, 0.f, 0.f}, invstd[4] = {1.f, 1.f, 1.f, 1.f};
   float gam[4] = {1.f, 1.f, 1.f, 1.f}, bet[4] = {0.f, 0.f, 0.f, 0.f};
   if (a.norm == PKC_NORM_BN_TRAIN) {
-    const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+    const float* fin = part + (int64_t)((a.M + rb - 1) / rb) * 2 * N;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       mean[j] = fin[c + j];
@@ -785,8 +792,9 @@ __global__ __launch_bounds__(ET) void dense_apply_v4_kernel(pkc_dense_fwd_args a
     const int r = r0 + t + ER * i;
     if (r >= a.M) break;
     const int64_t idx = r * N + c;
-    const float4 zz = (a.norm == PKC_NORM_BN_TRAIN) ? ld4(a.xhat + idx)
-                                                    : f4add(slab_sum_v4(a.zslab + idx, a.slab_stride, a.nslab), b);
+    const float4 zz = (a.norm == PKC_NORM_BN_TRAIN && staged)
+                          ? ld4(a.xhat + idx)
+                          : f4add(slab_sum_v4(a.zslab + idx, a.slab_stride, a.nslab), b);
     float4 xh, o;
     uint32_t kw = 0;
     uchar4 kin = make_uchar4(1, 1, 1, 1);
@@ -1002,11 +1010,38 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
     { if (v4) hipLaunchKernelGGL(dense_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
     PKC_LAUNCH_CHECK("pkc_dense_fwd stats");
     hipLaunchKernelGGL(dense_finalize_kernel<false>, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0,
-                       S(stream), *a, work, nullptr);
+                       S(stream), *a, work, nullptr, ERB);
     PKC_LAUNCH_CHECK("pkc_dense_fwd finalize");
   }
-  { if (v4) hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
+  { if (v4) hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, ERB, true); else hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, ERB, true); }
   PKC_LAUNCH_CHECK("pkc_dense_fwd apply");
+  return PKC_OK;
+}
+
+// BatchNorm training forward whose column partials (mean incl. bias, M2 per part_rows-row block)
+// the producing matmul already wrote into work (pkc_gemm_colstats, part_rows = 128): the merge and
+// the apply pass only — no stats pass, z read once, from the one slab.
+extern "C" int pkc_dense_fwd_pre(const pkc_dense_fwd_args* a, float* work, int part_rows,
+                                 void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab == 1 && a->zslab && a->out && work,
+                "pkc_dense_fwd_pre: bad arguments (one slab)");
+  PKC_CHECK_ARG(a->norm == PKC_NORM_BN_TRAIN && a->gamma && a->beta && a->running_mean &&
+                    a->running_var && a->save_mean && a->save_invstd && a->xhat,
+                "pkc_dense_fwd_pre: BN training only (gamma/beta/running stats/save buffers/xhat)");
+  PKC_CHECK_ARG(part_rows >= ERB, "pkc_dense_fwd_pre: part_rows %d < %d", part_rows, ERB);
+  PKC_CHECK_ARG(a->drop_p >= 0.f && a->drop_p < 1.f, "pkc_dense_fwd_pre: drop_p out of range");
+  dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  hipLaunchKernelGGL(dense_finalize_kernel<false>, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F),
+                     0, S(stream), *a, work, nullptr, part_rows);
+  PKC_LAUNCH_CHECK("pkc_dense_fwd_pre finalize");
+  if (v4)
+    hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, part_rows, false);
+  else
+    hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, part_rows, false);
+  PKC_LAUNCH_CHECK("pkc_dense_fwd_pre apply");
   return PKC_OK;
 }
 
@@ -1065,7 +1100,7 @@ extern "C" int pkc_dense_fwd_stats(const pkc_dense_fwd_args* a, float* work, flo
   const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
   { if (v4) hipLaunchKernelGGL(dense_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   hipLaunchKernelGGL(dense_finalize_kernel<true>, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0,
-                     S(stream), *a, work, state);
+                     S(stream), *a, work, state, ERB);
   PKC_LAUNCH_CHECK("pkc_dense_fwd_stats");
   return PKC_OK;
 }
@@ -1081,7 +1116,7 @@ extern "C" int pkc_dense_fwd_sync_apply(const pkc_dense_fwd_args* a, float* work
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
   const bool v4 = v4_fwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
-  { if (v4) hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
+  { if (v4) hipLaunchKernelGGL(dense_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, ERB, true); else hipLaunchKernelGGL(dense_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, ERB, true); }
   PKC_LAUNCH_CHECK("pkc_dense_fwd_sync_apply");
   return PKC_OK;
 }

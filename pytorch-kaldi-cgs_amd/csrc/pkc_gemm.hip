@@ -418,31 +418,35 @@ __device__ __forceinline__ void xcd_tile(int remap, int& bx, int& by, int& bz) {
   bz = id / (nx * ny);
 }
 
-template <int NB, bool AKC, bool BKC>
+// STATS: the tile's BatchNorm column statistics in the epilogue (pkc_gemm_colstats)
+template <int NB, bool AKC, bool BKC, bool STATS>
 __global__ __launch_bounds__(big::NT) void gemm_glds_kernel(int M, int N, int K,
                                                            const void* __restrict__ A, int64_t lda,
                                                            const void* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc,
                                                            int kchunk, int64_t slab_stride,
-                                                           int remap) {
+                                                           int remap, const float* __restrict__ bias,
+                                                           float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char lds[big::gl_lds_bytes<NB>()];
   int bx, by, bz;
   xcd_tile(remap, bx, by, bz);
-  big::body_glds<NB, AKC, BKC>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk, slab_stride);
+  big::body_glds<NB, AKC, BKC, STATS>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk,
+                                      slab_stride, bias, part);
 }
 
-template <int PREC, bool BIN, bool AKC, bool BKC>
+template <int PREC, bool BIN, bool AKC, bool BKC, bool STATS>
 __global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
                                                           const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,
                                                           float* __restrict__ C, int64_t ldc,
                                                           int kchunk, int64_t slab_stride,
-                                                          int remap) {
+                                                          int remap, const float* __restrict__ bias,
+                                                          float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char lds[big::LDS_BYTES];
   int bx, by, bz;
   xcd_tile(remap, bx, by, bz);
-  big::body<PREC, BIN, AKC, BKC>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk,
-                                 slab_stride);
+  big::body<PREC, BIN, AKC, BKC, STATS>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk,
+                                        slab_stride, bias, part);
 }
 
 // Several independent matmuls in ONE launch (e.g. a layer's dW and dX, both heads' logits):
@@ -614,10 +618,10 @@ static int glds_bufs() {                      // PKC_GLDS_BUFS: LDS-DMA ring dep
   return nb;
 }
 
-template <int PREC, bool BIN>
+template <int PREC, bool BIN, bool STATS = false>
 static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, float* C, int64_t ldc, int splits, int64_t slab,
-                      hipStream_t s) {
+                      hipStream_t s, const float* bias = nullptr, float* part = nullptr) {
   constexpr int BKB = big::Cfg<PREC, BIN>::BK;
   int kchunk = (K + splits - 1) / splits;
   kchunk = ((kchunk + BKB - 1) / BKB) * BKB;
@@ -628,8 +632,8 @@ static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int6
   // 8192^3 755 -> 656 TF/s), same run
   if (BIN && K % 64 == 0 && (int64_t)grid.x * grid.y * grid.z <= 256 && glds_enabled()) {
 #define PKC_L(NB, AK, BK_)                                                                      \
-  hipLaunchKernelGGL((gemm_glds_kernel<NB, AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, lda,  \
-                     B, ldb, C, ldc, kchunk, slab, xcd_remap())
+  hipLaunchKernelGGL((gemm_glds_kernel<NB, AK, BK_, STATS>), grid, dim3(big::NT), 0, s, M, N, K, A, \
+                     lda, B, ldb, C, ldc, kchunk, slab, xcd_remap(), bias, part)
 #define PKC_LN(NB)                                                                              \
   if (akc && bkc) PKC_L(NB, true, true);                                                        \
   else if (akc) PKC_L(NB, true, false);                                                         \
@@ -645,8 +649,8 @@ static int launch_big(int akc, int bkc, int M, int N, int K, const void* A, int6
     return PKC_OK;
   }
 #define PKC_L(AK, BK_)                                                                          \
-  hipLaunchKernelGGL((gemm_big_kernel<PREC, BIN, AK, BK_>), grid, dim3(big::NT), 0, s, M, N, K, A, \
-                     lda, B, ldb, C, ldc, kchunk, slab, xcd_remap())
+  hipLaunchKernelGGL((gemm_big_kernel<PREC, BIN, AK, BK_, STATS>), grid, dim3(big::NT), 0, s, M, N, \
+                     K, A, lda, B, ldb, C, ldc, kchunk, slab, xcd_remap(), bias, part)
   if (akc && bkc) PKC_L(true, true);
   else if (akc) PKC_L(true, false);
   else if (bkc) PKC_L(false, true);
@@ -736,6 +740,33 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
                                          ldc, splits, slab_stride, S(stream));
   return dispatch<PKC_PREC_BF16, false>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C, ldc,
                                         splits, slab_stride, S(stream));
+}
+
+extern "C" int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                                    const void* A, int64_t lda, const void* B, int64_t ldb) {
+  using namespace pkc;
+  return (prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN) && M > 0 &&
+                 N > 0 && K > 0 && big_enabled() &&
+                 big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, BIG_MIN_TILES)
+             ? 1
+             : 0;
+}
+
+extern "C" int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                                 const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
+                                 int64_t ldc, const float* bias, float* part, void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(A && B && C && part && ldc >= N, "pkc_gemm_colstats: bad arguments");
+  PKC_CHECK_ARG(pkc_gemm_colstats_ok(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb),
+                "pkc_gemm_colstats: %dx%dx%d (prec %d) does not take the 128x128 body", M, N, K, prec);
+  if (prec == PKC_PREC_FP32)
+    return launch_big<PKC_PREC_FP32, false, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
+                                                  ldc, 1, 0, S(stream), bias, part);
+  if (prec == PKC_PREC_BF16IN)
+    return launch_big<PKC_PREC_BF16, true, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
+                                                 ldc, 1, 0, S(stream), bias, part);
+  return launch_big<PKC_PREC_BF16, false, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
+                                                ldc, 1, 0, S(stream), bias, part);
 }
 
 extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream) {

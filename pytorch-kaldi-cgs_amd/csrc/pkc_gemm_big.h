@@ -262,14 +262,92 @@ __device__ __forceinline__ void tile_mfma(const char* __restrict__ sa, const cha
   }
 }
 
+// Column statistics of a finished 128x128 tile for the BatchNorm that consumes it (the large-batch
+// MLP forward, pkc_gemm_colstats): per column, the mean of its rows < M in this tile plus bias[c],
+// and M2 = sum (z - mean)^2 — two passes over the accumulators (sums, then squared deviations from
+// the tile mean), combined over the two 32-lane halves (shuffle) and the two row waves (LDS) in a
+// fixed order.  -> part[by * 2N + c] = mean, part[by * 2N + N + c] = M2 (by = 128-row block), the
+// per-block partials pkc_dense_fwd_pre merges with Chan's formula.  Every wave calls it (barriers).
+__device__ __forceinline__ void tile_colstats(const f32x16 (&acc)[2][2], char* __restrict__ lds,
+                                              int m0, int n0, int by, int M, int N, int wm, int wn,
+                                              int lane, const float* __restrict__ bias,
+                                              float* __restrict__ part) {
+  float* red = reinterpret_cast<float*>(lds);     // [2 passes][2 row waves][128 columns]
+  const int r = lane & 31, h = lane >> 5;
+  const int nv = min(TM, M - m0);                 // valid rows of the tile (>= 1)
+  float mean[2];
+  __syncthreads();                                // every wave is done with the operand buffers
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int rl = wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        s += rl < nv ? acc[a][b][reg] : 0.f;
+      }
+    s += __shfl_xor(s, 32);
+    if (h == 0) red[wm * TN + wn * 64 + 32 * b + r] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int cl = wn * 64 + 32 * b + r;
+    mean[b] = (red[cl] + red[TN + cl]) / (float)nv;
+    float q = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int rl = wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const float d = acc[a][b][reg] - mean[b];
+        q += rl < nv ? d * d : 0.f;
+      }
+    q += __shfl_xor(q, 32);
+    if (h == 0) red[2 * TN + wm * TN + cl] = q;
+  }
+  __syncthreads();
+  if (wm != 0 || h != 0) return;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int cl = wn * 64 + 32 * b + r, col = n0 + cl;
+    if (col >= N) continue;
+    part[(int64_t)by * 2 * N + col] = mean[b] + (bias ? bias[col] : 0.f);
+    part[(int64_t)by * 2 * N + N + col] = red[2 * TN + cl] + red[3 * TN + cl];
+  }
+}
+
+// C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+__device__ __forceinline__ void tile_store(const f32x16 (&acc)[2][2], int m0, int n0, int M, int N,
+                                           int wm, int wn, int lane, float* __restrict__ Cz,
+                                           int64_t ldc) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int col = n0 + wn * 64 + 32 * b + r;
+    if (col >= N) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = m0 + wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < M) Cz[(int64_t)row * ldc + col] = acc[a][b][reg];
+      }
+    }
+  }
+}
+
 // C[bz slab][m0.., n0..] = A[m0.., kbeg..kend) . B[n0.., kbeg..kend)^T for one 128x128 tile.
-// `lds` is LDS_BYTES of workgroup memory.
-template <int PREC, bool BIN, bool AKC, bool BKC>
+// `lds` is LDS_BYTES of workgroup memory.  STATS: also the tile's column statistics
+// (tile_colstats; one slab, kchunk >= K).
+template <int PREC, bool BIN, bool AKC, bool BKC, bool STATS = false>
 __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int bz, int M, int N,
                                      int K, const void* __restrict__ Av, int64_t lda,
                                      const void* __restrict__ Bv, int64_t ldb,
                                      float* __restrict__ Cp, int64_t ldc, int kchunk,
-                                     int64_t slab_stride) {
+                                     int64_t slab_stride, const float* __restrict__ bias = nullptr,
+                                     float* __restrict__ part = nullptr) {
   using Cf = Cfg<PREC, BIN>;
   using HE = typename Cf::HE;
   constexpr int BK = Cf::BK;
@@ -331,22 +409,8 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
       __syncthreads();
     }
   }
-  // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
-  float* Cz = Cp + (int64_t)bz * slab_stride;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int col = n0 + wn * 64 + 32 * b + r;
-    if (col >= N) continue;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int row = m0 + wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (row < M) Cz[(int64_t)row * ldc + col] = acc[a][b][reg];
-      }
-    }
-  }
+  tile_store(acc, m0, n0, M, N, wm, wn, lane, Cp + (int64_t)bz * slab_stride, ldc);
+  if constexpr (STATS) tile_colstats(acc, lds, m0, n0, by, M, N, wm, wn, lane, bias, part);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -401,12 +465,13 @@ __device__ __forceinline__ void wait_tiles(int n) {
   }
 }
 
-template <int NB, bool AKC, bool BKC>
+template <int NB, bool AKC, bool BKC, bool STATS = false>
 __device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by, int bz, int M,
                                           int N, int K, const void* __restrict__ Av, int64_t lda,
                                           const void* __restrict__ Bv, int64_t ldb,
                                           float* __restrict__ Cp, int64_t ldc, int kchunk,
-                                          int64_t slab_stride) {
+                                          int64_t slab_stride, const float* __restrict__ bias = nullptr,
+                                          float* __restrict__ part = nullptr) {
   const __bf16* A = reinterpret_cast<const __bf16*>(Av);
   const __bf16* B = reinterpret_cast<const __bf16*>(Bv);
   const int m0 = by * TM, n0 = bx * TN;
@@ -441,24 +506,11 @@ __device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by
     const char* cur = buf(t);
     tile_mfma<PKC_PREC_BF16, !AKC, !BKC>(cur, cur + TILE_BYTES, wm, wn, lane, acc);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();             // every wave has read buffer t % 3
+    __builtin_amdgcn_s_barrier();             // every wave has read buffer t % NB
     asm volatile("" ::: "memory");
   }
-  float* Cz = Cp + (int64_t)bz * slab_stride;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int col = n0 + wn * 64 + 32 * b + r;
-    if (col >= N) continue;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int row = m0 + wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (row < M) Cz[(int64_t)row * ldc + col] = acc[a][b][reg];
-      }
-    }
-  }
+  tile_store(acc, m0, n0, M, N, wm, wn, lane, Cp + (int64_t)bz * slab_stride, ldc);
+  if constexpr (STATS) tile_colstats(acc, lds, m0, n0, by, M, N, wm, wn, lane, bias, part);
 }
 
 // Which problems take this body: 16-byte operand paths (aligned bases and leading dimensions,

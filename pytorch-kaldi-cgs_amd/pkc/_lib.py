@@ -113,6 +113,11 @@ _SIGS = {
                            vp, i64, C.c_int, i64, vp]),
     "pkc_gemm_pick_splits": (C.c_int, [C.c_int, C.c_int, C.c_int]),
     "pkc_dense_fwd": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp]),
+    "pkc_dense_fwd_pre": (C.c_int, [C.POINTER(DenseFwdArgs), vp, C.c_int, vp]),
+    "pkc_gemm_colstats_ok": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64,
+                                       vp, i64]),
+    "pkc_gemm_colstats": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64, vp,
+                                    i64, vp, i64, vp, vp, vp]),
     "pkc_dense_bwd": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp]),
     "pkc_dense_work_size": (i64, [C.c_int, C.c_int]),
     "pkc_dense_fwd_stats": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp, vp]),

@@ -56,6 +56,9 @@ DW_SPLIT_ROWS = int(os.environ.get("PKC_DW_SPLIT_ROWS", "1024"))
 # dW of the step's last matmul launch) rides in the NEXT step's first launch, beside that step's
 # batch gather (PKC_OP_GATHER): one launch per step fewer; 0: off (A/B)
 DEFER_TAIL = os.environ.get("PKC_DEFER_TAIL", "1") != "0"
+# large-batch BatchNorm'd MLP layers: column statistics in the forward matmul's epilogue
+# (pkc_gemm_colstats + pkc_dense_fwd_pre); PKC_GEMM_COLSTATS=0: matmul + stats/finalize/apply (A/B)
+COLSTATS = os.environ.get("PKC_GEMM_COLSTATS", "1") != "0"
 # recurrent layers' dW / dU split-K cap (1: unsplit, A/B)
 REC_DW_SPLITS = int(os.environ.get("PKC_REC_DW_SPLITS", "4"))
 # recurrent layers: sum the output-gradient slabs before the BPTT loop (0: per step, A/B)
@@ -1237,12 +1240,40 @@ class Engine:
 
     def _dense_fwd(self, n, s, train):
         self._quant_chain(n, s)
-        self._gemms([self._fwd_problem(n)], s)
+        prob = self._fwd_problem(n)
+        if train and self._colstats_fwd(n, prob, s):
+            return
+        self._gemms([prob], s)
         self._fwd_epilogue(n, s, train)
 
-    def _fwd_epilogue(self, n, s, train, out=None):
+    def _colstats_fwd(self, n, prob, s):
+        """Large-batch BatchNorm'd MLP layer in training: the forward matmul writes the BatchNorm
+        column partials of its 128-row tiles in its epilogue (pkc_gemm_colstats) and
+        pkc_dense_fwd_pre merges them and applies, so no statistics pass re-reads z.  Only where
+        the 128x128 tile body takes the matmul (one slab); sequence models keep the stats-pass
+        blocking their recurrent lifecycle tests are pinned to.  Returns False when not taken."""
+        if not (COLSTATS and n.bn and not n.ln and not n.head and n.W is not None and not self.seq
+                and self.M > 128 and getattr(n, "bn_states", None) is None):
+            return False
+        lab, fl, nb, p = prob[:4]
+        if p.splits != 1 or p.ktiles:
+            return False
+        prec = self.prec
+        if len(prob) > 4 and prob[4] is not None:
+            prec, (nb, p) = L.PREC_BF16IN, prob[4]
+        if not L.lib().pkc_gemm_colstats_ok(prec, p.a_kcontig, p.b_kcontig, p.M, p.N, p.K,
+                                            C.c_void_p(p.A), p.lda, C.c_void_p(p.B), p.ldb):
+            return False
+        self._k("gemm_colstats " + lab, fl, nb + 8.0 * p.N * -(-p.M // 128), "pkc_gemm_colstats",
+                prec, p.a_kcontig, p.b_kcontig, p.M, p.N, p.K, C.c_void_p(p.A), p.lda,
+                C.c_void_p(p.B), p.ldb, C.c_void_p(p.C), p.ldc, ptr(n.b), ptr(n.work), s)
+        self._fwd_epilogue(n, s, True, pre_rows=128)
+        return True
+
+    def _fwd_epilogue(self, n, s, train, out=None, pre_rows=0):
         """The layer's epilogue launch (BN/act/dropout, or a head's LogSoftmax/NLL); with `out`
-        the head's NllArgs are only filled in (for a grouped launch)."""
+        the head's NllArgs are only filled in (for a grouped launch).  pre_rows: the BatchNorm
+        column partials are already in n.work at that blocking (pkc_gemm_colstats)."""
         M = self.M
         if n.W is None:                      # input normalisation: no matmul in front
             x_ptr, ldx = self._src(n)
@@ -1301,6 +1332,10 @@ class Engine:
             self.sync_bn(n.bn_states)
             self._k("dense_fwd_sync_apply N=%d" % n.N, 0, 4.0 * M * n.N * 3,
                     "pkc_dense_fwd_sync_apply", C.byref(a), ptr(n.work), ptr(n.bn_states), R, s)
+            return
+        if pre_rows:
+            self._k("dense_fwd_pre N=%d" % n.N, 0, 4.0 * M * n.N * 3, "pkc_dense_fwd_pre",
+                    C.byref(a), ptr(n.work), pre_rows, s)
             return
         self._k("dense_fwd N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_dense_fwd",
                 C.byref(a), ptr(n.work), s)
@@ -1437,7 +1472,11 @@ class Engine:
                 grp.append(nodes[i + len(grp)])
             for g in grp:
                 self._quant_chain(g, s)
-            self._gemms([self._fwd_problem(g) for g in grp], s)
+            probs = [self._fwd_problem(g) for g in grp]
+            if len(grp) == 1 and train and self._colstats_fwd(n, probs[0], s):
+                i += 1
+                continue
+            self._gemms(probs, s)
             if len(grp) > 1:
                 self._nll_multi(grp, s, train)
             else:

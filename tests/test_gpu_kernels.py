@@ -521,3 +521,70 @@ def test_gemm_grouped_sparse_big_slabsum(L, prec):
     torch.testing.assert_close(C2.cpu(), (A2.double() @ B2.double().t()).float(), rtol=1e-4,
                                atol=tol * 1024 ** 0.5)
     assert torch.equal(Cs.cpu(), (slabs[0] + slabs[1]) + slabs[2])
+
+
+# the large-batch forward with the BatchNorm column statistics in the matmul epilogue: shapes that
+# take the 128x128 body (LDS-DMA ring: bf16-stored operands, K % 64 == 0; register body otherwise),
+# ragged row / column tails, the first layer's K = 440
+COLSTATS_SHAPES = [(4096, 1024, 1024, 2), (4096, 1024, 440, 2), (2056, 1288, 1024, 2),
+                   (2056, 1288, 1000, 1), (4096, 4096, 256, 0)]
+
+
+@pytest.mark.parametrize("M,N,K,prec", COLSTATS_SHAPES)
+def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
+    """pkc_gemm_colstats: the one-slab product and per-128-row-block column (mean + bias, M2) vs
+    fp64 of the same operands; pkc_dense_fwd_pre on those partials vs pkc_dense_fwd (the
+    stats-pass form) on the same slab — the same BatchNorm up to fp32 summation order."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * K ** -0.5
+    bias = torch.randn(N, generator=g) * 0.1
+    dt = torch.bfloat16 if prec == 2 else torch.float32
+    Ad, Wd, bd = A.to(DEV).to(dt).contiguous(), W.to(DEV).to(dt).contiguous(), bias.to(DEV)
+    if prec >= 1:
+        A, W = A.bfloat16().float(), W.bfloat16().float()
+    ok = L.lib().pkc_gemm_colstats_ok(prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K)
+    assert ok == 1, "shape should take the 128x128 body"
+    Cd = torch.full((M, N), float("nan"), device=DEV)
+    work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
+    L.call("pkc_gemm_colstats", prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K, L.ptr(Cd), N,
+           L.ptr(bd), L.ptr(work), _s())
+    ref = A.double() @ W.double().t()
+    tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
+    torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-4, atol=tol)
+    nb = -(-M // 128)
+    part = work[:2 * N * nb].view(nb, 2, N).cpu().double()
+    z = Cd.cpu().double() + bias.double()
+    for b in range(nb):
+        blk = z[128 * b:128 * (b + 1)]
+        mu = blk.mean(0)
+        torch.testing.assert_close(part[b, 0], mu, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(part[b, 1], ((blk - mu) ** 2).sum(0), rtol=1e-4, atol=1e-4)
+    # the apply from the partials vs the stats-pass form on the same slab
+    gamma = (torch.rand(N, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    outs = []
+    for fn in ("pkc_dense_fwd", "pkc_dense_fwd_pre"):
+        rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+        sm, si = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+        xhat, out = torch.zeros(M, N, device=DEV), torch.zeros(M, N, device=DEV)
+        keep = torch.zeros(M, N, dtype=torch.uint8, device=DEV)
+        a_ = L.DenseFwdArgs(M=M, N=N, nslab=1, zslab=Cd.data_ptr(), slab_stride=M * N,
+                            bias=bd.data_ptr(), norm=L.NORM_BN_TRAIN, gamma=gamma.data_ptr(),
+                            beta=beta.data_ptr(), running_mean=rm.data_ptr(),
+                            running_var=rv.data_ptr(), momentum=0.05, eps=1e-5,
+                            save_mean=sm.data_ptr(), save_invstd=si.data_ptr(), act=L.ACT["relu"],
+                            drop_p=0.15, seed=5, step_ctr=None, stream_id=3, keep_in=None,
+                            keep_out=keep.data_ptr(), xhat=xhat.data_ptr(), out=out.data_ptr())
+        if fn == "pkc_dense_fwd":
+            w2 = torch.zeros_like(work)
+            L.call(fn, C.byref(a_), L.ptr(w2), _s())
+        else:
+            L.call(fn, C.byref(a_), L.ptr(work), 128, _s())
+        outs.append((out.cpu(), xhat.cpu(), keep.cpu(), rm.cpu(), rv.cpu(), sm.cpu(), si.cpu()))
+    (o0, x0, k0, rm0, rv0, sm0, si0), (o1, x1, k1, rm1, rv1, sm1, si1) = outs
+    assert torch.equal(k0, k1)                   # same dropout bits
+    torch.testing.assert_close(x1, x0, rtol=1e-4, atol=2e-5)
+    torch.testing.assert_close(o1, o0, rtol=1e-4, atol=2e-5)
+    for u, v in ((rm1, rm0), (rv1, rv0), (sm1, sm0), (si1, si0)):
+        torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
