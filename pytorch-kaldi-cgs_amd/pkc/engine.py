@@ -39,7 +39,10 @@ MAX_SPLITS = int(os.environ.get("PKC_MAX_SPLITS", "4"))
 # the 1928-wide head's dX gets 7 K-splits instead of 3).  C2, same run, frames/s: 4 -> 668-670k,
 # 5 -> 674-677k, 6 -> 675-677k, 8 -> 682-683k
 SLAB_BUDGET_MULTI = min(8, int(os.environ.get("PKC_SLAB_BUDGET_MULTI", "8")))
-MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", str(MAX_SPLITS)))   # forward Z = X W^T
+# forward Z = X W^T (0: by precision — MAX_SPLITS for bf16 operands; 8 for exact fp32, whose
+# 128-row forward matmuls are bound by each workgroup's fp32 operand bytes and MFMA chain: C2 fp32
+# 565k -> 578k frames/s with 8, 487k with 2, same box, profiles/r03_fp32_splits_ab.txt)
+MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", "0"))
 # spread optimizer updates: a layer's update larger than this many parameters is cut into parts
 # that ride in successive backward launches (0: one part).  Round 1 (fp32-stored operands), C2
 # frames/s: 0 -> 653-657k, 1.2M -> 663k, 700k -> 666-667k, 400k-520k -> 669-671k, 250k -> 644k.
@@ -627,7 +630,8 @@ class Engine:
                 self._alloc_rec(n)
                 continue
             N, K = n.N, n.K
-            n.scap = self.cap or _splits(M, N, K, MAX_SPLITS_FWD)
+            n.scap = self.cap or _splits(M, N, K, MAX_SPLITS_FWD or
+                                         (8 if self.prec == L.PREC_FP32 else MAX_SPLITS))
             n.zslab = _f32(n.scap * M * N, dev) if n.W is not None else None
             if n.ln:
                 n.ln_y, n.ln_xhat = _f32(M * N, dev), _f32(M * N, dev)
