@@ -94,6 +94,41 @@ struct Stage {
       }
     }
   }
+  // VEC form with the row part of the addresses hoisted (StageH::lane_base / load_at): chunk i of
+  // this thread is row (t >> 3) + 32 i, k (t & 7) * 4 (KC) or row (t & 15) * 4, k (t >> 4) + 16 i
+  struct Base {
+    const float* p[2];
+    bool ok[2];
+  };
+  __device__ __forceinline__ static Base lane_base(const void* __restrict__ Pv, int64_t ld, int r0,
+                                                   int rmax) {
+    const float* P = reinterpret_cast<const float*>(Pv);
+    const int t = threadIdx.x;
+    Base b;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = KC ? (t >> 3) + 32 * i : (t & 15) * 4;
+      const int rr = min(r0 + r, rmax - (KC ? 1 : 4));
+      b.p[i] = KC ? P + (int64_t)rr * ld : P + rr;
+      b.ok[i] = r0 + r < rmax;
+    }
+    return b;
+  }
+  __device__ __forceinline__ void load_at(const Base& b, int ld, int k0, int kend) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = KC ? (t & 7) * 4 : (t >> 4) + 16 * i;
+      const bool ok = b.ok[i] && (k0 + k < kend);
+      const int kk = min(k0 + k, kend - (KC ? 4 : 1));
+      const float4 x = KC ? *reinterpret_cast<const float4*>(b.p[i] + kk)
+                          : *reinterpret_cast<const float4*>(b.p[i] + (int64_t)kk * ld);
+      v[4 * i + 0] = ok ? x.x : 0.f;
+      v[4 * i + 1] = ok ? x.y : 0.f;
+      v[4 * i + 2] = ok ? x.z : 0.f;
+      v[4 * i + 3] = ok ? x.w : 0.f;
+    }
+  }
   template <typename T, int LD>
   __device__ __forceinline__ void store(T* __restrict__ s) const {
     const int t = threadIdx.x;
@@ -194,6 +229,29 @@ struct StageH {
       }
     }
   }
+  // VEC form with the row part of the address hoisted: lane_base() once per launch (the row clamp
+  // and, for KC, the 64-bit row product), load_at() per k-tile (a 32-bit k offset, or one
+  // 32x32->64 product for m-contiguous operands).  Same clamps and zeroing as load().
+  struct Base {
+    const __bf16* p;
+    bool ok;
+  };
+  __device__ __forceinline__ static Base lane_base(const void* __restrict__ Pv, int64_t ld, int r0,
+                                                   int rmax) {
+    const __bf16* P = reinterpret_cast<const __bf16*>(Pv);
+    const int t = threadIdx.x;
+    const int r = KC ? t >> 2 : (t & 7) * 8;
+    const int rr = min(r0 + r, rmax - (KC ? 1 : 8));
+    return Base{KC ? P + (int64_t)rr * ld : P + rr, r0 + r < rmax};
+  }
+  __device__ __forceinline__ void load_at(const Base& b, int ld, int k0, int kend) {
+    const int t = threadIdx.x;
+    const int k = KC ? (t & 3) * 8 : t >> 3;
+    const bool ok = b.ok && (k0 + k < kend);
+    const int kk = min(k0 + k, kend - (KC ? 8 : 1));
+    const bf16x8 x = KC ? ld8h(b.p + kk) : ld8h(b.p + (int64_t)kk * ld);
+    v = ok ? x : zero8h();
+  }
   template <typename T, int LD>
   __device__ __forceinline__ void store(T* __restrict__ s) const {
     const int t = threadIdx.x;
@@ -285,7 +343,60 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
 
   SA sa[DEPTH];
   SB sb[DEPTH];
-  if (kbeg < kend) {   // uniform: an empty trailing split writes zeros
+  bool done = false;
+  if constexpr (VEC) {
+    // 16-byte operands whose whole k-range fits one round of DEPTH tiles (every forward / dX / dW
+    // matmul of the B = 128 step): the row part of each address computed once (lane_base), no
+    // refill loads for tiles past the range and no zero tiles.  Longer ranges take the general
+    // loop below.  (Leading dimensions are below 2^31 elements: pkc_gemm checks.)
+    const int nk = (kend - kbeg + BK - 1) / BK;             // uniform
+    if (kbeg < kend && nk <= DEPTH) {
+      const typename SA::Base ab = SA::lane_base(A, lda, m0, M);
+      const typename SB::Base bb = SB::lane_base(B, ldb, n0, N);
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        if (d >= nk) break;                                  // uniform
+        sa[d].load_at(ab, (int)lda, kbeg + d * BK, kend);
+        sb[d].load_at(bb, (int)ldb, kbeg + d * BK, kend);
+      }
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        if (d >= nk) break;                                  // uniform
+        __syncthreads();
+        sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
+        sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+        __syncthreads();
+        mfma_tile<PREC, AKC, BKC, BIN && !AKC, BIN && !BKC>(sm, wm, wn, r, h, acc);
+      }
+      done = true;
+    }
+  }
+  if constexpr (VEC) {
+    if (!done && kbeg < kend) {   // uniform; the same rounds as below, row addresses hoisted
+      const typename SA::Base ab = SA::lane_base(A, lda, m0, M);
+      const typename SB::Base bb = SB::lane_base(B, ldb, n0, N);
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        sa[d].load_at(ab, (int)lda, kbeg + d * BK, kend);
+        sb[d].load_at(bb, (int)ldb, kbeg + d * BK, kend);
+      }
+      for (int kt = kbeg; kt < kend; kt += DEPTH * BK) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+          __syncthreads();
+          sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
+          sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+          __syncthreads();
+          const int kn = kt + (d + DEPTH) * BK;
+          sa[d].load_at(ab, (int)lda, kn, kend);
+          sb[d].load_at(bb, (int)ldb, kn, kend);
+          mfma_tile<PREC, AKC, BKC, BIN && !AKC, BIN && !BKC>(sm, wm, wn, r, h, acc);
+        }
+      }
+      done = true;
+    }
+  }
+  if (!done && kbeg < kend) {   // uniform: an empty trailing split writes zeros
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
       sa[d].load(A, lda, m0, M, kbeg + d * BK, kend);
@@ -308,12 +419,14 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
   }
   // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
   const int col = n0 + wn * 32 + r;
-  float* Cz = C + (int64_t)bz * slab_stride;
+  const int row0 = m0 + wm * 32 + 4 * h;
   if (col < N) {
+    float* Cr = C + (int64_t)bz * slab_stride + (int64_t)row0 * ldc + col;
+    const int ldci = (int)ldc;          // < 2^26 (pkc_gemm checks): dr * ldci fits 32 bits
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int row = m0 + wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (row < M) Cz[(int64_t)row * ldc + col] = acc[reg];
+      const int dr = (reg & 3) + 8 * (reg >> 2);
+      if (row0 + dr < M) Cr[dr * ldci] = acc[reg];
     }
   }
 }
@@ -714,7 +827,9 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
                 "pkc_gemm: bad precision %d", prec);
   if (M == 0 || N == 0) return PKC_OK;
   PKC_CHECK_ARG(A && B && C, "pkc_gemm: null operand");
-  PKC_CHECK_ARG(ldc >= N, "pkc_gemm: ldc < N");
+  PKC_CHECK_ARG(lda > 0 && ldb > 0 && lda < (1ll << 31) && ldb < (1ll << 31),
+                "pkc_gemm: leading dimensions must be in [1, 2^31)");
+  PKC_CHECK_ARG(ldc >= N && ldc < (1ll << 26), "pkc_gemm: ldc must be in [N, 2^26)");
   if (splits <= 0) splits = pkc_gemm_pick_splits(M, N, K);
   PKC_CHECK_ARG(splits == 1 || slab_stride >= (int64_t)M * ldc, "pkc_gemm: slab_stride too small");
   // 16-byte path: aligned bases, leading dims and contiguous extents multiple of 16 bytes
@@ -836,9 +951,12 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
       continue;
     }
     PKC_CHECK_ARG(q.kind == PKC_OP_GEMM, "pkc_gemm_grouped: problem %d kind %d", i, q.kind);
-    PKC_CHECK_ARG(q.M >= 0 && q.N >= 0 && q.K >= 0 && q.ldc >= q.N, "pkc_gemm_grouped: problem %d shape", i);
+    PKC_CHECK_ARG(q.M >= 0 && q.N >= 0 && q.K >= 0 && q.ldc >= q.N && q.ldc < (1ll << 26),
+                  "pkc_gemm_grouped: problem %d shape", i);
     if (q.M == 0 || q.N == 0) continue;
     PKC_CHECK_ARG(q.A && q.B && q.C, "pkc_gemm_grouped: problem %d null operand", i);
+    PKC_CHECK_ARG(q.lda > 0 && q.ldb > 0 && q.lda < (1ll << 31) && q.ldb < (1ll << 31),
+                  "pkc_gemm_grouped: problem %d leading dimensions must be in [1, 2^31)", i);
     int splits = q.splits <= 0 ? pkc_gemm_pick_splits(q.M, q.N, q.K) : q.splits;
     PKC_CHECK_ARG(!q.ktiles || (splits == 1 && q.kmax >= 0 && q.a_kcontig),
                   "pkc_gemm_grouped: problem %d: k-tile lists need splits == 1 and a k-contiguous A",
