@@ -44,6 +44,8 @@ const char* pkc_last_error(void);
  * backward dW = dY^T X    : a_kcontig=0, b_kcontig=0
  * Split-K partial slabs are summed by the consumer kernels (dense_fwd/dense_bwd/nll) in a fixed
  * order, so results are deterministic.  splits<=0 picks a split count for the shape.
+ * Leading dimensions (elements): lda, ldb in [1, 2^31), ldc in [N, 2^26) — the kernels keep row
+ * offsets in 32 bits (PKC_ERR_ARG otherwise; pkc_gemm_grouped checks the same per problem).
  * ------------------------------------------------------------------------------------------- */
 int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
              const void* A, int64_t lda, const void* B, int64_t ldb,
