@@ -69,10 +69,15 @@ __device__ __forceinline__ float quant_w(float p, int bits) {
   return ceilf(fabsf(p) * sc) / sc * sg;
 }
 
-// Elements per thread of one optimizer work item (256 threads): measured on the C2 step, 4 and 16
-// give 0.200 ms, 8 gives 0.203 ms and 32 0.259 ms (register pressure); 16 = 4096-element items.
+// Elements per thread of one optimizer work item (256 threads).  The update also runs inside the
+// grouped backward launches (PKC_OP_OPTIM), whose register allocation is the maximum over every
+// operation they carry: at 16 elements per thread the update set it (193 VGPRs + 16 AGPRs: two
+// waves per SIMD for the whole launch), at 8 the matmul body does (145 + 16: three waves).  C2 step,
+// same box, two rounds (profiles/r03_opt_per_ab.txt): 16 -> 801-803k, 8 -> 846-848k, 4 -> 814-822k
+// frames/s; B = 4096 5.15-5.16M -> 5.20-5.21M.  (Round 1, one-kernel updates: 4 / 16 0.200 ms,
+// 8 0.203, 32 0.259.)  2048-element items.
 #ifndef PKC_OPT_PER
-#define PKC_OPT_PER 16
+#define PKC_OPT_PER 8
 #endif
 constexpr int OPT_T = 256, OPT_PER = PKC_OPT_PER, OPT_CHUNK = OPT_T * OPT_PER;
 

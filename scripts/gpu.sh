@@ -160,7 +160,7 @@ r_ab() {
   for i in 1 2; do for v in $AB_VALUES; do
     env "$AB_VAR=$v" timeout -k 10 300 python -u $AB_CMD > gpurun_out/ab_run.log 2>&1
     ok $? "ab $AB_VAR=$v"
-    grep -E '^\{|^ *[a-z0-9].*(TF/s|us)' gpurun_out/ab_run.log | sed "s/^/$AB_VAR=$v  /" | cut -c1-400 >> gpurun_out/ab.txt
+    grep -E '^\{|^ *[a-z0-9].*(TF/s|us)' gpurun_out/ab_run.log | sed "s|^|$AB_VAR=$v  |" | cut -c1-400 >> gpurun_out/ab.txt
   done; done
   cat gpurun_out/ab.txt
 }
