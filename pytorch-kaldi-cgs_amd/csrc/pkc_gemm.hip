@@ -582,8 +582,10 @@ struct GroupArgs {
 // SUM: the launch carries slab-sum operations (large-batch split-K dW); a separate instance,
 // because that body alone raises the kernel's VGPRs from 152 to 191 (occupancy 3 -> 2), which the
 // B = 128 step's lean launches cannot afford
-template <int PREC, bool BIN, bool BIG, bool SP = false, bool SUM = false, int GD = 4>
-__global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
+// VO: every matmul of the launch takes the 16-byte operand path (the B = 128 step's): the 2-byte
+// element-wise forms are not compiled in, so they do not set the launch's register allocation
+template <int PREC, bool BIN, bool BIG, bool SP, bool SUM, int GD, bool VO>
+__device__ __forceinline__ void grouped_body(const GroupArgs& g) {
   // BIG: at least one problem takes the 128x128 body; its LDS also holds the 64x64 tiles
   union alignas(16) Shm {
     Lds<PREC> t;
@@ -661,6 +663,15 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
 #define PKC_GB(AK, BK_, V)                                                                      \
   gemm_body<PREC, AK, BK_, V, GD, BIN>(sm, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, \
                                       p.ldc, p.kchunk, p.slab)
+  if constexpr (VO) {
+    switch (p.code) {
+      case 7: PKC_GB(true, true, true); break;
+      case 5: PKC_GB(true, false, true); break;
+      case 1: PKC_GB(false, false, true); break;
+      default: PKC_GB(false, true, true); break;
+    }
+    return;
+  }
   switch (p.code) {
     case 7: PKC_GB(true, true, true); break;
     case 6: PKC_GB(true, true, false); break;
@@ -674,11 +685,37 @@ __global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
 #undef PKC_GB
 }
 
+template <int PREC, bool BIN, bool BIG, bool SP = false, bool SUM = false, int GD = 4,
+          bool VO = false>
+__global__ __launch_bounds__(NT) void gemm_grouped_kernel(GroupArgs g) {
+  grouped_body<PREC, BIN, BIG, SP, SUM, GD, VO>(g);
+}
+
+// The vec-only instance held to 4 waves per SIMD (128 registers): at 113 VGPRs + 16 AGPRs the
+// bf16 form sits one register above that step (PKC_GROUPED_VO=2)
+template <int PREC, bool BIN>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void gemm_grouped_vo4_kernel(GroupArgs g) {
+  grouped_body<PREC, BIN, false, false, false, 4, true>(g);
+}
+
 // k-tiles in flight per workgroup for bf16-stored operands: a stage is one 16-byte register per
 // operand, so depth 8 costs 32 VGPRs more and puts a B = 128 split's whole k-range in flight at
 // once.  Standalone launches (PKC_GEMM_DEPTH, default 8): C2 706k -> 720k, B = 1024 1.97M ->
 // 2.06M frames/s; grouped launches (PKC_GEMM_DEPTH_G, default 4): 8 measured 664-669k, the
 // extra VGPRs cost their optimizer / dW work items residency (same runs)
+// Launches whose matmuls are all 16-byte: PKC_GROUPED_VO=2 (default) the vec-only instance held to
+// 4 waves per SIMD, 1 the vec-only instance, 0 the general instance.  Same box, two rounds
+// (profiles/r03_grouped_vo_ab.txt): C2 bf16 847-851k / 852-854k / 856-859k frames/s for 0 / 1 / 2,
+// the fp32 entry 622k (0) -> 634k (2)
+static int grouped_vo() {
+  static const int m = [] {
+    const char* v = getenv("PKC_GROUPED_VO");
+    return v ? atoi(v) : 2;
+  }();
+  return m;
+}
+
 static int bin_depth(bool grouped = false) {
   static const int d[2] = {[] {
     const char* v = getenv("PKC_GEMM_DEPTH");
@@ -892,7 +929,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   GroupArgs g;
   memset(&g, 0, sizeof(g));
   int wg = 0, k = 0;
-  bool any_big = false, any_sparse = false, any_sum = false;
+  bool any_big = false, any_sparse = false, any_sum = false, all_vec = true;
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   // a launch with block-sparse problems runs the sparse instance, which has no 128x128 body
   for (int i = 0; i < n; ++i) any_sparse |= probs[i].kind == PKC_OP_GEMM && probs[i].ktiles != nullptr;
@@ -970,6 +1007,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
                                                      q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED,
                                                      BIG_MIN_K_GROUPED);
     any_big |= bigp;
+    all_vec &= vec;
     const int bk = bigp ? (prec == PKC_PREC_FP32 ? 32 : 64) : BK;
     int kchunk = (q.K + splits - 1) / splits;
     kchunk = ((kchunk + bk - 1) / bk) * bk;
@@ -1005,6 +1043,11 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     else if (BIN && bin_depth(true) == 8)                                                       \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false, false, false, 8>), dim3(wg), dim3(NT), \
                          0, S(stream), g);                                                      \
+    else if (all_vec && grouped_vo() == 2)                                                      \
+      hipLaunchKernelGGL((gemm_grouped_vo4_kernel<P, BIN>), dim3(wg), dim3(NT), 0, S(stream), g); \
+    else if (all_vec && grouped_vo() == 1)                                                      \
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false, false, false, 4, true>), dim3(wg),  \
+                         dim3(NT), 0, S(stream), g);                                            \
     else                                                                                        \
       hipLaunchKernelGGL((gemm_grouped_kernel<P, BIN, false>), dim3(wg), dim3(NT), 0, S(stream), g); \
   } while (0)
