@@ -67,7 +67,7 @@ r_bench_prof() {
   cp "$S" gpurun_out/bprof/bench_kernel_stats.csv
   # anchor: the heads' NLL launch (once per step; with the deferred tail the gather rides in a
   # grouped launch inside the multi-step graphs): the listing starts there, one whole step long
-  python3 scripts/trace_gaps.py "$T" nll_multi_kernel "gemm_grouped_kernel<1, true" > gpurun_out/bprof/timeline.txt
+  python3 scripts/trace_gaps.py "$T" nll_multi_kernel "<1, true" > gpurun_out/bprof/timeline.txt
   tail -3 gpurun_out/bprof/timeline.txt
 }
 
@@ -126,7 +126,7 @@ r_b4k_prof() {
   ok $? b4k_prof
   cp "$(find /tmp/b4k -name 'b4k_kernel_stats.csv' -print -quit)" gpurun_out/b4k/kernel_stats.csv
   python3 scripts/trace_gaps.py "$(find /tmp/b4k -name 'b4k_kernel_trace.csv' -print -quit)" batch_gather \
-    "gemm_grouped_kernel<1, true" > gpurun_out/b4k/timeline.txt
+    "<1, true" > gpurun_out/b4k/timeline.txt
   tail -5 gpurun_out/b4k/timeline.txt
 }
 
