@@ -123,12 +123,13 @@ __device__ __forceinline__ float qin(float x, const QParams& p) {
   return ceilf(fabsf(q) * p.scale) * p.iscale * p.var * s;
 }
 
-template <bool FAST, int S>
+// R16: the tile's second row strip is all zeros (Q(0) = 0): only va is quantised
+template <bool FAST, int S, bool R16 = false>
 __device__ __forceinline__ void qin_strips(float* va, float* vb, const QParams& p) {
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     va[s] = qin<FAST>(va[s], p);
-    vb[s] = qin<FAST>(vb[s], p);
+    if constexpr (!R16) vb[s] = qin<FAST>(vb[s], p);
   }
 }
 
@@ -635,16 +636,29 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     }
     const QParams qp = qparams(vars[0], qscale);
     const bool qon = vars[0] != 0.f;
+    // gate g's columns take the product of q_{g+1}: one chain per gate into its own accumulators
+    // over the unmasked U strip, and each output column (lane & 15, gate gi) keeps its gate's
+    // accumulator — the same sums as masking the other gates' U columns to zero, without the
+    // per-gate mask pass (S selects per lane per gate)
+    f32x4 ag0[NG], ag1[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       if (qon) {
-        if (qp.fast) qin_strips<true, S>(va, vb, qp);
-        else qin_strips<false, S>(va, vb, qp);
+        if (qp.fast) qin_strips<true, S, R16>(va, vb, qp);
+        else qin_strips<false, S, R16>(va, vb, qp);
       }
-      float vg[S];
+      ag0[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ag1[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mfma_chain<S, R16>(va, vb, vu, ag0[g], ag1[g]);
+    }
+    acc0 = ag0[0];
+    acc1 = ag1[0];
 #pragma unroll
-      for (int s = 0; s < S; ++s) vg[s] = gi == g ? vu[s] : 0.f;
-      mfma_chain<S, R16>(va, vb, vg, acc0, acc1);
+    for (int g = 1; g < NG; ++g) {
+      if (gi == g) {
+        acc0 = ag0[g];
+        acc1 = ag1[g];
+      }
     }
   } else {
     mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
