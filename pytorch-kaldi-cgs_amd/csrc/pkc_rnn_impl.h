@@ -615,7 +615,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     // Only var_1 needs the reduction: Q maps the max-abs element x* (|x*| = var) to exactly
     // +-var (x*/var = +-1, ceil(2^(b-1)) / 2^(b-1) = 1) and every other element to a magnitude
     // <= var (monotone rounding of ceil(.) / 2^(b-1) <= 1), so var_{g+1} = max|q_{g+1}| = var_g.
-    __shared__ float qred[8];
+    // (NW waves x 4 lane groups x S = H: with 8 waves each holds half a 4-wave strip)
+    __shared__ float qred[2 * NW];
     {
       float mx = -INFINITY, mn = INFINITY;
 #pragma unroll
@@ -623,13 +624,17 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
         mx = fmaxf(mx, fmaxf(va[s], vb[s]));
         mn = fminf(mn, fminf(va[s], vb[s]));
       }
-      static_assert(NW == 4 || !QH, "quantised h: 4-wave tiles");
       mx = warp_max(mx);
       mn = -warp_max(-mn);
-      if (lane == 0) { qred[w] = mx; qred[4 + w] = mn; }
+      if (lane == 0) { qred[w] = mx; qred[NW + w] = mn; }
       __syncthreads();
-      mx = fmaxf(fmaxf(qred[0], qred[1]), fmaxf(qred[2], qred[3]));
-      mn = fminf(fminf(qred[4], qred[5]), fminf(qred[6], qred[7]));
+      mx = qred[0];
+      mn = qred[NW];
+#pragma unroll
+      for (int i = 1; i < NW; ++i) {
+        mx = fmaxf(mx, qred[i]);
+        mn = fminf(mn, qred[NW + i]);
+      }
       const float v1 = fabsf(mx) > fabsf(mn) ? fabsf(mx) : fabsf(mn);
 #pragma unroll
       for (int g = 0; g < 4; ++g) vars[g] = v1;
@@ -861,6 +866,17 @@ static bool rows16(int B2) {
 // per lane and half the MFMA chain per wave.  Same-run A/B (PKC_RNN_WAVES=4 / 8): C4 89.2k / 90.8k,
 // C5 (8-wave BPTT only; its quantised forward keeps 4) 117.6k / 120.3k frames/s — the step is
 // bound by h_{t-1} arriving from the other XCDs, not by the per-lane load or MFMA work.
+// PKC_RNN_QH_WAVES (8 / 4): the quantised-h forward step (C5) as 8-wave tiles — half the strip,
+// quantisation passes and MFMA chains per wave, two waves per SIMD to overlap one's
+// quantisation arithmetic with the other's MFMAs
+static bool qh_eight_waves(int S) {
+  static const int w = [] {
+    const char* v = getenv("PKC_RNN_QH_WAVES");
+    return v ? atoi(v) : 8;
+  }();
+  return w == 8 && S >= 32;
+}
+
 static bool eight_waves(int S) {
   static const int w = [] {
     const char* v = getenv("PKC_RNN_WAVES");
@@ -902,6 +918,9 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
         if constexpr (SP)
           hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), g16, dim3(RT), 0, s,
                              *a, t, vw);
+        else if (a->qbits > 0 && qh_eight_waves(S))
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), g16,
+                             dim3(2 * RT), 0, s, *a, t, vw);
         else if (a->qbits > 0)
           hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), g16, dim3(RT), 0, s,
                              *a, t, vw);
