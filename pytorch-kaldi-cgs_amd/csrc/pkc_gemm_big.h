@@ -138,6 +138,40 @@ struct Stage {
     }
   }
 
+  // The row part of each chunk's address, computed once per tile loop (load_at adds the k-tile's
+  // offset): recomputing the clamps and 64-bit row products for every chunk of every k-tile put
+  // the staging instructions on par with the tile's MFMAs (cf. GldsOperand).
+  struct Base {
+    const HE* p[NCH];
+    bool ok[NCH];
+  };
+  __device__ __forceinline__ static Base base(const HE* __restrict__ P, int64_t ld, int r0,
+                                              int rmax) {
+    Base b;
+    Stage tmp;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int r, k;
+      tmp.coord(i, r, k);
+      const int rr = min(r0 + r, rmax - (KC ? 1 : EPC));
+      b.p[i] = KC ? P + (int64_t)rr * ld : P + rr;
+      b.ok[i] = r0 + r < rmax;
+    }
+    return b;
+  }
+  __device__ __forceinline__ void load_at(const Base& b, int ld, int k0, int kend) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int r, k;
+      coord(i, r, k);
+      const bool ok = b.ok[i] && (k0 + k < kend);
+      const int kk = min(k0 + k, kend - (KC ? EPC : 1));
+      const float4 x = KC ? *reinterpret_cast<const float4*>(b.p[i] + kk)
+                          : *reinterpret_cast<const float4*>(b.p[i] + (int64_t)kk * ld);
+      v[i] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
   // Element access by value only: taking the address of v[] makes the compiler promote the
   // staging array into extra LDS (16 KB per workgroup), with a round trip per element.
   __device__ __forceinline__ static uint32_t word(const float4& x, int w) {
@@ -377,15 +411,19 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
   Stage<PREC, BIN, BKC> nb, nnb;
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;   // uniform
   if (nk > 0) {
-    na.load(A, lda, m0, M, kbeg, kend);
-    nb.load(B, ldb, n0, N, kbeg, kend);
+    // leading dimensions < 2^31 elements (pkc_gemm / pkc_gemm_grouped check)
+    const typename Stage<PREC, BIN, AKC>::Base ab = Stage<PREC, BIN, AKC>::base(A, lda, m0, M);
+    const typename Stage<PREC, BIN, BKC>::Base bb = Stage<PREC, BIN, BKC>::base(B, ldb, n0, N);
+    const int la = (int)lda, lb = (int)ldb;
+    na.load_at(ab, la, kbeg, kend);
+    nb.load_at(bb, lb, kbeg, kend);
     na.store(lds);
     nb.store(lds + TILE_BYTES);
-    na.load(A, lda, m0, M, kbeg + BK, kend);           // past kend: clamped, zeroed, never stored
-    nb.load(B, ldb, n0, N, kbeg + BK, kend);
+    na.load_at(ab, la, kbeg + BK, kend);               // past kend: clamped, zeroed, never stored
+    nb.load_at(bb, lb, kbeg + BK, kend);
     if constexpr (DEPTH == 2) {
-      nna.load(A, lda, m0, M, kbeg + 2 * BK, kend);
-      nnb.load(B, ldb, n0, N, kbeg + 2 * BK, kend);
+      nna.load_at(ab, la, kbeg + 2 * BK, kend);
+      nnb.load_at(bb, lb, kbeg + 2 * BK, kend);
     }
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
@@ -399,11 +437,11 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
         if constexpr (DEPTH == 2) {
           na = nna;
           nb = nnb;
-          nna.load(A, lda, m0, M, kbeg + (t + 3) * BK, kend);
-          nnb.load(B, ldb, n0, N, kbeg + (t + 3) * BK, kend);
+          nna.load_at(ab, la, kbeg + (t + 3) * BK, kend);
+          nnb.load_at(bb, lb, kbeg + (t + 3) * BK, kend);
         } else {
-          na.load(A, lda, m0, M, kbeg + (t + 2) * BK, kend);
-          nb.load(B, ldb, n0, N, kbeg + (t + 2) * BK, kend);
+          na.load_at(ab, la, kbeg + (t + 2) * BK, kend);
+          nb.load_at(bb, lb, kbeg + (t + 2) * BK, kend);
         }
       }
       __syncthreads();

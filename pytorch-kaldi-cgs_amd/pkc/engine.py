@@ -48,8 +48,11 @@ MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", "0"))
 # frames/s: 0 -> 653-657k, 1.2M -> 663k, 700k -> 666-667k, 400k-520k -> 669-671k, 250k -> 644k.
 # With bf16-stored operands and the 8-column BatchNorm kernels the backward launches are shorter
 # and the heads' 2M-parameter update no longer needs cutting: 500k 762-763k, 1M 768-771k,
-# 2.5M (heads in one part) 768-772k, 300k 728k (profiles/r02_opt_spread_ab.txt)
-OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "2500000"))
+# 2.5M (heads in one part) 768-772k, 300k 728k (profiles/r02_opt_spread_ab.txt).  Round 3, with the
+# grouped launches at 4 waves per SIMD the heads' update again sets its launch's length (11.3 of
+# 14.3 us, profiles/r03_launch_probe.txt): 2.5M 863-869k, 1M 874-876k, 700k 878-879k, 500k
+# 874-875k (profiles/r03_opt_spread_ab.txt)
+OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "700000"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
 # 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
