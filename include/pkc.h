@@ -84,11 +84,12 @@ typedef struct {
 int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream);
 /* Large-batch forward matmul of a BatchNorm'd layer (neural_networks.py:306-311: BN(wx(x)) over
  * the batch) with the BatchNorm column statistics in the matmul's epilogue: one slab
- * C = A B^T (as pkc_gemm, splits = 1) and, per 128-row block b of C, the block's column mean of
+ * C = A B^T (as pkc_gemm, splits = 1) and, per row block b of C, the block's column mean of
  * C + bias and M2 = sum (C - mean)^2 into part[b*2N + n], part[b*2N + N + n] — the partials
- * pkc_dense_fwd_pre(part_rows = 128) merges, so no separate statistics pass reads C.  Only for
- * shapes that take the 128x128 tile body: pkc_gemm_colstats_ok says which (1 / 0); bias may be
- * NULL; part holds 2 N ceil(M / 128) floats (a pkc_dense_work_size(M, N) buffer does). */
+ * pkc_dense_fwd_pre merges, so no separate statistics pass reads C.  pkc_gemm_colstats_ok returns
+ * the rows per partial block for the shape — 128 (128x128 tile body), 64 (64x64 body, 16-byte
+ * operand paths), 0 (not available) — which is the part_rows to pass to pkc_dense_fwd_pre; bias
+ * may be NULL; part holds 2 N ceil(M / rows) floats (a pkc_dense_work_size(M, N) buffer does). */
 int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
                          const void* A, int64_t lda, const void* B, int64_t ldb);
 int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,

@@ -319,12 +319,52 @@ __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, i
 // DEPTH k-tiles are in flight in registers at any time: with M = 128-row batches a workgroup's
 // k-range is only a few tiles long, so the whole range is requested up front instead of one
 // HBM/L2 round trip per tile.
-template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN>
+// Column statistics of a finished 64x64 tile (pkc_gemm_colstats on the 64x64 body): per column,
+// the mean of its rows < M plus bias[c] and M2 = sum (z - mean)^2 over the tile's 64 rows — two
+// passes over the accumulators, the two 32-lane halves combined by a shuffle and the two row waves
+// through LDS in a fixed order (big::tile_colstats at 64 rows).  part[by*2N + c], part[by*2N+N+c].
+template <int PREC>
+__device__ __forceinline__ void tile_colstats64(const f32x16& acc, Lds<PREC>& sm, int m0, int n0,
+                                                int by, int M, int N, int wm, int wn, int r, int h,
+                                                const float* __restrict__ bias,
+                                                float* __restrict__ part) {
+  float* red = reinterpret_cast<float*>(&sm);      // [2 passes][2 row waves][64 columns]
+  const int nv = min(BM, M - m0);
+  const int cl = wn * 32 + r;
+  __syncthreads();                                 // the last k-tile's fragment reads are done
+  float sum = 0.f;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int rl = wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    sum += rl < nv ? acc[reg] : 0.f;
+  }
+  sum += __shfl_xor(sum, 32);
+  if (h == 0) red[wm * BN + cl] = sum;
+  __syncthreads();
+  const float mean = (red[cl] + red[BN + cl]) / (float)nv;
+  float q = 0.f;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int rl = wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const float d = acc[reg] - mean;
+    q += rl < nv ? d * d : 0.f;
+  }
+  q += __shfl_xor(q, 32);
+  if (h == 0) red[2 * BN + wm * BN + cl] = q;
+  __syncthreads();
+  const int col = n0 + cl;
+  if (wm != 0 || h != 0 || col >= N) return;
+  part[(int64_t)by * 2 * N + col] = mean + (bias ? bias[col] : 0.f);
+  part[(int64_t)by * 2 * N + N + col] = red[2 * BN + cl] + red[3 * BN + cl];
+}
+
+template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN, bool STATS = false>
 __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz, int M, int N, int K,
                                           const void* __restrict__ Av, int64_t lda,
                                           const void* __restrict__ Bv, int64_t ldb,
                                           float* __restrict__ C, int64_t ldc, int kchunk,
-                                          int64_t slab_stride) {
+                                          int64_t slab_stride, const float* __restrict__ bias = nullptr,
+                                          float* __restrict__ part = nullptr) {
   using SA = typename StageSel<BIN, AKC, VEC>::T;
   using SB = typename StageSel<BIN, BKC, VEC>::T;
   const auto* A = reinterpret_cast<const typename StageSel<BIN, AKC, VEC>::E*>(Av);
@@ -429,6 +469,7 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
       if (row0 + dr < M) Cr[dr * ldci] = acc[reg];
     }
   }
+  if constexpr (STATS) tile_colstats64<PREC>(acc, sm, m0, n0, by, M, N, wm, wn, r, h, bias, part);
 }
 
 // Block-sparse W (klist): the tile's k-tiles are klist[1..klist[0]] instead of a contiguous
@@ -499,6 +540,20 @@ __device__ __forceinline__ void gemm_body_sparse(Lds<PREC>& sm, int bx, int by, 
       if (row < M) Cz[(int64_t)row * ldc + col] = acc[reg];
     }
   }
+}
+
+// one-slab product + 64-row column statistics (pkc_gemm_colstats on the 64x64 body)
+template <int PREC, bool AKC, bool BKC, int DEPTH, bool BIN>
+__global__ __launch_bounds__(NT) void gemm_stats_kernel(int M, int N, int K,
+                                                        const void* __restrict__ A, int64_t lda,
+                                                        const void* __restrict__ B, int64_t ldb,
+                                                        float* __restrict__ C, int64_t ldc,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ part) {
+  __shared__ Lds<PREC> sm;
+  gemm_body<PREC, AKC, BKC, true, DEPTH, BIN, true>(sm, blockIdx.x, blockIdx.y, 0, M, N, K, A, lda,
+                                                    B, ldb, C, ldc, ((K + BK - 1) / BK) * BK, 0,
+                                                    bias, part);
 }
 
 template <int PREC, bool AKC, bool BKC, bool VEC, int DEPTH, bool BIN>
@@ -751,6 +806,15 @@ static int xcd_remap() {                      // PKC_GEMM_XCD=0: launch order (A
   return on;
 }
 
+// PKC_GEMM_COLSTATS64=0: column statistics in the 128x128 body only (A/B)
+static bool colstats64_enabled() {
+  static const int on = [] {
+    const char* v = getenv("PKC_GEMM_COLSTATS64");
+    return v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
+
 static bool glds_enabled() {                   // PKC_GEMM_GLDS=0: register-staged body (A/B)
   static const int on = [] {
     const char* v = getenv("PKC_GEMM_GLDS");
@@ -894,14 +958,22 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
                                         splits, slab_stride, S(stream));
 }
 
+// rows per partial block pkc_gemm_colstats writes for this shape: 128 (the 128x128 tile body),
+// 64 (the 64x64 body, 16-byte operand paths), 0 (not taken)
 extern "C" int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
                                     const void* A, int64_t lda, const void* B, int64_t ldb) {
   using namespace pkc;
-  return (prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN) && M > 0 &&
-                 N > 0 && K > 0 && big_enabled() &&
-                 big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, BIG_MIN_TILES)
-             ? 1
-             : 0;
+  if (!(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN) || M <= 0 ||
+      N <= 0 || K <= 0 || lda <= 0 || ldb <= 0 || lda >= (1ll << 31) || ldb >= (1ll << 31))
+    return 0;
+  if (big_enabled() &&
+      big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, BIG_MIN_TILES))
+    return 128;
+  const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
+  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
+                   ldb % e == 0 && (a_kcontig ? K % e == 0 : M % e == 0) &&
+                   (b_kcontig ? K % e == 0 : N % e == 0);
+  return vec && colstats64_enabled() ? 64 : 0;
 }
 
 extern "C" int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
@@ -909,8 +981,30 @@ extern "C" int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, 
                                  int64_t ldc, const float* bias, float* part, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(A && B && C && part && ldc >= N, "pkc_gemm_colstats: bad arguments");
-  PKC_CHECK_ARG(pkc_gemm_colstats_ok(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb),
-                "pkc_gemm_colstats: %dx%dx%d (prec %d) does not take the 128x128 body", M, N, K, prec);
+  const int rows = pkc_gemm_colstats_ok(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb);
+  PKC_CHECK_ARG(rows > 0, "pkc_gemm_colstats: %dx%dx%d (prec %d): no column-statistics body", M, N,
+                K, prec);
+  PKC_CHECK_ARG(ldc < (1ll << 26), "pkc_gemm_colstats: ldc must be below 2^26");
+  if (rows == 64) {
+    dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
+#define PKC_CS(P, BIN, AK, BK_)                                                                  \
+  hipLaunchKernelGGL((gemm_stats_kernel<P, AK, BK_, BIN ? 8 : 4, BIN>), grid, dim3(NT), 0, S(stream), \
+                     M, N, K, A, lda, B, ldb, C, ldc, bias, part)
+#define PKC_CSO(P, BIN)                                                                          \
+  do {                                                                                         \
+    if (a_kcontig && b_kcontig) PKC_CS(P, BIN, true, true);                                    \
+    else if (a_kcontig) PKC_CS(P, BIN, true, false);                                           \
+    else if (b_kcontig) PKC_CS(P, BIN, false, true);                                           \
+    else PKC_CS(P, BIN, false, false);                                                         \
+  } while (0)
+    if (prec == PKC_PREC_FP32) PKC_CSO(PKC_PREC_FP32, false);
+    else if (prec == PKC_PREC_BF16IN) PKC_CSO(PKC_PREC_BF16, true);
+    else PKC_CSO(PKC_PREC_BF16, false);
+#undef PKC_CSO
+#undef PKC_CS
+    PKC_LAUNCH_CHECK("pkc_gemm_colstats (64x64)");
+    return PKC_OK;
+  }
   if (prec == PKC_PREC_FP32)
     return launch_big<PKC_PREC_FP32, false, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
                                                   ldc, 1, 0, S(stream), bias, part);

@@ -1255,10 +1255,10 @@ class Engine:
 
     def _colstats_fwd(self, n, prob, s):
         """Large-batch BatchNorm'd MLP layer in training: the forward matmul writes the BatchNorm
-        column partials of its 128-row tiles in its epilogue (pkc_gemm_colstats) and
-        pkc_dense_fwd_pre merges them and applies, so no statistics pass re-reads z.  Only where
-        the 128x128 tile body takes the matmul (one slab); sequence models keep the stats-pass
-        blocking their recurrent lifecycle tests are pinned to.  Returns False when not taken."""
+        column partials of its 128- or 64-row tiles in its epilogue (pkc_gemm_colstats) and
+        pkc_dense_fwd_pre merges them and applies, so no statistics pass re-reads z.  One slab
+        only; sequence models keep the stats-pass blocking their recurrent lifecycle tests are
+        pinned to.  Returns False when not taken."""
         if not (COLSTATS and n.bn and not n.ln and not n.head and n.W is not None and not self.seq
                 and self.M > 128 and getattr(n, "bn_states", None) is None):
             return False
@@ -1268,13 +1268,14 @@ class Engine:
         prec = self.prec
         if len(prob) > 4 and prob[4] is not None:
             prec, (nb, p) = L.PREC_BF16IN, prob[4]
-        if not L.lib().pkc_gemm_colstats_ok(prec, p.a_kcontig, p.b_kcontig, p.M, p.N, p.K,
-                                            C.c_void_p(p.A), p.lda, C.c_void_p(p.B), p.ldb):
+        rows = L.lib().pkc_gemm_colstats_ok(prec, p.a_kcontig, p.b_kcontig, p.M, p.N, p.K,
+                                            C.c_void_p(p.A), p.lda, C.c_void_p(p.B), p.ldb)
+        if rows <= 0:
             return False
-        self._k("gemm_colstats " + lab, fl, nb + 8.0 * p.N * -(-p.M // 128), "pkc_gemm_colstats",
+        self._k("gemm_colstats " + lab, fl, nb + 8.0 * p.N * -(-p.M // rows), "pkc_gemm_colstats",
                 prec, p.a_kcontig, p.b_kcontig, p.M, p.N, p.K, C.c_void_p(p.A), p.lda,
                 C.c_void_p(p.B), p.ldb, C.c_void_p(p.C), p.ldc, ptr(n.b), ptr(n.work), s)
-        self._fwd_epilogue(n, s, True, pre_rows=128)
+        self._fwd_epilogue(n, s, True, pre_rows=rows)
         return True
 
     def _fwd_epilogue(self, n, s, train, out=None, pre_rows=0):

@@ -527,14 +527,17 @@ def test_gemm_grouped_sparse_big_slabsum(L, prec):
 # take the 128x128 body (LDS-DMA ring: bf16-stored operands, K % 64 == 0; register body otherwise),
 # ragged row / column tails, the first layer's K = 440
 COLSTATS_SHAPES = [(4096, 1024, 1024, 2), (4096, 1024, 440, 2), (2056, 1288, 1024, 2),
-                   (2056, 1288, 1000, 1), (4096, 4096, 256, 0)]
+                   (2056, 1288, 1000, 1), (4096, 4096, 256, 0),
+                   # fewer than 160 128x128 tiles: the 64x64 body's 64-row partials (B = 1024)
+                   (1024, 1024, 1024, 2), (1000, 1032, 440, 2), (1032, 520, 1000, 1), (264, 200, 96, 0)]
 
 
 @pytest.mark.parametrize("M,N,K,prec", COLSTATS_SHAPES)
 def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
-    """pkc_gemm_colstats: the one-slab product and per-128-row-block column (mean + bias, M2) vs
-    fp64 of the same operands; pkc_dense_fwd_pre on those partials vs pkc_dense_fwd (the
-    stats-pass form) on the same slab — the same BatchNorm up to fp32 summation order."""
+    """pkc_gemm_colstats: the one-slab product and per-block column (mean + bias, M2) vs fp64 of
+    the same operands (128-row blocks from the 128x128 body, 64-row ones from the 64x64 body);
+    pkc_dense_fwd_pre on those partials vs pkc_dense_fwd (the stats-pass form) on the same slab —
+    the same BatchNorm up to fp32 summation order."""
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
     W = torch.randn(N, K, generator=g) * K ** -0.5
@@ -543,8 +546,9 @@ def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
     Ad, Wd, bd = A.to(DEV).to(dt).contiguous(), W.to(DEV).to(dt).contiguous(), bias.to(DEV)
     if prec >= 1:
         A, W = A.bfloat16().float(), W.bfloat16().float()
-    ok = L.lib().pkc_gemm_colstats_ok(prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K)
-    assert ok == 1, "shape should take the 128x128 body"
+    rows = L.lib().pkc_gemm_colstats_ok(prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K)
+    tiles = -(-M // 128) * -(-N // 128)
+    assert rows == (128 if tiles >= (1024 if prec == 0 else 160) else 64), rows
     Cd = torch.full((M, N), float("nan"), device=DEV)
     work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
     L.call("pkc_gemm_colstats", prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K, L.ptr(Cd), N,
@@ -552,11 +556,11 @@ def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
     ref = A.double() @ W.double().t()
     tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
     torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-4, atol=tol)
-    nb = -(-M // 128)
+    nb = -(-M // rows)
     part = work[:2 * N * nb].view(nb, 2, N).cpu().double()
     z = Cd.cpu().double() + bias.double()
     for b in range(nb):
-        blk = z[128 * b:128 * (b + 1)]
+        blk = z[rows * b:rows * (b + 1)]
         mu = blk.mean(0)
         torch.testing.assert_close(part[b, 0], mu, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(part[b, 1], ((blk - mu) ** 2).sum(0), rtol=1e-4, atol=1e-4)
@@ -580,7 +584,7 @@ def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
             w2 = torch.zeros_like(work)
             L.call(fn, C.byref(a_), L.ptr(w2), _s())
         else:
-            L.call(fn, C.byref(a_), L.ptr(work), 128, _s())
+            L.call(fn, C.byref(a_), L.ptr(work), rows, _s())
         outs.append((out.cpu(), xhat.cpu(), keep.cpu(), rm.cpu(), rv.cpu(), sm.cpu(), si.cpu()))
     (o0, x0, k0, rm0, rv0, sm0, si0), (o1, x1, k1, rm1, rv1, sm1, si1) = outs
     assert torch.equal(k0, k1)                   # same dropout bits
