@@ -113,7 +113,7 @@ def _bn_ref(z, gamma, beta, act, keep, p):
 @pytest.mark.parametrize("p", [0.0, 0.15])
 @pytest.mark.parametrize("M,N,S", [(128, 1024, 4), (16, 48, 1), (50, 70, 3), (100, 1028, 7), (300, 64, 2),
                                    (2000, 256, 1), (1700, 100, 3), (200, 24, 2), (256, 64, 1),
-                                   (129, 40, 8)])
+                                   (129, 40, 8), (4096, 1024, 1), (4112, 1280, 2)])
 def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
     g = torch.Generator().manual_seed(M + N + S)
     slabs = torch.randn(S, M, N, generator=g)
