@@ -118,7 +118,7 @@ typedef struct {
   const uint8_t* keep_in;                     /* optional injected dropout mask (M x N) */
   uint8_t* keep_out;                          /* M x N, may be NULL when drop_p == 0 */
   float* xhat;                                /* M x N (BN input normalised), may be NULL in eval */
-  float* out;                                 /* M x N */
+  float* out;        /* M x N; may be NULL when out_bf16 is set (no reader of the fp32 copy) */
   int64_t count_n;   /* rows BatchNorm1d sees for the unbiased running_var (0 -> M); a shared-
                         weight bidirectional layer normalises 2x duplicated rows (2*M) */
   void* out_bf16;    /* optional bf16 copy of out (M x N): the next layer's PKC_PREC_BF16IN operand */

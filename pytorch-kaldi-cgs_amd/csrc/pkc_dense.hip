@@ -283,7 +283,7 @@ __global__ __launch_bounds__(ET) void dense_apply_kernel(pkc_dense_fwd_args a, c
       o = k ? o * scale : 0.f;
     }
     if (a.xhat) a.xhat[idx] = xh;
-    a.out[idx] = o;
+    if (a.out) a.out[idx] = o;
     if (a.out_bf16) st_h1(a.out_bf16, idx, o);
   }
 }
@@ -590,7 +590,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
     }
     if (drop && a.keep_out) *reinterpret_cast<uint32_t*>(a.keep_out + idx) = kw;
     if (a.xhat) *reinterpret_cast<float4*>(a.xhat + idx) = xh;
-    *reinterpret_cast<float4*>(a.out + idx) = o;
+    if (a.out) *reinterpret_cast<float4*>(a.out + idx) = o;
     if (a.out_bf16) st_h4(a.out_bf16, idx, o);
   }
 }
@@ -817,7 +817,7 @@ __global__ __launch_bounds__(ET) void dense_apply_v4_kernel(pkc_dense_fwd_args a
     }
     if (drop && a.keep_out) *reinterpret_cast<uint32_t*>(a.keep_out + idx) = kw;
     if (a.xhat) st4(a.xhat + idx, xh);
-    st4(a.out + idx, o);
+    if (a.out) st4(a.out + idx, o);
     if (a.out_bf16) st_h4(a.out_bf16, idx, o);
   }
 }
@@ -980,7 +980,7 @@ extern "C" int64_t pkc_dense_work_size(int M, int N) {
 
 extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream) {
   using namespace pkc;
-  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab >= 1 && a->zslab && a->out,
+  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab >= 1 && a->zslab && (a->out || a->out_bf16),
                 "pkc_dense_fwd: bad arguments");
   PKC_CHECK_ARG(a->norm != PKC_NORM_BN_TRAIN ||
                     (a->gamma && a->beta && a->running_mean && a->running_var && a->save_mean &&
@@ -992,7 +992,7 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
   PKC_CHECK_ARG(a->drop_p >= 0.f && a->drop_p < 1.f, "pkc_dense_fwd: drop_p out of range");
   PKC_CHECK_ARG(a->nslab == 1 || a->slab_stride >= (int64_t)a->M * a->N,
                 "pkc_dense_fwd: slab_stride too small");
-  if (small_ok(a->M, a->N, a->nslab, a->zslab, a->out, a->slab_stride) &&
+  if (small_ok(a->M, a->N, a->nslab, a->zslab, a->out ? a->out : a->zslab, a->slab_stride) &&
       (uintptr_t)a->xhat % 16 == 0 && (uintptr_t)a->out_bf16 % 8 == 0 && (!a->bias || (uintptr_t)a->bias % 16 == 0) &&
       (a->norm == PKC_NORM_NONE || ((uintptr_t)a->gamma % 16 == 0 && (uintptr_t)a->beta % 16 == 0 &&
                                     (uintptr_t)a->running_mean % 16 == 0 &&
@@ -1024,7 +1024,7 @@ extern "C" int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* str
 extern "C" int pkc_dense_fwd_pre(const pkc_dense_fwd_args* a, float* work, int part_rows,
                                  void* stream) {
   using namespace pkc;
-  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab == 1 && a->zslab && a->out && work,
+  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->nslab == 1 && a->zslab && (a->out || a->out_bf16) && work,
                 "pkc_dense_fwd_pre: bad arguments (one slab)");
   PKC_CHECK_ARG(a->norm == PKC_NORM_BN_TRAIN && a->gamma && a->beta && a->running_mean &&
                     a->running_var && a->save_mean && a->save_invstd && a->xhat,

@@ -738,16 +738,23 @@ class Engine:
         self.x_h = None
         for n in self.nodes:
             n.W_h = n.out_h = n.dz_h = None
+            n.f32_dead = False
         if not self.h16:
             return
         M, dev, bf = self.Mmax, self.dev, torch.bfloat16
         mm = [n for n in self.nodes if not n.rec and n.W is not None and not n.qbits]
         if any(n.src[0] == "fea" for n in mm):
             self.x_h = torch.zeros(M * self.F, dtype=bf, device=dev)
+        keep_f32 = os.environ.get("PKC_F32_OUT", "0") != "0"
         for n in mm:
             n.W_h = torch.zeros(n.W.numel(), dtype=bf, device=dev)
             if not n.head and any(c in mm for c in n.consumers):
                 n.out_h = torch.zeros(M * n.N, dtype=bf, device=dev)
+                # every consumer reads the bf16 copy (forward and dW operands): a training step
+                # stores no fp32 output for this layer (eval passes still do; PKC_F32_OUT=1: A/B)
+                n.f32_dead = (not keep_f32 and not n.ln and all(c in mm for c in n.consumers)
+                              and not any(getattr(c, "qv0", 0) or getattr(c, "reads", 0)
+                                          for c in n.consumers))
             if self.needs_grad[n] and not n.ln:
                 n.dz_h = torch.zeros(M * n.N, dtype=bf, device=dev)
         for e in self.opt_entries:
@@ -1328,7 +1335,9 @@ class Engine:
             step_ctr=self.ctr.data_ptr(), stream_id=zlib.crc32(n.name.encode()),
             keep_in=keep_in.data_ptr() if keep_in is not None else None,
             keep_out=n.keep.data_ptr() if (n.keep is not None and train) else None,
-            xhat=n.xhat.data_ptr(), out=n.out.data_ptr(), count_n=0,
+            xhat=n.xhat.data_ptr(), count_n=0,
+            out=None if (train and getattr(n, "f32_dead", False)
+                         and getattr(n, "bn_states", None) is None) else n.out.data_ptr(),
             out_bf16=n.out_h.data_ptr() if n.out_h is not None else None)
         if train and n.bn and getattr(n, "bn_states", None) is not None:
             # SyncBN: this rank's column state into its row of bn_states, all-reduce (gather),

@@ -551,3 +551,50 @@ def test_engine_bf16_store_matches_bf16_staging(B, mode):
         err = (g1[0] - g0[0]).abs().max().item()
         assert err <= 1e-5 * g0[0].abs().max().item(), "gradient max abs diff %.3g" % err
         assert t0 == pytest.approx(t1, rel=1e-5)
+
+
+@pytest.mark.parametrize("B,mode", [(128, "graph"), (4096, "eager")])
+def test_engine_dead_f32_outputs_skipped(B, mode, monkeypatch):
+    """With bf16-stored operands every consumer of a body layer reads its bf16 copy, so a training
+    step stores no fp32 output for it (pkc_dense_fwd with out = NULL).  Same step as the form that
+    stores it (PKC_F32_OUT=1): bit-identical gradients, posteriors, weights and loss over 2 steps,
+    on the small-batch kernels (B = 128, graph-replayed) and the 16-byte colstats path (B = 4096)."""
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config(drop="0.15")
+    steps = 2
+    rs = np.random.RandomState(11)
+    X = torch.from_numpy(rs.randn(B * steps, 440).astype(np.float32)).to(DEV)
+    lab = torch.from_numpy(np.stack([rs.randint(0, 1928, B * steps), rs.randint(0, 48, B * steps)],
+                                    1).astype(np.int32)).to(DEV)
+    runs = []
+    for keep in ("1", "0"):
+        monkeypatch.setenv("PKC_F32_OUT", keep)
+        nets, opts = build_nets(cfg, C1_DIMS)
+        for n in nets.values():
+            n.to(DEV).train()
+        eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                     ["lab_cd", "lab_mono"], batch=B, seed=7, prec=L.PREC_BF16, bf16_store=True)
+        dead = [l.name for l in eng.layers if getattr(l, "f32_dead", False)]
+        assert (len(dead) == 5) if keep == "0" else not dead, dead
+        eng.bind_chunk(X, lab, B * steps)
+        if mode == "graph":
+            assert eng.capture(steps_per_graph=1)
+            eng.ctr.zero_()
+            eng.loss_acc.zero_()
+        grads, posts = [], []
+        head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
+        for _ in range(steps):
+            eng.train_step()
+            torch.cuda.synchronize()
+            grads.append(eng.gflat.detach().cpu().clone())
+            posts.append(head.out.view(B, -1).cpu().clone())
+        sd = {a + "/" + k: v.detach().cpu().clone() for a in nets for k, v in nets[a].state_dict().items()}
+        runs.append((grads, posts, sd, eng.chunk_totals()))
+    (g0, p0, s0, t0), (g1, p1, s1, t1) = runs
+    for s in range(steps):
+        assert torch.equal(g0[s], g1[s]), "step %d gradients differ" % s
+        assert torch.equal(p0[s], p1[s]), "step %d posteriors differ" % s
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+    assert t0 == t1
