@@ -144,6 +144,8 @@ typedef struct {
   const float* xhat; const uint8_t* keep; float drop_p;
   float* dz; float* dgamma; float* dbeta; float* dbias;
   void* dz_bf16;     /* optional bf16 copy of dz (M x N): the dW / dX PKC_PREC_BF16IN operand */
+  int dz_scratch;    /* 1 (training BatchNorm with dz_bf16): the caller reads only dz_bf16; dz is
+                        scratch between the passes and the final fp32 gradient is not stored */
 } pkc_dense_bwd_args;
 int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* stream);
 /* SyncBN (cross-rank BatchNorm statistics): the training-mode BatchNorm of

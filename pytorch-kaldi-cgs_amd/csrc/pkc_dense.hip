@@ -346,7 +346,7 @@ __global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args 
     if (r >= a.M) break;
     const int64_t idx = r * N + c;
     const float d = k * (a.dz[idx] - mdy - a.xhat[idx] * mdyx);
-    a.dz[idx] = d;
+    if (!a.dz_scratch) a.dz[idx] = d;
     if (a.dz_bf16) st_h1(a.dz_bf16, idx, d);
   }
 }
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
       const float d = f4get(dy[i], j);
       f4set(o, j, bn ? f4get(k, j) * (d - f4get(mdy, j) - f4get(xh[i], j) * f4get(mdyx, j)) : d);
     }
-    *reinterpret_cast<float4*>(a.dz + (int64_t)row * N + c) = o;
+    if (!a.dz_scratch) *reinterpret_cast<float4*>(a.dz + (int64_t)row * N + c) = o;
     if (a.dz_bf16) st_h4(a.dz_bf16, (int64_t)row * N + c, o);
   }
 }
@@ -892,7 +892,7 @@ __global__ __launch_bounds__(ET) void dense_bwd_apply_v4_kernel(pkc_dense_bwd_ar
     float4 d;
 #pragma unroll
     for (int j = 0; j < 4; ++j) f4set(d, j, k[j] * (f4get(dz, j) - mdy[j] - f4get(xh, j) * mdyx[j]));
-    st4(a.dz + idx, d);
+    if (!a.dz_scratch) st4(a.dz + idx, d);
     if (a.dz_bf16) st_h4(a.dz_bf16, idx, d);
   }
 }
@@ -1053,6 +1053,8 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
                 "pkc_dense_bwd: BN needs gamma/beta/save_invstd");
   PKC_CHECK_ARG(a->norm != PKC_NORM_BN_EVAL, "pkc_dense_bwd: backward through eval BN unsupported");
   PKC_CHECK_ARG(a->drop_p == 0.f || a->keep, "pkc_dense_bwd: dropout needs the keep mask");
+  PKC_CHECK_ARG(!a->dz_scratch || (a->dz_bf16 && a->norm == PKC_NORM_BN_TRAIN),
+                "pkc_dense_bwd: dz_scratch needs dz_bf16 and training BatchNorm");
   if (small_ok(a->M, a->N, a->nslab, a->gslab, a->dz, a->slab_stride) &&
       (uintptr_t)a->xhat % 16 == 0 && (uintptr_t)a->dz_bf16 % 8 == 0 && (!a->dbias || (uintptr_t)a->dbias % 16 == 0) &&
       (a->norm == PKC_NORM_NONE ||
@@ -1126,6 +1128,7 @@ static int sync_bwd_check(const pkc_dense_bwd_args* a, const float* work) {
                     a->norm == PKC_NORM_BN_TRAIN && a->gamma && a->beta && a->save_invstd,
                 "pkc_dense_bwd sync: BN training arguments");
   PKC_CHECK_ARG(a->drop_p == 0.f || a->keep, "pkc_dense_bwd sync: dropout needs the keep mask");
+  PKC_CHECK_ARG(!a->dz_scratch || a->dz_bf16, "pkc_dense_bwd sync: dz_scratch needs dz_bf16");
   return PKC_OK;
 }
 

@@ -36,7 +36,7 @@ class DenseBwdArgs(C.Structure):
                 ("gslab", vp), ("slab_stride", i64), ("norm", C.c_int), ("act", C.c_int),
                 ("gamma", vp), ("beta", vp), ("save_invstd", vp), ("xhat", vp), ("keep", vp),
                 ("drop_p", C.c_float), ("dz", vp), ("dgamma", vp), ("dbeta", vp), ("dbias", vp),
-                ("dz_bf16", vp)]
+                ("dz_bf16", vp), ("dz_scratch", C.c_int)]
 
 
 class NllArgs(C.Structure):

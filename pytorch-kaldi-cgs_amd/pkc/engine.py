@@ -738,7 +738,8 @@ class Engine:
         self.x_h = None
         for n in self.nodes:
             n.W_h = n.out_h = n.dz_h = None
-            n.f32_dead = False
+            n.f32_dead = n.dz_scratch = False
+        self.scratch_dz = set()
         if not self.h16:
             return
         M, dev, bf = self.Mmax, self.dev, torch.bfloat16
@@ -757,6 +758,15 @@ class Engine:
                                           for c in n.consumers))
             if self.needs_grad[n] and not n.ln:
                 n.dz_h = torch.zeros(M * n.N, dtype=bf, device=dev)
+        # every matmul of the step has bf16 operand copies (so every launch runs PKC_PREC_BF16IN):
+        # a BatchNorm body layer's fp32 dz is then only scratch of its own backward passes and the
+        # final gradient is stored as the bf16 copy alone (pkc_dense_bwd_args.dz_scratch)
+        full = all(m in mm and not m.ln for m in self.nodes if m.W is not None)
+        for n in mm:
+            n.dz_scratch = bool(full and not keep_f32 and not n.head and n.bn
+                                and n.dz_h is not None)
+            if n.dz_scratch:
+                self.scratch_dz.add(n.dz.data_ptr())
         for e in self.opt_entries:
             nd = e["node"]
             if nd is not None and getattr(nd, "W_h", None) is not None and e["p"] is nd.W:
@@ -1241,6 +1251,10 @@ class Engine:
                         for q in part]
             else:
                 part = [q[:4] for q in part]
+                sd = getattr(self, "scratch_dz", None)
+                if sd and any(q[3].A in sd or q[3].B in sd for q in part):
+                    raise RuntimeError("fp32 matmul on a bf16-only gradient: %s"
+                                       % [q[0] for q in part])
             if len(part) == 1 and part[0][3].kind == L.OP_GEMM and not part[0][3].ktiles:
                 lab, fl, nb, p = part[0]
                 self._k("gemm_" + lab, fl, nb, "pkc_gemm", prec, p.a_kcontig, p.b_kcontig,
@@ -1576,7 +1590,7 @@ class Engine:
                            dbeta=n.dbeta.data_ptr() if n.bn else None,
                            dbias=n.db.data_ptr() if (n.b is not None and not n.ln) else None,
                            dz_bf16=n.dz_h.data_ptr() if (n.W is not None and n.dz_h is not None)
-                           else None)
+                           else None, dz_scratch=int(getattr(n, "dz_scratch", False)))
         if n.bn and getattr(n, "bn_sums", None) is not None:
             # SyncBN: local column sums (and local dgamma / dbeta), all-reduce, global apply
             self._k("dense_bwd_stats N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 2), "pkc_dense_bwd_stats",

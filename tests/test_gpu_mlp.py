@@ -556,8 +556,8 @@ def test_engine_bf16_store_matches_bf16_staging(B, mode):
 @pytest.mark.parametrize("B,mode", [(128, "graph"), (4096, "eager")])
 def test_engine_dead_f32_outputs_skipped(B, mode, monkeypatch):
     """With bf16-stored operands every consumer of a body layer reads its bf16 copy, so a training
-    step stores no fp32 output for it (pkc_dense_fwd with out = NULL).  Same step as the form that
-    stores it (PKC_F32_OUT=1): bit-identical gradients, posteriors, weights and loss over 2 steps,
+    step stores no fp32 output for it (pkc_dense_fwd with out = NULL) and no final fp32 dz (the
+    BatchNorm backward's dz_scratch).  Same step as the form that stores both (PKC_F32_OUT=1): bit-identical gradients, posteriors, weights and loss over 2 steps,
     on the small-batch kernels (B = 128, graph-replayed) and the 16-byte colstats path (B = 4096)."""
     from pkc import _lib as L
     from pkc.engine import Engine, parse_model
@@ -577,6 +577,8 @@ def test_engine_dead_f32_outputs_skipped(B, mode, monkeypatch):
                      ["lab_cd", "lab_mono"], batch=B, seed=7, prec=L.PREC_BF16, bf16_store=True)
         dead = [l.name for l in eng.layers if getattr(l, "f32_dead", False)]
         assert (len(dead) == 5) if keep == "0" else not dead, dead
+        scratch = [l.name for l in eng.layers if getattr(l, "dz_scratch", False)]
+        assert (len(scratch) == 5) if keep == "0" else not scratch, scratch
         eng.bind_chunk(X, lab, B * steps)
         if mode == "graph":
             assert eng.capture(steps_per_graph=1)
