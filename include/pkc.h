@@ -18,7 +18,10 @@
 extern "C" {
 #endif
 
-#define PKC_ABI_VERSION 1
+/* Bumped whenever an entry point is added or a struct changes (tests/test_abi_layout.py asserts it):
+ * 1: rounds 1-3; 2: pkc_logsoftmax_bwd, and the structs as they stand after round 3 (which appended
+ * pkc_dense_bwd_args.dz_scratch without a bump). */
+#define PKC_ABI_VERSION 2
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
@@ -188,6 +191,11 @@ typedef struct {
   void* dlogits_bf16;  /* optional bf16 copy of dlogits (operand of the fused row backward) */
 } pkc_nll_args;
 int pkc_nll_fused(const pkc_nll_args* a, void* stream);
+
+/* LogSoftmax backward for an upstream gradient dy (M x N, row-major): dz = dy - exp(logp) *
+ * rowsum(dy).  The architecture plug-in's trainable head forward (neural_networks.py:73-74 under
+ * the reference's autograd, core.py:221-232); dz may alias dy. */
+int pkc_logsoftmax_bwd(int M, int N, const float* logp, const float* dy, float* dz, void* stream);
 
 /* Reduce per-row losses of up to 8 heads: loss_final = sum_h w_h * mean(row_loss_h),
  * err = mean(row_err_of_err_head); writes out[0]=loss_final, out[1]=err, out[2+h]=mean loss h and

@@ -361,6 +361,23 @@ __global__ __launch_bounds__(64 * LW) void nll_multi_kernel(NllMulti g) {
   }
 }
 
+// autograd backward of LogSoftmax(dim=1) under an arbitrary upstream gradient (a head of the
+// architecture plug-in's trainable forward, whose loss is computed outside the library):
+// dz = dy - exp(logp) * sum_c dy, one wave per row (torch's log_softmax backward)
+__global__ __launch_bounds__(64 * LW) void logsoftmax_bwd_kernel(int M, int N, const float* logp,
+                                                                 const float* dy, float* dz) {
+  const int r = blockIdx.x * LW + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= M) return;
+  const float* g = dy + (int64_t)r * N;
+  const float* lp = logp + (int64_t)r * N;
+  float* d = dz + (int64_t)r * N;
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s += g[c];
+#pragma unroll
+  for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+  for (int c = lane; c < N; c += 64) d[c] = g[c] - expf(lp[c]) * s;
+}
+
 __global__ __launch_bounds__(256) void loss_finalize_kernel(int nheads, const float* const* rl,
                                                             const float* w, int M,
                                                             const float* rerr, float* out,
@@ -463,5 +480,15 @@ extern "C" int pkc_loss_finalize(int nheads, const float* const* row_loss, const
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, S(stream), nheads, row_loss,
                      weights, M, row_err, out, acc, advance_ctr);
   PKC_LAUNCH_CHECK("pkc_loss_finalize");
+  return PKC_OK;
+}
+
+extern "C" int pkc_logsoftmax_bwd(int M, int N, const float* logp, const float* dy, float* dz,
+                                  void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(M > 0 && N > 0 && logp && dy && dz, "pkc_logsoftmax_bwd: bad arguments");
+  hipLaunchKernelGGL(logsoftmax_bwd_kernel, dim3((M + LW - 1) / LW), dim3(64 * LW), 0, S(stream), M,
+                     N, logp, dy, dz);
+  PKC_LAUNCH_CHECK("pkc_logsoftmax_bwd");
   return PKC_OK;
 }

@@ -9,6 +9,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
+ABI_VERSION = 2         # include/pkc.h PKC_ABI_VERSION
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 PREC_FP32, PREC_BF16, PREC_BF16IN = 0, 1, 2
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
@@ -127,6 +128,7 @@ _SIGS = {
     "pkc_nll_fused": (C.c_int, [C.POINTER(NllArgs), vp]),
     "pkc_loss_finalize": (C.c_int, [C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp]),
     "pkc_nll_fused_multi": (C.c_int, [vp, C.c_int, vp]),
+    "pkc_logsoftmax_bwd": (C.c_int, [C.c_int, C.c_int, vp, vp, vp, vp]),
     "pkc_colsum": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, vp, C.c_int, vp]),
     "pkc_optim_step": (C.c_int, [vp, C.c_int, vp, C.c_int, vp]),
     "pkc_optim_chunks": (C.c_int, [C.POINTER(i64), C.c_int, C.POINTER(C.c_int32), C.c_int]),
@@ -164,7 +166,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.pkc_abi_version() != 1:
+        if L.pkc_abi_version() != ABI_VERSION:
             raise PkcError("libpkc ABI mismatch")
         _lib = L
     return _lib

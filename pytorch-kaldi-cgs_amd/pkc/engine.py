@@ -402,8 +402,13 @@ class Engine:
 
     def __init__(self, nets, arch_opts, lines, fea_cols, lab_names, batch, prec=L.PREC_FP32,
                  device="cuda", seed=0, train=True, drop_keep_in=None, grad_scale=1.0, max_len=None,
-                 rnn_drop_in=None, sync_bn=None, bf16_store=None):
+                 rnn_drop_in=None, sync_bn=None, bf16_store=None, external=False):
         self.dev = torch.device(device)
+        # external: the architecture plug-in's trainable forward (pkc.plugin) — the input comes
+        # from the caller, the output gradient from autograd, and the parameter / input gradients
+        # go back to autograd; no loss heads, no optimizer (torch.optim steps the parameters)
+        self.external = bool(external)
+        self.want_dx = False
         self.nets, self.arch_opts, self.lines = nets, arch_opts, lines
         self.B = int(batch)
         self.prec = prec
@@ -583,7 +588,7 @@ class Engine:
                 raise NotImplementedError("[model] operation %s is not on the pkc path" % op)
         self.produced = produced
         self.heads = [l for l in self.nodes if l.head]
-        if self.train and "loss_final" not in scal:
+        if self.train and "loss_final" not in scal and not self.external:
             raise ValueError("[model] has no loss_final")
         for lay, w in scal.get("loss_final", {}).items():
             lay.loss_weight = w
@@ -680,7 +685,7 @@ class Engine:
         self.needs_grad = {}
         for n in reversed(self.nodes):
             rc = getattr(n, "rec_consumer", None)
-            self.needs_grad[n] = (n.head and n.loss_weight != 0.0) or any(
+            self.needs_grad[n] = self.external or (n.head and n.loss_weight != 0.0) or any(
                 self.needs_grad[c] for c in n.consumers) or (rc is not None and self.needs_grad[rc])
         # all gradients in ONE flat buffer (a single RCCL all-reduce under data parallelism)
         plist = [(n, p, key, m) for n in self.nodes for (p, key, m) in n.params()]
@@ -688,9 +693,11 @@ class Engine:
         off = 0
         self.grads = {}
         self.grad_off = {}
+        self.param_grads = []                  # [(parameter, its gradient view of gflat)]
         for n, p, key, m in plist:
             self.grad_off.setdefault(n, off)
             g = self.gflat[off:off + p.numel()].view_as(p)
+            self.param_grads.append((p, g))
             off += p.numel()
             if isinstance(key, tuple):
                 n.lbuf[key[1]][key[0]][key[2]] = g
@@ -712,6 +719,8 @@ class Engine:
                                        device=dev)
         if self.seq:
             self.seq_meta = torch.zeros(4 * self.B, dtype=torch.int64, device=dev)
+        if self.external:
+            self.ext_dx = _f32(M * self.F, dev)   # dL/dx of the caller's input
 
     def _dw_splits(self, N, K):
         """K-splits of a dense layer's dW = dz^T X (contraction over the M batch rows): enough
@@ -740,6 +749,7 @@ class Engine:
             n.W_h = n.out_h = n.dz_h = None
             n.f32_dead = n.dz_scratch = False
         self.scratch_dz = set()
+        self.dead_out = set()
         if not self.h16:
             return
         M, dev, bf = self.Mmax, self.dev, torch.bfloat16
@@ -753,7 +763,12 @@ class Engine:
                 n.out_h = torch.zeros(M * n.N, dtype=bf, device=dev)
                 # every consumer reads the bf16 copy (forward and dW operands): a training step
                 # stores no fp32 output for this layer (eval passes still do; PKC_F32_OUT=1: A/B)
-                n.f32_dead = (not keep_f32 and not n.ln and all(c in mm for c in n.consumers)
+                # ... only when every consumer has the whole bf16 path: a LayerNorm'd consumer
+                # keeps no bf16 dz (its dW then runs in fp32 on the fp32 output), nor does a
+                # consumer that needs no gradient
+                n.f32_dead = (not keep_f32 and not n.ln
+                              and all(c in mm and not c.ln and self.needs_grad[c]
+                                      for c in n.consumers)
                               and not any(getattr(c, "qv0", 0) or getattr(c, "reads", 0)
                                           for c in n.consumers))
             if self.needs_grad[n] and not n.ln:
@@ -767,6 +782,8 @@ class Engine:
                                 and n.dz_h is not None)
             if n.dz_scratch:
                 self.scratch_dz.add(n.dz.data_ptr())
+            if n.f32_dead:
+                self.dead_out.add(n.out.data_ptr())
         for e in self.opt_entries:
             nd = e["node"]
             if nd is not None and getattr(nd, "W_h", None) is not None and e["p"] is nd.W:
@@ -925,7 +942,7 @@ class Engine:
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
         self.opt_entries = []
         for n in self.nodes:
-            if not self.needs_grad[n]:
+            if not self.needs_grad[n] or self.external:
                 continue
             o = self.arch_opts[n.arch]
             if _b(o.get("arch_freeze", "False")):
@@ -988,10 +1005,15 @@ class Engine:
                 self.prune_list.append((n_.W, float(n_.spec["prune"])) + n_.quant_of(n_.W))
         self.prune_work = (torch.zeros(L.lib().pkc_prune_work_size(), dtype=torch.uint8,
                                        device=self.dev) if self.prune_list else None)
+        self.apply_weight_masks(self._stream())
+
+    def apply_weight_masks(self, s):
+        """The reference multiplies the masks into W in place (and QuantizeLinear clamps W to
+        [-1, 1]) before every forward (neural_networks.py:256-278, 858-896;
+        quantized_modules.py:207-222); the optimizer epilogue keeps that true between steps, so
+        the Engine does it once here; the external mode (torch.optim steps the weights) before
+        every forward.  Then prune, then fake-quantise the copy the GEMMs multiply with."""
         pruned = {id(t[0]) for t in self.prune_list}
-        # the reference multiplies the masks in (and QuantizeLinear clamps W to [-1, 1]) before
-        # the first forward; do it once here, then fake-quantise the copy the GEMMs multiply with
-        s = self._stream()
         for n_ in self.nodes:
             for p, key, m in n_.params():
                 q, qb = n_.quant_of(p)
@@ -1255,6 +1277,11 @@ class Engine:
                 if sd and any(q[3].A in sd or q[3].B in sd for q in part):
                     raise RuntimeError("fp32 matmul on a bf16-only gradient: %s"
                                        % [q[0] for q in part])
+                do = getattr(self, "dead_out", None)
+                if do and any(q[3].kind == L.OP_GEMM and (q[3].A in do or q[3].B in do)
+                              for q in part):
+                    raise RuntimeError("fp32 matmul on a layer output stored as bf16 only: %s"
+                                       % [q[0] for q in part])
             if len(part) == 1 and part[0][3].kind == L.OP_GEMM and not part[0][3].ktiles:
                 lab, fl, nb, p = part[0]
                 self._k("gemm_" + lab, fl, nb, "pkc_gemm", prec, p.a_kcontig, p.b_kcontig,
@@ -1481,7 +1508,7 @@ class Engine:
         with this step's gather."""
         if pending:
             self._gemms([self._gather_op()] + list(pending), s)
-        else:
+        elif not self.external:
             self._gather(s, batch)
         if self.reg_terms and self.loss_heads:
             self._reg_loss_kernels(s)
@@ -1644,6 +1671,17 @@ class Engine:
         out += [("dW %dx%dx%d%s" % (n.N, n.K, M, " s%d" % sdw if sdw > 1 else ""),
                  2.0 * M * n.N * n.K, 4.0 * (M * n.N + M * n.K + sdw * n.N * n.K), pr,
                  None if prh is None else (2.0 * (M * n.N + M * n.K) + 4.0 * sdw * n.N * n.K, prh))]
+        if n.src[0] == "fea" and self.want_dx:
+            # external mode: dL/dx of the caller's input, one slab straight into ext_dx
+            W = n.Wq if n.qbits else n.W
+            pr = L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=n.K, K=n.N, splits=1,
+                               A=n.dz.data_ptr(), lda=n.N, B=W.data_ptr(), ldb=n.K,
+                               C=self.ext_dx.data_ptr() + 4 * n.src[1], ldc=self.F, slab_stride=0)
+            kt = self._wt(n.W, True)
+            if kt is not None:
+                pr.ktiles, pr.kmax = kt[0].data_ptr(), kt[1]
+            out.append(("dX %dx%dx%d ext" % (M, n.K, n.N), 2.0 * M * n.N * n.K,
+                        4.0 * (M * n.N + n.N * n.K + M * n.K), pr))
         if n.src[0] == "node" and self.needs_grad[n.src[1]]:
             P = n.src[1]
             off = P.cons_off[P.consumers.index(n)]
@@ -1674,8 +1712,12 @@ class Engine:
 
     def _rec_bwd(self, n, s, want_dx0=False):
         M, T = self.M, self.T
-        dy_ptr, dy_ns = n.gslab.data_ptr(), n.sb
-        dy_stride = M * n.N
+        gs = getattr(n, "gsrc", None)
+        if gs is not None:                   # external mode: the caller's output gradient
+            dy_ptr, dy_ns, dy_stride = gs[0].data_ptr(), gs[1], gs[2]
+        else:
+            dy_ptr, dy_ns = n.gslab.data_ptr(), n.sb
+            dy_stride = M * n.N
         for li in reversed(range(len(n.layers))):
             sp, lb = n.layers[li], n.lbuf[li]
             H, K = lb["H"], lb["K"]
@@ -1743,6 +1785,8 @@ class Engine:
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
             if li == 0 and n.src[0] == "node":
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
+            elif li == 0 and want_dx0:               # external mode: dL/dx of the caller's input
+                self._rec_slab_sum_ptr(lb["dx"].data_ptr(), nx, M * K, M * K, self.ext_dx, s)
 
     def _rec_slab_sum(self, slab, ns, numel, out, s):
         """out = sum of ns split-K slabs of a recurrent weight gradient (one grouped launch)."""
@@ -1836,7 +1880,7 @@ class Engine:
                 continue
             if n.rec:
                 flush()
-                self._rec_bwd(n, s, want_dx0=n.src[0] == "node")
+                self._rec_bwd(n, s, want_dx0=n.src[0] == "node" or self.want_dx)
                 continue
             if not n.head:
                 flush()

@@ -11,7 +11,9 @@ so a state_dict / .pkl checkpoint moves between the reference and this package u
 same seed gives the same initial weights and HCGS masks.
 
 The math is NOT executed here: training and forward passes run through pkc.engine (HIP kernels in
-libpkc.so), driven by pkc.core.run_nn or by ``forward()`` below.
+libpkc.so), driven by pkc.core.run_nn, or by ``forward()`` below — an autograd Function over the
+same kernels (pkc.plugin), so the reference's own forward_model + loss.backward() + torch.optim
+loop (utils.py:1884-2050, core.py:216-232) trains these classes too.
 """
 import math
 
@@ -20,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from .cgs import guided_hcgs_mask, hcgs_mask
+from .plugin import arch_forward
 
 
 def strtobool(v):
@@ -220,7 +223,6 @@ class MLP(_PatternSet, nn.Module):
                                                          lin.weight.data)))
             cur = n
         self.out_dim = cur
-        self._engine = None
 
     # --------------------------------------------------------------------- reference hooks
     def prune_parameters(self):
@@ -278,12 +280,8 @@ class MLP(_PatternSet, nn.Module):
                                       "pattern_num / pattern_nnz for the KMeans search")
 
     def forward(self, x):
-        """Forward of this architecture alone on the pkc kernels (eval semantics of BatchNorm when
-        ``self.training`` is False, batch statistics otherwise; no autograd)."""
-        from .engine import ModuleRunner
-        if self._engine is None or self._engine.rows < x.shape[0]:
-            self._engine = ModuleRunner(self, x.shape[0], x.shape[1])
-        return self._engine.forward(x, train=self.training)
+        """(B, F) -> (B, out_dim) on the pkc kernels, trainable under autograd (pkc.plugin)."""
+        return arch_forward(self, x)
 
 
 class liGRU(nn.Module):
@@ -352,6 +350,11 @@ class liGRU(nn.Module):
 
     def prune_parameters(self):
         raise NotImplementedError("the reference liGRU has no prune hook")
+
+    def forward(self, x):
+        """(T, B, F) -> (T, B, out_dim) on the pkc kernels (the shared-weight bidirectional
+        convention when bidir), trainable under autograd (pkc.plugin)."""
+        return arch_forward(self, x)
 
     def check_supported(self):
         pass
@@ -435,6 +438,11 @@ class GRU(nn.Module):
     def prune_parameters(self):
         raise NotImplementedError("the reference GRU has no prune hook")
 
+    def forward(self, x):
+        """(T, B, F) -> (T, B, out_dim) on the pkc kernels (the shared-weight bidirectional
+        convention when bidir), trainable under autograd (pkc.plugin)."""
+        return arch_forward(self, x)
+
     def check_supported(self):
         pass
 
@@ -512,6 +520,11 @@ class _PlainRec(nn.Module):
 
     def prune_parameters(self):
         raise NotImplementedError("the reference %s has no prune hook" % type(self).__name__)
+
+    def forward(self, x):
+        """(T, B, F) -> (T, B, out_dim) on the pkc kernels (the shared-weight bidirectional
+        convention when bidir), trainable under autograd (pkc.plugin)."""
+        return arch_forward(self, x)
 
     def check_supported(self):
         pass
@@ -696,6 +709,11 @@ class LSTM(_PatternSet, nn.Module):
 
     def input_norm_specs(self):
         return _input_norm_specs(self, self.lstm_use_laynorm_inp, self.lstm_use_batchnorm_inp)
+
+    def forward(self, x):
+        """(T, B, F) -> (T, B, out_dim) on the pkc kernels (the shared-weight bidirectional
+        convention when bidir), trainable under autograd (pkc.plugin)."""
+        return arch_forward(self, x)
 
     def check_supported(self):
         if self.if_pattern and self.pattern_kernels is None and not self.can_search_patterns():

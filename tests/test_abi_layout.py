@@ -41,3 +41,31 @@ def test_ctypes_structs_match_header(tmp_path):
     assert len(got) == len(expect)
     bad = [(k, v, g) for (k, v), g in zip(expect, got) if v != g]
     assert not bad, "ctypes vs C layout (name, ctypes, C): %s" % bad
+
+
+# sha256 over the (field, offset) list + sizes of every mirrored struct, per PKC_ABI_VERSION: a
+# struct that changes without a version bump fails here (bump PKC_ABI_VERSION in include/pkc.h and
+# pkc._lib.ABI_VERSION, then record the new digest under the new version)
+LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa09b47"}
+
+
+def _layout_digest(L):
+    import hashlib
+    h = hashlib.sha256()
+    for py, cname in PAIRS:
+        cls = getattr(L, py)
+        h.update(("%s %d;" % (cname, C.sizeof(cls))).encode())
+        for f in cls._fields_:
+            h.update(("%s@%d;" % (f[0], getattr(cls, f[0]).offset)).encode())
+    return h.hexdigest()
+
+
+def test_abi_version_matches_header_and_layout():
+    import re
+    from pkc import _lib as L
+    hdr = open(os.path.join(ROOT, "include", "pkc.h")).read()
+    v = int(re.search(r"#define PKC_ABI_VERSION (\d+)", hdr).group(1))
+    assert v == L.ABI_VERSION
+    assert v in LAYOUT_DIGEST, "PKC_ABI_VERSION %d has no recorded layout digest" % v
+    assert _layout_digest(L) == LAYOUT_DIGEST[v], (
+        "struct layout changed under PKC_ABI_VERSION %d: bump the version" % v)

@@ -600,3 +600,48 @@ def test_engine_dead_f32_outputs_skipped(B, mode, monkeypatch):
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
     assert t0 == t1
+
+
+@pytest.mark.parametrize("where", ["ln_body", "ln_head"])
+def test_engine_dead_f32_outputs_kept_for_layernorm_consumers(where, monkeypatch):
+    """A BatchNorm body layer whose consumer is LayerNorm'd (an LN body layer, or an LN output
+    head) keeps its fp32 output: the LN consumer has no bf16 dz, so its dW runs in fp32 on that
+    output.  The step is bit-identical to the form storing every fp32 output (PKC_F32_OUT=1)."""
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config()
+    if where == "ln_body":
+        cfg["architecture1"].update(dnn_use_batchnorm="True,True,True,True,False",
+                                    dnn_use_laynorm="False,False,False,False,True")
+    else:
+        cfg["architecture2"].update(dnn_use_laynorm="True")
+    B, steps = 128, 2
+    rs = np.random.RandomState(12)
+    X = torch.from_numpy(rs.randn(B * steps, 440).astype(np.float32)).to(DEV)
+    lab = torch.from_numpy(np.stack([rs.randint(0, 1928, B * steps), rs.randint(0, 48, B * steps)],
+                                    1).astype(np.int32)).to(DEV)
+    runs = []
+    for keep in ("1", "0"):
+        monkeypatch.setenv("PKC_F32_OUT", keep)
+        nets, opts = build_nets(cfg, C1_DIMS)
+        for n in nets.values():
+            n.to(DEV).train()
+        eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                     ["lab_cd", "lab_mono"], batch=B, seed=7, prec=L.PREC_BF16, bf16_store=True)
+        dead = {l.name for l in eng.layers if getattr(l, "f32_dead", False)}
+        if keep == "0":
+            last = "MLP_layers1.%d" % (3 if where == "ln_body" else 4)
+            assert last not in dead and dead, dead
+        eng.bind_chunk(X, lab, B * steps)
+        grads = []
+        for _ in range(steps):
+            eng.train_step()
+            torch.cuda.synchronize()
+            grads.append(eng.gflat.detach().cpu().clone())
+        sd = {a + "/" + k: v.detach().cpu().clone() for a in nets for k, v in nets[a].state_dict().items()}
+        runs.append((grads, sd))
+    (g0, s0), (g1, s1) = runs
+    for s in range(steps):
+        assert torch.equal(g0[s], g1[s]), "step %d gradients differ" % s
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
