@@ -96,6 +96,32 @@ __device__ __forceinline__ float drop_val(const pkc_rnn_args& a, int r, int j, i
 // h = o * tanh(c) has |h| < 1) a smaller |x| has x/var < 2^-20, where both quotients give
 // ceil(.) = 1 (x != 0) or 0: the FAST form is bit-identical to the IEEE one (the sign of a zero
 // quotient is dropped by the fabsf either way); any other var takes the IEEE division.
+// Step-kernel grid packed onto x of the 8 XCDs (x = 8: the plain 3-D grid).  Workgroup b of a 1-D
+// grid runs on XCD b % 8 (round-robin dispatch: placement is a speed matter only, never
+// correctness); those on XCDs >= x exit at once and the others take logical tiles (b / 8) x + b % 8.
+// With all of a step's tiles on few XCDs, the h_{t-1} / dgates the previous step's tiles wrote sit
+// in those XCDs' own L2 instead of arriving over the fabric.
+struct PackGrid {
+  int gx, gy, gz, x;
+};
+
+__device__ __forceinline__ bool pack_tile(const PackGrid& p, int& bx, int& by, int& bz) {
+  if (p.x >= 8) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
+    return true;
+  }
+  const int b = blockIdx.x, xcd = b & 7;
+  if (xcd >= p.x) return false;
+  const int l = (b >> 3) * p.x + xcd;
+  if (l >= p.gx * p.gy * p.gz) return false;
+  bx = l % p.gx;
+  by = (l / p.gx) % p.gy;
+  bz = l / (p.gx * p.gy);
+  return true;
+}
+
 struct QParams {
   float var, rcp, scale, iscale;
   bool fast;
@@ -561,8 +587,10 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 // NW waves (4: 256 threads, or 8: the contraction in 32 strips of S — half the operand loads per
 // lane and half the MFMA chain per wave, for the long-H layers whose step is load-latency-bound)
 template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4, bool R16 = false>
-__global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
+__global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw, PackGrid pg) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  int bx, by, bz;
+  if (!pack_tile(pg, bx, by, bz)) return;
   constexpr int NTH = 64 * NW;
   __shared__ float red[NW * 32 * 17];
   __shared__ float tile[32 * 17];
@@ -571,7 +599,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   const int H = a.H, B2 = ix.B2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, q = lane >> 4;
-  const int u0 = blockIdx.x * NU, r0 = blockIdx.y * (R16 ? 16 : 32);
+  const int u0 = bx * NU, r0 = by * (R16 ? 16 : 32);
   const float* src = (PH == 0 ? a.hs : a.rh) + (int64_t)t * B2 * H;
   const int ra = r0 + c, rb = r0 + 16 + c;
   const int gi = c / NU, u = u0 + c % NU;
@@ -588,7 +616,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   if constexpr (SP) {
     static_assert(!QH && PH == 0, "block-sparse U: no quantised h, one-phase cells");
     int blk[S / 16];
-    tile_blocks<S>(a.kmap_fwd + (int64_t)blockIdx.x * S, blk);
+    tile_blocks<S>(a.kmap_fwd + (int64_t)bx * S, blk);
     load_blocks<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
     if constexpr (!R16) load_blocks<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
     load_blocks<S>(pu, u < H, blk, H, vw, vu);
@@ -744,8 +772,11 @@ __device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, 
 // MODE 1: one-gate product + bwd_step_epi (t = tt + 1); MODE 2: one-gate product + rh_epi.
 // out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
 template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4, bool R16 = false>
-__global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
+__global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw,
+                                                      PackGrid pg) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  int bx, by, bz;
+  if (!pack_tile(pg, bx, by, bz)) return;
   constexpr int NTH = 64 * NW;
   __shared__ float red[NW * 32 * 17];
   __shared__ float tile[32 * 17];
@@ -753,8 +784,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   const int H = a.H, B2 = ix.B2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = lane & 15, q = lane >> 4;
-  const int k0 = blockIdx.x * 16, r0 = blockIdx.y * (R16 ? 16 : 32);
-  const int g = g0 + blockIdx.z;
+  const int k0 = bx * 16, r0 = by * (R16 ? 16 : 32);
+  const int g = g0 + bz;
   const int64_t TB2H = (int64_t)a.T * B2 * H;
   const float* dg = a.dgates + g * TB2H + (int64_t)t * B2 * H;
   const int ra = r0 + c, rb = r0 + 16 + c, k = k0 + c;
@@ -763,7 +794,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   if constexpr (SP) {
     static_assert(MODE == 0, "block-sparse U: gate-split BPTT products only");
     int blk[S / 16];
-    tile_blocks<S>(a.kmap_bwd + ((int64_t)g * gridDim.x + blockIdx.x) * S, blk);
+    tile_blocks<S>(a.kmap_bwd + ((int64_t)g * pg.gx + bx) * S, blk);
     load_blocks<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
     if constexpr (!R16) load_blocks<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
     load_blocks<S>(pu, k < H, blk, H, vw, vu);
@@ -782,7 +813,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
     const int r = r0 + rl, kk = k0 + kl;
     if ((R16 && rl >= 16) || r >= B2 || kk >= H) continue;
     const float v = tile[rl * 17 + kl];
-    if constexpr (MODE == 0) a.work[(4 + blockIdx.z) * n + (int64_t)r * H + kk] = v;
+    if constexpr (MODE == 0) a.work[(4 + bz) * n + (int64_t)r * H + kk] = v;
     else if constexpr (MODE == 1) bwd_step_epi<G, CELL>(a, ix, t - 1, r, kk, v);
     else rh_epi<CELL>(a, ix, t, r, kk, v);
   }
@@ -790,11 +821,13 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
 
 // Sum of the NS gate slabs + bwd_step_epi for target tt (elementwise over B2 x H).
 template <int G, int CELL, int NS>
-__global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt) {
+__global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt, PackGrid pg) {
+  int bx, by, bz;
+  if (!pack_tile(pg, bx, by, bz)) return;
   const RnnIdx ix = mkidx(a);
   const int64_t n = (int64_t)ix.B2 * a.H;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t e = bx * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)pg.gx * blockDim.x) {
     float acc = 0.f;
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc += a.work[(4 + s) * n + e];
@@ -885,6 +918,33 @@ static bool eight_waves(int S) {
   return w == 8 && S >= 32;
 }
 
+// XCDs a step kernel's tiles are packed onto (PKC_RNN_XCDS: 8 = the plain grid, 1 / 2 / 4 = that
+// many XCDs; 0 = by tile count, PKC_RNN_TILES_PER_CU tiles per CU at most)
+static PackGrid pack_grid(dim3 g) {
+  static const int mode = [] {
+    const char* v = getenv("PKC_RNN_XCDS");
+    return v ? atoi(v) : 8;
+  }();
+  static const int per_cu = [] {
+    const char* v = getenv("PKC_RNN_TILES_PER_CU");
+    return v ? atoi(v) : 1;
+  }();
+  const int n = (int)(g.x * g.y * g.z);
+  int x = mode;
+  if (x <= 0) {                        // smallest power of two with <= per_cu tiles per CU (32 / XCD)
+    x = 1;
+    while (x < 8 && n > 32 * per_cu * x) x *= 2;
+  }
+  x = x >= 8 ? 8 : (x >= 4 ? 4 : (x >= 2 ? 2 : 1));
+  return PackGrid{(int)g.x, (int)g.y, (int)g.z, x};
+}
+
+static dim3 pack_dim(const PackGrid& p) {
+  if (p.x >= 8) return dim3(p.gx, p.gy, p.gz);
+  const int n = p.gx * p.gy * p.gz;
+  return dim3((unsigned)(((n + p.x - 1) / p.x) * 8));
+}
+
 #ifdef PKC_RNN_FWD
 template <int G, int CELL, int S, bool SP = false>
 static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
@@ -898,13 +958,13 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     const dim3 g1r(g1.x, rows_16), g2r(g2.x, rows_16);
     for (int t = 0; t < a->T; ++t) {
       if (r16) {
-        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false, false, 4, true>), g1r, dim3(RT), 0, s,
-                           *a, t, vw);
-        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false, false, 4, true>), g2r, dim3(RT), 0, s,
-                           *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false, false, 4, true>), pack_dim(pack_grid(g1r)), dim3(RT), 0, s,
+                           *a, t, vw, pack_grid(g1r));
+        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false, false, 4, true>), pack_dim(pack_grid(g2r)), dim3(RT), 0, s,
+                           *a, t, vw, pack_grid(g2r));
       } else {
-        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
-        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), g2, dim3(RT), 0, s, *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), pack_dim(pack_grid(g2)), dim3(RT), 0, s, *a, t, vw, pack_grid(g2));
       }
       if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
@@ -916,29 +976,29 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     for (int t = 0; t < a->T; ++t) {
       if (r16) {
         if constexpr (SP)
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), g16, dim3(RT), 0, s,
-                             *a, t, vw);
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0, s,
+                             *a, t, vw, pack_grid(g16));
         else if (a->qbits > 0 && qh_eight_waves(S))
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), g16,
-                             dim3(2 * RT), 0, s, *a, t, vw);
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), pack_dim(pack_grid(g16)),
+                             dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
         else if (a->qbits > 0)
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), g16, dim3(RT), 0, s,
-                             *a, t, vw);
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0, s,
+                             *a, t, vw, pack_grid(g16));
         else if (eight_waves(S))
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true>), g16,
-                             dim3(2 * RT), 0, s, *a, t, vw);
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true>), pack_dim(pack_grid(g16)),
+                             dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
         else
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true>), g16, dim3(RT), 0,
-                             s, *a, t, vw);
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0,
+                             s, *a, t, vw, pack_grid(g16));
       } else if constexpr (SP)
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), g1, dim3(RT), 0, s, *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
       else if (a->qbits > 0)
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
       else if (eight_waves(S))
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), g1, dim3(2 * RT), 0, s,
-                           *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), pack_dim(pack_grid(g1)), dim3(2 * RT), 0, s,
+                           *a, t, vw, pack_grid(g1));
       else
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
       if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
   }
@@ -969,29 +1029,29 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
     // the candidate gate's U^T product (MODE 2) and the gates' sum (MODE 0 / 1)
     auto mm2 = [&](int t) {
       if (r16)
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S, false, 4, true>), dim3(kt, rows_16, 1),
-                           dim3(RT), 0, s, *a, t, HG, vw);
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 1))),
+                           dim3(RT), 0, s, *a, t, HG, vw, pack_grid(dim3(kt, rows_16, 1)));
       else
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a, t,
-                           HG, vw);
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a, t,
+                           HG, vw, pack_grid(dim3(kt, rows, 1)));
     };
     mm2(a->T - 1);
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (CELL == PKC_CELL_GRU) {           // Uz^T dz + Ur^T dr: two gate slabs
         if (r16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true>), dim3(kt, rows_16, 2),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 2))),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, 2)));
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, 2), dim3(RT), 0, s, *a,
-                             tt + 1, 0, vw);
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, 2>), dim3(eb), dim3(256), 0, s, *a, tt);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), pack_dim(pack_grid(dim3(kt, rows, 2))), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw, pack_grid(dim3(kt, rows, 2)));
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, 2>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
       } else {                                        // minimalGRU: Uz^T dz, one gate
         if (r16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), dim3(kt, rows_16, 1),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 1))),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, 1)));
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
-                             tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw, pack_grid(dim3(kt, rows, 1)));
       }
       if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
       mm2(tt);
@@ -1000,27 +1060,26 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (G == 1) {
         if (r16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), dim3(kt, rows_16, 1),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 1))),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, 1)));
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
-                             tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw, pack_grid(dim3(kt, rows, 1)));
       } else if (r16) {                               // 16-row tiles (C3, C5)
         if (!SP && eight_waves(S))
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>),
-                             dim3(kt, rows_16, G), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), dim3(kt, rows_16, G),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
       } else if (!SP && eight_waves(S)) {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), dim3(kt, rows, G),
-                           dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), pack_dim(pack_grid(dim3(kt, rows, G))),
+                           dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
       } else {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
-                           tt + 1, 0, vw);
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), pack_dim(pack_grid(dim3(kt, rows, G))), dim3(RT), 0, s, *a,
+                           tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
       }
       if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
     }

@@ -1785,7 +1785,7 @@ class Engine:
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
             if li == 0 and n.src[0] == "node":
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
-            elif li == 0 and want_dx0:               # external mode: dL/dx of the caller's input
+            elif li == 0 and self.want_dx:           # external mode: dL/dx of the caller's input
                 self._rec_slab_sum_ptr(lb["dx"].data_ptr(), nx, M * K, M * K, self.ext_dx, s)
 
     def _rec_slab_sum(self, slab, ns, numel, out, s):
