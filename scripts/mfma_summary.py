@@ -11,6 +11,12 @@ GUI_ACTIVE / 8.  (Round 2 divided by the whole GUI_ACTIVE: utilisation 8x too lo
 weak #6.)  Beside it the kernel's achieved TF/s from its dispatch timestamps and that over the
 dense peak of the dtype it issues (tflops_pct_of_peak); the two agree up to the clock the chip
 ran at (util counts cycles, TF/s counts nanoseconds at the 2.4 GHz the peak assumes).
+
+The kernel's cycles: GUI_ACTIVE / 8 counts the whole counter-collection window, which for a
+kernel of a few microseconds is wider than its dispatch (start, end) timestamps — round 3 read
+4.1-5.9 GHz "clocks" off it.  So cycles = ns x min(GUI_ACTIVE / 8 / ns,
+2.4 GHz): the window's clock where the window is the kernel (long kernels), capped at the chip's
+2.4 GHz where it is not; the raw window figure stays in window_clock_ghz.
 Usage: mfma_summary.py <pass dir> [top]"""
 import collections
 import csv
@@ -24,6 +30,7 @@ top = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 SIMDS = 256 * 4
 XCDS = 8
 PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3}     # dense MFMA at 2.4 GHz, 256 CUs
+MAX_CLOCK_GHZ = 2.4
 # per dispatch: SQ counters summed over their instances, GRBM_GUI_ACTIVE the max over its
 # instances (rocprofv3's reduce(GRBM_GUI_ACTIVE, max)), then summed over the kernel's dispatches
 disp = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -51,10 +58,14 @@ for k, c in acc.items():
     busy, gui = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0), c.get("GRBM_GUI_ACTIVE", 0.0)
     dt = "bf16" if c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) >= c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) else "f32"
     tf = fl / c["ns"] / 1e3 if c["ns"] else None
+    wclk = gui / XCDS / c["ns"] if c["ns"] else None          # GHz over the counter window
+    clk = min(wclk, MAX_CLOCK_GHZ) if wclk else None
+    cycles = c["ns"] * clk if clk else 0.0
     rows.append({"kernel": k[:110], "dispatches": len(seen[k]), "mfma_gflop": round(fl / 1e9, 3),
                  "mfma_dtype": dt, "tflops": round(tf, 1) if tf is not None else None,
                  "tflops_pct_of_peak": round(100.0 * tf / PEAK_TFLOPS[dt], 2) if tf else None,
-                 "mfma_util_pct": round(100.0 * busy / (gui / XCDS * SIMDS), 2) if gui else None,
-                 "effective_clock_ghz": round(gui / XCDS / c["ns"], 3) if c["ns"] else None})
+                 "mfma_util_pct": round(100.0 * busy / (cycles * SIMDS), 2) if cycles else None,
+                 "effective_clock_ghz": round(clk, 3) if clk else None,
+                 "window_clock_ghz": round(wclk, 3) if wclk else None})
 rows.sort(key=lambda r: -r["mfma_gflop"])
 print(json.dumps(rows[:top], indent=1))
