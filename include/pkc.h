@@ -20,8 +20,8 @@ extern "C" {
 
 /* Bumped whenever an entry point is added or a struct changes (tests/test_abi_layout.py asserts it):
  * 1: rounds 1-3; 2: pkc_logsoftmax_bwd, and the structs as they stand after round 3 (which appended
- * pkc_dense_bwd_args.dz_scratch without a bump). */
-#define PKC_ABI_VERSION 2
+ * pkc_dense_bwd_args.dz_scratch without a bump); 3: pkc_opt_seg (direct PKC_OP_OPTIM). */
+#define PKC_ABI_VERSION 3
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
@@ -65,7 +65,14 @@ int pkc_gemm_pick_splits(int M, int N, int K);
  *   PKC_OP_LOSS  : pkc_loss_finalize(nheads = M, row_loss = A, weights = B, rows = N,
  *                  row_err = X1, out = C, acc = X2, advance_ctr = X3)
  *   PKC_OP_OPTIM : pkc_optim_step(tensors_dev = A, chunk_map_dev = B, nchunks = M) — the update of
- *                  a layer whose gradients are complete rides in a later launch of the backward
+ *                  a layer whose gradients are complete rides in a later launch of the backward.
+ *                  Direct form (X1 != NULL): X1 is a HOST array of N pkc_opt_seg (read during the
+ *                  call) listing the op's work items as runs of chunks of single tensors, M = the
+ *                  sum of their nchunks.  Their pointers travel in the kernel arguments, so a work
+ *                  item's loads start without the map -> descriptor round trips; the
+ *                  hyper-parameters (lr, step, ...) are still read from tensors_dev[tensor], so a
+ *                  captured graph sees set_lr / step updates.  When a launch's direct segments would
+ *                  exceed PKC_OPT_SEGS_MAX the op falls back to the map (B then required).
  *   PKC_OP_GATHER: pkc_batch_gather(feats = A, ld_feats = lda, F = N, labels = B, nlab = ldb,
  *                  B = M rows, n_batches = slab_stride, step_ctr = X1, x_out = C, lab_out = X2,
  *                  advance = 0, x_bf16 = X3) — the next batch's gather sharing a launch with the
@@ -228,6 +235,18 @@ typedef struct pkc_opt_tensor_s {
 } pkc_opt_tensor;
 int pkc_optim_step(const pkc_opt_tensor* tensors_dev, int ntensors, const int32_t* chunk_map_dev,
                    int nchunks, void* stream);
+/* One run of work items of a direct PKC_OP_OPTIM operation (pkc_gemm_grouped): chunks
+ * [chunk0, chunk0 + nchunks) (pkc_optim_chunks' 2048-element items) of tensor `tensor` of the
+ * descriptor array.  p .. bout and n repeat that descriptor's, except that s1 / s2 / s3 / qout are
+ * NULL where the update keeps no such state (SGD without momentum: s1 NULL; qout NULL unless
+ * qbits > 0): the kernel decides which streams to touch from these pointers alone. */
+#define PKC_OPT_SEGS_MAX 8     /* direct segments per grouped launch */
+typedef struct pkc_opt_seg_s {
+  int tensor, chunk0, nchunks, reserved;
+  float* p; const float* g; float* s1; float* s2; float* s3; const float* mask;
+  float* qout; void* bout;
+  int64_t n;
+} pkc_opt_seg;
 /* Host helper: size of the chunk map (pairs tensor,start) for pkc_optim_step. */
 int pkc_optim_chunks(const int64_t* sizes, int ntensors, int32_t* map_out, int cap);
 

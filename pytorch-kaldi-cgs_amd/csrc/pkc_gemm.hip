@@ -632,6 +632,7 @@ struct GroupProb {
 struct GroupArgs {
   GroupProb p[GMAX];
   int n;
+  OptSegK seg[PKC_OPT_SEGS_MAX];   // direct PKC_OP_OPTIM runs (GroupProb: code 1, segments K .. K+N)
 };
 
 // SUM: the launch carries slab-sum operations (large-batch split-K dW); a separate instance,
@@ -667,6 +668,17 @@ __device__ __forceinline__ void grouped_body(const GroupArgs& g) {
     }
   }
   if (p.kind == PKC_OP_OPTIM) {
+    if (p.code) {                    // direct runs: pointers in the kernel arguments
+      int j = p.K;
+#pragma unroll
+      for (int u = 1; u < PKC_OPT_SEGS_MAX; ++u) {
+        const int jj = min(p.K + u, PKC_OPT_SEGS_MAX - 1);   // in bounds even when speculated
+        if (u < p.N && local >= g.seg[jj].begin) j = jj;
+      }
+      const OptSegK& sg = g.seg[j];
+      optim_seg_wg(reinterpret_cast<const pkc_opt_tensor*>(p.A), sg, local - sg.begin);
+      return;
+    }
     optim_wg(reinterpret_cast<const pkc_opt_tensor*>(p.A), reinterpret_cast<const int32_t*>(p.B),
              local);
     return;
@@ -1022,7 +1034,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
                 "pkc_gemm_grouped: bad precision %d", prec);
   GroupArgs g;
   memset(&g, 0, sizeof(g));
-  int wg = 0, k = 0;
+  int wg = 0, k = 0, nseg = 0;
   bool any_big = false, any_sparse = false, any_sum = false, all_vec = true;
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   // a launch with block-sparse problems runs the sparse instance, which has no 128x128 body
@@ -1030,12 +1042,33 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   for (int i = 0; i < n; ++i) {
     const pkc_gemm_problem& q = probs[i];
     if (q.kind == PKC_OP_OPTIM) {
-      PKC_CHECK_ARG(q.M > 0 && q.A && q.B, "pkc_gemm_grouped: optimizer op %d arguments", i);
+      const pkc_opt_seg* sg = reinterpret_cast<const pkc_opt_seg*>(q.X1);
+      const bool direct = sg && q.N >= 1 && nseg + q.N <= PKC_OPT_SEGS_MAX;
+      PKC_CHECK_ARG(q.M > 0 && q.A && (q.B || direct), "pkc_gemm_grouped: optimizer op %d arguments",
+                    i);
       GroupProb& p = g.p[k++];
       memset(&p, 0, sizeof(p));
       p.kind = q.kind;
       p.A = q.A; p.B = q.B;
       p.wg0 = wg;
+      if (direct) {
+        int c = 0;
+        for (int j = 0; j < q.N; ++j) {
+          PKC_CHECK_ARG(sg[j].nchunks > 0 && sg[j].chunk0 >= 0 && sg[j].tensor >= 0 && sg[j].p &&
+                            sg[j].g && sg[j].n > (int64_t)(sg[j].chunk0 + sg[j].nchunks - 1) * OPT_CHUNK,
+                        "pkc_gemm_grouped: optimizer op %d segment %d", i, j);
+          OptSegK& d = g.seg[nseg + j];
+          d.p = sg[j].p; d.g = sg[j].g; d.s1 = sg[j].s1; d.s2 = sg[j].s2; d.s3 = sg[j].s3;
+          d.mask = sg[j].mask; d.qout = sg[j].qout; d.bout = sg[j].bout; d.n = sg[j].n;
+          d.tensor = sg[j].tensor; d.chunk0 = sg[j].chunk0; d.begin = c;
+          c += sg[j].nchunks;
+          d.end = c;
+        }
+        PKC_CHECK_ARG(c == q.M, "pkc_gemm_grouped: optimizer op %d: segments hold %d chunks, M = %d",
+                      i, c, q.M);
+        p.code = 1; p.K = nseg; p.N = q.N;
+        nseg += q.N;
+      }
       wg += q.M;
       continue;
     }

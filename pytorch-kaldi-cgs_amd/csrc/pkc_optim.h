@@ -84,11 +84,14 @@ constexpr int OPT_T = 256, OPT_PER = PKC_OPT_PER, OPT_CHUNK = OPT_T * OPT_PER;
 // Every operand of a thread's OPT_PER elements is requested before any is used (independent
 // loads in flight instead of one round trip per element); states the optimizer does not keep are
 // never touched.  VEC: the tensor's pointers are 16-byte aligned and n % 4 == 0.
-template <bool VEC>
+// DIRECT: the streams to touch follow from the pointers alone (pkc_opt_seg: s1 NULL when the update
+// keeps no first state, qout NULL unless quantised), so no load waits on the descriptor's fields.
+template <bool VEC, bool DIRECT = false>
 __device__ __forceinline__ void optim_chunk(const pkc_opt_tensor& t, int64_t start) {
   constexpr int V = 4, NV = OPT_PER / V;
-  const bool st1 = t.kind != PKC_OPT_SGD || t.momentum != 0.f;
+  const bool st1 = DIRECT ? t.s1 != nullptr : (t.kind != PKC_OPT_SGD || t.momentum != 0.f);
   const bool st2 = t.s2 != nullptr, st3 = t.s3 != nullptr, msk = t.mask != nullptr;
+  const bool qw = DIRECT ? t.qout != nullptr : t.qbits > 0;
   if (VEC) {
     float4 P[NV], G[NV], S1[NV], S2[NV], S3[NV], MK[NV];
     int64_t idx[NV];
@@ -116,17 +119,19 @@ __device__ __forceinline__ void optim_chunk(const pkc_opt_tensor& t, int64_t sta
                    msk ? mm[l] : 1.f};
         opt_update(t, e);
         pp[l] = e.p; a1[l] = e.s1; a2[l] = e.s2; a3[l] = e.s3;
-        if (t.qbits > 0) qq[l] = quant_w(e.p, t.qbits);
+        if (qw) qq[l] = quant_w(e.p, t.qbits);
       }
       const int64_t i = idx[j];
       *reinterpret_cast<float4*>(t.p + i) = P[j];
       if (st1) *reinterpret_cast<float4*>(t.s1 + i) = S1[j];
       if (st2) *reinterpret_cast<float4*>(t.s2 + i) = S2[j];
       if (st3) *reinterpret_cast<float4*>(t.s3 + i) = S3[j];
-      if (t.qbits > 0) *reinterpret_cast<float4*>(t.qout + i) = Q;
-      if (t.bout) {
-        __bf16* bo = reinterpret_cast<__bf16*>(t.bout) + i;
-        bo[0] = (__bf16)P[j].x; bo[1] = (__bf16)P[j].y; bo[2] = (__bf16)P[j].z; bo[3] = (__bf16)P[j].w;
+      if (qw) *reinterpret_cast<float4*>(t.qout + i) = Q;
+      if (t.bout) {   // one 8-byte store (bout % 8 == 0 on this path)
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 h;
+        h[0] = (__bf16)P[j].x; h[1] = (__bf16)P[j].y; h[2] = (__bf16)P[j].z; h[3] = (__bf16)P[j].w;
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(t.bout) + i) = h;
       }
     }
   } else {
@@ -151,10 +156,36 @@ __device__ __forceinline__ void optim_chunk(const pkc_opt_tensor& t, int64_t sta
       if (st1) t.s1[i] = e[j].s1;
       if (st2) t.s2[i] = e[j].s2;
       if (st3) t.s3[i] = e[j].s3;
-      if (t.qbits > 0) t.qout[i] = quant_w(e[j].p, t.qbits);
+      if (qw) t.qout[i] = quant_w(e[j].p, t.qbits);
       if (t.bout) reinterpret_cast<__bf16*>(t.bout)[i] = (__bf16)e[j].p;
     }
   }
+}
+
+// A direct work-item run (pkc_opt_seg) as the grouped launch's kernel arguments carry it: op-local
+// work items [begin, end) are chunks chunk0 .. of tensor `tensor`.
+struct OptSegK {
+  float* p; const float* g; float* s1; float* s2; float* s3; const float* mask; float* qout; void* bout;
+  int64_t n;
+  int tensor, chunk0, begin, end;
+};
+
+__device__ __forceinline__ bool optim_vec(const pkc_opt_tensor& t) {
+  return (t.n % 4 == 0) && ((uintptr_t)t.p % 16 == 0) && ((uintptr_t)t.g % 16 == 0) &&
+         ((uintptr_t)t.s1 % 16 == 0) && ((uintptr_t)t.s2 % 16 == 0) &&
+         ((uintptr_t)t.s3 % 16 == 0) && ((uintptr_t)t.mask % 16 == 0) &&
+         ((uintptr_t)t.qout % 16 == 0) && ((uintptr_t)t.bout % 8 == 0);
+}
+
+// work item `chunk` of a direct run: pointers from the kernel arguments, hyper-parameters from the
+// descriptor (its scalar loads are in flight with the first data loads)
+__device__ __forceinline__ void optim_seg_wg(const pkc_opt_tensor* ts, const OptSegK& sg, int chunk) {
+  pkc_opt_tensor t = ts[sg.tensor];
+  t.p = sg.p; t.g = sg.g; t.s1 = sg.s1; t.s2 = sg.s2; t.s3 = sg.s3; t.mask = sg.mask;
+  t.qout = sg.qout; t.bout = sg.bout; t.n = sg.n;
+  const int64_t start = (int64_t)(sg.chunk0 + chunk) * OPT_CHUNK;
+  if (optim_vec(t)) optim_chunk<true, true>(t, start);
+  else optim_chunk<false, true>(t, start);
 }
 
 // work item `wg` of a chunk map (pairs tensor, chunk) over the descriptor array ts
@@ -162,11 +193,7 @@ __device__ __forceinline__ void optim_wg(const pkc_opt_tensor* ts, const int32_t
   const int ti = map[2 * wg];
   const int64_t start = (int64_t)map[2 * wg + 1] * OPT_CHUNK;
   const pkc_opt_tensor t = ts[ti];
-  const bool vec = (t.n % 4 == 0) && ((uintptr_t)t.p % 16 == 0) && ((uintptr_t)t.g % 16 == 0) &&
-                   ((uintptr_t)t.s1 % 16 == 0) && ((uintptr_t)t.s2 % 16 == 0) &&
-                   ((uintptr_t)t.s3 % 16 == 0) && ((uintptr_t)t.mask % 16 == 0) &&
-                   ((uintptr_t)t.qout % 16 == 0) && ((uintptr_t)t.bout % 8 == 0);
-  if (vec) optim_chunk<true>(t, start);
+  if (optim_vec(t)) optim_chunk<true>(t, start);
   else optim_chunk<false>(t, start);
 }
 

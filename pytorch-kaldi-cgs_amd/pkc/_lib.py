@@ -9,7 +9,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
-ABI_VERSION = 2         # include/pkc.h PKC_ABI_VERSION
+ABI_VERSION = 3         # include/pkc.h PKC_ABI_VERSION
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 PREC_FP32, PREC_BF16, PREC_BF16IN = 0, 1, 2
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
@@ -54,6 +54,15 @@ class OptTensor(C.Structure):
                 ("beta1", C.c_float), ("beta2", C.c_float), ("clampv", C.c_float),
                 ("nesterov", C.c_int), ("centered", C.c_int), ("amsgrad", C.c_int), ("step", C.c_int),
                 ("qout", vp), ("qbits", C.c_int), ("bout", vp)]
+
+
+class OptSeg(C.Structure):
+    _fields_ = [("tensor", C.c_int), ("chunk0", C.c_int), ("nchunks", C.c_int), ("reserved", C.c_int),
+                ("p", vp), ("g", vp), ("s1", vp), ("s2", vp), ("s3", vp), ("mask", vp), ("qout", vp),
+                ("bout", vp), ("n", i64)]
+
+
+OPT_SEGS_MAX = 8        # include/pkc.h PKC_OPT_SEGS_MAX
 
 
 CELL_LIGRU, CELL_LSTM, CELL_GRU, CELL_MINGRU, CELL_RNN = 0, 1, 2, 3, 4

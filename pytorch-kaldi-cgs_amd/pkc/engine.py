@@ -53,6 +53,9 @@ MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", "0"))
 # 14.3 us, profiles/r03_launch_probe.txt): 2.5M 863-869k, 1M 874-876k, 700k 878-879k, 500k
 # 874-875k (profiles/r03_opt_spread_ab.txt)
 OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "700000"))
+# the spread updates' work items take their tensors' pointers from the launch's kernel arguments
+# (pkc_opt_seg) instead of a chunk map -> descriptor -> data chain of dependent loads (0: map form)
+OPT_DIRECT = os.environ.get("PKC_OPT_DIRECT", "1") != "0"
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
 # 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
@@ -941,6 +944,7 @@ class Engine:
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
         self.opt_entries = []
+        self._host_maps, self._seg_keep = {}, []
         for n in self.nodes:
             if not self.needs_grad[n] or self.external:
                 continue
@@ -1053,7 +1057,39 @@ class Engine:
         L.lib().pkc_optim_chunks(sizes, len(idx), cmap, nch)
         m = np.frombuffer(cmap, dtype=np.int32).copy().reshape(-1, 2)
         m[:, 0] = np.asarray(idx, dtype=np.int32)[m[:, 0]]
-        return nch, torch.from_numpy(m.reshape(-1)).to(self.dev)
+        dev = torch.from_numpy(m.reshape(-1)).to(self.dev)
+        self._host_maps[dev.data_ptr()] = m
+        return nch, dev
+
+    def _opt_segs(self, cmap, b, e):
+        """Direct form of work items [b, e) of a chunk map (pkc_opt_seg runs: one per tensor, the
+        pointers passed in the launch's kernel arguments), or None (PKC_OPT_DIRECT=0)."""
+        if not OPT_DIRECT:
+            return None
+        m = self._host_maps[cmap.data_ptr()][b:e]
+        runs = []
+        for ti, c in m:
+            if runs and runs[-1][0] == ti and runs[-1][1] + runs[-1][2] == c:
+                runs[-1][2] += 1
+            else:
+                runs.append([int(ti), int(c), 1])
+        segs = (L.OptSeg * len(runs))()
+        for k, (ti, c0, nc) in enumerate(runs):
+            ent = self.opt_entries[ti]
+            kind, o = ent["o"]["arch_opt"], ent["o"]
+            sg = segs[k]
+            sg.tensor, sg.chunk0, sg.nchunks = ti, c0, nc
+            sg.p, sg.g = ent["p"].data_ptr(), ent["g"].data_ptr()
+            keeps_s1 = kind != "sgd" or float(o.get("opt_momentum", "0")) != 0.0
+            sg.s1 = ent["s1"].data_ptr() if keeps_s1 else None
+            sg.s2 = ent["s2"].data_ptr() if ent["s2"] is not None else None
+            sg.s3 = ent["s3"].data_ptr() if ent["s3"] is not None else None
+            sg.mask = ent["mask"].data_ptr() if ent["mask"] is not None else None
+            sg.qout = ent["q"].data_ptr() if ent["qbits"] else None
+            sg.bout = ent["bout"].data_ptr() if ent.get("bout") is not None else None
+            sg.n = ent["p"].numel()
+        self._seg_keep.append(segs)
+        return segs
 
     def _upload_opt_desc(self, step_inc):
         n = len(self.opt_entries)
@@ -1810,10 +1846,13 @@ class Engine:
         ops, b = [], 0
         for k in range(parts):
             e = (nch * (k + 1)) // parts
+            segs = self._opt_segs(cmap, b, e)
             ops.append(("opt %s%s" % (n.name, "" if parts == 1 else " [%d/%d]" % (k + 1, parts)), 0.0,
                         (20.0 * nparam + 2.0 * nbout) * (e - b) / nch,
                         L.GemmProblem(kind=L.OP_OPTIM, M=e - b, A=self.opt_desc.data_ptr(),
-                                      B=cmap.data_ptr() + 8 * b)))
+                                      B=cmap.data_ptr() + 8 * b,
+                                      X1=C.addressof(segs) if segs is not None else None,
+                                      N=len(segs) if segs is not None else 0)))
             b = e
         return ops
 

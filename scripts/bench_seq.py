@@ -62,12 +62,13 @@ def rec_opts(cfg_name):
     return "LSTM", d, (16 if cfg_name == "c4" else 12)
 
 
-def build(cfg_name, seed=2234, rank=0, world=1):
+def build(cfg_name, seed=2234, rank=0, world=1, prec="fp32"):
     """Engine + nets of `cfg_name` bound to a synthetic length-sorted chunk of 64 * B sentences.
     Data parallelism (world > 1): every rank builds the same model from the same seeds and draws
     its OWN chunk (weak scaling: B sentences per rank and step), its loss scaled per batch by its
     share of the global batch's padded rows (pkc.dist.frame_weights, one collective per chunk)."""
     import pkc.neural_networks as NN
+    from pkc import _lib as L
     from pkc.engine import Engine, parse_model
     cls, ropts, B = rec_opts(cfg_name)
     cfg = configparser.ConfigParser()
@@ -109,7 +110,8 @@ def build(cfg_name, seed=2234, rank=0, world=1):
         from pkc import dist as DP
         max_len = -DP.agree_min(-max_len, device="cuda")
     eng = Engine(nets, opts, parse_model(model), {"fea": (0, 440)}, ["lab_cd", "lab_mono"],
-                 batch=B, max_len=max_len, seed=seed + rank, grad_scale=1.0 / world)
+                 batch=B, max_len=max_len, seed=seed + rank, grad_scale=1.0 / world,
+                 prec=L.PREC_BF16 if prec == "bf16" else L.PREC_FP32)
     eng.bind_chunk(feats, labs, N, end_index=end)
     if world > 1:
         from pkc import dist as DP
@@ -137,11 +139,11 @@ def alg_flops_per_row(nets):
     return per_dir_row, head
 
 
-def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1):
+def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32"):
     """Times `steps` sentence batches after `warmup` (barrier + synchronize on both sides of the
     timed region; the max over ranks).  frames_per_s is the whole job's: every rank's real frames
     over that time."""
-    eng, nets, B = build(cfg_name, rank=rank, world=world)
+    eng, nets, B = build(cfg_name, rank=rank, world=world, prec=prec)
     rng = random.Random(7)
     # sample the batches across the length-sorted chunk (short and long sentences alike)
     nb = eng.n_batches
@@ -179,7 +181,7 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1):
     dirs = 2 if specs[0]["bidir"] else 1
     per_row, head = alg_flops_per_row(nets)
     flops = world * tsteps * B * (dirs * per_row + head)  # padded rows, as the reference computes
-    return {"config": cfg_name, "batch_sentences": B, "steps": steps, "n_ranks": world,
+    return {"config": cfg_name, "prec": prec, "batch_sentences": B, "steps": steps, "n_ranks": world,
             "frames_per_s": frames / dt, "ms_per_step": dt * 1e3 / steps,
             "us_per_time_step_per_layer_fwd_bwd": dt * 1e6 / (tsteps * nl),
             "mean_T": tsteps / steps, "alg_tflops_per_s": flops / dt / 1e12,
@@ -280,10 +282,11 @@ def main():
     ap.add_argument("--configs", default="c3,c4,c5,gru")
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     out = []
     for c in a.configs.split(","):
-        r = run(c, a.steps, a.warmup)
+        r = run(c, a.steps, a.warmup, prec=a.prec)
         print(json.dumps(r), flush=True)
         out.append(r)
         torch.cuda.empty_cache()

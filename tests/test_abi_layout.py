@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"))
 
 PAIRS = [("DenseFwdArgs", "pkc_dense_fwd_args"), ("DenseBwdArgs", "pkc_dense_bwd_args"),
          ("NllArgs", "pkc_nll_args"), ("OptTensor", "pkc_opt_tensor"), ("RnnArgs", "pkc_rnn_args"),
-         ("GemmProblem", "pkc_gemm_problem"), ("RegItem", "pkc_reg_item")]
+         ("GemmProblem", "pkc_gemm_problem"), ("RegItem", "pkc_reg_item"), ("OptSeg", "pkc_opt_seg")]
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
@@ -46,7 +46,8 @@ def test_ctypes_structs_match_header(tmp_path):
 # sha256 over the (field, offset) list + sizes of every mirrored struct, per PKC_ABI_VERSION: a
 # struct that changes without a version bump fails here (bump PKC_ABI_VERSION in include/pkc.h and
 # pkc._lib.ABI_VERSION, then record the new digest under the new version)
-LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa09b47"}
+LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa09b47",
+                 3: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012"}
 
 
 def _layout_digest(L):
