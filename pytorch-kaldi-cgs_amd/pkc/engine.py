@@ -41,8 +41,10 @@ MAX_SPLITS = int(os.environ.get("PKC_MAX_SPLITS", "4"))
 SLAB_BUDGET_MULTI = min(8, int(os.environ.get("PKC_SLAB_BUDGET_MULTI", "8")))
 # forward Z = X W^T (0: by precision — MAX_SPLITS for bf16 operands; 8 for exact fp32, whose
 # 128-row forward matmuls are bound by each workgroup's fp32 operand bytes and MFMA chain: C2 fp32
-# 565k -> 578k frames/s with 8, 487k with 2, same box, profiles/r03_fp32_splits_ab.txt)
+# 565k -> 578k frames/s with 8, 487k with 2, same box, profiles/r03_fp32_splits_ab.txt); an
+# explicit PKC_MAX_SPLITS still caps the fp32 forward splits when PKC_MAX_SPLITS_FWD is unset
 MAX_SPLITS_FWD = int(os.environ.get("PKC_MAX_SPLITS_FWD", "0"))
+_FP32_FWD_SPLITS = MAX_SPLITS if "PKC_MAX_SPLITS" in os.environ else 8
 # spread optimizer updates: a layer's update larger than this many parameters is cut into parts
 # that ride in successive backward launches (0: one part).  Round 1 (fp32-stored operands), C2
 # frames/s: 0 -> 653-657k, 1.2M -> 663k, 700k -> 666-667k, 400k-520k -> 669-671k, 250k -> 644k.
@@ -56,6 +58,10 @@ OPT_SPREAD_PARAMS = int(os.environ.get("PKC_OPT_SPREAD_PARAMS", "700000"))
 # the spread updates' work items take their tensors' pointers from the launch's kernel arguments
 # (pkc_opt_seg) instead of a chunk map -> descriptor -> data chain of dependent loads (0: map form)
 OPT_DIRECT = os.environ.get("PKC_OPT_DIRECT", "1") != "0"
+# sequence models: pinned host slots of the per-batch metadata upload, and the number of captured
+# per-T step graphs kept (least recently used dropped first)
+SEQ_META_SLOTS = 4
+SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
 # 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
@@ -123,6 +129,16 @@ class RegTerm:
                     items.append((p, g, Cc, a, min(a + per, r1), c0, c1, len(bstart) - 1))
                 bstart.append(len(items))
         return items, bstart
+
+
+class SeqBatch(tuple):
+    """(begin rows, lengths, left pads, T) of one sentence batch, plus .index: the batch's
+    position in the bound chunk (its data-parallel frame weight, Engine.frame_scales)."""
+
+    def __new__(cls, items, index):
+        t = tuple.__new__(cls, items)
+        t.index = index
+        return t
 
 
 def _f32(n, dev):
@@ -462,6 +478,7 @@ class Engine:
         self.graph_opt = None
         self.graph_multi, self.steps_per_graph = None, 1
         self.graph_tail = None
+        self.seq_graphs = None                 # sequence models: padded T -> captured step
         self.steps_done = 0
         self.skip_labels = set()
         self.n_launches = 0                    # libpkc launches issued (or captured) so far
@@ -642,7 +659,7 @@ class Engine:
                 continue
             N, K = n.N, n.K
             n.scap = self.cap or _splits(M, N, K, MAX_SPLITS_FWD or
-                                         (8 if self.prec == L.PREC_FP32 else MAX_SPLITS))
+                                         (_FP32_FWD_SPLITS if self.prec == L.PREC_FP32 else MAX_SPLITS))
             n.zslab = _f32(n.scap * M * N, dev) if n.W is not None else None
             if n.ln:
                 n.ln_y, n.ln_xhat = _f32(M * N, dev), _f32(M * N, dev)
@@ -722,6 +739,13 @@ class Engine:
                                        device=dev)
         if self.seq:
             self.seq_meta = torch.zeros(4 * self.B, dtype=torch.int64, device=dev)
+            # host side of the per-batch metadata upload: a ring of pinned slots, each reused only
+            # after the copy that read it has run (its event), so the upload never waits on the
+            # device queue (the reference's per-batch host round trip, core.py:186-214)
+            self.meta_ring = [torch.zeros(4 * self.B, dtype=torch.int64).pin_memory()
+                              for _ in range(SEQ_META_SLOTS)]
+            self.meta_ev = [None] * SEQ_META_SLOTS
+            self.meta_k = 0
         if self.external:
             self.ext_dx = _f32(M * self.F, dev)   # dL/dx of the caller's input
 
@@ -1141,6 +1165,10 @@ class Engine:
         lengths) subset of them (a data-parallel rank's share, pkc.dist.shard_sentences)."""
         assert feats.dtype == torch.float32 and labels.dtype == torch.int32
         assert feats.shape[1] >= self.F and labels.shape[1] == self.nlab
+        key = (feats.data_ptr(), feats.stride(0), labels.data_ptr())
+        if self.seq_graphs and key != getattr(self, "_chunk_key", None):
+            self.seq_graphs.clear()            # the captured gathers read the old chunk
+        self._chunk_key = key
         self.chunk_feats, self.chunk_labels = feats, labels
         if self.seq:
             if sentences is None:
@@ -1169,7 +1197,7 @@ class Engine:
         lefts = np.array([rng.randint(0, T - int(l)) for l in lens], dtype=np.int64)
         self.batch_i = i0 // self.B
         self.snt += self.B
-        return begs.astype(np.int64), lens.astype(np.int64), lefts, T
+        return SeqBatch((begs.astype(np.int64), lens.astype(np.int64), lefts, T), self.batch_i)
 
     # ------------------------------------------------------------------ launch helpers
     @staticmethod
@@ -1247,19 +1275,31 @@ class Engine:
                     self.n_batches, ptr(self.ctr), ptr(self.x), ptr(self.labs),
                     0 if self.loss_heads else 1, ptr(self.x_h), s)
             return
-        begs, lens, lefts, T = batch
-        # [B x int64 begin rows][B x int32 lengths][B x int32 left pads]
-        host = np.zeros(4 * self.B, dtype=np.int64)
-        host[:self.B] = begs
-        h32 = host[self.B:].view(np.int32)
-        h32[:self.B] = lens
-        h32[self.B:2 * self.B] = lefts
-        self.seq_meta.copy_(torch.from_numpy(host), non_blocking=False)
+        T = batch[3]
         mp = self.seq_meta.data_ptr()
         self._k("seq_gather", 0, 8.0 * T * self.B * self.F, "pkc_seq_gather", ptr(self.chunk_feats),
                 self.chunk_feats.stride(0), self.F, ptr(self.chunk_labels), self.nlab,
                 C.c_void_p(mp), C.c_void_p(mp + 8 * self.B), C.c_void_p(mp + 8 * self.B + 4 * self.B),
                 self.B, T, ptr(self.x), ptr(self.labs), s)
+
+    def _upload_seq_meta(self, batch):
+        """[B x int64 begin rows][B x int32 lengths][B x int32 left pads] of a sentence batch into
+        seq_meta: an asynchronous copy from a pinned ring slot, ordered on the stream before the
+        step's gather (no host synchronisation per batch)."""
+        begs, lens, lefts, _ = batch[:4]
+        k = self.meta_k % SEQ_META_SLOTS
+        self.meta_k += 1
+        if self.meta_ev[k] is not None:
+            self.meta_ev[k].synchronize()        # the copy that last read this slot has run
+        host = self.meta_ring[k].numpy()
+        host[:self.B] = begs
+        h32 = host[self.B:].view(np.int32)
+        h32[:self.B] = lens
+        h32[self.B:2 * self.B] = lefts
+        self.seq_meta.copy_(self.meta_ring[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.meta_ev[k] = ev
 
     def _gather_op(self):
         """The frame batch gather as an operation of a grouped launch (PKC_OP_GATHER)."""
@@ -2058,9 +2098,13 @@ class Engine:
                 # sequence DP: rank r's padded batch has T_r * B rows; scale its mean loss by its
                 # share of all ranks' rows, so the summed gradient is that of the mean over every
                 # row of the global batch, not the mean of unequal batch means
-                self.grad_scale = float(self.frame_scales[self.batch_i])
-            self._train_step_kernels(allreduce, batch)
-            self.ctr.add_(1)           # step counter of the dropout RNG streams
+                self.grad_scale = float(self.frame_scales[getattr(batch, "index", self.batch_i)])
+            self._upload_seq_meta(batch)
+            if self.seq_graphs is not None and allreduce is None and self.frame_scales is None:
+                self._seq_graph(batch).replay()
+            else:
+                self._train_step_kernels(allreduce, batch)
+                self.ctr.add_(1)           # step counter of the dropout RNG streams
         elif self.graph is not None:
             if self.graph_opt is not None and self.graph_tail is not None:
                 # bucketed: first bucket all-reduced while the rest of the backward replays
@@ -2103,6 +2147,8 @@ class Engine:
         if self.seq:
             batch = batch or self.next_seq_batch()
         self._set_rows(batch)
+        if self.seq:
+            self._upload_seq_meta(batch)
         self._forward_kernels(self._stream(), False, batch)
 
     def profile_step(self):
@@ -2173,14 +2219,43 @@ class Engine:
         if self.opt_entries and not self.static_opt and self.graph is None:
             self._upload_opt_desc(step_inc=1)
 
+    def _seq_graph(self, batch):
+        """The captured training step of a sentence batch of padded length T (captured on first
+        use, kept in an LRU of SEQ_GRAPHS): every launch of the step — gather, recurrent time
+        loops, heads, backward, optimizer — and the dropout step counter's increment.  Its inputs
+        are the device-side batch metadata (seq_meta, uploaded before the replay), the chunk and
+        the device step counters, so one graph serves every batch of that T."""
+        T = int(batch[3])
+        g = self.seq_graphs.pop(T, None)
+        if g is None:
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st, pool=self.seq_pool):
+                self._train_step_kernels(None, batch)
+                self.ctr.add_(1)
+            torch.cuda.current_stream().wait_stream(st)
+            self.seq_captures += 1
+            while len(self.seq_graphs) >= max(1, SEQ_GRAPHS):
+                self.seq_graphs.pop(next(iter(self.seq_graphs)))
+        self.seq_graphs[T] = g                  # most recently used last
+        return g
+
     def capture(self, split_optimizer=False, steps_per_graph=8):
-        """Capture the training step into hipGraph(s) (non-sequential models with step-independent
-        optimizer descriptors: RMSprop / momentum-free SGD).  split_optimizer=True captures
+        """Capture the training step into hipGraph(s) (models with step-independent optimizer
+        descriptors: RMSprop / momentum-free SGD).  split_optimizer=True captures
         forward+backward and the optimizer separately so a gradient all-reduce fits in between.
         Without the split, a second graph holds steps_per_graph consecutive steps (the batch
         counter lives on the device), so train_steps() pays one graph launch per that many
-        batches instead of one per batch."""
-        if not self.static_opt or self.seq or self.sync_bn is not None:
+        batches instead of one per batch.  Sequence models: per padded length T, each step's
+        launches are captured the first time a batch of that T trains and replayed after that
+        (single-process steps with a fixed loss scale; data-parallel steps stay eager)."""
+        if self.seq:
+            if not self.static_opt or self.sync_bn is not None or self.external:
+                return False
+            self.seq_graphs, self.seq_pool, self.seq_captures = {}, torch.cuda.graph_pool_handle(), 0
+            return True
+        if not self.static_opt or self.sync_bn is not None:
             return False             # SyncBN: collectives inside the forward / backward, eager
         self._set_rows(None)
         s = torch.cuda.Stream()

@@ -139,11 +139,16 @@ def alg_flops_per_row(nets):
     return per_dir_row, head
 
 
-def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32"):
+def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32", graphs=False):
     """Times `steps` sentence batches after `warmup` (barrier + synchronize on both sides of the
     timed region; the max over ranks).  frames_per_s is the whole job's: every rank's real frames
-    over that time."""
+    over that time.  graphs: the steps replay per-T captured graphs (Engine.capture), captured in
+    an untimed pass over the timed batches first (steady state: every T seen before); the
+    capture pass's rate is reported beside it."""
     eng, nets, B = build(cfg_name, rank=rank, world=world, prec=prec)
+    cap_s = None
+    if graphs:
+        assert world == 1 and eng.capture()
     rng = random.Random(7)
     # sample the batches across the length-sorted chunk (short and long sentences alike)
     nb = eng.n_batches
@@ -155,6 +160,13 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32"):
     for i, b in zip(order[:warmup], batches[:warmup]):
         eng.batch_i = i                   # the frame weight of batch i (data parallelism)
         eng.train_step(allreduce, batch=b)
+    if graphs:                            # capture pass (each timed T once)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in batches[warmup:]:
+            eng.train_step(batch=b)
+        torch.cuda.synchronize()
+        cap_s = time.perf_counter() - t0
     frames, tsteps = 0, 0
     if world > 1:
         torch.distributed.barrier()
@@ -181,7 +193,12 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32"):
     dirs = 2 if specs[0]["bidir"] else 1
     per_row, head = alg_flops_per_row(nets)
     flops = world * tsteps * B * (dirs * per_row + head)  # padded rows, as the reference computes
-    return {"config": cfg_name, "prec": prec, "batch_sentences": B, "steps": steps, "n_ranks": world,
+    extra = {}
+    if graphs:
+        extra = {"graphs": True, "captures": eng.seq_captures,
+                 "capture_pass_ms_per_step": cap_s * 1e3 / steps}
+    return {"config": cfg_name, "prec": prec, **extra, "batch_sentences": B, "steps": steps,
+            "n_ranks": world,
             "frames_per_s": frames / dt, "ms_per_step": dt * 1e3 / steps,
             "us_per_time_step_per_layer_fwd_bwd": dt * 1e6 / (tsteps * nl),
             "mean_T": tsteps / steps, "alg_tflops_per_s": flops / dt / 1e12,
@@ -283,10 +300,11 @@ def main():
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--prec", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--graphs", action="store_true", help="replay per-T captured step graphs")
     a = ap.parse_args()
     out = []
     for c in a.configs.split(","):
-        r = run(c, a.steps, a.warmup, prec=a.prec)
+        r = run(c, a.steps, a.warmup, prec=a.prec, graphs=a.graphs)
         print(json.dumps(r), flush=True)
         out.append(r)
         torch.cuda.empty_cache()
