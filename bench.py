@@ -28,7 +28,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense MFMA peaks (spec)
+# dense MFMA peaks (spec); the compensated bf16 form (PKC_PREC_BF16X3) issues 3 bf16 MFMAs per
+# product: its peak in algorithmic flops is a third of bf16's
+MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "bf16x3": 2500.0 / 3}
+PREC_NAMES = {"fp32": 0, "bf16": 1, "bf16x3": 3}          # pkc._lib.PREC_*
 
 
 def c1_cfg(drop="0.15"):
@@ -297,17 +300,19 @@ def mfma_profile(name):
     return None
 
 
-def seq_entry(name, steps, warmup, with_cpu, cpu_seconds):
+def seq_entry(name, steps, warmup, with_cpu, cpu_seconds, prec="fp32"):
     """A BASELINE sequence configuration measured like the headline: frames/s over `steps` timed
     sentence batches, its roofline (max(F_alg / MFMA peak, B_alg / HBM peak) over the
-    measured time, fp32 — the parity precision — and the serial-step figure) and a CPU baseline."""
+    measured time, and the serial-step figure) and a CPU baseline.  prec "fp32": the parity
+    precision; "bf16": the performance mode (W projections, weight gradients and heads on bf16
+    MFMA, the serial U products exact fp32), priced against the bf16 peak."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_seq
-    r = bench_seq.run(name, steps=steps, warmup=warmup)
+    r = bench_seq.run(name, steps=steps, warmup=warmup, prec=prec)
     achieved = r["alg_tflops_per_s"]
-    peak = MFMA_PEAK_TFLOPS["fp32"]
+    peak = MFMA_PEAK_TFLOPS[prec]
     out = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items() if k != "config"}
-    out["dtype"] = "fp32"
+    out["dtype"] = prec
     out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
                        "unit": "TFLOP/s", "frac": round(achieved / peak, 5),
                        "note": "algorithmic flops (W, U scaled by mask density, heads; x3 for "
@@ -365,7 +370,8 @@ def measure_mlp(prec, args, rank, world, allreduce):
         # counter runs (scripts/gpu.sh pmc): the dominant kernel's launches, N rounds, last
         dom_fn = args.pmc_kernel or pick_dominant()[0]
         nl = eng.replay_launches(dom_fn, args.pmc_replay)
-        tag = dom_fn + ("@fp32" if prec == _lib.PREC_FP32 else "")
+        tag = dom_fn + ("" if prec == _lib.PREC_BF16 else
+                        "@" + {v: k for k, v in PREC_NAMES.items()}[prec])
         print(json.dumps({"pmc_replay": tag, "launches": nl * args.pmc_replay}), flush=True)
         sys.exit(0)
     eng.capture(split_optimizer=world > 1)
@@ -379,8 +385,8 @@ def measure_mlp(prec, args, rank, world, allreduce):
     per_launch_fl = d["flops"] / cnt
     per_launch_nb = d["bytes"] / cnt
     avg_ms = dom_us / cnt * 1e-3
-    pname = "bf16" if prec == _lib.PREC_BF16 else "fp32"
-    traffic = pmc_traffic(dom_fn if pname == "bf16" else dom_fn + "@fp32")
+    pname = {v: k for k, v in PREC_NAMES.items()}[prec]
+    traffic = pmc_traffic(dom_fn if pname == "bf16" else dom_fn + "@" + pname)
     del eng
     torch.cuda.empty_cache()
     # MFMA-bound only where the launch's arithmetic intensity exceeds the machine balance
@@ -465,7 +471,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128)
-    ap.add_argument("--prec", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--prec", choices=["bf16", "fp32", "bf16x3"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-batch-sweep", action="store_true")
@@ -503,16 +509,20 @@ def main():
             torch.distributed.destroy_process_group()
         return
     from pkc import _lib
-    prec = _lib.PREC_BF16 if args.prec == "bf16" else _lib.PREC_FP32
+    prec = PREC_NAMES[args.prec]
     head = measure_mlp(prec, args, rank, world, allreduce)
     extra = {}
     if rank == 0 and world == 1 and args.prec == "bf16" and not args.no_fp32:
-        # the same configuration in fp32 (the reference's precision: the entry whose posteriors
-        # meet north_star's 1e-4), measured the same way, with its own roofline and timeline
+        # the same configuration in fp32 (the reference's precision) and in compensated bf16
+        # (bf16 MFMA, fp32-class products): the entries whose posteriors meet north_star's 1e-4,
+        # measured the same way, each with its own roofline
         extra["fp32_entry"] = measure_mlp(_lib.PREC_FP32, args, 0, 1, None)
         extra["fp32_value"] = extra["fp32_entry"]["value"]
+        extra["bf16x3_entry"] = measure_mlp(_lib.PREC_BF16X3, args, 0, 1, None)
+        extra["bf16x3_value"] = extra["bf16x3_entry"]["value"]
         if not args.no_cpu_baseline:
             extra["fp32_entry"].update(parity_leg(_lib.PREC_FP32, args.batch))
+            extra["bf16x3_entry"].update(parity_leg(_lib.PREC_BF16X3, args.batch))
     sweep = {}
     if rank == 0 and world == 1 and not args.no_batch_sweep:
         sweep = batch_sweep(prec)
@@ -522,8 +532,12 @@ def main():
         # C4 / C5 informational
         seq["c3"] = seq_entry("c3", max(20, args.steps), 3, False, 0)
         torch.cuda.empty_cache()
+        seq["c3"]["bf16_entry"] = seq_entry("c3", max(20, args.steps), 3, False, 0, "bf16")
+        torch.cuda.empty_cache()
         for c in ("c4", "c5"):
             seq[c] = seq_entry(c, 8, 2, False, 0)
+            torch.cuda.empty_cache()
+            seq[c]["bf16_entry"] = seq_entry(c, 8, 2, False, 0, "bf16")
             torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         extra.update(parity_leg(prec, args.batch))

@@ -20,13 +20,19 @@ extern "C" {
 
 /* Bumped whenever an entry point is added or a struct changes (tests/test_abi_layout.py asserts it):
  * 1: rounds 1-3; 2: pkc_logsoftmax_bwd, and the structs as they stand after round 3 (which appended
- * pkc_dense_bwd_args.dz_scratch without a bump); 3: pkc_opt_seg (direct PKC_OP_OPTIM). */
-#define PKC_ABI_VERSION 3
+ * pkc_dense_bwd_args.dz_scratch without a bump); 3: pkc_opt_seg (direct PKC_OP_OPTIM);
+ * 4: PKC_PREC_BF16X3; 5: pkc_rnn_args.step_bf16 and its bf16 operand copies. */
+#define PKC_ABI_VERSION 5
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
- * BF16IN: operands stored as bf16 in HBM (A and B point at bf16 arrays), fp32 accumulation */
-enum { PKC_PREC_FP32 = 0, PKC_PREC_BF16 = 1, PKC_PREC_BF16IN = 2 };
+ * BF16IN: operands stored as bf16 in HBM (A and B point at bf16 arrays), fp32 accumulation;
+ * BF16X3: compensated bf16 — fp32 operands split at staging into a bf16 head and a bf16 tail
+ * (a = hi + lo, lo = bf16(a - hi)) and multiplied as hi*hi + hi*lo + lo*hi on the bf16 MFMA with
+ * fp32 accumulation: products to ~2^-16 relative (the dropped lo*lo term), i.e. fp32-class
+ * results at 3/16 of the exact-fp32 MFMA cost.  The 64x64 tile bodies (pkc_gemm,
+ * pkc_gemm_grouped, the 64-row pkc_gemm_colstats) take it; the 128x128 body does not. */
+enum { PKC_PREC_FP32 = 0, PKC_PREC_BF16 = 1, PKC_PREC_BF16IN = 2, PKC_PREC_BF16X3 = 3 };
 /* neural_networks.py:54-78 act_fun */
 enum { PKC_ACT_LINEAR = 0, PKC_ACT_RELU = 1, PKC_ACT_TANH = 2, PKC_ACT_SIGMOID = 3,
        PKC_ACT_HTANH = 4, PKC_ACT_LEAKY = 5, PKC_ACT_ELU = 6 };
@@ -396,6 +402,16 @@ typedef struct {
    *     of gate g reads.
    * NULL: dense contraction over all H. */
   const int32_t* kmap_fwd; const int32_t* kmap_bwd; int kmap_s_fwd, kmap_s_bwd;
+  /* bf16 step products (the performance mode of the sequence configs; liGRU / LSTM / RNN, dense U,
+   * no quantised h, no LayerNorm): step_bf16 = 1 runs U h_{t-1} and the BPTT products dgates U^T on
+   * v_mfma_f32_16x16x32_bf16 with fp32 accumulation, reading bf16 copies of their operands:
+   *   hs_h (T+1, B2, H) bf16 copy of hs, written by the forward steps (hs_h[0] = 0);
+   *   U_h[g] (H x H) bf16 copies of U[g] (the caller keeps them current);
+   *   ut_h (G x H x H) bf16 U^T, written by pkc_rnn_bwd's transpose;
+   *   dgates_h (G, T, B2, H) bf16 copy of dgates, written by the backward steps.
+   * Cell state, gates, h and every other quantity stay fp32.  0: exact-fp32 products. */
+  int step_bf16;
+  void* hs_h; const void* U_h[4]; void* ut_h; void* dgates_h;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
 /* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that

@@ -736,3 +736,40 @@ def use_bf16_matmuls(net):
     for lin in net.wx:
         lin.forward = (lambda x, _l=lin: _BF16Linear.apply(x, _l.weight, _l.bias))
     return net
+
+
+class _BF16dWLinear(torch.autograd.Function):
+    """A recurrent U product in pkc's bf16 performance mode for sequence models: the per-step
+    forward U h_{t-1} and its BPTT product dgates U stay exact fp32 (the step kernels), only the
+    weight gradient dU = sum_t dgates_t^T h_{t-1} — one matmul over all T x B rows in pkc — takes
+    bf16-rounded operands with fp32 accumulation.  Test restatement of pkc's arithmetic, not a
+    reference function (the reference's products are fp32: neural_networks.py:1077-1097)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        return dy @ w, _bf16(dy).t() @ _bf16(x)
+
+
+def use_bf16_rec_matmuls(net, steps=False):
+    """pkc's bf16 mode of a recurrent oracle net: the input projections W (every product of their
+    training step, _BF16Linear) and the U weight gradients (_BF16dWLinear) on bf16 operands;
+    steps=True (pkc_rnn_args.step_bf16: dense liGRU / LSTM / RNN) the per-step U products and their
+    BPTT products too (_BF16Linear on U)."""
+    for name, mods in net.named_children():
+        if not isinstance(mods, nn.ModuleList) or not name[:1] in ("w", "u"):
+            continue
+        for lin in mods:
+            if not isinstance(lin, nn.Linear) or isinstance(lin, QLinear):
+                raise NotImplementedError("bf16 restatement of %s" % type(lin).__name__)
+            if name[0] == "w" or steps:
+                lin.forward = (lambda x, _l=lin: _BF16Linear.apply(x, _l.weight, _l.bias))
+            else:
+                assert lin.bias is None
+                lin.forward = (lambda x, _l=lin: _BF16dWLinear.apply(x, _l.weight))
+    return net

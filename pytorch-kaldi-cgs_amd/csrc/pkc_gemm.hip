@@ -14,6 +14,9 @@
 //   PREC_BF16IN: the same MFMA with operands already stored as bf16 in HBM (the bf16 copies of
 //              weights / activations / gradients the step keeps): half the bytes per workgroup,
 //              one 16-byte load per thread per operand per k-tile.
+//   PREC_BF16X3: compensated bf16 — fp32 operands split at staging into bf16 head + tail tiles
+//              (hi = bf16(v), lo = bf16(v - hi)), 6 MFMA per k-tile (hi*hi + hi*lo + lo*hi): fp32-
+//              class products (~2^-16 relative) on the bf16 MFMA, 3/16 of the exact-fp32 chain.
 // Split-K over blockIdx.z writes deterministic partial slabs (summed by the consumer kernels).
 #include "pkc_gemm_big.h"
 #include "pkc_ops.h"
@@ -28,10 +31,12 @@ constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
 
 template <int PREC>
 struct Lds;
+// LO: element offset of the bf16 tail tiles from the head tiles (PREC_BF16X3; 0: none)
 template <>
 struct Lds<PKC_PREC_FP32> {
   using T = float;
   static constexpr int LD = BK + 4;  // 144-byte rows
+  static constexpr int LO = 0;
   float a[BM * LD];
   float b[BN * LD];
 };
@@ -39,9 +44,28 @@ template <>
 struct Lds<PKC_PREC_BF16> {
   using T = __bf16;
   static constexpr int LD = BK + 8;  // 80-byte rows
+  static constexpr int LO = 0;
   __bf16 a[BM * LD];
   __bf16 b[BN * LD];
 };
+template <>
+struct Lds<PKC_PREC_BF16X3> {
+  using T = __bf16;
+  static constexpr int LD = BK + 8;
+  static constexpr int LO = (BM + BN) * LD;   // al = a + LO, bl = b + LO
+  __bf16 a[BM * LD];
+  __bf16 b[BN * LD];
+  __bf16 al[BM * LD];
+  __bf16 bl[BN * LD];
+};
+
+// one staged element: its bf16 head, and (LO > 0) its bf16 tail LO elements further
+template <typename T, int LO>
+__device__ __forceinline__ void put(T* __restrict__ s, int i, float v) {
+  const T hv = (T)v;
+  s[i] = hv;
+  if constexpr (LO > 0) s[i + LO] = (T)(v - (float)hv);
+}
 
 // LDS swizzle of an m-contiguous (not k-contiguous) fp32 operand.  Its register stage holds 4
 // consecutive ROWS of one k, so the store into the [row][k] tile is a column write: with the plain
@@ -129,7 +153,7 @@ struct Stage {
       v[4 * i + 3] = ok ? x.w : 0.f;
     }
   }
-  template <typename T, int LD>
+  template <typename T, int LD, int LO = 0>
   __device__ __forceinline__ void store(T* __restrict__ s) const {
     const int t = threadIdx.x;
     if (VEC) {
@@ -139,7 +163,7 @@ struct Stage {
         if (KC) {
           const int r = idx >> 3, k = (idx & 7) * 4;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) s[r * LD + k + j] = (T)v[4 * i + j];
+          for (int j = 0; j < 4; ++j) put<T, LO>(s, r * LD + k + j, v[4 * i + j]);
         } else {
           const int k = idx >> 4, r = (idx & 15) * 4;
           if constexpr (sizeof(T) == 4) {
@@ -148,7 +172,7 @@ struct Stage {
               s[(r + j) * LD + 4 * swz4(r + j, k >> 2) + (k & 3)] = (T)v[4 * i + j];
           } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s[(r + j) * LD + k] = (T)v[4 * i + j];
+            for (int j = 0; j < 4; ++j) put<T, LO>(s, (r + j) * LD + k, v[4 * i + j]);
           }
         }
       }
@@ -158,11 +182,11 @@ struct Stage {
         const int idx = t + NT * i;
         if (KC) {
           const int r = idx >> 5, k = idx & 31;
-          s[r * LD + k] = (T)v[i];
+          put<T, LO>(s, r * LD + k, v[i]);
         } else {
           const int k = idx >> 6, r = idx & 63;
           if constexpr (sizeof(T) == 4) s[r * LD + 4 * swz4(r, k >> 2) + (k & 3)] = (T)v[i];
-          else s[r * LD + k] = (T)v[i];
+          else put<T, LO>(s, r * LD + k, v[i]);
         }
       }
     }
@@ -252,8 +276,9 @@ struct StageH {
     const bf16x8 x = KC ? ld8h(b.p + kk) : ld8h(b.p + (int64_t)kk * ld);
     v = ok ? x : zero8h();
   }
-  template <typename T, int LD>
+  template <typename T, int LD, int LO = 0>
   __device__ __forceinline__ void store(T* __restrict__ s) const {
+    static_assert(LO == 0, "bf16-stored operands have no tail");
     const int t = threadIdx.x;
     if (KC) {
       const int r = t >> 2, k = (t & 3) * 8;
@@ -302,6 +327,19 @@ __device__ __forceinline__ void mfma_tile(const Lds<PREC>& sm, int wm, int wn, i
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc, 0, 0, 0);
+  } else if constexpr (PREC == PKC_PREC_BF16X3) {
+    // tails first (the small terms), then the heads, into the same fp32 accumulator
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ia = (wm * 32 + r) * LD + 16 * t + 8 * h, ib = (wn * 32 + r) * LD + 16 * t + 8 * h;
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(&sm.a[ia]);
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sm.b[ib]);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(&sm.al[ia]);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&sm.bl[ib]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bv, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+    }
   } else {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -403,8 +441,8 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
       for (int d = 0; d < DEPTH; ++d) {
         if (d >= nk) break;                                  // uniform
         __syncthreads();
-        sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
-        sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+        sa[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.a);
+        sb[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.b);
         __syncthreads();
         mfma_tile<PREC, AKC, BKC, BIN && !AKC, BIN && !BKC>(sm, wm, wn, r, h, acc);
       }
@@ -424,8 +462,8 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
 #pragma unroll
         for (int d = 0; d < DEPTH; ++d) {
           __syncthreads();
-          sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
-          sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+          sa[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.a);
+          sb[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.b);
           __syncthreads();
           const int kn = kt + (d + DEPTH) * BK;
           sa[d].load_at(ab, (int)lda, kn, kend);
@@ -447,8 +485,8 @@ __device__ __forceinline__ void gemm_body(Lds<PREC>& sm, int bx, int by, int bz,
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d) {
         __syncthreads();
-        sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
-        sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+        sa[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.a);
+        sb[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.b);
         __syncthreads();
         const int kn = kt + (d + DEPTH) * BK;
         sa[d].load(A, lda, m0, M, kn, kend);
@@ -520,8 +558,8 @@ __device__ __forceinline__ void gemm_body_sparse(Lds<PREC>& sm, int bx, int by, 
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d) {
         __syncthreads();
-        sa[d].template store<typename Lds<PREC>::T, LD>(sm.a);
-        sb[d].template store<typename Lds<PREC>::T, LD>(sm.b);
+        sa[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.a);
+        sb[d].template store<typename Lds<PREC>::T, LD, Lds<PREC>::LO>(sm.b);
         __syncthreads();
         const int kn = k0_of(i0 + d + DEPTH);
         sa[d].load(A, lda, m0, M, kn, kend);
@@ -936,7 +974,8 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
                         int64_t ldc, int splits, int64_t slab_stride, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "pkc_gemm: negative shape");
-  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN,
+  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN ||
+                    prec == PKC_PREC_BF16X3,
                 "pkc_gemm: bad precision %d", prec);
   if (M == 0 || N == 0) return PKC_OK;
   PKC_CHECK_ARG(A && B && C, "pkc_gemm: null operand");
@@ -963,6 +1002,9 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
   if (prec == PKC_PREC_FP32)
     return dispatch<PKC_PREC_FP32, false>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C,
                                           ldc, splits, slab_stride, S(stream));
+  if (prec == PKC_PREC_BF16X3)
+    return dispatch<PKC_PREC_BF16X3, false>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C,
+                                            ldc, splits, slab_stride, S(stream));
   if (prec == PKC_PREC_BF16IN)
     return dispatch<PKC_PREC_BF16, true>(a_kcontig, b_kcontig, vec, M, N, K, A, lda, B, ldb, C,
                                          ldc, splits, slab_stride, S(stream));
@@ -975,7 +1017,8 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
 extern "C" int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
                                     const void* A, int64_t lda, const void* B, int64_t ldb) {
   using namespace pkc;
-  if (!(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN) || M <= 0 ||
+  if (!(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN ||
+        prec == PKC_PREC_BF16X3) || M <= 0 ||
       N <= 0 || K <= 0 || lda <= 0 || ldb <= 0 || lda >= (1ll << 31) || ldb >= (1ll << 31))
     return 0;
   if (big_enabled() &&
@@ -1010,6 +1053,7 @@ extern "C" int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, 
     else PKC_CS(P, BIN, false, false);                                                         \
   } while (0)
     if (prec == PKC_PREC_FP32) PKC_CSO(PKC_PREC_FP32, false);
+    else if (prec == PKC_PREC_BF16X3) PKC_CSO(PKC_PREC_BF16X3, false);
     else if (prec == PKC_PREC_BF16IN) PKC_CSO(PKC_PREC_BF16, true);
     else PKC_CSO(PKC_PREC_BF16, false);
 #undef PKC_CSO
@@ -1030,7 +1074,8 @@ extern "C" int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, 
 extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream) {
   using namespace pkc;
   PKC_CHECK_ARG(probs && n >= 1 && n <= GMAX, "pkc_gemm_grouped: 1..%d problems", GMAX);
-  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN,
+  PKC_CHECK_ARG(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN ||
+                    prec == PKC_PREC_BF16X3,
                 "pkc_gemm_grouped: bad precision %d", prec);
   GroupArgs g;
   memset(&g, 0, sizeof(g));
@@ -1180,7 +1225,22 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   } while (0)
   if (prec == PKC_PREC_FP32) PKC_GL(PKC_PREC_FP32, false);
   else if (prec == PKC_PREC_BF16IN) PKC_GL(PKC_PREC_BF16, true);
-  else PKC_GL(PKC_PREC_BF16, false);
+  else if (prec == PKC_PREC_BF16X3) {     // no 128x128 body: its slab sums ride the 64x64 instance
+    constexpr int P = PKC_PREC_BF16X3;
+    if (any_sparse && any_sum)
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false, true, true>), dim3(wg), dim3(NT), 0,
+                         S(stream), g);
+    else if (any_sparse)
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false, true>), dim3(wg), dim3(NT), 0,
+                         S(stream), g);
+    else if (any_sum)
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false, false, true>), dim3(wg), dim3(NT), 0,
+                         S(stream), g);
+    else if (all_vec && grouped_vo() == 2)
+      hipLaunchKernelGGL((gemm_grouped_vo4_kernel<P, false>), dim3(wg), dim3(NT), 0, S(stream), g);
+    else
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false>), dim3(wg), dim3(NT), 0, S(stream), g);
+  } else PKC_GL(PKC_PREC_BF16, false);
 #undef PKC_GL
   PKC_LAUNCH_CHECK("pkc_gemm_grouped");
   return PKC_OK;

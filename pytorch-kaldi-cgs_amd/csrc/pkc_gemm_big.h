@@ -582,6 +582,7 @@ __device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by
 __host__ inline bool eligible(int prec, int akc, int bkc, int M, int N, int K, const void* A,
                               int64_t lda, const void* B, int64_t ldb, int min_tiles,
                               int min_k = 128) {
+  if (prec == PKC_PREC_BF16X3) return false;        // the compensated form: 64x64 bodies only
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
                    ldb % e == 0 && (akc ? K % e == 0 : M % e == 0) && (bkc ? K % e == 0 : N % e == 0);

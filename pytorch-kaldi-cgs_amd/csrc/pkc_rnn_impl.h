@@ -254,6 +254,10 @@ __device__ __forceinline__ void gate_part(const pkc_rnn_args& a, const RnnIdx& i
   } else {
 #pragma unroll
     for (int q = 0; q < G; ++q) a.dgates[q * TB2H + si] = dg[q];
+    if (a.dgates_h) {     // the next BPTT product's bf16 operand (step_bf16)
+#pragma unroll
+      for (int q = 0; q < G; ++q) reinterpret_cast<__bf16*>(a.dgates_h)[q * TB2H + si] = (__bf16)dg[q];
+    }
   }
   a.work[p * n + e] = go;
   if constexpr (CELL == PKC_CELL_LSTM) a.work[2 * n + p * n + e] = dco;
@@ -467,6 +471,47 @@ __device__ __forceinline__ void mfma_chain(const float* va, const float* vb, con
   }
 }
 
+// bf16 step products (pkc_rnn_args.step_bf16): v_mfma_f32_16x16x32_bf16 takes 8 consecutive k of
+// one row per lane (A: row lane & 15, B: column lane & 15, k = 8 (lane >> 4) + 0..7), so a lane
+// group's strip of S contiguous k feeds S / 8 MFMAs, 8 values each, in place of the fp32 chain's S
+// one-value MFMAs.  A and B lanes of one lane group hold the same k, so the sums are the same
+// contraction (in another order) with bf16-rounded operands and fp32 accumulation.
+typedef __attribute__((ext_vector_type(8))) __bf16 rbf16x8;
+
+// v[i] = 8 bf16 of row[kb + 8i ..] (zeros past kmax or when !ok); v8: rows 16-byte aligned and
+// kmax % 8 == 0 (then an 8-chunk is wholly inside or outside), else element loads
+template <int S>
+__device__ __forceinline__ void load_strip_h(const __bf16* row, bool ok, int kb, int kmax, bool v8,
+                                             rbf16x8* v) {
+#pragma unroll
+  for (int i = 0; i < S / 8; ++i) {
+    const int k = kb + 8 * i;
+    if (v8) {
+      const bool in = ok && k < kmax;
+      const rbf16x8 x = *reinterpret_cast<const rbf16x8*>(row + (in ? k : 0));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = in ? x[j] : (__bf16)0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool in = ok && k + j < kmax;
+        const __bf16 x = row[in ? k + j : 0];
+        v[i][j] = in ? x : (__bf16)0.f;
+      }
+    }
+  }
+}
+
+template <int S, bool R16 = false>
+__device__ __forceinline__ void mfma_chain_h(const rbf16x8* va, const rbf16x8* vb,
+                                             const rbf16x8* vu, f32x4& acc0, f32x4& acc1) {
+#pragma unroll
+  for (int i = 0; i < S / 8; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[i], vu[i], acc0, 0, 0, 0);
+    if constexpr (!R16) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[i], vu[i], acc1, 0, 0, 0);
+  }
+}
+
 // ------------------------------------------------------------------------------- forward step
 // The cell update's inputs at (r, j) that do not depend on this step's products: the gate
 // pre-activations W x (+BN), h_{t-1}, c_{t-1} (LSTM) and the dropout mask.  rnn_fwd_mm requests
@@ -561,6 +606,8 @@ __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix,
     a.gates[3 * TB2H + si] = cc;
   }
   a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+  if (a.hs_h)      // the next step's bf16 operand (step_bf16)
+    reinterpret_cast<__bf16*>(a.hs_h)[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = (__bf16)h;
   a.y[ix.out(t, r, j)] = h;
 }
 
@@ -586,9 +633,12 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 // cell, reading rh).  Tile: rows [32*blockIdx.y, +32) x NG gates of NU = 16/NG units.
 // NW waves (4: 256 threads, or 8: the contraction in 32 strips of S — half the operand loads per
 // lane and half the MFMA chain per wave, for the long-H layers whose step is load-latency-bound)
-template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4, bool R16 = false>
+// BF: bf16 step product (step_bf16: hs_h / U_h operands, mfma_chain_h)
+template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4, bool R16 = false,
+          bool BF = false>
 __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw, PackGrid pg) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  static_assert(!BF || (!QH && !SP && PH == 0), "bf16 steps: dense one-phase cells");
   int bx, by, bz;
   if (!pack_tile(pg, bx, by, bz)) return;
   constexpr int NTH = 64 * NW;
@@ -612,6 +662,20 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     const int rr = min(r0 + rl, B2 - 1), jj = min(u0 + ul, H - 1);
     if ((int)threadIdx.x < 32 * NU) pre = epi_load<CELL, NG>(a, ix, t, rr, jj);
   }
+  float vars[4] = {0.f, 0.f, 0.f, 0.f};
+  const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (BF) {
+    const __bf16* srch = reinterpret_cast<const __bf16*>(a.hs_h) + (int64_t)t * B2 * H;
+    const __bf16* puh = reinterpret_cast<const __bf16*>(a.U_h[gi]) + (int64_t)(u < H ? u : 0) * H;
+    const int kb = (w * 4 + q) * S;
+    const bool v8 = vw == 4 && H % 8 == 0;
+    rbf16x8 ha[S / 8], hb[S / 8], hu[S / 8];
+    load_strip_h<S>(srch + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, v8, ha);
+    if constexpr (!R16) load_strip_h<S>(srch + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
+    load_strip_h<S>(puh, u < H, kb, H, v8, hu);
+    mfma_chain_h<S, R16>(ha, hb, hu, acc0, acc1);
+  } else {
   float va[S], vb[S], vu[S];
   if constexpr (SP) {
     static_assert(!QH && PH == 0, "block-sparse U: no quantised h, one-phase cells");
@@ -630,9 +694,6 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
 #pragma unroll
     for (int s = 0; s < S; ++s) vb[s] = 0.f;
   }
-  float vars[4] = {0.f, 0.f, 0.f, 0.f};
-  const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   if constexpr (QH) {
     // each gate's QuantizeLinear re-quantises h in place (q1..q4): gate g's product reads
     // q_{g+1} = Q(q_g) with var_g = max|q_g| over the whole tensor.  With all B2 <= 32 rows in this
@@ -696,6 +757,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   } else {
     mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
   }
+  }   // !BF
   reduce_tile<NW>(acc0, acc1, red, tile);
   for (int p = threadIdx.x; p < 32 * NU; p += NTH) {
     const int rl = p / NU, ul = p % NU;
@@ -771,10 +833,12 @@ __device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, 
 // MODE 0: the product of gate g0 + blockIdx.z into slab blockIdx.z (a.work + (4 + z) n);
 // MODE 1: one-gate product + bwd_step_epi (t = tt + 1); MODE 2: one-gate product + rh_epi.
 // out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
-template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4, bool R16 = false>
+template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4, bool R16 = false,
+          bool BF = false>
 __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw,
                                                       PackGrid pg) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  static_assert(!BF || (!SP && MODE <= 1), "bf16 steps: dense one-phase cells");
   int bx, by, bz;
   if (!pack_tile(pg, bx, by, bz)) return;
   constexpr int NTH = 64 * NW;
@@ -790,6 +854,19 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   const float* dg = a.dgates + g * TB2H + (int64_t)t * B2 * H;
   const int ra = r0 + c, rb = r0 + 16 + c, k = k0 + c;
   const float* pu = a.ut + (int64_t)g * H * H + (int64_t)(k < H ? k : 0) * H;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (BF) {
+    const __bf16* dgh = reinterpret_cast<const __bf16*>(a.dgates_h) + g * TB2H + (int64_t)t * B2 * H;
+    const __bf16* puh = reinterpret_cast<const __bf16*>(a.ut_h) + (int64_t)g * H * H +
+                        (int64_t)(k < H ? k : 0) * H;
+    const int kb = (w * 4 + q) * S;
+    const bool v8 = vw == 4 && H % 8 == 0;
+    rbf16x8 ha[S / 8], hb[S / 8], hu[S / 8];
+    load_strip_h<S>(dgh + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, v8, ha);
+    if constexpr (!R16) load_strip_h<S>(dgh + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
+    load_strip_h<S>(puh, k < H, kb, H, v8, hu);
+    mfma_chain_h<S, R16>(ha, hb, hu, acc0, acc1);
+  } else {
   float va[S], vb[S], vu[S];
   if constexpr (SP) {
     static_assert(MODE == 0, "block-sparse U: gate-split BPTT products only");
@@ -804,8 +881,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
     if constexpr (!R16) load_strip<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
     load_strip<S>(pu, k < H, kb, H, vw, vu);
   }
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
+  }   // !BF
   reduce_tile<NW>(acc0, acc1, red, tile);
   const int64_t n = (int64_t)B2 * H;
   for (int p = threadIdx.x; p < 32 * 16; p += NTH) {
@@ -849,9 +926,13 @@ __global__ __launch_bounds__(256) void rnn_transpose_u(pkc_rnn_args a) {
     tl[i][tx] = (j < H && k < H) ? U[(int64_t)j * H + k] : 0.f;
   }
   __syncthreads();
+  __bf16* uth = a.ut_h ? reinterpret_cast<__bf16*>(a.ut_h) + (int64_t)g * H * H : nullptr;
   for (int i = ty; i < 32; i += 8) {
     const int k = k0 + i, j = j0 + tx;
-    if (k < H && j < H) ut[(int64_t)k * H + j] = tl[tx][i];
+    if (k < H && j < H) {
+      ut[(int64_t)k * H + j] = tl[tx][i];
+      if (uth) uth[(int64_t)k * H + j] = (__bf16)tl[tx][i];
+    }
   }
 }
 
@@ -973,6 +1054,27 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     // 2B <= 16 rows (C3, C5): 16-row tiles, no second MFMA chain or operand strip
     const bool r16 = rows16(B2);
     const dim3 g16(g1.x, rows_16);
+    if constexpr (!SP) {
+      if (a->step_bf16) {              // bf16 step products (check(): dense, no qbits / LN)
+        const bool ew = eight_waves(S);
+        for (int t = 0; t < a->T; ++t) {
+          if (r16 && ew)
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true, true>),
+                               pack_dim(pack_grid(g16)), dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
+          else if (r16)
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true, true>),
+                               pack_dim(pack_grid(g16)), dim3(RT), 0, s, *a, t, vw, pack_grid(g16));
+          else if (ew)
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, false, true>),
+                               pack_dim(pack_grid(g1)), dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g1));
+          else
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, false, true>),
+                               pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+        }
+        PKC_LAUNCH_CHECK("pkc_rnn_fwd bf16 step");
+        return PKC_OK;
+      }
+    }
     for (int t = 0; t < a->T; ++t) {
       if (r16) {
         if constexpr (SP)
@@ -1057,6 +1159,43 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       mm2(tt);
     }
   } else {
+    if constexpr (!SP) {
+      if (a->step_bf16) {              // bf16 BPTT products (dgates_h x ut_h)
+        const bool ew = eight_waves(S);
+        for (int tt = a->T - 2; tt >= 0; --tt) {
+          if constexpr (G == 1) {
+            if (r16)
+              hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true, true>),
+                                 pack_dim(pack_grid(dim3(kt, rows_16, 1))), dim3(RT), 0, s, *a, tt + 1,
+                                 0, vw, pack_grid(dim3(kt, rows_16, 1)));
+            else
+              hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, false, true>),
+                                 pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a, tt + 1, 0,
+                                 vw, pack_grid(dim3(kt, rows, 1)));
+          } else {
+            const dim3 gg(kt, r16 ? rows_16 : rows, G);
+            if (r16 && ew)
+              hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true, true>),
+                                 pack_dim(pack_grid(gg)), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+            else if (r16)
+              hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true, true>),
+                                 pack_dim(pack_grid(gg)), dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+            else if (ew)
+              hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, false, true>),
+                                 pack_dim(pack_grid(gg)), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+            else
+              hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, false, true>),
+                                 pack_dim(pack_grid(gg)), dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+            hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s,
+                               *a, tt, pack_grid(dim3(eb)));
+          }
+        }
+        PKC_LAUNCH_CHECK("pkc_rnn_bwd bf16 step");
+        hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
+        PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
+        return PKC_OK;
+      }
+    }
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (G == 1) {
         if (r16)
@@ -1106,6 +1245,8 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   const int B2 = a->bidir ? 2 * a->B : a->B;
   PKC_HIP_CHECK(hipMemsetAsync(a->hs, 0, sizeof(float) * (size_t)B2 * a->H, s),   // h_init = 0
                 "pkc_rnn_fwd h_init");
+  if (a->hs_h)
+    PKC_HIP_CHECK(hipMemsetAsync(a->hs_h, 0, 2 * (size_t)B2 * a->H, s), "pkc_rnn_fwd h_init (bf16)");
   if constexpr (CELL == PKC_CELL_LSTM)
     PKC_HIP_CHECK(hipMemsetAsync(a->cs, 0, sizeof(float) * (size_t)B2 * a->H, s), "pkc_rnn_fwd c_init");
   if (a->train && a->drop_p > 0.f) {
@@ -1154,6 +1295,15 @@ static int check(const pkc_rnn_args* a, bool bwd) {
                 "pkc_rnn: LayerNorm needs beta, xhat, stat (+ g, dgamma, dbeta for the backward)");
   PKC_CHECK_ARG(a->qbits <= 0 || (a->hq && !a->bidir && a->B <= 32), "pkc_rnn: quantised h needs "
                 "hq, a uni-directional layer and B <= 32");
+  if (a->step_bf16) {
+    PKC_CHECK_ARG((a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM || a->cell == PKC_CELL_RNN) &&
+                      a->qbits <= 0 && !a->kmap_fwd && !a->kmap_bwd && !a->ln_gamma,
+                  "pkc_rnn: bf16 steps only for dense liGRU / LSTM / RNN without quantised h or "
+                  "LayerNorm");
+    PKC_CHECK_ARG(a->hs_h, "pkc_rnn: bf16 steps need hs_h");
+    for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U_h[g], "pkc_rnn: bf16 steps need U_h[%d]", g);
+    if (bwd) PKC_CHECK_ARG(a->ut_h && a->dgates_h, "pkc_rnn_bwd: bf16 steps need ut_h, dgates_h");
+  }
   if (a->kmap_fwd || a->kmap_bwd) {
     PKC_CHECK_ARG((a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM) && a->qbits <= 0,
                   "pkc_rnn: block-sparse U only for liGRU / LSTM without quantised h");

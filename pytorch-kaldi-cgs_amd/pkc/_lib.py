@@ -9,9 +9,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
-ABI_VERSION = 3         # include/pkc.h PKC_ABI_VERSION
+ABI_VERSION = 5         # include/pkc.h PKC_ABI_VERSION
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
-PREC_FP32, PREC_BF16, PREC_BF16IN = 0, 1, 2
+PREC_FP32, PREC_BF16, PREC_BF16IN, PREC_BF16X3 = 0, 1, 2, 3
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
 NORM_NONE, NORM_BN_TRAIN, NORM_BN_EVAL = 0, 1, 2
 OPT = {"sgd": 0, "rmsprop": 1, "adam": 2}
@@ -77,7 +77,8 @@ class RnnArgs(C.Structure):
                 ("dgates", vp), ("work", vp), ("qbits", C.c_int), ("hq", vp), ("rh", vp), ("ut", vp),
                 ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", C.c_float), ("ln_xhat", vp),
                 ("ln_stat", vp), ("ln_g", vp), ("ln_dgamma", vp), ("ln_dbeta", vp),
-                ("kmap_fwd", vp), ("kmap_bwd", vp), ("kmap_s_fwd", C.c_int), ("kmap_s_bwd", C.c_int)]
+                ("kmap_fwd", vp), ("kmap_bwd", vp), ("kmap_s_fwd", C.c_int), ("kmap_s_bwd", C.c_int),
+                ("step_bf16", C.c_int), ("hs_h", vp), ("U_h", vp * 4), ("ut_h", vp), ("dgates_h", vp)]
 
 
 class GemmProblem(C.Structure):

@@ -61,6 +61,10 @@ OPT_DIRECT = os.environ.get("PKC_OPT_DIRECT", "1") != "0"
 # sequence models: pinned host slots of the per-batch metadata upload, and the number of captured
 # per-T step graphs kept (least recently used dropped first)
 SEQ_META_SLOTS = 4
+# bf16 performance mode of the sequence models (Engine prec PKC_PREC_BF16): the recurrent step
+# products U h_{t-1} / dgates U^T on bf16 operand copies too (pkc_rnn_args.step_bf16; dense liGRU /
+# LSTM / RNN layers without quantised h or LayerNorm).  0: exact-fp32 steps, bf16 matmuls only.
+RNN_BF16 = os.environ.get("PKC_RNN_BF16", "1") != "0"
 SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
@@ -853,6 +857,13 @@ class Engine:
             if sp.get("ln"):
                 lb.update(ln_xhat=_f32(T * B2 * H, dev), ln_stat=_f32(2 * T * B2, dev),
                           ln_g=_f32(T * B2 * H, dev), ln_pg=_f32(2 * H, dev))
+            if (self.prec == L.PREC_BF16 and RNN_BF16 and not sp.get("ln") and not sp["ibits"]
+                    and n.cell in (L.CELL_LIGRU, L.CELL_LSTM, L.CELL_RNN)):
+                bf = torch.bfloat16            # bf16 operand copies of the step products
+                lb.update(hs_h=torch.zeros((T + 1) * B2 * H, dtype=bf, device=dev),
+                          U_h=torch.zeros(G * H * H, dtype=bf, device=dev),
+                          ut_h=torch.zeros(G * H * H, dtype=bf, device=dev),
+                          dgates_h=torch.zeros(G * T * B2 * H, dtype=bf, device=dev))
             if sp["ibits"]:
                 lb["hq"] = _f32((T + 1) * B2 * H, dev)      # q4(h_{t-1}) per step
                 if n.lbuf:                                   # layers >= 1: q1..qG of y_{l-1}
@@ -1504,6 +1515,12 @@ class Engine:
             a.kmap_fwd, a.kmap_s_fwd = lb["kmap_fwd"].data_ptr(), lb["kmap_s_fwd"]
         if lb.get("kmap_bwd") is not None:
             a.kmap_bwd, a.kmap_s_bwd = lb["kmap_bwd"].data_ptr(), lb["kmap_s_bwd"]
+        if lb.get("hs_h") is not None and lb.get("kmap_fwd") is None and lb.get("kmap_bwd") is None:
+            a.step_bf16 = 1
+            a.hs_h, a.ut_h, a.dgates_h = (lb["hs_h"].data_ptr(), lb["ut_h"].data_ptr(),
+                                          lb["dgates_h"].data_ptr())
+            for g in range(n.G):
+                a.U_h[g] = lb["U_h"].data_ptr() + 2 * g * H * H
         if sp.get("ln"):
             a.ln_gamma, a.ln_beta, a.ln_eps = sp["ln_gamma"].data_ptr(), sp["ln_beta"].data_ptr(), 1e-6
             a.ln_xhat, a.ln_stat = lb["ln_xhat"].data_ptr(), lb["ln_stat"].data_ptr()
@@ -1576,6 +1593,10 @@ class Engine:
                 self._k("rnn_bn_fwd H=%d" % H, 0, 4.0 * M * H * (sf + 2), "pkc_dense_fwd",
                         C.byref(a), ptr(lb["work"]), s)
             ra = self._rnn_args(n, li, train, T)
+            if ra.step_bf16:                  # this step's U (after the last update) as bf16
+                for g in range(n.G):
+                    self._k("cast_bf16 U", 0, 6.0 * H * H, "pkc_cast_bf16", ptr(n.wq(li, "U", g)),
+                            C.c_void_p(ra.U_h[g]), H * H, s)
             self._k("rnn_fwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_fwd", C.byref(ra), s)
 
@@ -1786,7 +1807,9 @@ class Engine:
         self._dense_bwd_pre(n, s)
         self._gemms(self._bwd_problems(n), s)
 
-    def _rec_bwd(self, n, s, want_dx0=False):
+    def _rec_bwd(self, n, s, want_dx0=False, on_layer=None):
+        """BPTT of a recurrent node, top layer first; on_layer(li) after layer li's weight
+        gradients are queued (the data-parallel bucket cut)."""
         M, T = self.M, self.T
         gs = getattr(n, "gsrc", None)
         if gs is not None:                   # external mode: the caller's output gradient
@@ -1858,6 +1881,8 @@ class Engine:
                                 K, H, dz, H, ptr(n.wq(li, "W", g)), K,
                                 C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
                     nx += sx
+            if on_layer is not None:
+                on_layer(li)
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
             if li == 0 and n.src[0] == "node":
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
@@ -1902,10 +1927,24 @@ class Engine:
         the first all-reduce bucket — about a third of the buffer or more — so that collective
         overlaps the rest of the backward.  Returns (node, gflat offset) or (None, 0)."""
         if not hasattr(self, "_cut"):
-            self._cut = (None, 0)
+            self._cut, self._cut_layer = (None, 0), None
             total = self.gflat.numel()
             for n in reversed(self.nodes):
-                if not self.needs_grad[n] or n.rec or n not in self.grad_off:
+                if not self.needs_grad[n] or n not in self.grad_off:
+                    continue
+                if n.rec:
+                    # a recurrent node's gradients are laid out layer by layer (RecNode.params) and
+                    # finish top layer first: the cut is after layer li's weight gradients
+                    starts, off = {}, self.grad_off[n]
+                    for p, key, _m in n.params():
+                        starts.setdefault(key[1], off)
+                        off += p.numel()
+                    for li in sorted(starts, reverse=True):
+                        if total - starts[li] >= total // 3 and starts[li] > 0:
+                            self._cut, self._cut_layer = (n, starts[li]), li
+                            break
+                    if self._cut[0] is not None:
+                        break
                     continue
                 off = self.grad_off[n]
                 if total - off >= total // 3 and off > 0:
@@ -1959,7 +1998,11 @@ class Engine:
                 continue
             if n.rec:
                 flush()
-                self._rec_bwd(n, s, want_dx0=n.src[0] == "node" or self.want_dx)
+                on_layer = None
+                if cut_node is n:               # sequence DP: first bucket after a layer's grads
+                    cut_node = None
+                    on_layer = (lambda li: on_cut() if li == self._cut_layer else None)
+                self._rec_bwd(n, s, want_dx0=n.src[0] == "node" or self.want_dx, on_layer=on_layer)
                 continue
             if not n.head:
                 flush()

@@ -47,7 +47,9 @@ def test_ctypes_structs_match_header(tmp_path):
 # struct that changes without a version bump fails here (bump PKC_ABI_VERSION in include/pkc.h and
 # pkc._lib.ABI_VERSION, then record the new digest under the new version)
 LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa09b47",
-                 3: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012"}
+                 3: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012",
+                 4: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012",
+                 5: "2c453ea47366535096140ab754d5ecfcd019ccecde60defafc6b607b14f5eb2d"}
 
 
 def _layout_digest(L):

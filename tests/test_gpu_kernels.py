@@ -27,7 +27,14 @@ GEMM_SHAPES = [(128, 1024, 1024), (128, 1928, 1024), (128, 48, 1024), (128, 1024
                (37, 70, 45), (16, 96, 32), (64, 64, 32), (1, 5, 3), (200, 130, 260)]
 
 
-@pytest.mark.parametrize("prec", [0, 1, 2])
+def _tol(prec, K):
+    """Absolute tolerance of a K-deep product of N(0,1) operands: exact fp32 (0), bf16-rounded
+    operands vs their own rounded values (1, 2), compensated bf16 vs the UNROUNDED fp32 operands
+    (3: the dropped lo*lo term and the tails' own rounding, ~2^-16 relative per product)."""
+    return {0: 2e-5, 1: 1e-3, 2: 1e-3, 3: 6e-5}[prec] * K ** 0.5
+
+
+@pytest.mark.parametrize("prec", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("orient", ["nt", "nn", "tn"])
 def test_gemm(L, prec, M, N, K, orient):
@@ -38,7 +45,7 @@ def test_gemm(L, prec, M, N, K, orient):
     akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
     Ast = A if akc else A.t().contiguous()      # stored (M,K) or (K,M)
     Bst = B if bkc else B.t().contiguous()
-    if prec >= 1:
+    if prec in (1, 2):
         A = A.bfloat16().float()
         B = B.bfloat16().float()
     ref = (A.double() @ B.double().t()).float()
@@ -50,11 +57,15 @@ def test_gemm(L, prec, M, N, K, orient):
     L.call("pkc_gemm", prec, akc, bkc, M, N, K, L.ptr(Ad), Ast.shape[1], L.ptr(Bd), Bst.shape[1],
            L.ptr(Cd), N, splits, M * N, _s())
     out = Cd.sum(0).cpu()
-    tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
-    torch.testing.assert_close(out, ref, rtol=1e-4, atol=tol)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=_tol(prec, K))
+    if prec == 3 and K >= 256:    # and it is fp32-class: well inside plain bf16's error
+        exact = A.double() @ B.double().t()
+        e3 = (out.double() - exact).abs().max().item()
+        eb = ((A.bfloat16().double() @ B.bfloat16().double().t()) - exact).abs().max().item()
+        assert e3 < 0.05 * eb, (e3, eb)
 
 
-@pytest.mark.parametrize("prec", [0, 2])
+@pytest.mark.parametrize("prec", [0, 2, 3])
 def test_gemm_grouped(L, prec):
     """Several matmuls of different orientation / shape / split count in one launch."""
     g = torch.Generator().manual_seed(11)
@@ -67,7 +78,7 @@ def test_gemm_grouped(L, prec):
         akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
         Ast = A if akc else A.t().contiguous()
         Bst = B if bkc else B.t().contiguous()
-        if prec:
+        if prec in (1, 2):
             A, B = A.bfloat16().float(), B.bfloat16().float()
         refs.append((A.double() @ B.double().t()).float())
         Ad, Bd = Ast.to(DEV), Bst.to(DEV)
@@ -82,8 +93,37 @@ def test_gemm_grouped(L, prec):
     L.call("pkc_gemm_grouped", prec, arr, len(probs), _s())
     torch.cuda.synchronize()
     for (orient, M, N, K, sp), ref, Cd in zip(specs, refs, keep[2::3]):
-        tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
-        torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=tol)
+        torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=_tol(prec, K))
+
+
+@pytest.mark.parametrize("prec", [0, 3])
+def test_gemm_grouped_c2_backward(L, prec):
+    """The C2 step's backward launch shapes, every problem on the 16-byte path (the vec-only
+    grouped instance held to 4 waves per SIMD): dW (K = 128 batch rows) and split-K dX."""
+    g = torch.Generator().manual_seed(13)
+    specs = [("nn", 128, 1024, 1024, 4), ("tn", 1024, 1024, 128, 1), ("nn", 128, 1024, 1928, 7),
+             ("tn", 1928, 1024, 128, 1), ("tn", 1024, 440, 128, 1)]
+    probs, keep, refs = [], [], []
+    for orient, M, N, K, sp in specs:
+        A = torch.randn(M, K, generator=g) * 1e-3
+        B = torch.randn(N, K, generator=g)
+        akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
+        Ast = A if akc else A.t().contiguous()
+        Bst = B if bkc else B.t().contiguous()
+        refs.append((A.double() @ B.double().t()))
+        Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+        Cd = torch.full((sp, M, N), float("nan"), device=DEV)
+        keep += [Ad, Bd, Cd]
+        probs.append(L.GemmProblem(a_kcontig=akc, b_kcontig=bkc, M=M, N=N, K=K, splits=sp,
+                                   A=Ad.data_ptr(), lda=Ast.shape[1], B=Bd.data_ptr(),
+                                   ldb=Bst.shape[1], C=Cd.data_ptr(), ldc=N, slab_stride=M * N))
+    arr = (L.GemmProblem * len(probs))(*probs)
+    L.call("pkc_gemm_grouped", prec, arr, len(probs), _s())
+    torch.cuda.synchronize()
+    for (orient, M, N, K, sp), ref, Cd in zip(specs, refs, keep[2::3]):
+        got = Cd.sum(0).cpu().double()
+        rel = ((got - ref).norm() / ref.norm()).item()
+        assert rel < (1e-6 if prec == 0 else 3e-5), (orient, M, N, K, rel)
 
 
 def test_gemm_unaligned_lda(L):
@@ -423,7 +463,7 @@ def test_gemm_grouped_big(L, prec):
         akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
         Ast = A if akc else A.t().contiguous()
         Bst = B if bkc else B.t().contiguous()
-        if prec:
+        if prec in (1, 2):
             A, B = A.bfloat16().float(), B.bfloat16().float()
         refs.append((A.double() @ B.double().t()).float())
         Ad, Bd = Ast.to(DEV), Bst.to(DEV)
@@ -437,8 +477,7 @@ def test_gemm_grouped_big(L, prec):
     arr = (L.GemmProblem * len(probs))(*probs)
     L.call("pkc_gemm_grouped", prec, arr, len(probs), _s())
     for (orient, M, N, K, sp), ref, Cd in zip(specs, refs, keep[2::3]):
-        tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
-        torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=tol)
+        torch.testing.assert_close(Cd.sum(0).cpu(), ref, rtol=1e-4, atol=_tol(prec, K))
 
 
 @pytest.mark.parametrize("prec", [0, 2])
@@ -529,7 +568,9 @@ def test_gemm_grouped_sparse_big_slabsum(L, prec):
 COLSTATS_SHAPES = [(4096, 1024, 1024, 2), (4096, 1024, 440, 2), (2056, 1288, 1024, 2),
                    (2056, 1288, 1000, 1), (4096, 4096, 256, 0),
                    # fewer than 160 128x128 tiles: the 64x64 body's 64-row partials (B = 1024)
-                   (1024, 1024, 1024, 2), (1000, 1032, 440, 2), (1032, 520, 1000, 1), (264, 200, 96, 0)]
+                   (1024, 1024, 1024, 2), (1000, 1032, 440, 2), (1032, 520, 1000, 1), (264, 200, 96, 0),
+                   # compensated bf16: the 64x64 body at every size (no 128x128 form)
+                   (1024, 1024, 1024, 3), (4096, 1024, 440, 3)]
 
 
 @pytest.mark.parametrize("M,N,K,prec", COLSTATS_SHAPES)
@@ -544,18 +585,17 @@ def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
     bias = torch.randn(N, generator=g) * 0.1
     dt = torch.bfloat16 if prec == 2 else torch.float32
     Ad, Wd, bd = A.to(DEV).to(dt).contiguous(), W.to(DEV).to(dt).contiguous(), bias.to(DEV)
-    if prec >= 1:
+    if prec in (1, 2):
         A, W = A.bfloat16().float(), W.bfloat16().float()
     rows = L.lib().pkc_gemm_colstats_ok(prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K)
     tiles = -(-M // 128) * -(-N // 128)
-    assert rows == (128 if tiles >= (1024 if prec == 0 else 160) else 64), rows
+    assert rows == (128 if tiles >= (1024 if prec == 0 else 160) and prec != 3 else 64), rows
     Cd = torch.full((M, N), float("nan"), device=DEV)
     work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
     L.call("pkc_gemm_colstats", prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K, L.ptr(Cd), N,
            L.ptr(bd), L.ptr(work), _s())
     ref = A.double() @ W.double().t()
-    tol = 2e-5 * K ** 0.5 if prec == 0 else 1e-3 * K ** 0.5
-    torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-4, atol=tol)
+    torch.testing.assert_close(Cd.cpu().double(), ref, rtol=1e-4, atol=_tol(prec, K))
     nb = -(-M // rows)
     part = work[:2 * N * nb].view(nb, 2, N).cpu().double()
     z = Cd.cpu().double() + bias.double()

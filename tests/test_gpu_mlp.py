@@ -128,11 +128,23 @@ def c1_config(drop="0.0"):
 C1_DIMS = (("architecture1", 440), ("architecture2", 1024), ("architecture3", 1024))
 
 
-def test_engine_c1_full_size_vs_oracle():
-    """BASELINE C1/C2 shape, dropout injected identically (reference dnn_drop = 0.15)."""
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3"])
+def test_engine_c1_full_size_vs_oracle(prec):
+    """BASELINE C1/C2 shape, dropout injected identically (reference dnn_drop = 0.15).  fp32: exact
+    fp32 MFMA; bf16x3: compensated bf16 (PKC_PREC_BF16X3, fp32-class products on the bf16 MFMA) —
+    the same north_star bound on the first step's posteriors (1e-4; measured 3.8e-7).  Its ~2^-16
+    product error (1e-5 relative on the body's outputs, 100x the exact path's) puts an element
+    with |x_hat| < 1e-5 on the other side of a ReLU about once per layer: that element's whole
+    dX entry moves into or out of the BatchNorm's dbeta column sum (dgamma weighs it by
+    x_hat ~ 0 and stays at 1.6e-5), measured 5-7e-3 relative on dbeta and on every gradient
+    below it (the oracle restated with compensated products on the CPU: 1.1e-5, no flip).  So its
+    gradients are held to 2e-2, and the later steps, which inherit the flips through this model's
+    chaotic first updates (see test_engine_c2_bf16_vs_oracle), to 1e-2 on the posteriors."""
     from oracle import nets as ON
     from oracle import run as OR
+    from pkc import _lib as L
     from pkc.engine import Engine, parse_model
+    x3 = prec == "bf16x3"
     cfg = c1_config(drop="0.15")
     nets, opts = build_nets(cfg, C1_DIMS)
     onets, _ = build_nets(cfg, C1_DIMS, cls=ON.MLP)
@@ -148,6 +160,7 @@ def test_engine_c1_full_size_vs_oracle():
              for i in range(5)}
     eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
                  ["lab_cd", "lab_mono"], batch=B, seed=1,
+                 prec=L.PREC_BF16X3 if x3 else L.PREC_FP32,
                  drop_keep_in={k: v.to(DEV) for k, v in keeps.items()})
     eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), B * steps)
     ooptim = {a: ON.make_optimizer(onets[a].parameters(), cfg[s]) for s, a in
@@ -169,7 +182,8 @@ def test_engine_c1_full_size_vs_oracle():
         post = head.out.view(B, -1).cpu()
         ref = outs["out_dnn2"].detach()
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
-        assert rel < 1e-4, "step %d posterior max rel err %.3g" % (s, rel)
+        print("%s step %d posterior max rel err %.3g" % (prec, s, rel))
+        assert rel < (1e-2 if x3 and s > 0 else 1e-4), "step %d posterior max rel err %.3g" % (s, rel)
         if s == 0:
             # the first step's gradients, every parameter, before any optimizer drift: the
             # engine's flat gradient buffer vs the oracle's autograd .grad
@@ -186,13 +200,14 @@ def test_engine_c1_full_size_vs_oracle():
                     d = (g - r).norm().item()
                     # (a Linear bias in front of BatchNorm has an exactly zero gradient, which
                     # pkc writes; autograd leaves rounding residue of ~1e-8 there)
-                    assert d <= 1e-4 * r.norm().item() + 1e-6 * r.numel() ** 0.5, \
+                    assert d <= (2e-2 if x3 else 1e-4) * r.norm().item() + 1e-6 * r.numel() ** 0.5, \
                         "%s %s grad rel frob err %.3g" % (
                         a, name, d / max(r.norm().item(), 1e-30))
                     checked += 1
             assert checked >= 20
-        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-5)
-        np.testing.assert_allclose(err, outs["err_final"].item())
+        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-3 if x3 else 1e-5)
+        if not x3 or s == 0:
+            np.testing.assert_allclose(err, outs["err_final"].item())
     # Parameters after 3 steps: a pre-activation within rounding of 0 can take the other ReLU
     # branch on the GPU than on the CPU (an fp32 ordering effect the reference shows between its
     # own CPU and GPU runs too); through BatchNorm's 1/std that one element moves a whole column of
@@ -205,7 +220,7 @@ def test_engine_c1_full_size_vs_oracle():
                 continue
             ref = onets[a].state_dict()[k].double()
             diff = (v.cpu().double() - ref).norm().item()
-            assert diff <= 2e-2 * ref.norm().item() + 1e-7, "%s %s rel frob err %.3g" % (
+            assert diff <= (5e-2 if x3 else 2e-2) * ref.norm().item() + 1e-7, "%s %s rel frob err %.3g" % (
                 a, k, diff / max(ref.norm().item(), 1e-30))
 
 

@@ -105,9 +105,27 @@ def make_cfg(body):
                                   "ligru_inpnorm", "lstm_bninp", "gru_lninp", "mingru_inpnorm",
                                   "ligru_hcgs_sparse"])
 def test_seq_engine_vs_oracle(body):
+    _seq_vs_oracle(body)
+
+
+@pytest.mark.parametrize("body", ["ligru_hcgs", "lstm", "lstm_bidir", "gru", "ligru", "rnn"])
+def test_seq_engine_bf16_vs_bf16_oracle(body):
+    """The bf16 performance mode of the sequence configs (Engine(prec=PKC_PREC_BF16): the input
+    projections W, their dX / dW, the U weight gradients and the heads on bf16-rounded operands
+    with fp32 accumulation; for dense liGRU / LSTM / RNN layers also the serial U products and
+    their BPTT products (step_bf16); cell state, BN and loss fp32) against the oracle run with
+    exactly that rounding (oracle.nets.use_bf16_rec_matmuls / use_bf16_matmuls).  Only fp32
+    summation order differs, but a last-bit difference in front of a bf16 rounding moves that
+    operand by 2^-9, so the bounds are 1e-3 relative on the posteriors (the fp32 mode: 1e-4)
+    and 2e-3 on the parameters after 3 steps."""
+    _seq_vs_oracle(body, bf16=True)
+
+
+def _seq_vs_oracle(body, bf16=False):
     import pkc.neural_networks as NN
     from oracle import nets as ON
     from oracle import run as OR
+    from pkc import _lib as L
     from pkc.engine import Engine, parse_model
     cfg = make_cfg(body)
     F, B = 20, 4
@@ -130,6 +148,11 @@ def test_seq_engine_vs_oracle(body):
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
         onets[o["arch_name"]].load_state_dict(nets[o["arch_name"]].state_dict())
+        if bf16 and sec == "a1":        # dense liGRU / LSTM / RNN: bf16 step products too
+            ON.use_bf16_rec_matmuls(onets[o["arch_name"]],
+                                    steps=body in ("lstm", "lstm_bidir", "ligru", "rnn"))
+        elif bf16:
+            ON.use_bf16_matmuls(onets[o["arch_name"]])
         opts[o["arch_name"]] = o
     for k in nets:
         nets[k].to(DEV).train()
@@ -149,6 +172,7 @@ def test_seq_engine_vs_oracle(body):
     try:
         eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fea": (0, F)},
                      ["lab_cd", "lab_mono"], batch=B, max_len=16, seed=1,
+                     prec=L.PREC_BF16 if bf16 else L.PREC_FP32,
                      rnn_drop_in={k: v.to(DEV) for k, v in masks.items()})
     finally:
         E.RNN_SPARSE = old_sparse
@@ -180,12 +204,14 @@ def test_seq_engine_vs_oracle(body):
         body_net.forward = f
         eng.train_step(batch=batch)
         loss, err = eng.loss_values()
-        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-4)
-        np.testing.assert_allclose(err, outs["err_final"].item(), atol=1e-6)
+        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-3 if bf16 else 1e-4)
+        if not bf16:
+            np.testing.assert_allclose(err, outs["err_final"].item(), atol=1e-6)
         post = eng.head_output("o2").cpu()
         ref = outs["o2"].detach()
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
-        assert rel < 1e-4, "step %d posterior rel err %.3g" % (step, rel)
+        print("%s%s step %d posterior rel err %.3g" % (body, " bf16" if bf16 else "", step, rel))
+        assert rel < (1e-3 if bf16 else 1e-4), "step %d posterior rel err %.3g" % (step, rel)
     for k in nets:
         for name, v in nets[k].state_dict().items():
             if name.endswith("num_batches_tracked"):
@@ -205,7 +231,7 @@ def test_seq_engine_vs_oracle(body):
                 perc = (60.0, 40.0)[int(parts[1])]
                 ref = ref * prune_mask(sd_o[name], perc).double()
             d = (v.cpu().double() - ref).norm().item()
-            tol = 1e-3 * ref.norm().item() + 1e-7
+            tol = (2e-3 if bf16 else 1e-3) * ref.norm().item() + 1e-7
             if name.endswith("running_mean") and body.endswith("inpnorm"):
                 # the gate pre-activations of a BN-normalised input have column means of 0 up to
                 # fp32 rounding: compare against the spread of the columns instead
