@@ -502,6 +502,15 @@ __device__ __forceinline__ void load_strip_h(const __bf16* row, bool ok, int kb,
   }
 }
 
+// block-sparse form (kmap tiles): S/16 blocks of 16 contiguous k, two 8-value chunks each
+template <int S>
+__device__ __forceinline__ void load_blocks_h(const __bf16* row, bool ok, const int* blk, int kmax,
+                                              bool v8, rbf16x8* v) {
+#pragma unroll
+  for (int i = 0; i < S / 16; ++i)
+    load_strip_h<16>(row, ok && blk[i] >= 0, blk[i] >= 0 ? blk[i] * 16 : 0, kmax, v8, v + 2 * i);
+}
+
 template <int S, bool R16 = false>
 __device__ __forceinline__ void mfma_chain_h(const rbf16x8* va, const rbf16x8* vb,
                                              const rbf16x8* vu, f32x4& acc0, f32x4& acc1) {
@@ -638,7 +647,7 @@ template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4,
           bool BF = false>
 __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw, PackGrid pg) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
-  static_assert(!BF || (!QH && !SP && PH == 0), "bf16 steps: dense one-phase cells");
+  static_assert(!BF || (!QH && PH == 0), "bf16 steps: one-phase cells, no quantised h");
   int bx, by, bz;
   if (!pack_tile(pg, bx, by, bz)) return;
   constexpr int NTH = 64 * NW;
@@ -668,12 +677,20 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   if constexpr (BF) {
     const __bf16* srch = reinterpret_cast<const __bf16*>(a.hs_h) + (int64_t)t * B2 * H;
     const __bf16* puh = reinterpret_cast<const __bf16*>(a.U_h[gi]) + (int64_t)(u < H ? u : 0) * H;
-    const int kb = (w * 4 + q) * S;
     const bool v8 = vw == 4 && H % 8 == 0;
     rbf16x8 ha[S / 8], hb[S / 8], hu[S / 8];
-    load_strip_h<S>(srch + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, v8, ha);
-    if constexpr (!R16) load_strip_h<S>(srch + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
-    load_strip_h<S>(puh, u < H, kb, H, v8, hu);
+    if constexpr (SP) {
+      int blk[S / 16];
+      tile_blocks<S>(a.kmap_fwd + (int64_t)bx * S, blk);
+      load_blocks_h<S>(srch + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, v8, ha);
+      if constexpr (!R16) load_blocks_h<S>(srch + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, v8, hb);
+      load_blocks_h<S>(puh, u < H, blk, H, v8, hu);
+    } else {
+      const int kb = (w * 4 + q) * S;
+      load_strip_h<S>(srch + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, v8, ha);
+      if constexpr (!R16) load_strip_h<S>(srch + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
+      load_strip_h<S>(puh, u < H, kb, H, v8, hu);
+    }
     mfma_chain_h<S, R16>(ha, hb, hu, acc0, acc1);
   } else {
   float va[S], vb[S], vu[S];
@@ -838,7 +855,7 @@ template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4, bool R1
 __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw,
                                                       PackGrid pg) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
-  static_assert(!BF || (!SP && MODE <= 1), "bf16 steps: dense one-phase cells");
+  static_assert(!BF || MODE <= 1, "bf16 steps: one-phase cells");
   int bx, by, bz;
   if (!pack_tile(pg, bx, by, bz)) return;
   constexpr int NTH = 64 * NW;
@@ -859,12 +876,20 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
     const __bf16* dgh = reinterpret_cast<const __bf16*>(a.dgates_h) + g * TB2H + (int64_t)t * B2 * H;
     const __bf16* puh = reinterpret_cast<const __bf16*>(a.ut_h) + (int64_t)g * H * H +
                         (int64_t)(k < H ? k : 0) * H;
-    const int kb = (w * 4 + q) * S;
     const bool v8 = vw == 4 && H % 8 == 0;
     rbf16x8 ha[S / 8], hb[S / 8], hu[S / 8];
-    load_strip_h<S>(dgh + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, v8, ha);
-    if constexpr (!R16) load_strip_h<S>(dgh + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
-    load_strip_h<S>(puh, k < H, kb, H, v8, hu);
+    if constexpr (SP) {
+      int blk[S / 16];
+      tile_blocks<S>(a.kmap_bwd + ((int64_t)g * pg.gx + bx) * S, blk);
+      load_blocks_h<S>(dgh + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, v8, ha);
+      if constexpr (!R16) load_blocks_h<S>(dgh + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, v8, hb);
+      load_blocks_h<S>(puh, k < H, blk, H, v8, hu);
+    } else {
+      const int kb = (w * 4 + q) * S;
+      load_strip_h<S>(dgh + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, v8, ha);
+      if constexpr (!R16) load_strip_h<S>(dgh + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
+      load_strip_h<S>(puh, k < H, kb, H, v8, hu);
+    }
     mfma_chain_h<S, R16>(ha, hb, hu, acc0, acc1);
   } else {
   float va[S], vb[S], vu[S];
@@ -1077,10 +1102,14 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     }
     for (int t = 0; t < a->T; ++t) {
       if (r16) {
-        if constexpr (SP)
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0, s,
-                             *a, t, vw, pack_grid(g16));
-        else if (a->qbits > 0 && qh_eight_waves(S))
+        if constexpr (SP) {
+          if (a->step_bf16)
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true, true>), pack_dim(pack_grid(g16)),
+                               dim3(RT), 0, s, *a, t, vw, pack_grid(g16));
+          else
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0, s,
+                               *a, t, vw, pack_grid(g16));
+        } else if (a->qbits > 0 && qh_eight_waves(S))
           hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), pack_dim(pack_grid(g16)),
                              dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
         else if (a->qbits > 0)
@@ -1092,9 +1121,13 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
         else
           hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0,
                              s, *a, t, vw, pack_grid(g16));
-      } else if constexpr (SP)
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
-      else if (a->qbits > 0)
+      } else if constexpr (SP) {
+        if (a->step_bf16)
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, false, true>), pack_dim(pack_grid(g1)),
+                             dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+        else
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+      } else if (a->qbits > 0)
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
       else if (eight_waves(S))
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), pack_dim(pack_grid(g1)), dim3(2 * RT), 0, s,
@@ -1207,6 +1240,9 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       } else if (r16) {                               // 16-row tiles (C3, C5)
         if (!SP && eight_waves(S))
           hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
+        else if (SP && a->step_bf16)
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
         else
           hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))),
                              dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
@@ -1214,6 +1250,10 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       } else if (!SP && eight_waves(S)) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), pack_dim(pack_grid(dim3(kt, rows, G))),
                            dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
+      } else if (SP && a->step_bf16) {
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, false, true>), pack_dim(pack_grid(dim3(kt, rows, G))),
+                           dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
         hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
       } else {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), pack_dim(pack_grid(dim3(kt, rows, G))), dim3(RT), 0, s, *a,
@@ -1297,8 +1337,8 @@ static int check(const pkc_rnn_args* a, bool bwd) {
                 "hq, a uni-directional layer and B <= 32");
   if (a->step_bf16) {
     PKC_CHECK_ARG((a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM || a->cell == PKC_CELL_RNN) &&
-                      a->qbits <= 0 && !a->kmap_fwd && !a->kmap_bwd && !a->ln_gamma,
-                  "pkc_rnn: bf16 steps only for dense liGRU / LSTM / RNN without quantised h or "
+                      a->qbits <= 0 && !a->ln_gamma,
+                  "pkc_rnn: bf16 steps only for liGRU / LSTM / RNN without quantised h or "
                   "LayerNorm");
     PKC_CHECK_ARG(a->hs_h, "pkc_rnn: bf16 steps need hs_h");
     for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U_h[g], "pkc_rnn: bf16 steps need U_h[%d]", g);

@@ -62,8 +62,9 @@ OPT_DIRECT = os.environ.get("PKC_OPT_DIRECT", "1") != "0"
 # per-T step graphs kept (least recently used dropped first)
 SEQ_META_SLOTS = 4
 # bf16 performance mode of the sequence models (Engine prec PKC_PREC_BF16): the recurrent step
-# products U h_{t-1} / dgates U^T on bf16 operand copies too (pkc_rnn_args.step_bf16; dense liGRU /
-# LSTM / RNN layers without quantised h or LayerNorm).  0: exact-fp32 steps, bf16 matmuls only.
+# products U h_{t-1} / dgates U^T on bf16 operand copies too (pkc_rnn_args.step_bf16; liGRU /
+# LSTM / RNN layers without quantised h or LayerNorm, dense or block-sparse U).  0: exact-fp32
+# steps, bf16 matmuls only.
 RNN_BF16 = os.environ.get("PKC_RNN_BF16", "1") != "0"
 SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
@@ -1515,7 +1516,7 @@ class Engine:
             a.kmap_fwd, a.kmap_s_fwd = lb["kmap_fwd"].data_ptr(), lb["kmap_s_fwd"]
         if lb.get("kmap_bwd") is not None:
             a.kmap_bwd, a.kmap_s_bwd = lb["kmap_bwd"].data_ptr(), lb["kmap_s_bwd"]
-        if lb.get("hs_h") is not None and lb.get("kmap_fwd") is None and lb.get("kmap_bwd") is None:
+        if lb.get("hs_h") is not None:
             a.step_bf16 = 1
             a.hs_h, a.ut_h, a.dgates_h = (lb["hs_h"].data_ptr(), lb["ut_h"].data_ptr(),
                                           lb["dgates_h"].data_ptr())

@@ -108,12 +108,13 @@ def test_seq_engine_vs_oracle(body):
     _seq_vs_oracle(body)
 
 
-@pytest.mark.parametrize("body", ["ligru_hcgs", "lstm", "lstm_bidir", "gru", "ligru", "rnn"])
+@pytest.mark.parametrize("body", ["ligru_hcgs", "lstm", "lstm_bidir", "gru", "ligru", "rnn",
+                                  "ligru_hcgs_sparse"])
 def test_seq_engine_bf16_vs_bf16_oracle(body):
     """The bf16 performance mode of the sequence configs (Engine(prec=PKC_PREC_BF16): the input
     projections W, their dX / dW, the U weight gradients and the heads on bf16-rounded operands
-    with fp32 accumulation; for dense liGRU / LSTM / RNN layers also the serial U products and
-    their BPTT products (step_bf16); cell state, BN and loss fp32) against the oracle run with
+    with fp32 accumulation; for liGRU / LSTM / RNN layers (dense or block-sparse U) also the serial
+    U products and their BPTT products (step_bf16); cell state, BN and loss fp32) against the oracle run with
     exactly that rounding (oracle.nets.use_bf16_rec_matmuls / use_bf16_matmuls).  Only fp32
     summation order differs, but a last-bit difference in front of a bf16 rounding moves that
     operand by 2^-9, so the bounds are 1e-3 relative on the posteriors (the fp32 mode: 1e-4)
@@ -148,9 +149,8 @@ def _seq_vs_oracle(body, bf16=False):
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
         onets[o["arch_name"]].load_state_dict(nets[o["arch_name"]].state_dict())
-        if bf16 and sec == "a1":        # dense liGRU / LSTM / RNN: bf16 step products too
-            ON.use_bf16_rec_matmuls(onets[o["arch_name"]],
-                                    steps=body in ("lstm", "lstm_bidir", "ligru", "rnn"))
+        if bf16 and sec == "a1":        # liGRU / LSTM / RNN: bf16 step products too
+            ON.use_bf16_rec_matmuls(onets[o["arch_name"]], steps=not body.startswith("gru"))
         elif bf16:
             ON.use_bf16_matmuls(onets[o["arch_name"]])
         opts[o["arch_name"]] = o
