@@ -21,8 +21,9 @@ extern "C" {
 /* Bumped whenever an entry point is added or a struct changes (tests/test_abi_layout.py asserts it):
  * 1: rounds 1-3; 2: pkc_logsoftmax_bwd, and the structs as they stand after round 3 (which appended
  * pkc_dense_bwd_args.dz_scratch without a bump); 3: pkc_opt_seg (direct PKC_OP_OPTIM);
- * 4: PKC_PREC_BF16X3; 5: pkc_rnn_args.step_bf16 and its bf16 operand copies. */
-#define PKC_ABI_VERSION 5
+ * 4: PKC_PREC_BF16X3; 5: pkc_rnn_args.step_bf16 and its bf16 operand copies;
+ * 6: pkc_bn_bwd_epi, pkc_gemm_bnbwd_ok, pkc_dense_bwd_pre. */
+#define PKC_ABI_VERSION 6
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
@@ -98,6 +99,20 @@ typedef struct {
   const int32_t* ktiles; int kmax;              /* block-sparse k-tile lists (device), or NULL */
 } pkc_gemm_problem;
 int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, void* stream);
+/* The first half of a large-batch BatchNorm'd layer's backward in the epilogue of the dX matmul
+ * that produces its output gradient g (neural_networks.py:306-317 under autograd): a PKC_OP_GEMM
+ * problem of pkc_gemm_grouped with X1 = a HOST pointer to a pkc_bn_bwd_epi (read during the call)
+ * stores dy = g * keep / (1 - drop_p) * act'(gamma * xhat + beta) in C instead of g, and per
+ * 128-row block b the column sums sum dy and sum dy * xhat in part[b*2N + n], part[b*2N + N + n]
+ * — what pkc_dense_bwd's statistics pass computes, without re-reading g.  The problem must be
+ * one slab (splits = 1) with ldc = N and take the 128x128 body: pkc_gemm_bnbwd_ok says whether it
+ * does.  pkc_dense_bwd_pre (dz = that C, part in work, part_rows = 128) finishes the backward. */
+typedef struct pkc_bn_bwd_epi_s {
+  const float* xhat; const uint8_t* keep; const float* gamma; const float* beta;
+  float* part; int act; float drop_p;
+} pkc_bn_bwd_epi;
+int pkc_gemm_bnbwd_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K, const void* A,
+                      int64_t lda, const void* B, int64_t ldb);
 /* Large-batch forward matmul of a BatchNorm'd layer (neural_networks.py:306-311: BN(wx(x)) over
  * the batch) with the BatchNorm column statistics in the matmul's epilogue: one slab
  * C = A B^T (as pkc_gemm, splits = 1) and, per row block b of C, the block's column mean of
@@ -164,6 +179,9 @@ typedef struct {
                         scratch between the passes and the final fp32 gradient is not stored */
 } pkc_dense_bwd_args;
 int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* stream);
+/* pkc_dense_bwd after a dX matmul with the pkc_bn_bwd_epi epilogue: a->dz holds dy, work the
+ * per-part_rows-block column sums; finalize (dgamma, dbeta) and apply only (BN training). */
+int pkc_dense_bwd_pre(const pkc_dense_bwd_args* a, float* work, int part_rows, void* stream);
 /* SyncBN (cross-rank BatchNorm statistics): the training-mode BatchNorm of
  * pkc_dense_fwd / pkc_dense_bwd split around a collective the caller runs (sync_bn of the
  * reference recipe; the reference itself has no multi-GPU training).

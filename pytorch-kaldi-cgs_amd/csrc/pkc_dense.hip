@@ -152,12 +152,15 @@ __global__ __launch_bounds__(ET) void dense_finalize_kernel(pkc_dense_fwd_args a
 // Column sums of the backward stats pass's per-16-row partials, once per column (same split as
 // dense_finalize_kernel): part[nrb*2N + c] = sum dy, part[nrb*2N + N + c] = sum dy * xhat; the
 // parameter gradients are written here.
-__global__ __launch_bounds__(ET) void dense_bwd_finalize_kernel(pkc_dense_bwd_args a, float* part) {
+// part_rows: rows per partial block (ERB from the statistics pass; 128 from the dX matmul's
+// pkc_bn_bwd_epi epilogue)
+__global__ __launch_bounds__(ET) void dense_bwd_finalize_kernel(pkc_dense_bwd_args a, float* part,
+                                                                int part_rows) {
   __shared__ float s1[ET], s2[ET];
   const int cl = threadIdx.x % FC_F, t = threadIdx.x / FC_F;
   const int c = blockIdx.x * FC_F + cl;
   const int64_t N = a.N;
-  const int nrb = (a.M + ERB - 1) / ERB;
+  const int nrb = (a.M + part_rows - 1) / part_rows;
   float tdy = 0.f, tdyx = 0.f;
   if (c < a.N) {
 #pragma unroll 4
@@ -328,13 +331,13 @@ __global__ __launch_bounds__(ET) void dense_bwd_stats_kernel(pkc_dense_bwd_args 
 
 // invM: 1 / the row count the column sums are over (this rank's M, or the global count: SyncBN)
 __global__ __launch_bounds__(ET) void dense_bwd_apply_kernel(pkc_dense_bwd_args a, const float* part,
-                                                             float invM) {
+                                                             float invM, int part_rows) {
   const int c = blockIdx.x * EC + threadIdx.x % EC;
   const int t = threadIdx.x / EC;
   const int r0 = blockIdx.y * ERB;
   if (c >= a.N) return;
   const int64_t N = a.N;
-  const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;   // dense_bwd_finalize
+  const float* fin = part + (int64_t)((a.M + part_rows - 1) / part_rows) * 2 * N;   // dense_bwd_finalize
   const float tdy = fin[c], tdyx = fin[N + c];
   const bool bn = a.norm == PKC_NORM_BN_TRAIN;
   if (!bn) return;
@@ -869,13 +872,13 @@ __global__ __launch_bounds__(ET) void dense_bwd_stats_v4_kernel(pkc_dense_bwd_ar
 }
 
 __global__ __launch_bounds__(ET) void dense_bwd_apply_v4_kernel(pkc_dense_bwd_args a, const float* part,
-                                                                float invM) {
+                                                                float invM, int part_rows) {
   const int c = (blockIdx.x * EC4 + threadIdx.x % EC4) * 4;
   const int t = threadIdx.x / EC4;
   const int r0 = blockIdx.y * ERB;
   if (c >= a.N || a.norm != PKC_NORM_BN_TRAIN) return;
   const int64_t N = a.N;
-  const float* fin = part + (int64_t)((a.M + ERB - 1) / ERB) * 2 * N;
+  const float* fin = part + (int64_t)((a.M + part_rows - 1) / part_rows) * 2 * N;
   float k[4], mdy[4], mdyx[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1071,11 +1074,35 @@ extern "C" int pkc_dense_bwd(const pkc_dense_bwd_args* a, float* work, void* str
   { if (v4) hipLaunchKernelGGL(dense_bwd_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd stats");
   hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0, S(stream),
-                     *a, work);
+                     *a, work, ERB);
   PKC_LAUNCH_CHECK("pkc_dense_bwd finalize");
   if (a->norm == PKC_NORM_BN_TRAIN)      // without BN, dz = dy is final after the stats pass
-    { if (v4) hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, 1.f / (float)a->M); else hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, 1.f / (float)a->M); }
+    { if (v4) hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, 1.f / (float)a->M, ERB); else hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, 1.f / (float)a->M, ERB); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd apply");
+  return PKC_OK;
+}
+
+extern "C" int pkc_dense_bwd_pre(const pkc_dense_bwd_args* a, float* work, int part_rows,
+                                 void* stream) {
+  using namespace pkc;
+  PKC_CHECK_ARG(a && a->M > 0 && a->N > 0 && a->xhat && a->dz && work && part_rows >= ERB,
+                "pkc_dense_bwd_pre: bad arguments");
+  PKC_CHECK_ARG(a->norm == PKC_NORM_BN_TRAIN && a->gamma && a->beta && a->save_invstd,
+                "pkc_dense_bwd_pre: BN training only");
+  PKC_CHECK_ARG(!a->dz_scratch || a->dz_bf16, "pkc_dense_bwd_pre: dz_scratch needs dz_bf16");
+  dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
+  const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
+  const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
+  hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F),
+                     0, S(stream), *a, work, part_rows);
+  PKC_LAUNCH_CHECK("pkc_dense_bwd_pre finalize");
+  if (v4)
+    hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work,
+                       1.f / (float)a->M, part_rows);
+  else
+    hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work,
+                       1.f / (float)a->M, part_rows);
+  PKC_LAUNCH_CHECK("pkc_dense_bwd_pre apply");
   return PKC_OK;
 }
 
@@ -1143,7 +1170,7 @@ extern "C" int pkc_dense_bwd_stats(const pkc_dense_bwd_args* a, float* work, flo
   const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
   { if (v4) hipLaunchKernelGGL(dense_bwd_stats_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work); else hipLaunchKernelGGL(dense_bwd_stats_kernel, grid, dim3(ET), 0, S(stream), *a, work); }
   hipLaunchKernelGGL(dense_bwd_finalize_kernel, dim3((a->N + FC_F - 1) / FC_F), dim3(FC_F * FR_F), 0,
-                     S(stream), *a, work);
+                     S(stream), *a, work, ERB);
   const float* fin = work + (int64_t)((a->M + ERB - 1) / ERB) * 2 * a->N;
   PKC_HIP_CHECK(hipMemcpyAsync(sums, fin, sizeof(float) * 2 * (size_t)a->N, hipMemcpyDeviceToDevice,
                                S(stream)), "pkc_dense_bwd_stats copy");
@@ -1163,7 +1190,7 @@ extern "C" int pkc_dense_bwd_sync_apply(const pkc_dense_bwd_args* a, float* work
   dim3 grid((a->N + EC - 1) / EC, (a->M + ERB - 1) / ERB);
   const dim3 grid4((a->N + 4 * EC4 - 1) / (4 * EC4), (a->M + ERB - 1) / ERB);
   const bool v4 = v4_bwd(a) && (int64_t)grid4.x * grid4.y >= V4_MIN_WG;
-  { if (v4) hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, 1.f / (float)total_rows); else hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, 1.f / (float)total_rows); }
+  { if (v4) hipLaunchKernelGGL(dense_bwd_apply_v4_kernel, grid4, dim3(ET), 0, S(stream), *a, work, 1.f / (float)total_rows, ERB); else hipLaunchKernelGGL(dense_bwd_apply_kernel, grid, dim3(ET), 0, S(stream), *a, work, 1.f / (float)total_rows, ERB); }
   PKC_LAUNCH_CHECK("pkc_dense_bwd_sync_apply");
   return PKC_OK;
 }

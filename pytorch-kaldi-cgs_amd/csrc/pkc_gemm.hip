@@ -666,11 +666,14 @@ struct GroupProb {
   const void* A; int64_t lda; const void* B; int64_t ldb; float* C; int64_t ldc; int64_t slab;
   const void* X1; void* X2; void* X3;
   const int32_t* ktiles; int kmax;
+  int bnb;               // >= 0: the BatchNorm-backward epilogue bnb[this] (dX problems)
 };
+constexpr int GBNB = 2;  // BatchNorm-backward epilogues per grouped launch
 struct GroupArgs {
   GroupProb p[GMAX];
   int n;
   OptSegK seg[PKC_OPT_SEGS_MAX];   // direct PKC_OP_OPTIM runs (GroupProb: code 1, segments K .. K+N)
+  big::BnEpi bnb[GBNB];
 };
 
 // SUM: the launch carries slab-sum operations (large-batch split-K dW); a separate instance,
@@ -737,6 +740,12 @@ __device__ __forceinline__ void grouped_body(const GroupArgs& g) {
   const int bz = local / p.tmn, rem = local % p.tmn;
   const int by = rem / p.tn, bx = rem % p.tn;
   if constexpr (BIG) {
+    if (p.code >= 8 && p.bnb >= 0) {       // dX with the BatchNorm-backward epilogue
+      big::body<PREC, BIN, true, false, false, true>(lds, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B,
+                                                     p.ldb, p.C, p.ldc, p.kchunk, p.slab, nullptr,
+                                                     nullptr, &g.bnb[p.bnb < GBNB ? p.bnb : 0]);
+      return;
+    }
     if (p.code >= 8) {
 #define PKC_BB(AK, BK_)                                                                          \
   big::body<PREC, BIN, AK, BK_>(lds, bx, by, bz, p.M, p.N, p.K, p.A, p.lda, p.B, p.ldb, p.C, p.ldc, \
@@ -1012,6 +1021,19 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
                                         splits, slab_stride, S(stream));
 }
 
+// 128 when a grouped dX problem of this shape takes the 128x128 body (the BatchNorm-backward
+// epilogue's precondition, pkc_bn_bwd_epi), else 0
+extern "C" int pkc_gemm_bnbwd_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                                 const void* A, int64_t lda, const void* B, int64_t ldb) {
+  using namespace pkc;
+  if (!(prec == PKC_PREC_FP32 || prec == PKC_PREC_BF16 || prec == PKC_PREC_BF16IN) || M <= 0 ||
+      N <= 0 || K <= 0 || lda <= 0 || ldb <= 0 || lda >= (1ll << 31) || ldb >= (1ll << 31) ||
+      !a_kcontig || b_kcontig)
+    return 0;
+  return big_enabled() && big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb,
+                                        BIG_MIN_TILES_GROUPED, BIG_MIN_K_GROUPED) ? 128 : 0;
+}
+
 // rows per partial block pkc_gemm_colstats writes for this shape: 128 (the 128x128 tile body),
 // 64 (the 64x64 body, 16-byte operand paths), 0 (not taken)
 extern "C" int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
@@ -1079,7 +1101,7 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
                 "pkc_gemm_grouped: bad precision %d", prec);
   GroupArgs g;
   memset(&g, 0, sizeof(g));
-  int wg = 0, k = 0, nseg = 0;
+  int wg = 0, k = 0, nseg = 0, nbnb = 0;
   bool any_big = false, any_sparse = false, any_sum = false, all_vec = true;
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   // a launch with block-sparse problems runs the sparse instance, which has no 128x128 body
@@ -1186,6 +1208,19 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     const int tm = bigp ? big::TM : BM, tnn = bigp ? big::TN : BN;
     GroupProb& p = g.p[k++];
     p.kind = PKC_OP_GEMM;
+    p.bnb = -1;
+    if (q.X1) {            // pkc_bn_bwd_epi (host): the BatchNorm-backward epilogue
+      const pkc_bn_bwd_epi* e = reinterpret_cast<const pkc_bn_bwd_epi*>(q.X1);
+      PKC_CHECK_ARG(bigp && splits == 1 && q.a_kcontig && !q.b_kcontig && q.ldc == q.N && nbnb < GBNB &&
+                        e->xhat && e->gamma && e->beta && e->part && (e->drop_p == 0.f || e->keep),
+                    "pkc_gemm_grouped: problem %d: the BatchNorm-backward epilogue needs a one-slab dX "
+                    "problem on the 128x128 body with ldc = N (pkc_gemm_bnbwd_ok), at most %d per "
+                    "launch, and xhat / gamma / beta / part (+ keep with dropout)", i, GBNB);
+      big::BnEpi& d = g.bnb[nbnb];
+      d.xhat = e->xhat; d.keep = e->keep; d.gamma = e->gamma; d.beta = e->beta; d.part = e->part;
+      d.act = e->act; d.drop_p = e->drop_p;
+      p.bnb = nbnb++;
+    }
     p.code = (q.a_kcontig ? 4 : 0) + (q.b_kcontig ? 2 : 0) + (vec ? 1 : 0) + (bigp ? 8 : 0);
     p.M = q.M; p.N = q.N; p.K = q.K; p.kchunk = kchunk;
     p.tn = (q.N + tnn - 1) / tnn;

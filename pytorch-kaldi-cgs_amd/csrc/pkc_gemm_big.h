@@ -352,6 +352,65 @@ __device__ __forceinline__ void tile_colstats(const f32x16 (&acc)[2][2], char* _
   }
 }
 
+// BatchNorm-backward epilogue of a dX tile (pkc_bn_bwd_epi): the product g becomes
+// dy = g * keep / (1 - p) * act'(gamma xhat + beta), stored in place of g, and the tile's column
+// sums of dy and dy * xhat over its rows < M go to part[by*2N + c], part[by*2N + N + c] — one pass
+// over the accumulators, the two 32-lane halves combined by a shuffle and the two row waves
+// through LDS in a fixed order (as tile_colstats).  ldc == N (the layout of xhat and keep).
+struct BnEpi {
+  const float* xhat; const uint8_t* keep; const float* gamma; const float* beta;
+  float* part; int act; float drop_p;
+};
+__device__ __forceinline__ void tile_bnbwd(f32x16 (&acc)[2][2], char* __restrict__ lds, int m0,
+                                           int n0, int by, int M, int N, int wm, int wn, int lane,
+                                           const BnEpi& e) {
+  float* red = reinterpret_cast<float*>(lds);     // [2 sums][2 row waves][128 columns]
+  const int r = lane & 31, h = lane >> 5;
+  const bool drop = e.drop_p > 0.f;
+  const float scale = drop ? 1.f / (1.f - e.drop_p) : 1.f;
+  __syncthreads();                                // every wave is done with the operand buffers
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int col = n0 + wn * 64 + 32 * b + r;
+    const bool cok = col < N;
+    const int cc = cok ? col : N - 1;
+    const float gam = e.gamma[cc], bet = e.beta[cc];
+    float sdy = 0.f, sdyx = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = m0 + wm * 64 + 32 * a + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const bool ok = cok && row < M;
+        const int64_t idx = (int64_t)(ok ? row : 0) * N + cc;
+        const float xh = e.xhat[idx];
+        float g = acc[a][b][reg];
+        if (drop) g = e.keep[idx] ? g * scale : 0.f;
+        const float y = xh * gam + bet;
+        const float dy = ok ? g * act_bwd(e.act, y, act_fwd(e.act, y)) : 0.f;
+        acc[a][b][reg] = dy;
+        sdy += dy;
+        sdyx += dy * xh;
+      }
+    }
+    sdy += __shfl_xor(sdy, 32);
+    sdyx += __shfl_xor(sdyx, 32);
+    if (h == 0) {
+      red[wm * TN + wn * 64 + 32 * b + r] = sdy;
+      red[2 * TN + wm * TN + wn * 64 + 32 * b + r] = sdyx;
+    }
+  }
+  __syncthreads();
+  if (wm != 0 || h != 0) return;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int cl = wn * 64 + 32 * b + r, col = n0 + cl;
+    if (col >= N) continue;
+    e.part[(int64_t)by * 2 * N + col] = red[cl] + red[TN + cl];
+    e.part[(int64_t)by * 2 * N + N + col] = red[2 * TN + cl] + red[3 * TN + cl];
+  }
+}
+
 // C/D map of the 32x32 MFMA: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
 __device__ __forceinline__ void tile_store(const f32x16 (&acc)[2][2], int m0, int n0, int M, int N,
                                            int wm, int wn, int lane, float* __restrict__ Cz,
@@ -375,13 +434,15 @@ __device__ __forceinline__ void tile_store(const f32x16 (&acc)[2][2], int m0, in
 // C[bz slab][m0.., n0..] = A[m0.., kbeg..kend) . B[n0.., kbeg..kend)^T for one 128x128 tile.
 // `lds` is LDS_BYTES of workgroup memory.  STATS: also the tile's column statistics
 // (tile_colstats; one slab, kchunk >= K).
-template <int PREC, bool BIN, bool AKC, bool BKC, bool STATS = false>
+// BNB: the BatchNorm-backward epilogue (tile_bnbwd with *bnb) before the store
+template <int PREC, bool BIN, bool AKC, bool BKC, bool STATS = false, bool BNB = false>
 __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int bz, int M, int N,
                                      int K, const void* __restrict__ Av, int64_t lda,
                                      const void* __restrict__ Bv, int64_t ldb,
                                      float* __restrict__ Cp, int64_t ldc, int kchunk,
                                      int64_t slab_stride, const float* __restrict__ bias = nullptr,
-                                     float* __restrict__ part = nullptr) {
+                                     float* __restrict__ part = nullptr,
+                                     const BnEpi* bnb = nullptr) {
   using Cf = Cfg<PREC, BIN>;
   using HE = typename Cf::HE;
   constexpr int BK = Cf::BK;
@@ -447,6 +508,7 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
       __syncthreads();
     }
   }
+  if constexpr (BNB) tile_bnbwd(acc, lds, m0, n0, by, M, N, wm, wn, lane, *bnb);
   tile_store(acc, m0, n0, M, N, wm, wn, lane, Cp + (int64_t)bz * slab_stride, ldc);
   if constexpr (STATS) tile_colstats(acc, lds, m0, n0, by, M, N, wm, wn, lane, bias, part);
 }

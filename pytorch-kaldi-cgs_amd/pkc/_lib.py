@@ -9,7 +9,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
-ABI_VERSION = 5         # include/pkc.h PKC_ABI_VERSION
+ABI_VERSION = 6         # include/pkc.h PKC_ABI_VERSION
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 PREC_FP32, PREC_BF16, PREC_BF16IN, PREC_BF16X3 = 0, 1, 2, 3
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
@@ -90,6 +90,11 @@ class GemmProblem(C.Structure):
 
 OP_GEMM, OP_COLSUM, OP_LOSS, OP_OPTIM, OP_SLABSUM, OP_GATHER = 0, 1, 2, 3, 4, 5
 
+
+class BnBwdEpi(C.Structure):
+    _fields_ = [("xhat", vp), ("keep", vp), ("gamma", vp), ("beta", vp), ("part", vp),
+                ("act", C.c_int), ("drop_p", C.c_float)]
+
 REG_L1, REG_L2 = 1, 2
 
 
@@ -130,6 +135,9 @@ _SIGS = {
     "pkc_gemm_colstats": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64, vp,
                                     i64, vp, i64, vp, vp, vp]),
     "pkc_dense_bwd": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp]),
+    "pkc_dense_bwd_pre": (C.c_int, [C.POINTER(DenseBwdArgs), vp, C.c_int, vp]),
+    "pkc_gemm_bnbwd_ok": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64,
+                                    vp, i64]),
     "pkc_dense_work_size": (i64, [C.c_int, C.c_int]),
     "pkc_dense_fwd_stats": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp, vp]),
     "pkc_dense_fwd_sync_apply": (C.c_int, [C.POINTER(DenseFwdArgs), vp, vp, C.c_int, vp]),

@@ -204,11 +204,14 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
     batch_size = {"train": int(config["batches"]["batch_size_train"]),
                   "valid": int(config["batches"]["batch_size_valid"])}.get(to_do, 1)
     # [exp] pkc_prec = bf16 (a pkc key): bf16 matmul operands with fp32 accumulation, master
-    # weights, BatchNorm, loss and optimizer; default fp32, the reference's arithmetic
-    prec = {"fp32": L.PREC_FP32, "bf16": L.PREC_BF16}.get(
+    # weights, BatchNorm, loss and optimizer; bf16x3: compensated bf16 matmuls
+    # (fp32-class products on the bf16 MFMA); default fp32, the reference's
+    # arithmetic
+    prec = {"fp32": L.PREC_FP32, "bf16": L.PREC_BF16, "bf16x3": L.PREC_BF16X3}.get(
         config["exp"].get("pkc_prec", "fp32").strip().lower())
     if prec is None:
-        raise ValueError("[exp] pkc_prec must be fp32 or bf16, not %r" % config["exp"]["pkc_prec"])
+        raise ValueError("[exp] pkc_prec must be fp32, bf16 or bf16x3, not %r"
+                         % config["exp"]["pkc_prec"])
 
     if processed_first:
         shared = []

@@ -76,6 +76,15 @@ DW_SPLIT_ROWS = int(os.environ.get("PKC_DW_SPLIT_ROWS", "1024"))
 # dW of the step's last matmul launch) rides in the NEXT step's first launch, beside that step's
 # batch gather (PKC_OP_GATHER): one launch per step fewer; 0: off (A/B)
 DEFER_TAIL = os.environ.get("PKC_DEFER_TAIL", "1") != "0"
+# multi-step graphs of the B = 128 MLP step: every weight update of step k rides in step k+1's
+# forward launches (the batch gather and the forward matmuls, latency-bound launches that move few
+# bytes) instead of the backward launches, each before the first launch that reads its parameters
+# (PKC_OPT_FWD=1; the graph's last step updates at its own end)
+OPT_FWD = os.environ.get("PKC_OPT_FWD", "0") != "0"
+# large-batch BatchNorm backward: its statistics (sum dy, sum dy * xhat per column) in the epilogue
+# of the dX matmul that produces the layer's output gradient (pkc_bn_bwd_epi), instead of a pass
+# that re-reads that gradient (PKC_BN_BWD_EPI=0: the statistics pass)
+BN_BWD_EPI = os.environ.get("PKC_BN_BWD_EPI", "1") != "0"
 # large-batch BatchNorm'd MLP layers: column statistics in the forward matmul's epilogue
 # (pkc_gemm_colstats + pkc_dense_fwd_pre); PKC_GEMM_COLSTATS=0: matmul + stats/finalize/apply (A/B)
 COLSTATS = os.environ.get("PKC_GEMM_COLSTATS", "1") != "0"
@@ -1294,6 +1303,40 @@ class Engine:
                 C.c_void_p(mp), C.c_void_p(mp + 8 * self.B), C.c_void_p(mp + 8 * self.B + 4 * self.B),
                 self.B, T, ptr(self.x), ptr(self.labs), s)
 
+    def _place_fwd_opt(self, ops):
+        """Slots of the previous step's weight updates in this step's forward: the gather launch
+        (key None) or a matmul launch (key: its first node), each update before the launch that
+        first reads its node's parameters, greedily balanced by bytes (8 operations per launch)."""
+        order, first, nprob = [None], {}, {None: 1}
+        i = 0
+        while i < len(self.nodes):
+            n = self.nodes[i]
+            if n.rec or n.W is None:
+                first.setdefault(n, order[-1])
+                i += 1
+                continue
+            grp = [n]
+            while (n.head and i + len(grp) < len(self.nodes) and not self.nodes[i + len(grp)].rec
+                   and self.nodes[i + len(grp)].head and self.nodes[i + len(grp)].src == n.src):
+                grp.append(self.nodes[i + len(grp)])
+            for g in grp:
+                first[g] = n
+            order.append(n)
+            nprob[n] = len(grp)
+            i += len(grp)
+        pos = {k: j for j, k in enumerate(order)}
+        load = {k: [0.0, nprob[k]] for k in order}     # bytes, operations of each launch
+        slots = {}
+        # tightest deadline first: an update may ride in any launch before its node's own
+        for n, op in sorted(ops, key=lambda t: pos.get(first.get(t[0]), 0)):
+            last = pos[first[n]] - 1 if first.get(n) is not None else 0
+            cands = [k for k in order[:max(1, last + 1)] if load[k][1] < 8]
+            k = min(cands, key=lambda c: load[c][0]) if cands else None
+            load[k][0] += op[2]
+            load[k][1] += 1
+            slots.setdefault(k, []).append(op)
+        return slots
+
     def _upload_seq_meta(self, batch):
         """[B x int64 begin rows][B x int32 lengths][B x int32 left pads] of a sentence batch into
         seq_meta: an asynchronous copy from a pinned ring slot, ordered on the stream before the
@@ -1604,7 +1647,11 @@ class Engine:
     def _forward_kernels(self, s, train, batch=None, defer_loss=False, pending=None):
         """pending: the previous step's deferred last launch (see _optim_kernels), run together
         with this step's gather."""
-        if pending:
+        slots = {}
+        if pending and pending[0] == "fwd":
+            slots = self._place_fwd_opt(pending[1])
+            self._gemms([self._gather_op()] + slots.pop(None, []), s)
+        elif pending:
             self._gemms([self._gather_op()] + list(pending), s)
         elif not self.external:
             self._gather(s, batch)
@@ -1632,7 +1679,7 @@ class Engine:
             if len(grp) == 1 and train and self._colstats_fwd(n, probs[0], s):
                 i += 1
                 continue
-            self._gemms(probs, s)
+            self._gemms(probs + slots.pop(n, []), s)
             if len(grp) > 1:
                 self._nll_multi(grp, s, train)
             else:
@@ -1724,6 +1771,9 @@ class Engine:
             self._k("dense_bwd_sync_apply N=%d" % n.N, 0, 4.0 * M * n.N * 3,
                     "pkc_dense_bwd_sync_apply", C.byref(a), ptr(n.work), ptr(n.bn_sums),
                     M * self.sync_bn.world, s)
+        elif getattr(n, "bnb_now", False):   # statistics came with the consumer's dX matmul
+            self._k("dense_bwd_pre N=%d" % n.N, 0, 4.0 * M * n.N * 3, "pkc_dense_bwd_pre",
+                    C.byref(a), ptr(n.work), 128, s)
         else:
             self._k("dense_bwd N=%d" % n.N, 0, 4.0 * M * n.N * (g_ns + 3), "pkc_dense_bwd",
                     C.byref(a), ptr(n.work), s)
@@ -1792,11 +1842,39 @@ class Engine:
             if kt is not None:
                 pr.ktiles, pr.kmax, d = kt[0].data_ptr(), kt[1], kt[2]
             prh = self._h_variant(pr, dzh, n.W_h.data_ptr() if n.W_h is not None else None)
+            P.bnb_now = False
+            if kt is None and self._bnb_ok(P, n, pr, prh):
+                # P's BatchNorm-backward statistics in this dX matmul's epilogue: it writes
+                # dy into P.dz and the column sums into P.work (_dense_bwd_pre finishes)
+                for q in (pr, prh[1] if prh is not None else None):
+                    if q is not None:
+                        q.C, q.X1 = P.dz.data_ptr(), C.addressof(P.bnb_epi)
+                P.bnb_now = True
             out.append(("dX %dx%dx%d%s" % (M, n.K, n.N, " sparse %.2f" % d if kt is not None else ""),
                         2.0 * M * n.N * n.K * d, 4.0 * (M * n.N + n.N * n.K * d + n.sx * M * n.K),
                         pr, None if prh is None else
                         (2.0 * (M * n.N + n.N * n.K * d) + 4.0 * n.sx * M * n.K, prh)))
         return out
+
+    def _bnb_ok(self, P, n, pr, prh):
+        """Whether producer P's BatchNorm backward can take its statistics from the epilogue of
+        consumer n's dX matmul pr (and its bf16 form prh): one consumer, one slab, training BN
+        without LayerNorm / SyncBN, a large batch, the 128x128 body for both operand forms."""
+        if not (BN_BWD_EPI and self.M > 128 and not self.seq and P.bn and not P.ln and not P.head
+                and P.W is not None and len(P.consumers) == 1 and pr.splits == 1
+                and getattr(P, "bn_sums", None) is None and (P.drop == 0 or P.keep is not None)):
+            return False
+        lib = L.lib()
+        for prec, q in ((self.prec, pr), (L.PREC_BF16IN, prh[1] if prh is not None else None)):
+            if q is not None and lib.pkc_gemm_bnbwd_ok(prec, 1, 0, q.M, q.N, q.K, C.c_void_p(q.A),
+                                                       q.lda, C.c_void_p(q.B), q.ldb) != 128:
+                return False
+        if getattr(P, "bnb_epi", None) is None:
+            P.bnb_epi = L.BnBwdEpi(xhat=P.xhat.data_ptr(),
+                                   keep=P.keep.data_ptr() if P.keep is not None else None,
+                                   gamma=P.gamma.data_ptr(), beta=P.beta.data_ptr(),
+                                   part=P.work.data_ptr(), act=L.ACT[P.act], drop_p=P.drop)
+        return True
 
     def _dw_sum_op(self, n):
         """The slab sum of a split-K dW into the gradient (an operation of the next launch)."""
@@ -1953,7 +2031,7 @@ class Engine:
                     break
         return self._cut
 
-    def _backward_kernels(self, s, loss_op=None, spread_opt=False, on_cut=None):
+    def _backward_kernels(self, s, loss_op=None, spread_opt=False, on_cut=None, fwd_defer=False):
         """Reverse pass.  The matmuls of a layer (dW, dX) are queued and launched together with
         those of the layers after it that are still pending, right before the first kernel that
         needs one of their results (the producer's BatchNorm backward reads the dX slabs).
@@ -1967,6 +2045,7 @@ class Engine:
             if n.gslab is not None:
                 n.sb = self._grad_slabs(n)
         pend = [loss_op] if loss_op is not None else []
+        self.fwd_opt = []       # fwd_defer: (node, update op) for the next step's forward
         future = [[], []]       # future[i]: operations riding in the i-th launch from now
         cut_node = self._bucket_cut()[0] if on_cut is not None else None
         cut_wait = -1           # launches until the cut node's gradient is final
@@ -2017,6 +2096,9 @@ class Engine:
             if spread_opt:
                 nparam = sum(self.opt_entries[i]["p"].numel() for i in self.node_opt.get(n, (0, 0, []))[2])
                 parts = -(-nparam // OPT_SPREAD_PARAMS) if OPT_SPREAD_PARAMS > 0 else 1
+                if fwd_defer:                   # the next step's forward launches carry them
+                    self.fwd_opt += [(n, op) for op in self._opt_op(n, parts)]
+                    continue
                 for k, op in enumerate(self._opt_op(n, parts)):
                     while len(future) <= lag + k:
                         future.append([])
@@ -2086,6 +2168,12 @@ class Engine:
         spread_opt = spread_opt and not self.reg_terms
         self._reg_grad_kernels(s)
         if spread_opt:
+            if getattr(self, "fwd_opt", None):
+                # fwd_defer: every update waits for the next step's forward (_place_fwd_opt)
+                for f in self.spread_tail:
+                    self._gemms(f, s)
+                pend, self.fwd_opt = ("fwd", self.fwd_opt), []
+                return pend
             tail, pend = self.spread_tail, None
             if (defer and DEFER_TAIL and tail and not self.prune_list and not self.seq
                     and self.loss_heads and len(tail[-1]) < 8
@@ -2308,8 +2396,10 @@ class Engine:
         def one_step(st, pending=None, defer_tail=False):
             defer = bool(self.loss_heads)
             self._forward_kernels(st, True, defer_loss=defer, pending=pending)
+            fwd = (OPT_FWD and defer_tail and not split_optimizer and not self.prune_list
+                   and not self.reg_terms and self.M <= 128 and bool(self.loss_heads))
             self._backward_kernels(st, self._loss_op() if defer else None,
-                                   spread_opt=not split_optimizer)
+                                   spread_opt=not split_optimizer, fwd_defer=fwd)
             if not split_optimizer:
                 return self._optim_kernels(st, spread_opt=True, defer=defer_tail)
             return None

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"))
 
 PAIRS = [("DenseFwdArgs", "pkc_dense_fwd_args"), ("DenseBwdArgs", "pkc_dense_bwd_args"),
          ("NllArgs", "pkc_nll_args"), ("OptTensor", "pkc_opt_tensor"), ("RnnArgs", "pkc_rnn_args"),
-         ("GemmProblem", "pkc_gemm_problem"), ("RegItem", "pkc_reg_item"), ("OptSeg", "pkc_opt_seg")]
+         ("GemmProblem", "pkc_gemm_problem"), ("RegItem", "pkc_reg_item"), ("OptSeg", "pkc_opt_seg"),
+         ("BnBwdEpi", "pkc_bn_bwd_epi")]
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
@@ -49,7 +50,8 @@ def test_ctypes_structs_match_header(tmp_path):
 LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa09b47",
                  3: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012",
                  4: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012",
-                 5: "2c453ea47366535096140ab754d5ecfcd019ccecde60defafc6b607b14f5eb2d"}
+                 5: "2c453ea47366535096140ab754d5ecfcd019ccecde60defafc6b607b14f5eb2d",
+                 6: "1bcf851b6b8c7c47b5d010bb84ad5bfed004e6061606a15f6e24fda230644bd9"}
 
 
 def _layout_digest(L):

@@ -126,6 +126,74 @@ def test_gemm_grouped_c2_backward(L, prec):
         assert rel < (1e-6 if prec == 0 else 3e-5), (orient, M, N, K, rel)
 
 
+@pytest.mark.parametrize("prec,M,p", [(2, 4096, 0.15), (2, 1000, 0.0), (1, 2048, 0.15), (0, 1024, 0.15)])
+def test_gemm_bnbwd_epilogue(L, prec, M, p):
+    """pkc_bn_bwd_epi: the dX matmul (M x 1024 x 1024, the 128x128 body in a grouped launch) stores
+    dy = g keep / (1 - p) relu'(gamma xhat + beta) and per-128-row-block column sums of dy and
+    dy * xhat; pkc_dense_bwd_pre on them = pkc_dense_bwd (statistics pass) on g."""
+    N, K = 1024, 1024
+    g = torch.Generator().manual_seed(M + int(100 * p))
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(K, N, generator=g) * K ** -0.5        # dX = A W (b stored as (K, N): m-contig)
+    xhat = torch.randn(M, N, generator=g)
+    keep = (torch.rand(M, N, generator=g) > p).to(torch.uint8)
+    gamma, beta = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g) * 0.1
+    dt = torch.bfloat16 if prec == 2 else torch.float32
+    Ad, Wd = A.to(DEV).to(dt).contiguous(), W.to(DEV).to(dt).contiguous()
+    if prec:
+        A, W = A.bfloat16().float(), W.bfloat16().float()
+    assert L.lib().pkc_gemm_bnbwd_ok(prec, 1, 0, M, N, K, L.ptr(Ad), K, L.ptr(Wd), N) == 128
+    dev = {k: v.to(DEV).contiguous() for k, v in dict(xhat=xhat, keep=keep, gamma=gamma, beta=beta).items()}
+    work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
+    dz = torch.full((M, N), float("nan"), device=DEV)
+    epi = L.BnBwdEpi(xhat=dev["xhat"].data_ptr(), keep=dev["keep"].data_ptr() if p > 0 else None,
+                     gamma=dev["gamma"].data_ptr(), beta=dev["beta"].data_ptr(),
+                     part=work.data_ptr(), act=L.ACT["relu"], drop_p=p)
+    pr = L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=N, K=K, splits=1, A=Ad.data_ptr(), lda=K,
+                       B=Wd.data_ptr(), ldb=N, C=dz.data_ptr(), ldc=N, slab_stride=0,
+                       X1=C.addressof(epi))
+    L.call("pkc_gemm_grouped", prec, C.byref(pr), 1, _s())
+    torch.cuda.synchronize()
+    gref = A.double() @ W.double()
+    y = xhat.double() * gamma.double() + beta.double()
+    dyr = gref * (keep.double() / (1 - p) if p > 0 else 1.0) * (y > 0).double()
+    tol = (2e-5 if prec == 0 else 1e-3) * K ** 0.5 * K ** -0.5 * 4
+    torch.testing.assert_close(dz.cpu().double(), dyr, rtol=1e-3, atol=tol)
+    nb = -(-M // 128)
+    part = work[:2 * N * nb].view(nb, 2, N).cpu().double()
+    got = dz.cpu().double()
+    for b in range(nb):
+        blk, xb = got[128 * b:128 * (b + 1)], xhat.double()[128 * b:128 * (b + 1)]
+        torch.testing.assert_close(part[b, 0], blk.sum(0), rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(part[b, 1], (blk * xb).sum(0), rtol=1e-4, atol=1e-4)
+    # the rest of the backward from the partials vs the statistics-pass form on the same g
+    gd = torch.from_numpy(gref.float().numpy()).to(DEV) if prec == 0 else None
+    if gd is None:      # the same g the epilogue saw: recompute the product without it
+        gd = torch.full((M, N), float("nan"), device=DEV)
+        L.call("pkc_gemm", prec, 1, 0, M, N, K, L.ptr(Ad), K, L.ptr(Wd), N, L.ptr(gd), N, 1, 0, _s())
+    invstd = (torch.rand(N, generator=g) + 0.5).to(DEV)
+    outs = []
+    for fn in ("pkc_dense_bwd", "pkc_dense_bwd_pre"):
+        dzo = dz.clone() if fn == "pkc_dense_bwd_pre" else torch.zeros(M, N, device=DEV)
+        dg, db, dbias = (torch.zeros(N, device=DEV) for _ in range(3))
+        a = L.DenseBwdArgs(M=M, N=N, nslab=1, gslab=gd.data_ptr(), slab_stride=M * N,
+                           norm=L.NORM_BN_TRAIN, act=L.ACT["relu"], gamma=dev["gamma"].data_ptr(),
+                           beta=dev["beta"].data_ptr(), save_invstd=invstd.data_ptr(),
+                           xhat=dev["xhat"].data_ptr(), keep=dev["keep"].data_ptr() if p > 0 else None,
+                           drop_p=p, dz=dzo.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(),
+                           dbias=dbias.data_ptr())
+        if fn == "pkc_dense_bwd":
+            w2 = torch.zeros_like(work)
+            L.call(fn, C.byref(a), L.ptr(w2), _s())
+        else:
+            L.call(fn, C.byref(a), L.ptr(work), 128, _s())
+        outs.append((dzo.cpu(), dg.cpu(), db.cpu()))
+    (z0, g0, b0), (z1, g1, b1) = outs
+    torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(b1, b0, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(z1, z0, rtol=1e-4, atol=1e-5)
+
+
 def test_gemm_unaligned_lda(L):
     """First layer reading straight out of a (N, 442) chunk matrix: scalar-load path."""
     M, N, K = 33, 64, 440

@@ -227,6 +227,53 @@ def test_engine_c1_full_size_vs_oracle(prec):
                 a, k, diff / max(ref.norm().item(), 1e-30))
 
 
+@pytest.mark.parametrize("prec", ["bf16"])
+def test_engine_bn_bwd_epilogue_matches_stats_pass(prec):
+    """Large batch (B = 1024, bf16: exact fp32 keeps the 64x64 body below 1024 tiles, so it has no
+    epilogue form): the BatchNorm backward statistics taken in the dX matmul's epilogue
+    (pkc_bn_bwd_epi + pkc_dense_bwd_pre, layers 0-3 of the body) against the statistics pass
+    (pkc_dense_bwd) — the same dy; only the column sums' order differs (128-row vs 16-row
+    partials), so the gradients agree to fp32 rounding."""
+    import copy
+    import pkc.engine as E
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config(drop="0.15")
+    nets0, opts = build_nets(cfg, C1_DIMS)
+    B = 1024
+    rs = np.random.RandomState(3)
+    X = torch.from_numpy(rs.randn(B * 2, 440).astype(np.float32)).to(DEV)
+    lab = torch.from_numpy(np.stack([rs.randint(0, 1928, 2 * B), rs.randint(0, 48, 2 * B)], 1)
+                           .astype(np.int32)).to(DEV)
+    res = []
+    try:
+        for on in (True, False):
+            E.BN_BWD_EPI = on
+            nets = copy.deepcopy(nets0)
+            for n in nets.values():
+                n.to(DEV).train()
+            eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                         ["lab_cd", "lab_mono"], batch=B, seed=5,
+                         prec=L.PREC_BF16 if prec == "bf16" else L.PREC_FP32)
+            eng.bind_chunk(X, lab, 2 * B)
+            eng.train_step()
+            torch.cuda.synchronize()
+            fused = sum(bool(getattr(n, "bnb_now", False)) for n in eng.nodes)
+            g = eng.gflat.detach().cpu().double().clone()
+            eng.train_step()
+            res.append((fused, g, {a + "/" + k: v.detach().cpu().double() for a in nets
+                                   for k, v in nets[a].state_dict().items()}))
+    finally:
+        E.BN_BWD_EPI = True
+    (f1, g1, s1), (f0, g0, s0) = res
+    assert f1 == 4 and f0 == 0, (f1, f0)           # layers 0-3 (layer 4 feeds two heads)
+    assert (g1 - g0).norm() <= 1e-4 * g0.norm()
+    for k in s0:
+        if k.endswith("num_batches_tracked"):
+            continue
+        assert (s1[k] - s0[k]).norm() <= 1e-3 * s0[k].norm() + 1e-6, k
+
+
 def test_engine_graph_replay_equals_eager():
     from pkc.engine import Engine, parse_model
     cfg = c1_config(drop="0.15")
@@ -235,7 +282,9 @@ def test_engine_graph_replay_equals_eager():
     def no_op_allreduce(t, async_op=False):     # world size 1: the data-parallel code path
         return None
 
-    for use_graph in (False, True, "multi", "dp_eager", "dp_graph"):
+    import pkc.engine as E
+    for use_graph in (False, True, "multi", "dp_eager", "dp_graph", "multi_fwd"):
+        E.OPT_FWD = use_graph == "multi_fwd"     # updates ride in the next step's forward
         nets, opts = build_nets(cfg, C1_DIMS)
         for n in nets.values():
             n.to(DEV).train()
@@ -246,7 +295,7 @@ def test_engine_graph_replay_equals_eager():
         eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
                      ["lab_cd", "lab_mono"], batch=128, seed=3)
         eng.bind_chunk(X, lab, 512)
-        if use_graph in (True, "multi"):
+        if use_graph in (True, "multi", "multi_fwd"):
             assert eng.capture(steps_per_graph=3)
             eng.ctr.zero_()
             eng.loss_acc.zero_()
@@ -256,7 +305,7 @@ def test_engine_graph_replay_equals_eager():
             assert eng.graph_tail is not None       # bucketed: two backward graphs
             eng.ctr.zero_()
             eng.loss_acc.zero_()
-        if use_graph == "multi":
+        if use_graph in ("multi", "multi_fwd"):
             eng.train_steps(4)            # one 3-step graph replay + one single step
         elif use_graph in ("dp_eager", "dp_graph"):
             for _ in range(4):
@@ -268,6 +317,7 @@ def test_engine_graph_replay_equals_eager():
         # the data-parallel ones run them in a separate pass after the all-reduce — bit-identical
         res.append((eng.chunk_totals(), {a + "/" + k: v.cpu() for a in nets
                                          for k, v in nets[a].state_dict().items()}))
+    E.OPT_FWD = False
     for other in res[1:]:
         assert res[0][0] == pytest.approx(other[0], rel=1e-6)
         for k in res[0][1]:
