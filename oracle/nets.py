@@ -727,8 +727,9 @@ class _BF16Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         g = _bf16(dy)
         dx = g @ _bf16(w)
-        dw = g.t() @ _bf16(x)
-        return dx, dw, (dy.sum(0) if ctx.has_b else None)
+        g2 = g.reshape(-1, g.shape[-1])             # (T, B, N) inputs of the recurrent W
+        dw = g2.t() @ _bf16(x).reshape(-1, x.shape[-1])
+        return dx, dw, (dy.reshape(-1, dy.shape[-1]).sum(0) if ctx.has_b else None)
 
 
 def use_bf16_matmuls(net):
@@ -753,7 +754,7 @@ class _BF16dWLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        return dy @ w, _bf16(dy).t() @ _bf16(x)
+        return dy @ w, _bf16(dy).reshape(-1, dy.shape[-1]).t() @ _bf16(x).reshape(-1, x.shape[-1])
 
 
 def use_bf16_rec_matmuls(net, steps=False):
