@@ -102,6 +102,13 @@ r_mfma() {
     ok $? mfma_$c
     python3 scripts/mfma_summary.py /tmp/mfma$c > gpurun_out/mfma/$c.json
   done
+  # the sequence configs' bf16 performance mode (bf16 projections and step products)
+  for c in c3 c4; do
+    timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d /tmp/mfmab$c -o p -- python3 scripts/bench_seq.py \
+      --configs $c --steps 2 --warmup 1 --prec bf16 > gpurun_out/mfma/${c}_bf16.log 2>&1
+    ok $? mfma_${c}_bf16
+    python3 scripts/mfma_summary.py /tmp/mfmab$c > gpurun_out/mfma/${c}_bf16.json
+  done
   head -c 1500 gpurun_out/mfma/b4096.json
 }
 

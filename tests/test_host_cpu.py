@@ -339,3 +339,42 @@ def test_quantcheck_flip_bound():
     n, dmax = quantum_flips(shifted, w)
     assert n > 0.9 * w.size and dmax == 1.0
     assert (np.abs(k) <= 128).all()
+
+
+def test_forward_update_placement_respects_deadlines():
+    """PKC_OPT_FWD: Engine._place_fwd_opt puts each weight update of step k into a launch of
+    step k+1's forward BEFORE the first launch that reads that node's parameters (the gather launch
+    = key None, then one launch per matmul node; two heads reading the same tensor share one), at
+    most 8 operations per launch, balanced by bytes.  Host logic only (mock nodes)."""
+    from pkc.engine import Engine
+
+    class NS:                         # hashable by identity, like the engine's node objects
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+    fea = ("fea", 0)
+    body = []
+    src = fea
+    for i in range(5):
+        n = NS(name="L%d" % i, rec=False, W=object(), head=False, src=src)
+        body.append(n)
+        src = ("node", n)
+    heads = [NS(name="H%d" % i, rec=False, W=object(), head=True, src=src) for i in range(2)]
+    nodes = body + heads
+    ops = []
+    for n in nodes:
+        for part in range(2 if n in body else 3):
+            ops.append((n, ("opt %s [%d]" % (n.name, part), 0.0, 7e6 if n in body else 15e6, None)))
+    slots = Engine._place_fwd_opt(NS(nodes=nodes), ops)
+    order = [None] + body + [heads[0]]
+    seen = {}
+    for pos, key in enumerate(order):
+        for op in slots.get(key, []):
+            seen[op[0]] = pos
+        assert len(slots.get(key, [])) + (2 if key is heads[0] else 1) <= 8
+    assert len(seen) == len(ops)
+    for n, op in ops:
+        first = order.index(heads[0] if n in heads else n)
+        assert seen[op[0]] < first, (op[0], seen[op[0]], first)
+    # the gather launch takes layer 0's update (nothing else can) and the load is spread
+    assert any(op[0].startswith("opt L0") for op in slots[None])
+    assert len([k for k in slots if slots[k]]) >= 4
