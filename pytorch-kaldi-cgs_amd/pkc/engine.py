@@ -1846,7 +1846,7 @@ class Engine:
             if kt is None and self._bnb_ok(P, n, pr, prh):
                 # P's BatchNorm-backward statistics in this dX matmul's epilogue: it writes
                 # dy into P.dz and the column sums into P.work (_dense_bwd_pre finishes)
-                for q in (pr, prh[1] if prh is not None else None):
+                for q in (pr, prh):
                     if q is not None:
                         q.C, q.X1 = P.dz.data_ptr(), C.addressof(P.bnb_epi)
                 P.bnb_now = True
@@ -1865,7 +1865,7 @@ class Engine:
                 and getattr(P, "bn_sums", None) is None and (P.drop == 0 or P.keep is not None)):
             return False
         lib = L.lib()
-        for prec, q in ((self.prec, pr), (L.PREC_BF16IN, prh[1] if prh is not None else None)):
+        for prec, q in ((self.prec, pr), (L.PREC_BF16IN, prh)):
             if q is not None and lib.pkc_gemm_bnbwd_ok(prec, 1, 0, q.M, q.N, q.K, C.c_void_p(q.A),
                                                        q.lda, C.c_void_p(q.B), q.ldb) != 128:
                 return False
