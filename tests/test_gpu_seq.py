@@ -233,7 +233,8 @@ def _seq_vs_oracle(body, bf16=False):
                 perc = (60.0, 40.0)[int(parts[1])]
                 ref = ref * prune_mask(sd_o[name], perc).double()
             d = (v.cpu().double() - ref).norm().item()
-            tol = (5e-2 if bf16 else 1e-3) * ref.norm().item() + 1e-7
+            # (bf16: plus four RMSprop steps of lr = 0.0016 for small vectors such as BN biases)
+            tol = (5e-2 if bf16 else 1e-3) * ref.norm().item() + (6.4e-3 if bf16 else 1e-7)
             if name.endswith("running_mean") and body.endswith("inpnorm"):
                 # the gate pre-activations of a BN-normalised input have column means of 0 up to
                 # fp32 rounding: compare against the spread of the columns instead
