@@ -479,10 +479,13 @@ __device__ __forceinline__ void mfma_chain(const float* va, const float* vb, con
 typedef __attribute__((ext_vector_type(8))) __bf16 rbf16x8;
 
 // v[i] = 8 bf16 of row[kb + 8i ..] (zeros past kmax or when !ok); v8: rows 16-byte aligned and
-// kmax % 8 == 0 (then an 8-chunk is wholly inside or outside), else element loads
+// kmax % 8 == 0 (then an 8-chunk is wholly inside or outside); else kmax % 2 == 0 (C3's H = 550):
+// four 4-byte pair loads per chunk; else element loads
+typedef __attribute__((ext_vector_type(2))) __bf16 rbf16x2;
 template <int S>
 __device__ __forceinline__ void load_strip_h(const __bf16* row, bool ok, int kb, int kmax, bool v8,
                                              rbf16x8* v) {
+  const bool v2 = !v8 && (kmax & 1) == 0;
 #pragma unroll
   for (int i = 0; i < S / 8; ++i) {
     const int k = kb + 8 * i;
@@ -491,6 +494,14 @@ __device__ __forceinline__ void load_strip_h(const __bf16* row, bool ok, int kb,
       const rbf16x8 x = *reinterpret_cast<const rbf16x8*>(row + (in ? k : 0));
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] = in ? x[j] : (__bf16)0.f;
+    } else if (v2) {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const bool in = ok && k + j < kmax;          // pairs never straddle kmax (both even)
+        const rbf16x2 x = *reinterpret_cast<const rbf16x2*>(row + (in ? k + j : 0));
+        v[i][j] = in ? x[0] : (__bf16)0.f;
+        v[i][j + 1] = in ? x[1] : (__bf16)0.f;
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {

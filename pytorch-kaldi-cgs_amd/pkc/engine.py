@@ -79,12 +79,15 @@ DEFER_TAIL = os.environ.get("PKC_DEFER_TAIL", "1") != "0"
 # multi-step graphs of the B = 128 MLP step: every weight update of step k rides in step k+1's
 # forward launches (the batch gather and the forward matmuls, latency-bound launches that move few
 # bytes) instead of the backward launches, each before the first launch that reads its parameters
-# (PKC_OPT_FWD=1; the graph's last step updates at its own end)
+# (PKC_OPT_FWD=1; the graph's last step updates at its own end).  Measured slower: C2 886-887 k ->
+# 868-870 k frames/s (profiles/r04_opt_fwd_ab.txt): the forward launches grow by more than the
+# backward ones shrink, so off by default
 OPT_FWD = os.environ.get("PKC_OPT_FWD", "0") != "0"
 # large-batch BatchNorm backward: its statistics (sum dy, sum dy * xhat per column) in the epilogue
 # of the dX matmul that produces the layer's output gradient (pkc_bn_bwd_epi), instead of a pass
-# that re-reads that gradient (PKC_BN_BWD_EPI=0: the statistics pass)
-BN_BWD_EPI = os.environ.get("PKC_BN_BWD_EPI", "1") != "0"
+# that re-reads that gradient.  Measured slower (B = 4096: 5.46-5.47 M -> 4.84-4.85 M frames/s,
+# profiles/r04_bn_bwd_epi_ab.txt), so off by default (PKC_BN_BWD_EPI=1: on)
+BN_BWD_EPI = os.environ.get("PKC_BN_BWD_EPI", "0") != "0"
 # large-batch BatchNorm'd MLP layers: column statistics in the forward matmul's epilogue
 # (pkc_gemm_colstats + pkc_dense_fwd_pre); PKC_GEMM_COLSTATS=0: matmul + stats/finalize/apply (A/B)
 COLSTATS = os.environ.get("PKC_GEMM_COLSTATS", "1") != "0"

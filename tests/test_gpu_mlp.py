@@ -248,7 +248,7 @@ def test_engine_bn_bwd_epilogue_matches_stats_pass(prec):
     res = []
     try:
         for on in (True, False):
-            E.BN_BWD_EPI = on
+            E.BN_BWD_EPI = on            # (off by default: measured slower, DESIGN round 4)
             nets = copy.deepcopy(nets0)
             for n in nets.values():
                 n.to(DEV).train()
@@ -262,7 +262,7 @@ def test_engine_bn_bwd_epilogue_matches_stats_pass(prec):
             g = eng.gflat.detach().cpu().double().clone()
             res.append((fused, g, None))
     finally:
-        E.BN_BWD_EPI = True
+        E.BN_BWD_EPI = False
     (f1, g1, s1), (f0, g0, s0) = res
     assert f1 == 4 and f0 == 0, (f1, f0)           # layers 0-3 (layer 4 feeds two heads)
     # the column sums' order moves dz by ~1e-7; its bf16 copy (the next matmuls' operand) then
