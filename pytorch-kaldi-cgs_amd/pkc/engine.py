@@ -66,6 +66,7 @@ SEQ_META_SLOTS = 4
 # LSTM / RNN layers without quantised h or LayerNorm, dense or block-sparse U).  0: exact-fp32
 # steps, bf16 matmuls only.
 RNN_BF16 = os.environ.get("PKC_RNN_BF16", "1") != "0"
+RNN_BF16_SPARSE = os.environ.get("PKC_RNN_BF16_SPARSE", "0") != "0"     # block-sparse U too
 SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
@@ -1562,7 +1563,10 @@ class Engine:
             a.kmap_fwd, a.kmap_s_fwd = lb["kmap_fwd"].data_ptr(), lb["kmap_s_fwd"]
         if lb.get("kmap_bwd") is not None:
             a.kmap_bwd, a.kmap_s_bwd = lb["kmap_bwd"].data_ptr(), lb["kmap_s_bwd"]
-        if lb.get("hs_h") is not None:
+        # (block-sparse U keeps the fp32 steps: C3's 16-row tiles over 16-wide blocks measured
+        # 16.6 vs 16.1 us per step and layer with bf16 operands, profiles/r04_rnn_bf16_ab.txt)
+        if lb.get("hs_h") is not None and (RNN_BF16_SPARSE or (lb.get("kmap_fwd") is None
+                                                               and lb.get("kmap_bwd") is None)):
             a.step_bf16 = 1
             a.hs_h, a.ut_h, a.dgates_h = (lb["hs_h"].data_ptr(), lb["ut_h"].data_ptr(),
                                           lb["dgates_h"].data_ptr())

@@ -125,6 +125,16 @@ def test_seq_engine_bf16_vs_bf16_oracle(body):
 
 
 def _seq_vs_oracle(body, bf16=False):
+    import pkc.engine as E
+    if bf16 and body.endswith("_sparse"):        # exercise the bf16 block-sparse step kernels
+        E.RNN_BF16_SPARSE = True
+    try:
+        _seq_vs_oracle_run(body, bf16)
+    finally:
+        E.RNN_BF16_SPARSE = False
+
+
+def _seq_vs_oracle_run(body, bf16):
     import pkc.neural_networks as NN
     from oracle import nets as ON
     from oracle import run as OR
