@@ -96,32 +96,6 @@ __device__ __forceinline__ float drop_val(const pkc_rnn_args& a, int r, int j, i
 // h = o * tanh(c) has |h| < 1) a smaller |x| has x/var < 2^-20, where both quotients give
 // ceil(.) = 1 (x != 0) or 0: the FAST form is bit-identical to the IEEE one (the sign of a zero
 // quotient is dropped by the fabsf either way); any other var takes the IEEE division.
-// Step-kernel grid packed onto x of the 8 XCDs (x = 8: the plain 3-D grid).  Workgroup b of a 1-D
-// grid runs on XCD b % 8 (round-robin dispatch: placement is a speed matter only, never
-// correctness); those on XCDs >= x exit at once and the others take logical tiles (b / 8) x + b % 8.
-// With all of a step's tiles on few XCDs, the h_{t-1} / dgates the previous step's tiles wrote sit
-// in those XCDs' own L2 instead of arriving over the fabric.
-struct PackGrid {
-  int gx, gy, gz, x;
-};
-
-__device__ __forceinline__ bool pack_tile(const PackGrid& p, int& bx, int& by, int& bz) {
-  if (p.x >= 8) {
-    bx = blockIdx.x;
-    by = blockIdx.y;
-    bz = blockIdx.z;
-    return true;
-  }
-  const int b = blockIdx.x, xcd = b & 7;
-  if (xcd >= p.x) return false;
-  const int l = (b >> 3) * p.x + xcd;
-  if (l >= p.gx * p.gy * p.gz) return false;
-  bx = l % p.gx;
-  by = (l / p.gx) % p.gy;
-  bz = l / (p.gx * p.gy);
-  return true;
-}
-
 struct QParams {
   float var, rcp, scale, iscale;
   bool fast;
@@ -558,7 +532,7 @@ __device__ __forceinline__ EpiIn epi_load(const pkc_rnn_args& a, const RnnIdx& i
 }
 
 // Cell update of step t at (r, j) from the recurrent products acc[g] = (U_g h_{t-1})[r][j].
-template <int CELL, bool QH>
+template <int CELL, bool QH, bool BF>
 __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
                                         int j, const float* acc, const float* vars, float qscale,
                                         const EpiIn& e) {
@@ -626,7 +600,7 @@ __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix,
     a.gates[3 * TB2H + si] = cc;
   }
   a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
-  if (a.hs_h)      // the next step's bf16 operand (step_bf16)
+  if constexpr (BF)   // the next step's bf16 operand (step_bf16: every step runs a BF instance)
     reinterpret_cast<__bf16*>(a.hs_h)[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = (__bf16)h;
   a.y[ix.out(t, r, j)] = h;
 }
@@ -656,11 +630,10 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 // BF: bf16 step product (step_bf16: hs_h / U_h operands, mfma_chain_h)
 template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4, bool R16 = false,
           bool BF = false>
-__global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw, PackGrid pg) {
+__global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
   static_assert(!BF || (!QH && PH == 0), "bf16 steps: one-phase cells, no quantised h");
-  int bx, by, bz;
-  if (!pack_tile(pg, bx, by, bz)) return;
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   constexpr int NTH = 64 * NW;
   __shared__ float red[NW * 32 * 17];
   __shared__ float tile[32 * 17];
@@ -797,8 +770,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < NG; ++g) acc[g] = tile[rl * 17 + g * NU + ul];
-      if constexpr (PF) fwd_epi<CELL, QH>(a, ix, t, r, j, acc, vars, qscale, pre);
-      else fwd_epi<CELL, QH>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
+      if constexpr (PF) fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, pre);
+      else fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
     }
   }
 }
@@ -863,12 +836,10 @@ __device__ __forceinline__ void rh_epi(const pkc_rnn_args& a, const RnnIdx& ix, 
 // out[r][k] = sum_j dg_g[t][r][j] * U_g[j][k], B operand from U^T (a.ut, G x H x H).
 template <int G, int CELL, int MODE, int S, bool SP = false, int NW = 4, bool R16 = false,
           bool BF = false>
-__global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw,
-                                                      PackGrid pg) {
+__global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int g0, int vw) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
   static_assert(!BF || MODE <= 1, "bf16 steps: one-phase cells");
-  int bx, by, bz;
-  if (!pack_tile(pg, bx, by, bz)) return;
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   constexpr int NTH = 64 * NW;
   __shared__ float red[NW * 32 * 17];
   __shared__ float tile[32 * 17];
@@ -891,7 +862,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
     rbf16x8 ha[S / 8], hb[S / 8], hu[S / 8];
     if constexpr (SP) {
       int blk[S / 16];
-      tile_blocks<S>(a.kmap_bwd + ((int64_t)g * pg.gx + bx) * S, blk);
+      tile_blocks<S>(a.kmap_bwd + ((int64_t)g * gridDim.x + bx) * S, blk);
       load_blocks_h<S>(dgh + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, v8, ha);
       if constexpr (!R16) load_blocks_h<S>(dgh + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, v8, hb);
       load_blocks_h<S>(puh, k < H, blk, H, v8, hu);
@@ -907,7 +878,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   if constexpr (SP) {
     static_assert(MODE == 0, "block-sparse U: gate-split BPTT products only");
     int blk[S / 16];
-    tile_blocks<S>(a.kmap_bwd + ((int64_t)g * pg.gx + bx) * S, blk);
+    tile_blocks<S>(a.kmap_bwd + ((int64_t)g * gridDim.x + bx) * S, blk);
     load_blocks<S>(dg + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, blk, H, vw, va);
     if constexpr (!R16) load_blocks<S>(dg + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, blk, H, vw, vb);
     load_blocks<S>(pu, k < H, blk, H, vw, vu);
@@ -934,13 +905,12 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
 
 // Sum of the NS gate slabs + bwd_step_epi for target tt (elementwise over B2 x H).
 template <int G, int CELL, int NS>
-__global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt, PackGrid pg) {
-  int bx, by, bz;
-  if (!pack_tile(pg, bx, by, bz)) return;
+__global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt) {
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   const RnnIdx ix = mkidx(a);
   const int64_t n = (int64_t)ix.B2 * a.H;
   for (int64_t e = bx * (int64_t)blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)pg.gx * blockDim.x) {
+       e += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.f;
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc += a.work[(4 + s) * n + e];
@@ -1035,33 +1005,6 @@ static bool eight_waves(int S) {
   return w == 8 && S >= 32;
 }
 
-// XCDs a step kernel's tiles are packed onto (PKC_RNN_XCDS: 8 = the plain grid, 1 / 2 / 4 = that
-// many XCDs; 0 = by tile count, PKC_RNN_TILES_PER_CU tiles per CU at most)
-static PackGrid pack_grid(dim3 g) {
-  static const int mode = [] {
-    const char* v = getenv("PKC_RNN_XCDS");
-    return v ? atoi(v) : 8;
-  }();
-  static const int per_cu = [] {
-    const char* v = getenv("PKC_RNN_TILES_PER_CU");
-    return v ? atoi(v) : 1;
-  }();
-  const int n = (int)(g.x * g.y * g.z);
-  int x = mode;
-  if (x <= 0) {                        // smallest power of two with <= per_cu tiles per CU (32 / XCD)
-    x = 1;
-    while (x < 8 && n > 32 * per_cu * x) x *= 2;
-  }
-  x = x >= 8 ? 8 : (x >= 4 ? 4 : (x >= 2 ? 2 : 1));
-  return PackGrid{(int)g.x, (int)g.y, (int)g.z, x};
-}
-
-static dim3 pack_dim(const PackGrid& p) {
-  if (p.x >= 8) return dim3(p.gx, p.gy, p.gz);
-  const int n = p.gx * p.gy * p.gz;
-  return dim3((unsigned)(((n + p.x - 1) / p.x) * 8));
-}
-
 #ifdef PKC_RNN_FWD
 template <int G, int CELL, int S, bool SP = false>
 static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
@@ -1075,13 +1018,13 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
     const dim3 g1r(g1.x, rows_16), g2r(g2.x, rows_16);
     for (int t = 0; t < a->T; ++t) {
       if (r16) {
-        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false, false, 4, true>), pack_dim(pack_grid(g1r)), dim3(RT), 0, s,
-                           *a, t, vw, pack_grid(g1r));
-        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false, false, 4, true>), pack_dim(pack_grid(g2r)), dim3(RT), 0, s,
-                           *a, t, vw, pack_grid(g2r));
+        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false, false, 4, true>), g1r, dim3(RT), 0, s,
+                           *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false, false, 4, true>), g2r, dim3(RT), 0, s,
+                           *a, t, vw);
       } else {
-        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
-        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), pack_dim(pack_grid(g2)), dim3(RT), 0, s, *a, t, vw, pack_grid(g2));
+        hipLaunchKernelGGL((rnn_fwd_mm<NG, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
+        hipLaunchKernelGGL((rnn_fwd_mm<1, CELL, 1, S, false>), g2, dim3(RT), 0, s, *a, t, vw);
       }
       if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
@@ -1096,16 +1039,16 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
         for (int t = 0; t < a->T; ++t) {
           if (r16 && ew)
             hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true, true>),
-                               pack_dim(pack_grid(g16)), dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
+                               g16, dim3(2 * RT), 0, s, *a, t, vw);
           else if (r16)
             hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true, true>),
-                               pack_dim(pack_grid(g16)), dim3(RT), 0, s, *a, t, vw, pack_grid(g16));
+                               g16, dim3(RT), 0, s, *a, t, vw);
           else if (ew)
             hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, false, true>),
-                               pack_dim(pack_grid(g1)), dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g1));
+                               g1, dim3(2 * RT), 0, s, *a, t, vw);
           else
             hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, false, true>),
-                               pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+                               g1, dim3(RT), 0, s, *a, t, vw);
         }
         PKC_LAUNCH_CHECK("pkc_rnn_fwd bf16 step");
         return PKC_OK;
@@ -1115,36 +1058,36 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
       if (r16) {
         if constexpr (SP) {
           if (a->step_bf16)
-            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true, true>), pack_dim(pack_grid(g16)),
-                               dim3(RT), 0, s, *a, t, vw, pack_grid(g16));
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true, true>), g16,
+                               dim3(RT), 0, s, *a, t, vw);
           else
-            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0, s,
-                               *a, t, vw, pack_grid(g16));
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), g16, dim3(RT), 0, s,
+                               *a, t, vw);
         } else if (a->qbits > 0 && qh_eight_waves(S))
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), pack_dim(pack_grid(g16)),
-                             dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), g16,
+                             dim3(2 * RT), 0, s, *a, t, vw);
         else if (a->qbits > 0)
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0, s,
-                             *a, t, vw, pack_grid(g16));
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), g16, dim3(RT), 0, s,
+                             *a, t, vw);
         else if (eight_waves(S))
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true>), pack_dim(pack_grid(g16)),
-                             dim3(2 * RT), 0, s, *a, t, vw, pack_grid(g16));
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true>), g16,
+                             dim3(2 * RT), 0, s, *a, t, vw);
         else
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true>), pack_dim(pack_grid(g16)), dim3(RT), 0,
-                             s, *a, t, vw, pack_grid(g16));
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, false, 4, true>), g16, dim3(RT), 0,
+                             s, *a, t, vw);
       } else if constexpr (SP) {
         if (a->step_bf16)
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, false, true>), pack_dim(pack_grid(g1)),
-                             dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, false, true>), g1,
+                             dim3(RT), 0, s, *a, t, vw);
         else
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), g1, dim3(RT), 0, s, *a, t, vw);
       } else if (a->qbits > 0)
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
       else if (eight_waves(S))
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), pack_dim(pack_grid(g1)), dim3(2 * RT), 0, s,
-                           *a, t, vw, pack_grid(g1));
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), g1, dim3(2 * RT), 0, s,
+                           *a, t, vw);
       else
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), pack_dim(pack_grid(g1)), dim3(RT), 0, s, *a, t, vw, pack_grid(g1));
+        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false>), g1, dim3(RT), 0, s, *a, t, vw);
       if (a->ln_gamma) hipLaunchKernelGGL(rnn_ln_fwd, dim3((B2 + 3) / 4), dim3(256), 0, s, *a, t);
     }
   }
@@ -1175,29 +1118,29 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
     // the candidate gate's U^T product (MODE 2) and the gates' sum (MODE 0 / 1)
     auto mm2 = [&](int t) {
       if (r16)
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 1))),
-                           dim3(RT), 0, s, *a, t, HG, vw, pack_grid(dim3(kt, rows_16, 1)));
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S, false, 4, true>), dim3(kt, rows_16, 1),
+                           dim3(RT), 0, s, *a, t, HG, vw);
       else
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a, t,
-                           HG, vw, pack_grid(dim3(kt, rows, 1)));
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 2, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a, t,
+                           HG, vw);
     };
     mm2(a->T - 1);
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (CELL == PKC_CELL_GRU) {           // Uz^T dz + Ur^T dr: two gate slabs
         if (r16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 2))),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, 2)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true>), dim3(kt, rows_16, 2),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), pack_dim(pack_grid(dim3(kt, rows, 2))), dim3(RT), 0, s, *a,
-                             tt + 1, 0, vw, pack_grid(dim3(kt, rows, 2)));
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, 2>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S>), dim3(kt, rows, 2), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, 2>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else {                                        // minimalGRU: Uz^T dz, one gate
         if (r16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 1))),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, 1)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), dim3(kt, rows_16, 1),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a,
-                             tt + 1, 0, vw, pack_grid(dim3(kt, rows, 1)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw);
       }
       if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
       mm2(tt);
@@ -1210,28 +1153,28 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
           if constexpr (G == 1) {
             if (r16)
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true, true>),
-                                 pack_dim(pack_grid(dim3(kt, rows_16, 1))), dim3(RT), 0, s, *a, tt + 1,
-                                 0, vw, pack_grid(dim3(kt, rows_16, 1)));
+                                 dim3(kt, rows_16, 1), dim3(RT), 0, s, *a, tt + 1,
+                                 0, vw);
             else
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, false, true>),
-                                 pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a, tt + 1, 0,
-                                 vw, pack_grid(dim3(kt, rows, 1)));
+                                 dim3(kt, rows, 1), dim3(RT), 0, s, *a, tt + 1, 0,
+                                 vw);
           } else {
             const dim3 gg(kt, r16 ? rows_16 : rows, G);
             if (r16 && ew)
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true, true>),
-                                 pack_dim(pack_grid(gg)), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+                                 gg, dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
             else if (r16)
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, true, true>),
-                                 pack_dim(pack_grid(gg)), dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+                                 gg, dim3(RT), 0, s, *a, tt + 1, 0, vw);
             else if (ew)
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, false, true>),
-                                 pack_dim(pack_grid(gg)), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
+                                 gg, dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
             else
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, false, true>),
-                                 pack_dim(pack_grid(gg)), dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(gg));
-            hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s,
-                               *a, tt, pack_grid(dim3(eb)));
+                                 gg, dim3(RT), 0, s, *a, tt + 1, 0, vw);
+            hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s,
+                               *a, tt);
           }
         }
         PKC_LAUNCH_CHECK("pkc_rnn_bwd bf16 step");
@@ -1243,33 +1186,33 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
     for (int tt = a->T - 2; tt >= 0; --tt) {
       if constexpr (G == 1) {
         if (r16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, 1))),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, 1)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S, false, 4, true>), dim3(kt, rows_16, 1),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), pack_dim(pack_grid(dim3(kt, rows, 1))), dim3(RT), 0, s, *a,
-                             tt + 1, 0, vw, pack_grid(dim3(kt, rows, 1)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 1, S>), dim3(kt, rows, 1), dim3(RT), 0, s, *a,
+                             tt + 1, 0, vw);
       } else if (r16) {                               // 16-row tiles (C3, C5)
         if (!SP && eight_waves(S))
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8, true>), dim3(kt, rows_16, G), dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
         else if (SP && a->step_bf16)
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true, true>), dim3(kt, rows_16, G),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
         else
-          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), pack_dim(pack_grid(dim3(kt, rows_16, G))),
-                             dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows_16, G)));
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
+          hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), dim3(kt, rows_16, G),
+                             dim3(RT), 0, s, *a, tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else if (!SP && eight_waves(S)) {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), pack_dim(pack_grid(dim3(kt, rows, G))),
-                           dim3(2 * RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), dim3(kt, rows, G),
+                           dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else if (SP && a->step_bf16) {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, false, true>), pack_dim(pack_grid(dim3(kt, rows, G))),
-                           dim3(RT), 0, s, *a, tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, false, true>), dim3(kt, rows, G),
+                           dim3(RT), 0, s, *a, tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else {
-        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), pack_dim(pack_grid(dim3(kt, rows, G))), dim3(RT), 0, s, *a,
-                           tt + 1, 0, vw, pack_grid(dim3(kt, rows, G)));
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), pack_dim(pack_grid(dim3(eb))), dim3(256), 0, s, *a, tt, pack_grid(dim3(eb)));
+        hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
+                           tt + 1, 0, vw);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       }
       if (ln) hipLaunchKernelGGL((rnn_ln_bwd_gates<G, CELL>), lg, dim3(256), 0, s, *a, tt);
     }

@@ -18,7 +18,8 @@ def per_dispatch(pass_dir, counter):
     rows.sort(key=lambda r: int(r.get("Dispatch_Id", r.get("Correlation_Id", 0))))
     tail = rows[-n:]
     vals = [float(r["Counter_Value"]) for r in tail]
-    return tail[-1]["Kernel_Name"] if tail else None, (sum(vals) / len(vals)) if vals else None
+    names = sorted({r["Kernel_Name"] for r in tail})     # every instance the replayed launches use
+    return names, (sum(vals) / len(vals)) if vals else None
 
 
 label, labels = None, set()
@@ -32,7 +33,7 @@ if len(labels) > 1:
     sys.exit("the two passes replayed different kernels: %s" % sorted(labels))
 kf, fetch = per_dispatch("fetch", "FETCH_SIZE")
 kw, write = per_dispatch("write", "WRITE_SIZE")
-out = {"label": label, "kernel": kf, "dispatches": n, "FETCH_SIZE_KiB": fetch,
+out = {"label": label, "kernels": kf, "dispatches": n, "FETCH_SIZE_KiB": fetch,
        "WRITE_SIZE_KiB": write,
        "traffic_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None
        else None}
