@@ -209,8 +209,10 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
 }
 
 // The gate gradients of step tt from the total dL/dh_tt = g (LSTM: plus the carried dc), into
-// dgates and the ping-pong slot of step tt ((T-1-tt) & 1) of the g / dc carries.
-template <int G, int CELL>
+// dgates and the ping-pong slot of step tt ((T-1-tt) & 1) of the g / dc carries.  HC: the bf16
+// copy of dgates for the next bf16 BPTT product — 0 none, 1 always (the BF instances), 2 when
+// dgates_h is set (one-off launches)
+template <int G, int CELL, int HC>
 __device__ __forceinline__ void gate_part(const pkc_rnn_args& a, const RnnIdx& ix, int tt, int r,
                                           int k, float g, float dc_carry) {
   const int64_t TB2H = (int64_t)a.T * ix.B2 * a.H;
@@ -228,7 +230,7 @@ __device__ __forceinline__ void gate_part(const pkc_rnn_args& a, const RnnIdx& i
   } else {
 #pragma unroll
     for (int q = 0; q < G; ++q) a.dgates[q * TB2H + si] = dg[q];
-    if (a.dgates_h) {     // the next BPTT product's bf16 operand (step_bf16)
+    if (HC == 1 || (HC == 2 && a.dgates_h)) {     // the next BPTT product's bf16 operand
 #pragma unroll
       for (int q = 0; q < G; ++q) reinterpret_cast<__bf16*>(a.dgates_h)[q * TB2H + si] = (__bf16)dg[q];
     }
@@ -249,7 +251,7 @@ __global__ void rnn_bwd_init(pkc_rnn_args a) {
     const int r = (int)(e / a.H), k = (int)(e % a.H);
     const float g = dy_at(a, ix.out(t, r, k));
     if (a.ln_gamma) a.ln_g[ix.st(t, r, k)] = g;
-    else gate_part<G, CELL>(a, ix, t, r, k, g, 0.f);
+    else gate_part<G, CELL, 2>(a, ix, t, r, k, g, 0.f);
   }
 }
 
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(256) void rnn_ln_bwd_gates(pkc_rnn_args a, int tt) 
     float dc_carry = 0.f;
     if constexpr (CELL == PKC_CELL_LSTM)
       if (tt < a.T - 1) dc_carry = a.work[2 * n + src * n + (int64_t)r * H + j];
-    gate_part<G, CELL>(a, ix, tt, r, j, g, dc_carry);
+    gate_part<G, CELL, 0>(a, ix, tt, r, j, g, dc_carry);
   }
 }
 
@@ -778,7 +780,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
 
 // BPTT step for target tt (t = tt + 1 has its gate gradients): dh = acc + carries, g = dy + dh,
 // then the gate gradients of step tt at (r, k).
-template <int G, int CELL>
+template <int G, int CELL, int HC>
 __device__ __forceinline__ void bwd_step_epi(const pkc_rnn_args& a, const RnnIdx& ix, int tt, int r,
                                              int k, float acc) {
   const int H = a.H;
@@ -806,7 +808,7 @@ __device__ __forceinline__ void bwd_step_epi(const pkc_rnn_args& a, const RnnIdx
     a.ln_g[ix.st(tt, r, k)] = g;
     return;
   }
-  gate_part<G, CELL>(a, ix, tt, r, k, g, dc_carry);
+  gate_part<G, CELL, HC>(a, ix, tt, r, k, g, dc_carry);
 }
 
 // d(rh)_t = Uh^T da_t (acc) of a two-phase cell -> dr_t (GRU) or dz_t (minimalGRU); d(rh) is kept
@@ -898,13 +900,13 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
     if ((R16 && rl >= 16) || r >= B2 || kk >= H) continue;
     const float v = tile[rl * 17 + kl];
     if constexpr (MODE == 0) a.work[(4 + bz) * n + (int64_t)r * H + kk] = v;
-    else if constexpr (MODE == 1) bwd_step_epi<G, CELL>(a, ix, t - 1, r, kk, v);
+    else if constexpr (MODE == 1) bwd_step_epi<G, CELL, BF ? 1 : 0>(a, ix, t - 1, r, kk, v);
     else rh_epi<CELL>(a, ix, t, r, kk, v);
   }
 }
 
 // Sum of the NS gate slabs + bwd_step_epi for target tt (elementwise over B2 x H).
-template <int G, int CELL, int NS>
+template <int G, int CELL, int NS, bool BF = false>
 __global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt) {
   const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   const RnnIdx ix = mkidx(a);
@@ -914,7 +916,7 @@ __global__ __launch_bounds__(256) void rnn_bwd_epi(pkc_rnn_args a, int tt) {
     float acc = 0.f;
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc += a.work[(4 + s) * n + e];
-    bwd_step_epi<G, CELL>(a, ix, tt, (int)(e / a.H), (int)(e % a.H), acc);
+    bwd_step_epi<G, CELL, BF ? 1 : 0>(a, ix, tt, (int)(e / a.H), (int)(e % a.H), acc);
   }
 }
 
@@ -1173,7 +1175,7 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
             else
               hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, false, 4, false, true>),
                                  gg, dim3(RT), 0, s, *a, tt + 1, 0, vw);
-            hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s,
+            hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G, true>), dim3(eb), dim3(256), 0, s,
                                *a, tt);
           }
         }
@@ -1200,7 +1202,10 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
         else
           hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, true>), dim3(kt, rows_16, G),
                              dim3(RT), 0, s, *a, tt + 1, 0, vw);
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
+        if (SP && a->step_bf16)
+          hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G, true>), dim3(eb), dim3(256), 0, s, *a, tt);
+        else
+          hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else if (!SP && eight_waves(S)) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S / 2, false, 8>), dim3(kt, rows, G),
                            dim3(2 * RT), 0, s, *a, tt + 1, 0, vw);
@@ -1208,7 +1213,7 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       } else if (SP && a->step_bf16) {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP, 4, false, true>), dim3(kt, rows, G),
                            dim3(RT), 0, s, *a, tt + 1, 0, vw);
-        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G>), dim3(eb), dim3(256), 0, s, *a, tt);
+        hipLaunchKernelGGL((rnn_bwd_epi<G, CELL, G, true>), dim3(eb), dim3(256), 0, s, *a, tt);
       } else {
         hipLaunchKernelGGL((rnn_bwd_mm<G, CELL, 0, S, SP>), dim3(kt, rows, G), dim3(RT), 0, s, *a,
                            tt + 1, 0, vw);
