@@ -174,20 +174,20 @@ def pmc_traffic(label):
     return None
 
 
-def batch_sweep(prec, batches=(1024, 4096), steps=30):
-    """Informational: the same step at larger frame batches — not `value`."""
+def batch_sweep(prec, batches=(1024, 4096), steps=150):
+    """Informational: the same step at larger frame batches — not `value`.
+    (150 steps: with 30, the 20-40 ms timed regions read 10-20 % low against bench.py --batch runs
+    of the same build, profiles/r04_bench_latest.json vs r04_bn_bwd_epi_ab.txt)"""
     out = {}
     for b in batches:
         eng, _, _, _ = build(prec, b, 0, 1)
         for _ in range(3):
             eng.train_step()
         eng.capture()
-        for _ in range(5):
-            eng.train_step()
+        eng.train_steps(16)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            eng.train_step()
+        eng.train_steps(steps)
         torch.cuda.synchronize()
         out[str(b)] = round(steps * b / (time.perf_counter() - t0), 1)
         del eng
