@@ -16,8 +16,3 @@ print("steps", len(gaps), "launches per step (mode)", np.bincount(lens).argmax()
 print("gap before %s over the last %d steps: p10 %.2f p50 %.2f p90 %.2f max %.2f mean %.2f us" % (
     first, len(steady), *np.percentile(steady, [10, 50, 90]), steady.max(), steady.mean()))
 print("last 24 gaps:", " ".join("%.1f" % g for g in gaps[-24:]))
-allg = []
-for a, b in zip(idx[-200:], idx[-199:]):
-    st = rows[a:b]
-    allg.append(sum(max(0, int(st[j]["Start_Timestamp"]) - int(st[j - 1]["End_Timestamp"])) for j in range(1, len(st))) / 1e3)
-print("in-step gaps (excluding the one before the gather): mean %.2f us per step" % np.mean(allg))
