@@ -263,6 +263,18 @@ def parity_leg(prec, batch, seed=2234):
             "posterior_ref": "oracle fp32 (reference algorithm), first training step, B=%d" % batch}
 
 
+def graph_steps(steps):
+    """Steps per multi-step graph replay: the largest divisor of the timed step count in [8, 50]
+    (8 when none), so the timed region is whole replays.  Each replay boundary leaves the GPU idle
+    ≈ 9 µs before the next graph's first launch (profiles/r04_bench_step_timeline.txt); PKC_GRAPH_STEPS
+    overrides."""
+    env = os.environ.get("PKC_GRAPH_STEPS")
+    if env:
+        return int(env)
+    divs = [d for d in range(8, 51) if steps % d == 0]
+    return max(divs) if divs else 8
+
+
 def time_steps(eng, steps, warmup, allreduce=None, world=1):
     eng.train_steps(warmup, allreduce)
     if world > 1:
@@ -374,7 +386,7 @@ def measure_mlp(prec, args, rank, world, allreduce):
                         "@" + {v: k for k, v in PREC_NAMES.items()}[prec])
         print(json.dumps({"pmc_replay": tag, "launches": nl * args.pmc_replay}), flush=True)
         sys.exit(0)
-    eng.capture(split_optimizer=world > 1)
+    eng.capture(split_optimizer=world > 1, steps_per_graph=graph_steps(args.steps))
     graph_lps = eng.graph_launches_per_step
     dt = time_steps(eng, args.steps, args.warmup, allreduce, world)
     loss_sum, err_sum = eng.chunk_totals()
