@@ -315,7 +315,10 @@ def run_nn(data_name, data_set, data_end_index, fea_dict, lab_dict, arch_dict, c
         n_batches = DP.agree_min((r1 - r0) // batch_size, device=eng.dev)
         eng.n_batches = n_batches
         if to_do == "train":
-            eng.capture(split_optimizer=allreduce is not None)
+            # 32-step graph replays when the chunk is long enough: one replay boundary (≈ 9 µs of
+            # GPU idle) per 32 batches instead of per 8 (profiles/r04_graph_steps_ab.txt)
+            eng.capture(split_optimizer=allreduce is not None,
+                        steps_per_graph=32 if n_batches >= 128 else 8)
             eng.train_steps(n_batches, allreduce)
         else:
             for i in range(n_batches):
