@@ -183,7 +183,7 @@ def batch_sweep(prec, batches=(1024, 4096), steps=150):
         eng, _, _, _ = build(prec, b, 0, 1)
         for _ in range(3):
             eng.train_step()
-        eng.capture()
+        eng.capture(steps_per_graph=graph_steps(steps))
         eng.train_steps(16)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
