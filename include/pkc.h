@@ -42,6 +42,9 @@ enum { PKC_OPT_SGD = 0, PKC_OPT_RMSPROP = 1, PKC_OPT_ADAM = 2 };
 
 int pkc_abi_version(void);
 const char* pkc_last_error(void);
+/* SHA-256 (hex) of the csrc/ + include/ sources this library was linked from (generated at build
+ * time; pkc._lib refuses a library whose digest differs from its tree's). */
+const char* pkc_src_digest(void);
 
 /* ---------------------------------------------------------------------------------------------
  * Matmul (replaces the cuBLAS GEMMs behind nn.Linear / F.linear in the reference:

@@ -5,6 +5,7 @@ pytorch-kaldi-cgs_amd/pkc/libpkc.so so it travels with the repository snapshot t
 """
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import re
 import subprocess
@@ -18,6 +19,40 @@ LIB = os.path.join(PKG, "libpkc.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PKC_ARCH", "gfx950")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wno-unused-result"]
+
+
+INCLUDE = os.path.join(os.path.dirname(TOP), "include")
+
+
+def src_digest(csrc=CSRC, include=INCLUDE):
+    """SHA-256 over every file of csrc/ and include/ (relative name + bytes, sorted): embedded in
+    libpkc.so at link time (pkc_src_digest) and recomputed by pkc._lib at load, so the library a
+    process runs is tied to the sources of the tree it runs from."""
+    h = hashlib.sha256()
+    for root in (csrc, include):
+        for f in sorted(os.listdir(root)):
+            p = os.path.join(root, f)
+            if os.path.isfile(p) and not f.startswith("."):
+                h.update(("%s/%s\0" % (os.path.basename(root), f)).encode())
+                with open(p, "rb") as fh:
+                    h.update(fh.read())
+                h.update(b"\0")
+    return h.hexdigest()
+
+
+def _digest_obj(digest):
+    """build/pkc_digest.o: the one symbol carrying the source digest (regenerated when it moves)."""
+    src = os.path.join(BUILD, "pkc_digest.cpp")
+    obj = src + ".o"
+    text = ('extern "C" const char* pkc_src_digest(void) { return "%s"; }\n' % digest)
+    if not (os.path.exists(src) and open(src).read() == text and os.path.exists(obj)):
+        with open(src, "w") as f:
+            f.write(text)
+        r = subprocess.run([HIPCC, "-O2", "-fPIC", "-x", "c++", "-c", src, "-o", obj],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("hipcc failed on %s:\n%s" % (src, r.stderr[-3000:]))
+    return obj
 
 
 def _sources():
@@ -58,8 +93,10 @@ def build(verbose=False):
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(_compile, srcs))
+    digest = src_digest()
+    objs.append(_digest_obj(digest))
     stamp = os.path.join(BUILD, "libpkc.objs")
-    listing = "\n".join(objs)
+    listing = "\n".join(objs + [digest])
     same = os.path.exists(stamp) and open(stamp).read() == listing
     if same and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB

@@ -172,6 +172,27 @@ class PkcError(RuntimeError):
     pass
 
 
+def tree_digest():
+    """The source digest of the tree this package runs from (None when csrc/ is absent, e.g. an
+    installed library used through PKC_LIB without sources)."""
+    from ._build import CSRC, INCLUDE, src_digest
+    if not (os.path.isdir(CSRC) and os.path.isdir(INCLUDE)):
+        return None
+    return src_digest()
+
+
+def check_provenance(L):
+    """Refuse a libpkc.so built from other sources than the tree's csrc/ + include/."""
+    L.pkc_src_digest.restype = C.c_char_p
+    L.pkc_src_digest.argtypes = []
+    built = L.pkc_src_digest().decode()
+    want = tree_digest()
+    if want is not None and built != want:
+        raise PkcError("libpkc.so was built from other sources (digest %s..., tree %s...): "
+                       "rebuild it (__graft_entry__.build())" % (built[:12], want[:12]))
+    return built
+
+
 def lib():
     """Load libpkc.so once; raise (never fall back) if it is not there."""
     global _lib
@@ -186,6 +207,7 @@ def lib():
             f.argtypes = args
         if L.pkc_abi_version() != ABI_VERSION:
             raise PkcError("libpkc ABI mismatch")
+        check_provenance(L)
         _lib = L
     return _lib
 

@@ -993,7 +993,7 @@ class Engine:
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
         self.opt_entries = []
-        self._host_maps, self._seg_keep = {}, []
+        self._host_maps, self._seg_keep = {}, {}
         for n in self.nodes:
             if not self.needs_grad[n] or self.external:
                 continue
@@ -1115,6 +1115,10 @@ class Engine:
         pointers passed in the launch's kernel arguments), or None (PKC_OPT_DIRECT=0)."""
         if not OPT_DIRECT:
             return None
+        key = (cmap.data_ptr(), b, e)
+        segs = self._seg_keep.get(key)
+        if segs is not None:           # step-invariant: built once per (map, range)
+            return segs
         m = self._host_maps[cmap.data_ptr()][b:e]
         runs = []
         for ti, c in m:
@@ -1137,7 +1141,7 @@ class Engine:
             sg.qout = ent["q"].data_ptr() if ent["qbits"] else None
             sg.bout = ent["bout"].data_ptr() if ent.get("bout") is not None else None
             sg.n = ent["p"].numel()
-        self._seg_keep.append(segs)
+        self._seg_keep[key] = segs
         return segs
 
     def _upload_opt_desc(self, step_inc):

@@ -14,9 +14,11 @@ ran at (util counts cycles, TF/s counts nanoseconds at the 2.4 GHz the peak assu
 
 The kernel's cycles: GUI_ACTIVE / 8 counts the whole counter-collection window, which for a
 kernel of a few microseconds is wider than its dispatch (start, end) timestamps — round 3 read
-4.1-5.9 GHz "clocks" off it.  So cycles = ns x min(GUI_ACTIVE / 8 / ns,
-2.4 GHz): the window's clock where the window is the kernel (long kernels), capped at the chip's
-2.4 GHz where it is not; the raw window figure stays in window_clock_ghz.
+4.1-5.9 GHz "clocks" off it.  Where GUI_ACTIVE / 8 / ns exceeds the chip's
+2.4 GHz the window is not the kernel, so the counters do not say how many cycles the kernel had:
+mfma_util_pct is null there (a clamp made it a copy of tflops_pct_of_peak)
+and only the timestamp-based tflops_pct_of_peak is reported.  The raw window figure stays in
+window_clock_ghz.
 Usage: mfma_summary.py <pass dir> [top]"""
 import collections
 import csv
@@ -59,7 +61,7 @@ for k, c in acc.items():
     dt = "bf16" if c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) >= c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) else "f32"
     tf = fl / c["ns"] / 1e3 if c["ns"] else None
     wclk = gui / XCDS / c["ns"] if c["ns"] else None          # GHz over the counter window
-    clk = min(wclk, MAX_CLOCK_GHZ) if wclk else None
+    clk = wclk if (wclk and wclk <= MAX_CLOCK_GHZ) else None     # the window is the kernel
     cycles = c["ns"] * clk if clk else 0.0
     rows.append({"kernel": k[:110], "dispatches": len(seen[k]), "mfma_gflop": round(fl / 1e9, 3),
                  "mfma_dtype": dt, "tflops": round(tf, 1) if tf is not None else None,

@@ -712,3 +712,31 @@ def test_engine_dead_f32_outputs_kept_for_layernorm_consumers(where, monkeypatch
         assert torch.equal(g0[s], g1[s]), "step %d gradients differ" % s
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+def test_engine_eager_adam_segs_bounded():
+    """eager steps (Adam heads: capture() refuses them) rebuild no optimizer segment
+    arrays: the direct-form pkc_opt_seg runs are step-invariant and built once per (map, range)."""
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config()
+    for sec in ("architecture2", "architecture3"):
+        cfg[sec].update(arch_opt="adam", opt_betas="0.9,0.999", opt_eps="1e-8", opt_amsgrad="False")
+    nets, opts = build_nets(cfg, C1_DIMS)
+    for n in nets.values():
+        n.to(DEV).train()
+    B = 128
+    rs = np.random.RandomState(2)
+    X = torch.from_numpy(rs.randn(B * 6, 440).astype(np.float32)).to(DEV)
+    lab = torch.from_numpy(np.stack([rs.randint(0, 1928, B * 6), rs.randint(0, 48, B * 6)], 1)
+                           .astype(np.int32)).to(DEV)
+    eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                 ["lab_cd", "lab_mono"], batch=B, seed=3)
+    eng.bind_chunk(X, lab, B * 6)
+    eng.train_step()
+    n0 = len(eng._seg_keep)
+    for _ in range(5):
+        eng.train_step()
+    torch.cuda.synchronize()
+    assert len(eng._seg_keep) == n0, (n0, len(eng._seg_keep))
+    loss, _ = eng.loss_values()
+    assert np.isfinite(loss)
