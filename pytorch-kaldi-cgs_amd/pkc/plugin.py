@@ -20,9 +20,16 @@ same architecture again before that backward raises (the reference's forward_mod
 architecture once per batch).  Eval mode (``net.eval()``) or ``torch.no_grad()``: forward only,
 BatchNorm with running statistics, recurrent dropout as x(1-p).
 
-Not supported here (raise NotImplementedError, run through pkc.core.run_nn instead): in-place
-input fake-quantisation of the architecture's own input (``*_quant_inp`` on the first layer: the
-reference rewrites the caller's tensor), SyncBN.
+In-place input fake-quantisation of the architecture's own input (``*_quant_inp`` with the first
+layer reading x, QuantizeLinear.forward's ``input.data = Quantize_inp(input.data, ...)``,
+quantized_modules.py:216-217, called by every gate projection of LSTM layer 0,
+neural_networks.py:686-692, 948-951): the chain q1..qQ runs on the GPU (pkc_fakequant_input), each
+gate's projection reads its own version, and the caller's tensor is rebound to the final version
+(``x.data = qQ``) before ``forward`` returns, so later readers of the same tensor object see it,
+as with the reference.  Autograd does not see the rebinding (the reference's is through
+``.data`` too): dL/dx is the plain dX of layer 0.
+
+Not supported here (raise NotImplementedError, run through pkc.core.run_nn instead): SyncBN.
 """
 import torch
 
@@ -58,9 +65,6 @@ class ArchRunner:
         lines = [["out", "compute", ARCH, "x"]]
         e = Engine({ARCH: self.net}, {ARCH: {}}, lines, {"x": (0, K)}, [], prec=L.PREC_FP32,
                    device=dev, seed=getattr(self.net, "pkc_seed", 0), external=True, **kw)
-        if any(n.reads and n.src[0] == "fea" for n in e.nodes):
-            raise NotImplementedError("pkc plug-in forward: input fake-quantisation of the "
-                                      "architecture's own input (use pkc.core.run_nn)")
         if self.eng is not None:
             e.ctr.copy_(self.eng.ctr)      # keep the dropout streams advancing
         # nn.BatchNorm1d counts its training forwards (the kernels update the running statistics)
@@ -105,6 +109,11 @@ class ArchRunner:
         last = e.nodes[-1]
         N = last.N
         y = last.out[:rows * N].view(rows, N).clone()
+        ent = e.qsrc.get(("fea", 0, K))
+        if ent is not None and ent["Q"]:
+            # quantized_modules.py:216-217: the caller's tensor now holds the last in-place version
+            n = rows * K
+            x.data = ent["buf"][(ent["Q"] - 1) * n:ent["Q"] * n].view(x.shape).clone()
         self.gen += 1
         self.pending = self.gen if train else None
         return (y.view(T, B, N) if self.seq else y), e

@@ -157,3 +157,120 @@ def test_plugin_shapes_eval_and_guards():
         y.sum().backward()
     with pytest.raises(ValueError):
         net(x[0].to(DEV))
+
+
+def test_plugin_mlp_pattern_trains_like_reference():
+    """Pattern masks through the plug-in (if_pattern, neural_networks.py:263-272, 339-361): the
+    8x8/k4/n16 pattern_file set on the HCGS body and cd head, the masks computed at the first layer
+    call from the weights and multiplied in once per layer call (pattern^L); 3 steps of the
+    reference loop vs the oracle, posteriors <= 1e-4 relative.  The masks the plug-in computed are
+    the oracle's, element for element."""
+    import os
+
+    from conftest import GOLDEN
+    cfg = build_mlp_config("hcgs")
+    pset = np.load(os.path.join(GOLDEN, "quant.npz"), allow_pickle=False)["pattern_set"].reshape(16, 8, 8)
+    for sec in ("architecture1", "architecture2"):
+        cfg[sec].update(if_pattern="True", pattern_mode="pattern", pattern_shape="8,8",
+                        pattern_nnz="4,4", pattern_num="16,16")
+    F, M = 40, 64
+    nets, onets, opts = _nets(cfg, [("architecture1", F), ("architecture2", None),
+                                    ("architecture3", None)], {})
+    for k in nets:
+        if nets[k].if_pattern:
+            nets[k].pattern_kernels = pset
+            onets[k].pattern_kernels = pset
+    rs = np.random.RandomState(6)
+    batches = []
+    for rows in (M, M, M):
+        x = rs.randn(rows, F).astype(np.float32)
+        lab = np.stack([rs.randint(0, 96, rows), rs.randint(0, 8, rows)], 1).astype(np.float32)
+        batches.append((torch.from_numpy(np.concatenate([x, lab], 1)), 0))
+    _run(cfg, nets, onets, opts, {k: False for k in nets}, {"fmllr": (0, F)},
+         {"lab_cd": F, "lab_mono": F + 1}, batches)
+    for k in ("MLP_layers1", "MLP_layers2"):
+        assert len(nets[k].pattern_mask) == len(onets[k].pattern_masks) > 0
+        for pm, opm in zip(nets[k].pattern_mask, onets[k].pattern_masks):
+            np.testing.assert_array_equal(pm.cpu().numpy(), opm.numpy())
+
+
+def test_plugin_input_quant_rebinds_caller_tensor():
+    """lstm_quant_inp on layer 0: the four gate projections quantise the caller's x in place in
+    turn (quantized_modules.py:216-217), and after net(x) the caller's tensor holds the last
+    version — as the oracle's x after onet(x).  16-bit grid of max|x| / 2^15; the values are the
+    same fp32 sequence on both sides (bit-exact expected, one quantum allowed)."""
+    from test_gpu_configs import build_pair
+    nets, onets, _, _, _ = build_pair("c5", drop="0.0")
+    net, onet = nets["rnn"].to(DEV).train(), onets["rnn"].train()
+    rs = np.random.RandomState(4)
+    x0 = torch.from_numpy((rs.randn(7, 3, 440) * 1.7).astype(np.float32))
+    xg, xc = x0.clone().to(DEV), x0.clone()
+    yg = net(xg)
+    yo = onet(xc)
+    assert not torch.equal(xc, x0)                  # the oracle rewrote its input
+    q = float(x0.abs().max()) / 2 ** 15
+    d = (xg.detach().cpu() - xc).abs().max().item()
+    assert d <= q * 1.0001, "caller tensor vs oracle's in-place version: %.3g (quantum %.3g)" % (d, q)
+    rel = ((yg.detach().cpu() - yo.detach()).abs() / yo.detach().abs().clamp_min(1e-3)).max().item()
+    assert rel < 1e-3, rel
+    yg.sum().backward()                             # the rebinding does not upset autograd
+
+
+def test_plugin_c5_lstm_pattern_quant_trains_like_reference():
+    """BASELINE C5 through the architecture plug-in: LSTM 3x512 + Pattern b08b08_k04_n16 (the
+    pattern_file set) + 8-bit weights + 16-bit input fake-quantisation of the arch's own input
+    (rebinding the caller's x, quantized_modules.py:216-217), heads 1928 cd + 48 mono, B = 12,
+    trained 3 steps by the reference loop (forward_model, NLLLoss, backward, torch.optim RMSprop)
+    vs the oracle on the CPU.  Tolerances as the engine's C5 test (test_gpu_configs.py): the 16-bit
+    grid moves an element by one quantum where a last-bit difference sits in front of a ceil, so
+    posteriors 1e-3 relative and 8-bit weights with a flip-count bound (tests/quantcheck.py)."""
+    from oracle import nets as ON
+    from oracle import run as OR
+    from pkc.engine import torch_optimizer
+    from quantcheck import assert_few_flips, rmsprop_quanta
+    from test_gpu_configs import build_pair
+    nets, onets, opts, model, B = build_pair("c5", drop="0.0")
+    for k in nets:
+        nets[k].to(DEV).train()
+        onets[k].train()
+    F = 440
+    lines = OR.parse_model(model)
+    popt = {k: torch_optimizer(nets[k].parameters(), opts[k]) for k in nets}
+    oopt = {k: ON.make_optimizer(onets[k].parameters(), opts[k]) for k in onets}
+    seq = {"rnn": True, "head": False, "mono": False}
+    rs = np.random.RandomState(8)
+    steps = 3
+    for step, T in enumerate((10, 14, 8)):
+        x = rs.randn(T, B, F).astype(np.float32)
+        lab = np.stack([rs.randint(0, 1928, (T, B)), rs.randint(0, 48, (T, B))], 2).astype(np.float32)
+        inp = torch.from_numpy(np.concatenate([x, lab], 2))
+        outs_p = OR.train_step(lines, nets, popt, seq, {"fea": (0, F)},
+                               {"lab_cd": F, "lab_mono": F + 1}, inp.to(DEV), T, B)
+        outs_o = OR.train_step(lines, onets, oopt, seq, {"fea": (0, F)},
+                               {"lab_cd": F, "lab_mono": F + 1}, inp, T, B)
+        np.testing.assert_allclose(outs_p["loss_final"].item(), outs_o["loss_final"].item(), rtol=1e-4)
+        post, ref = outs_p["o2"].detach().cpu(), outs_o["o2"].detach()
+        rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
+        print("c5 plug-in step %d posterior max rel err %.3g" % (step, rel))
+        assert rel < 1e-3, "step %d posterior rel err %.3g" % (step, rel)
+    sd_o = onets["rnn"].state_dict()
+    flips = {}
+    for pname, v in nets["rnn"].state_dict().items():
+        if pname.endswith("num_batches_tracked"):
+            assert int(v.item()) == int(sd_o[pname].item())
+            continue
+        r = sd_o[pname].double()
+        if pname.endswith("weight") and v.dim() == 2:
+            flips[pname] = assert_few_flips(v.cpu().numpy(), r.numpy(), pname, 2e-3,
+                                            max_quanta=rmsprop_quanta(float(opts["rnn"]["arch_lr"]), steps) + 1)
+            d = (v.cpu().double() - r).norm().item()
+            assert d <= 2e-2 * r.norm().item(), "%s rel err %.3g" % (pname, d / r.norm().item())
+        elif pname.startswith("bn") and pname.endswith(".bias"):
+            md = (v.cpu().double() - r).abs().max().item()      # RMSprop noise-step bound
+            assert md <= 2 * 4.48 * float(opts["rnn"]["arch_lr"]) * steps, (pname, md)
+        else:
+            d = (v.cpu().double() - r).norm().item()
+            assert d <= 2e-2 * r.norm().item() + 1e-6, (pname, d)
+    for k in nets["rnn"].pattern_mask:
+        assert len(nets["rnn"].pattern_mask[k]) == 3
+    print("c5 plug-in 8-bit grid flips", flips)
