@@ -116,6 +116,11 @@ typedef struct pkc_bn_bwd_epi_s {
 } pkc_bn_bwd_epi;
 int pkc_gemm_bnbwd_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K, const void* A,
                       int64_t lda, const void* B, int64_t ldb);
+/* Tile edge (128: the 128x128 body, else 64) a GEMM problem of pkc_gemm_grouped takes, so a
+ * host can size the launch's split-K over the tiles it will really have. */
+int pkc_gemm_grouped_tile(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                          const void* A, int64_t lda, const void* B, int64_t ldb);
+
 /* Large-batch forward matmul of a BatchNorm'd layer (neural_networks.py:306-311: BN(wx(x)) over
  * the batch) with the BatchNorm column statistics in the matmul's epilogue: one slab
  * C = A B^T (as pkc_gemm, splits = 1) and, per row block b of C, the block's column mean of

@@ -774,3 +774,40 @@ def use_bf16_rec_matmuls(net, steps=False):
                 assert lin.bias is None
                 lin.forward = (lambda x, _l=lin: _BF16dWLinear.apply(x, _l.weight))
     return net
+
+
+def _x3mm(a, b):
+    """Compensated bf16 product (pkc_gemm PKC_PREC_BF16X3): each fp32 operand split into a bf16
+    head hi = bf16(v) and tail lo = bf16(v - hi) (v - hi is exact in fp32), product
+    hi*hi + hi*lo + lo*hi (lo*lo dropped); the bf16 partial products are exact, summed here in
+    fp64 and rounded once to fp32 (the GPU sums them in fp32 in its own order).  Test restatement
+    of pkc's arithmetic, not a reference function (the reference's products are fp32)."""
+    ah, bh = _bf16(a), _bf16(b)
+    al, bl = _bf16(a - ah), _bf16(b - bh)
+    ah, bh, al, bl = ah.double(), bh.double(), al.double(), bl.double()
+    return (ah @ bh + ah @ bl + al @ bh).float()
+
+
+class _BF16X3Linear(torch.autograd.Function):
+    """F.linear with all three products of the layer's training step (Y = X W^T + b, dX = dY W,
+    dW = dY^T X) in pkc's compensated bf16 (_x3mm)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        y = _x3mm(x, w.t())
+        return y + b if b is not None else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        return (_x3mm(dy, w), _x3mm(dy.t(), x),
+                dy.sum(0) if ctx.has_b else None)
+
+
+def use_bf16x3_matmuls(net):
+    """Route every nn.Linear of an oracle MLP through _BF16X3Linear."""
+    for lin in net.wx:
+        lin.forward = (lambda x, _l=lin: _BF16X3Linear.apply(x, _l.weight, _l.bias))
+    return net

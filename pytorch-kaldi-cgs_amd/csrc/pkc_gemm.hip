@@ -1034,6 +1034,15 @@ extern "C" int pkc_gemm_bnbwd_ok(int prec, int a_kcontig, int b_kcontig, int M, 
                                         BIG_MIN_TILES_GROUPED, BIG_MIN_K_GROUPED) ? 128 : 0;
 }
 
+// Tile edge a GEMM problem of pkc_gemm_grouped runs on: 128 (the 128x128 body) or 64
+extern "C" int pkc_gemm_grouped_tile(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,
+                                     const void* A, int64_t lda, const void* B, int64_t ldb) {
+  using namespace pkc;
+  if (M <= 0 || N <= 0 || K <= 0 || lda <= 0 || ldb <= 0) return 64;
+  return big_enabled() && big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb,
+                                        BIG_MIN_TILES_GROUPED, BIG_MIN_K_GROUPED) ? 128 : 64;
+}
+
 // rows per partial block pkc_gemm_colstats writes for this shape: 128 (the 128x128 tile body),
 // 64 (the 64x64 body, 16-byte operand paths), 0 (not taken)
 extern "C" int pkc_gemm_colstats_ok(int prec, int a_kcontig, int b_kcontig, int M, int N, int K,

@@ -98,6 +98,7 @@ __device__ __forceinline__ float drop_val(const pkc_rnn_args& a, int r, int j, i
 // quotient is dropped by the fabsf either way); any other var takes the IEEE division.
 struct QParams {
   float var, rcp, scale, iscale;
+  float var_s, rcp_s;     // var * 2^-(b-1) and RN(1/var) * 2^(b-1) (exact power-of-two scalings)
   bool fast;
 };
 __device__ __forceinline__ QParams qparams(float var, float scale) {
@@ -106,21 +107,29 @@ __device__ __forceinline__ QParams qparams(float var, float scale) {
   p.rcp = var != 0.f ? 1.f / var : 0.f;
   p.scale = scale;
   p.iscale = 1.f / scale;
+  p.var_s = var * p.iscale;
+  p.rcp_s = p.rcp * scale;
   p.fast = var >= 0x1p-80f && var <= 1.f;
   return p;
 }
+// FAST (6 VALU): the quotient is formed against the scaled divisor var_s = var 2^-(b-1), so
+// RN(x / var_s) = 2^(b-1) RN(x / var) (a power-of-two scaling commutes with RN: x / var <= 1, and
+// for |x| >= 2^-149 with var <= 1 a subnormal RN(x / var) still has ceil = 1 either way), one
+// Markstein fma pair against rcp_s = RN(1 / var_s), ceil, then k * var_s = RN(k 2^-(b-1) var), the
+// reference's one rounding of (k / 2^(b-1)) * var, and the sign copied from x (sign(x) * m for
+// x != 0; a zero stays a zero).  Bit-identical to the IEEE form below in the FAST range.
 template <bool FAST>
 __device__ __forceinline__ float qin(float x, const QParams& p) {
-  float q;
   if constexpr (FAST) {
-    q = x * p.rcp;
-    const float e = __builtin_fmaf(-q, p.var, x);
-    q = __builtin_fmaf(e, p.rcp, q);
+    float q = x * p.rcp_s;
+    const float e = __builtin_fmaf(-q, p.var_s, x);
+    q = __builtin_fmaf(e, p.rcp_s, q);
+    return copysignf(ceilf(fabsf(q)) * p.var_s, x);
   } else {
-    q = x / p.var;
+    const float q = x / p.var;
+    const float s = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+    return ceilf(fabsf(q) * p.scale) * p.iscale * p.var * s;
   }
-  const float s = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
-  return ceilf(fabsf(q) * p.scale) * p.iscale * p.var * s;
 }
 
 // R16: the tile's second row strip is all zeros (Q(0) = 0): only va is quantised

@@ -136,6 +136,8 @@ _SIGS = {
                                     i64, vp, i64, vp, vp, vp]),
     "pkc_dense_bwd": (C.c_int, [C.POINTER(DenseBwdArgs), vp, vp]),
     "pkc_dense_bwd_pre": (C.c_int, [C.POINTER(DenseBwdArgs), vp, C.c_int, vp]),
+    "pkc_gemm_grouped_tile": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp,
+                                        i64, vp, i64]),
     "pkc_gemm_bnbwd_ok": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64,
                                     vp, i64]),
     "pkc_dense_work_size": (i64, [C.c_int, C.c_int]),

@@ -94,6 +94,10 @@ BN_BWD_EPI = os.environ.get("PKC_BN_BWD_EPI", "0") != "0"
 COLSTATS = os.environ.get("PKC_GEMM_COLSTATS", "1") != "0"
 # recurrent layers' dW / dU split-K cap (1: unsplit, A/B)
 REC_DW_SPLITS = int(os.environ.get("PKC_REC_DW_SPLITS", "4"))
+# bf16 step mode: the recurrent weight gradients on bf16 operand copies (BF16IN; 0: fp32 staged)
+REC_WGRAD_BF16 = os.environ.get("PKC_REC_WGRAD_BF16", "1") != "0"
+# workgroups a layer's grouped weight-gradient launch aims at before it splits the contraction
+REC_WG_TARGET = int(os.environ.get("PKC_REC_WG_TARGET", "512"))
 # recurrent layers: sum the output-gradient slabs before the BPTT loop (0: per step, A/B)
 REC_DY_PRESUM = os.environ.get("PKC_REC_DY_PRESUM", "1") != "0"
 
@@ -878,6 +882,9 @@ class Engine:
                           U_h=torch.zeros(G * H * H, dtype=bf, device=dev),
                           ut_h=torch.zeros(G * H * H, dtype=bf, device=dev),
                           dgates_h=torch.zeros(G * T * B2 * H, dtype=bf, device=dev))
+                if REC_WGRAD_BF16:            # bf16 operand copies of the weight gradients
+                    lb.update(dz_h=torch.zeros(G * M * H, dtype=bf, device=dev),
+                              xw_h=torch.zeros(M * K, dtype=bf, device=dev))
             if sp["ibits"]:
                 lb["hq"] = _f32((T + 1) * B2 * H, dev)      # q4(h_{t-1}) per step
                 if n.lbuf:                                   # layers >= 1: q1..qG of y_{l-1}
@@ -887,15 +894,14 @@ class Engine:
                 for g in range(G):
                     for p in (sp["W"][g], sp["U"][g]):
                         n.qw[id(p)] = (torch.zeros_like(p), sp["qbits"])
-            # split-K of the weight gradients dW = dz^T x (H x K over the T*B rows) and dU (H x H
-            # over the T*2B rows): their 64x64 tiles alone leave most CUs idle (C3: 81 tiles of
-            # dU), so the contraction is split into slabs that a slab-sum launch adds up
-            lb["sw"] = _splits(H, K, M, REC_DW_SPLITS)
-            lb["su"] = _splits(H, H, T * B2, REC_DW_SPLITS)
             n.lbuf.append(lb)
             K = D
-        need = max(max(lb["sw"] * lb["H"] * lb["K"] if lb["sw"] > 1 else 0,
-                       lb["su"] * lb["H"] * lb["H"] if lb["su"] > 1 else 0) for lb in n.lbuf)
+        # split-K slabs of the weight gradients dW = dz^T x (H x K over the T*B rows) and dU (H x H
+        # over the T*B2 rows): every gate's dW and dU of a layer run in ONE grouped launch, split
+        # over the contraction only when that launch has too few tiles to fill the chip
+        # (_rec_wgrads); room for every problem's slabs at the cap
+        need = (max(n.G * REC_DW_SPLITS * (lb["H"] * lb["K"] + lb["H"] * lb["H"]) for lb in n.lbuf)
+                if REC_DW_SPLITS > 1 else 0)
         n.rslab = _f32(need, dev) if need else None
         # dL/dy of a layer summed over its producers' slabs once, before the serial BPTT loop
         # (whose per-step epilogue would otherwise read every slab at every step)
@@ -1919,7 +1925,12 @@ class Engine:
                     4.0 * T * n.G * H * H, "pkc_rnn_bwd", C.byref(ra), ptr(lb["dpre"]), s)
             _, (x_ptr, ldx) = self._rec_inputs(n, li)
             hsrc = lb["hq"] if sp["ibits"] else lb["hs"]
-            nx = 0
+            # bf16 step mode: the weight gradients read bf16 operand copies (BF16IN: half the
+            # bytes each CU ingests) — dz_g written by the BatchNorm backward, dgates / h_{t-1}
+            # by the bf16 step kernels, the layer input cast once here
+            wbf = (bool(ra.step_bf16) and lb.get("dz_h") is not None and ldx == K
+                   and n.cand is None)
+            dzs = []
             for g in range(n.G):
                 bn = sp["bnm"][g]
                 a = L.DenseBwdArgs(M=M, N=H, nslab=1, gslab=lb["dpre"].data_ptr() + 4 * g * M * H,
@@ -1931,46 +1942,44 @@ class Engine:
                                    dz=lb["dz"].data_ptr() + 4 * g * M * H,
                                    dgamma=lb["dgamma"][g].data_ptr() if sp["bn"] else None,
                                    dbeta=lb["dbeta"][g].data_ptr() if sp["bn"] else None,
-                                   dbias=lb["db"][g].data_ptr() if lb["db"][g] is not None else None)
+                                   dbias=lb["db"][g].data_ptr() if lb["db"][g] is not None else None,
+                                   dz_bf16=lb["dz_h"].data_ptr() + 2 * g * M * H if wbf else None)
                 self._k("rnn_bn_bwd H=%d" % H, 0, 4.0 * M * H * 4, "pkc_dense_bwd", C.byref(a),
                         ptr(lb["work"]), s)
-                dz = C.c_void_p(lb["dz"].data_ptr() + 4 * g * M * H)
-                sw, su = lb["sw"], lb["su"]
-                self._k("rnn_gemm_dW %dx%dx%d%s" % (H, K, M, " s%d" % sw if sw > 1 else ""),
-                        2.0 * M * H * K, 4.0 * (M * H + M * K + sw * H * K), "pkc_gemm", self.prec,
-                        0, 0, H, K, M, dz, H, C.c_void_p(x_ptr), ldx,
-                        ptr(n.rslab if sw > 1 else lb["dW"][g]), K, sw, H * K if sw > 1 else 0, s)
-                if sw > 1:
-                    self._rec_slab_sum(n.rslab, sw, H * K, lb["dW"][g], s)
-                # dU = sum_t dgates[t]^T h_{t-1}: K = T*B2 rows of hs[0:T] (GRU Uh: r*h_{t-1})
-                R2 = T * lb["B2"]
-                usrc = lb["rh"] if g == n.cand else hsrc
-                self._k("rnn_gemm_dU %dx%dx%d%s" % (H, H, R2, " s%d" % su if su > 1 else ""),
-                        2.0 * R2 * H * H, 4.0 * (2 * R2 * H + su * H * H), "pkc_gemm", self.prec,
-                        0, 0, H, H, R2,
-                        C.c_void_p(lb["dgates"].data_ptr() + 4 * g * T * lb["B2"] * H), H,
-                        ptr(usrc), H, ptr(n.rslab if su > 1 else lb["dU"][g]), H, su,
-                        H * H if su > 1 else 0, s)
-                if su > 1:
-                    self._rec_slab_sum(n.rslab, su, H * H, lb["dU"][g], s)
-                if li > 0 or want_dx0:
+                dzs.append(lb["dz"].data_ptr() + 4 * g * M * H)
+            h16 = None
+            if wbf:
+                self._k("rnn_cast_x_bf16 %dx%d" % (M, K), 0, 6.0 * M * K, "pkc_cast_bf16",
+                        C.c_void_p(x_ptr), ptr(lb["xw_h"]), M * K, s)
+                h16 = ([lb["dz_h"].data_ptr() + 2 * g * M * H for g in range(n.G)],
+                       lb["xw_h"].data_ptr(), lb["hs_h"].data_ptr(), lb["dgates_h"].data_ptr())
+            sums = self._rec_wgrads(n, lb, dzs, x_ptr, ldx, hsrc, s, h16)
+            # dX = sum_g dz_g W_g (one slab group per gate) in one grouped launch, with the weight
+            # gradients' slab sums riding along
+            dxp, nx = [], 0
+            if li > 0 or want_dx0:
+                for g in range(n.G):
+                    dz = dzs[g]
                     kt = self._wt(sp["W"][g], True)
                     if kt is not None:        # block-sparse W^T: one slab per gate
                         sx = 1
                         pr = L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=K, K=H, splits=1,
-                                           A=dz.value, lda=H, B=n.wq(li, "W", g).data_ptr(), ldb=K,
+                                           A=dz, lda=H, B=n.wq(li, "W", g).data_ptr(), ldb=K,
                                            C=lb["dx"].data_ptr() + 4 * nx * M * K, ldc=K,
                                            slab_stride=M * K, ktiles=kt[0].data_ptr(), kmax=kt[1])
-                        self._k("rnn_gemm_dX %dx%dx%d sparse %.2f" % (M, K, H, kt[2]),
-                                2.0 * M * H * K * kt[2], 4.0 * (M * H + H * K * kt[2] + M * K),
-                                "pkc_gemm_grouped", self.prec, C.byref(pr), 1, s)
+                        dxp.append(("dX%d %dx%dx%d sparse %.2f" % (g, M, K, H, kt[2]),
+                                    2.0 * M * H * K * kt[2], 4.0 * (M * H + H * K * kt[2] + M * K), pr))
                     else:
                         sx = _splits(M, K, H, MAX_SPLITS)
-                        self._k("rnn_gemm_dX %dx%dx%d" % (M, K, H), 2.0 * M * H * K,
-                                4.0 * (M * H + H * K + sx * M * K), "pkc_gemm", self.prec, 1, 0, M,
-                                K, H, dz, H, ptr(n.wq(li, "W", g)), K,
-                                C.c_void_p(lb["dx"].data_ptr() + 4 * nx * M * K), K, sx, M * K, s)
+                        pr = L.GemmProblem(a_kcontig=1, b_kcontig=0, M=M, N=K, K=H, splits=sx,
+                                           A=dz, lda=H, B=n.wq(li, "W", g).data_ptr(), ldb=K,
+                                           C=lb["dx"].data_ptr() + 4 * nx * M * K, ldc=K,
+                                           slab_stride=M * K)
+                        dxp.append(("dX%d %dx%dx%d" % (g, M, K, H), 2.0 * M * H * K,
+                                    4.0 * (M * H + H * K + sx * M * K), pr))
                     nx += sx
+            if dxp or sums:
+                self._gemms(dxp + sums, s)
             if on_layer is not None:
                 on_layer(li)
             dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
@@ -1978,6 +1987,58 @@ class Engine:
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
             elif li == 0 and self.want_dx:           # external mode: dL/dx of the caller's input
                 self._rec_slab_sum_ptr(lb["dx"].data_ptr(), nx, M * K, M * K, self.ext_dx, s)
+
+    def _rec_wgrads(self, n, lb, dzs, x_ptr, ldx, hsrc, s, h16=None):
+        """Every gate's dW_g = dz_g^T x (H x K over the M rows) and dU_g = dgates_g^T h_{t-1} (H x H
+        over the T*B2 rows; GRU-type candidates: (r|z)*h_{t-1}) of one layer in ONE grouped launch.
+        Both operands are m-contiguous; with bf16 products the launch's problems take the 128x128
+        body (pkc_gemm_grouped_tile), whose tiles halve the bytes each CU ingests per flop against
+        the 64x64 body.  The contraction is split (slabs into n.rslab) only when the launch has fewer
+        than REC_WG_TARGET workgroups; returns the slab-sum operations for the next launch.
+        h16: (dz_g copies, x copy, h copy, dgates copy) bf16 operand pointers (BF16IN form)."""
+        H, K, M, T = lb["H"], lb["K"], self.M, self.T
+        R2 = T * lb["B2"]
+        lib = L.lib()
+        probs = []
+        for g in range(n.G):
+            usrc = lb["rh"] if g == n.cand else hsrc
+            hw = hu = None
+            if h16 is not None:
+                hw = (h16[0][g], H, h16[1], K)
+                hu = (h16[3] + 2 * g * R2 * H, H, h16[2], H)
+            probs.append(("dW%d" % g, H, K, M, dzs[g], H, x_ptr, ldx, lb["dW"][g], hw))
+            probs.append(("dU%d" % g, H, H, R2, lb["dgates"].data_ptr() + 4 * g * R2 * H, H,
+                          usrc.data_ptr(), H, lb["dU"][g], hu))
+        prec = L.PREC_BF16IN if h16 is not None else self.prec
+        tiles = 0
+        for (_, Mq, Nq, Kq, A, lda, B, ldb, _, hq) in probs:
+            if hq is not None:
+                A, lda, B, ldb = hq
+            te = lib.pkc_gemm_grouped_tile(prec, 0, 0, Mq, Nq, Kq, C.c_void_p(A), lda,
+                                           C.c_void_p(B), ldb)
+            tiles += -(-Mq // te) * -(-Nq // te)
+        split = max(1, min(REC_DW_SPLITS, -(-REC_WG_TARGET // max(1, tiles))))
+        gem, sums, off = [], [], 0
+        for (lab, Mq, Nq, Kq, A, lda, B, ldb, out, hq) in probs:
+            ss = max(1, min(split, Kq // 256))           # >= 256 rows of contraction per slab
+            dst = n.rslab.data_ptr() + 4 * off if ss > 1 else out.data_ptr()
+            pr = L.GemmProblem(a_kcontig=0, b_kcontig=0, M=Mq, N=Nq, K=Kq, splits=ss, A=A,
+                               lda=lda, B=B, ldb=ldb, C=dst, ldc=Nq,
+                               slab_stride=Mq * Nq if ss > 1 else 0)
+            q = ("%s %dx%dx%d%s" % (lab, Mq, Nq, Kq, " s%d" % ss if ss > 1 else ""),
+                 2.0 * Mq * Nq * Kq, 4.0 * (Mq * Kq + Nq * Kq + ss * Mq * Nq), pr)
+            if hq is not None:
+                ph = L.GemmProblem.from_buffer_copy(pr)
+                ph.A, ph.lda, ph.B, ph.ldb = hq
+                q = q + ((2.0 * (Mq * Kq + Nq * Kq) + 4.0 * ss * Mq * Nq, ph),)
+            gem.append(q)
+            if ss > 1:
+                sums.append(("rnn slab-sum %s x%d" % (lab, ss), 0.0, 4.0 * Mq * Nq * (ss + 1),
+                             L.GemmProblem(kind=L.OP_SLABSUM, M=ss, N=Mq * Nq, A=dst,
+                                           C=out.data_ptr(), slab_stride=Mq * Nq)))
+                off += ss * Mq * Nq
+        self._gemms(gem, s)
+        return sums
 
     def _rec_slab_sum(self, slab, ns, numel, out, s):
         """out = sum of ns split-K slabs of a recurrent weight gradient (one grouped launch)."""

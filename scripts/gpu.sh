@@ -23,6 +23,10 @@
 #   ab          same-run A/B of one environment knob: AB_VAR over AB_VALUES (space-separated), two
 #               alternating rounds of `python AB_CMD` (e.g. "bench.py --batch 4096 ...")
 #                                                             -> gpurun_out/ab.txt
+#   some        pytest of the files / node ids in PYTEST_SEL (space-separated) -> gpurun_out/pytest_some.log
+#   treeab      same-box A/B of this tree against the tree in AB_TREE (a built worktree, default
+#               _bis_r4): scripts/bench_seq.py $PKC_ARGS in each, two alternating rounds
+#                                                             -> gpurun_out/treeab.txt
 #   round       tests smoke bench bench_prof pmc
 #
 # Extra arguments for a recipe's python command: PKC_ARGS="..." (bench, seq, kprof).
@@ -44,6 +48,25 @@ r_tests() {
   local rc=$?
   grep -E "passed|failed|^FAILED|^ERROR" gpurun_out/pytest_gpu.log | tail -15
   ok $rc tests
+}
+
+r_some() {
+  timeout -k 10 900 python -u -m pytest $PYTEST_SEL -m gpu -v -x --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/pytest_some.log 2>&1
+  local rc=$?
+  grep -E "passed|failed|^FAILED|^ERROR" gpurun_out/pytest_some.log | tail -15
+  ok $rc some
+}
+
+r_treeab() {
+  local other=${AB_TREE:-_bis_r4}
+  : > gpurun_out/treeab.txt
+  for i in 1 2; do for t in . "$other"; do
+    (cd "$t" && timeout -k 10 300 python -u scripts/bench_seq.py $A) > gpurun_out/treeab_run.log 2>&1
+    ok $? "treeab $t"
+    grep -E '^\{' gpurun_out/treeab_run.log | sed "s|^|tree=$t  |" | cut -c1-600 >> gpurun_out/treeab.txt
+  done; done
+  cat gpurun_out/treeab.txt
 }
 
 r_smoke() {

@@ -211,8 +211,9 @@ def test_plugin_input_quant_rebinds_caller_tensor():
     q = float(x0.abs().max()) / 2 ** 15
     d = (xg.detach().cpu() - xc).abs().max().item()
     assert d <= q * 1.0001, "caller tensor vs oracle's in-place version: %.3g (quantum %.3g)" % (d, q)
-    rel = ((yg.detach().cpu() - yo.detach()).abs() / yo.detach().abs().clamp_min(1e-3)).max().item()
-    assert rel < 1e-3, rel
+    # (h near 0 after a one-quantum move of an input element: compare against the output scale)
+    err = (yg.detach().cpu() - yo.detach()).abs().max().item() / yo.detach().abs().max().item()
+    assert err < 1e-4, err
     yg.sum().backward()                             # the rebinding does not upset autograd
 
 
