@@ -648,7 +648,7 @@ __global__ __launch_bounds__(big::NT) void gemm_big_kernel(int M, int N, int K,
                                                           int kchunk, int64_t slab_stride,
                                                           int remap, const float* __restrict__ bias,
                                                           float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) char lds[big::LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[big::lds_bytes<PREC>()];
   int bx, by, bz;
   xcd_tile(remap, bx, by, bz);
   big::body<PREC, BIN, AKC, BKC, STATS>(lds, bx, by, bz, M, N, K, A, lda, B, ldb, C, ldc, kchunk,
@@ -686,7 +686,7 @@ __device__ __forceinline__ void grouped_body(const GroupArgs& g) {
   // BIG: at least one problem takes the 128x128 body; its LDS also holds the 64x64 tiles
   union alignas(16) Shm {
     Lds<PREC> t;
-    char big[BIG ? big::LDS_BYTES : 16];
+    char big[BIG ? big::lds_bytes<PREC>() : 16];
   };
   __shared__ Shm shm;
   Lds<PREC>& sm = shm.t;
@@ -1005,6 +1005,9 @@ extern "C" int pkc_gemm(int prec, int a_kcontig, int b_kcontig, int M, int N, in
     if (prec == PKC_PREC_BF16IN)
       return launch_big<PKC_PREC_BF16, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
                                              splits, slab_stride, S(stream));
+    if (prec == PKC_PREC_BF16X3)
+      return launch_big<PKC_PREC_BF16X3, false>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
+                                                ldc, splits, slab_stride, S(stream));
     return launch_big<PKC_PREC_BF16, false>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C, ldc,
                                             splits, slab_stride, S(stream));
   }
@@ -1098,6 +1101,9 @@ extern "C" int pkc_gemm_colstats(int prec, int a_kcontig, int b_kcontig, int M, 
   if (prec == PKC_PREC_BF16IN)
     return launch_big<PKC_PREC_BF16, true, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
                                                  ldc, 1, 0, S(stream), bias, part);
+  if (prec == PKC_PREC_BF16X3)
+    return launch_big<PKC_PREC_BF16X3, false, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb,
+                                                    C, ldc, 1, 0, S(stream), bias, part);
   return launch_big<PKC_PREC_BF16, false, true>(a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb, C,
                                                 ldc, 1, 0, S(stream), bias, part);
 }
@@ -1269,7 +1275,9 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
   } while (0)
   if (prec == PKC_PREC_FP32) PKC_GL(PKC_PREC_FP32, false);
   else if (prec == PKC_PREC_BF16IN) PKC_GL(PKC_PREC_BF16, true);
-  else if (prec == PKC_PREC_BF16X3) {     // no 128x128 body: its slab sums ride the 64x64 instance
+  else if (prec == PKC_PREC_BF16X3) {
+    // the 128x128 instances (128 KB of LDS for the head and tail images) only where a problem
+    // takes that body; its slab sums ride the 64x64 instance otherwise
     constexpr int P = PKC_PREC_BF16X3;
     if (any_sparse && any_sum)
       hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false, true, true>), dim3(wg), dim3(NT), 0,
@@ -1277,6 +1285,11 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     else if (any_sparse)
       hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false, true>), dim3(wg), dim3(NT), 0,
                          S(stream), g);
+    else if (any_big && any_sum)
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, false, true, false, true>), dim3(wg), dim3(NT), 0,
+                         S(stream), g);
+    else if (any_big)
+      hipLaunchKernelGGL((gemm_grouped_kernel<P, false, true>), dim3(wg), dim3(NT), 0, S(stream), g);
     else if (any_sum)
       hipLaunchKernelGGL((gemm_grouped_kernel<P, false, false, false, true>), dim3(wg), dim3(NT), 0,
                          S(stream), g);

@@ -33,6 +33,14 @@ constexpr int TM = 128, TN = 128, NT = 256;
 constexpr int ROWB = 128;                       // bytes of k per LDS row
 constexpr int TILE_BYTES = TM * ROWB;           // one operand tile in LDS (16 KB)
 constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;   // A and B, double-buffered (64 KB)
+// PKC_PREC_BF16X3 (compensated bf16) stages every fp32 operand tile as TWO bf16 images, the head
+// hi = bf16(v) and the tail lo = bf16(v - hi): a buffer is [A hi][B hi][A lo][B lo] (64 KB), two
+// buffers 128 KB (one workgroup per CU)
+template <int PREC>
+constexpr int buf_bytes() { return (PREC == PKC_PREC_BF16X3 ? 4 : 2) * TILE_BYTES; }
+template <int PREC>
+constexpr int lds_bytes() { return 2 * buf_bytes<PREC>(); }
+constexpr int LO_OFF = 2 * TILE_BYTES;          // the tail image of an operand, after both heads
 
 __device__ __forceinline__ int swz(int r) { return ((r >> 1) ^ (r >> 4)) & 7; }
 
@@ -76,6 +84,12 @@ struct Cfg<PKC_PREC_BF16, false> {
   static constexpr int BK = 64;
 };
 template <>
+struct Cfg<PKC_PREC_BF16X3, false> {
+  using HE = float;
+  using LE = __bf16;
+  static constexpr int BK = 64;
+};
+template <>
 struct Cfg<PKC_PREC_BF16, true> {
   using HE = __bf16;
   using LE = __bf16;
@@ -97,6 +111,7 @@ struct Stage {
   // (PAIR): two k-adjacent chunks packed into dwords and stored transposed
   static constexpr bool TR = !KC && sizeof(HE) == 2 && sizeof(LE) == 2;
   static constexpr bool PAIR = !KC && sizeof(LE) == 2 && !TR;
+  static constexpr bool X3 = PREC == PKC_PREC_BF16X3;   // also the tail image at + LO_OFF
   float4 v[NCH];
 
   // chunk i of this thread -> (row, k) of its first element
@@ -183,6 +198,10 @@ struct Stage {
   __device__ __forceinline__ static uint32_t bf16bits(float f) {
     return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f);
   }
+  // the tail of the compensated split: v - hi is exact in fp32, rounded once to bf16
+  __device__ __forceinline__ static uint32_t lobits(float f) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)(f - (float)(__bf16)f));
+  }
 
   __device__ __forceinline__ void store(char* __restrict__ s) const {
 #pragma unroll
@@ -199,6 +218,12 @@ struct Stage {
           h.x = bf16bits(v[i].x) | (bf16bits(v[i].y) << 16);
           h.y = bf16bits(v[i].z) | (bf16bits(v[i].w) << 16);
           *reinterpret_cast<uint2*>(dst) = h;
+          if constexpr (X3) {
+            uint2 l;
+            l.x = lobits(v[i].x) | (lobits(v[i].y) << 16);
+            l.y = lobits(v[i].z) | (lobits(v[i].w) << 16);
+            *reinterpret_cast<uint2*>(dst + LO_OFF) = l;
+          }
         }
       } else if (TR) {
         *reinterpret_cast<float4*>(s + tr_off(k, r >> 3)) = v[i];
@@ -216,7 +241,11 @@ struct Stage {
             p = bf16bits(fl(v[i], j)) | (bf16bits(fl(v[i + 1], j)) << 16);
           }
           const int rj = r + j;
-          *reinterpret_cast<uint32_t*>(s + rj * ROWB + 16 * ((kb >> 4) ^ swz(rj)) + co) = p;
+          char* dst = s + rj * ROWB + 16 * ((kb >> 4) ^ swz(rj)) + co;
+          *reinterpret_cast<uint32_t*>(dst) = p;
+          if constexpr (X3)
+            *reinterpret_cast<uint32_t*>(dst + LO_OFF) =
+                lobits(fl(v[i], j)) | (lobits(fl(v[i + 1], j)) << 16);
         }
       } else {                                                 // fp32 m-contiguous
         const int kb = k * 4;
@@ -264,6 +293,35 @@ __device__ __forceinline__ void tile_mfma(const char* __restrict__ sa, const cha
         for (int kk = 0; kk < 16; ++kk)
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc[a][b], 0, 0, 0);
       }
+    }
+  } else if constexpr (PREC == PKC_PREC_BF16X3) {
+    // compensated products: the tails' cross terms first, then the heads' product (lo*lo, 2^-16
+    // relative, dropped); the images are row-major ([row][128 B] swizzled), A/B tails at + LO_OFF
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const float4 x = lds16(sa, wm * 64 + 32 * a + r, 2 * t + h);
+        const float4 xl = lds16(sa + LO_OFF, wm * 64 + 32 * a + r, 2 * t + h);
+        ah[a] = *reinterpret_cast<const bf16x8*>(&x);
+        al[a] = *reinterpret_cast<const bf16x8*>(&xl);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float4 y = lds16(sb, wn * 64 + 32 * b + r, 2 * t + h);
+        const float4 yl = lds16(sb + LO_OFF, wn * 64 + 32 * b + r, 2 * t + h);
+        bh[b] = *reinterpret_cast<const bf16x8*>(&y);
+        bl[b] = *reinterpret_cast<const bf16x8*>(&yl);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+        }
     }
   } else {
 #pragma unroll
@@ -432,7 +490,7 @@ __device__ __forceinline__ void tile_store(const f32x16 (&acc)[2][2], int m0, in
 }
 
 // C[bz slab][m0.., n0..] = A[m0.., kbeg..kend) . B[n0.., kbeg..kend)^T for one 128x128 tile.
-// `lds` is LDS_BYTES of workgroup memory.  STATS: also the tile's column statistics
+// `lds` is lds_bytes<PREC>() of workgroup memory.  STATS: also the tile's column statistics
 // (tile_colstats; one slab, kchunk >= K).
 // BNB: the BatchNorm-backward epilogue (tile_bnbwd with *bnb) before the store
 template <int PREC, bool BIN, bool AKC, bool BKC, bool STATS = false, bool BNB = false>
@@ -488,8 +546,8 @@ __device__ __forceinline__ void body(char* __restrict__ lds, int bx, int by, int
     }
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
-      char* cur = lds + (t & 1) * 2 * TILE_BYTES;
-      char* nxt = lds + ((t + 1) & 1) * 2 * TILE_BYTES;
+      char* cur = lds + (t & 1) * buf_bytes<PREC>();
+      char* nxt = lds + ((t + 1) & 1) * buf_bytes<PREC>();
       tile_mfma<PREC, Stage<PREC, BIN, AKC>::TR, Stage<PREC, BIN, BKC>::TR>(cur, cur + TILE_BYTES,
                                                                          wm, wn, lane, acc);
       if (t + 1 < nk) {                               // uniform
@@ -644,7 +702,6 @@ __device__ __forceinline__ void body_glds(char* __restrict__ lds, int bx, int by
 __host__ inline bool eligible(int prec, int akc, int bkc, int M, int N, int K, const void* A,
                               int64_t lda, const void* B, int64_t ldb, int min_tiles,
                               int min_k = 128) {
-  if (prec == PKC_PREC_BF16X3) return false;        // the compensated form: 64x64 bodies only
   const int e = prec == PKC_PREC_BF16IN ? 8 : 4;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 &&
                    ldb % e == 0 && (akc ? K % e == 0 : M % e == 0) && (bkc ? K % e == 0 : N % e == 0);

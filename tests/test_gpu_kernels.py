@@ -65,6 +65,44 @@ def test_gemm(L, prec, M, N, K, orient):
         assert e3 < 0.05 * eb, (e3, eb)
 
 
+@pytest.mark.parametrize("orient", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("M,N,K,grouped,splits", [(2048, 1280, 1024, False, 1),
+                                                  (2048, 1280, 2048, False, 2),
+                                                  (1000, 700, 1100, True, 1),
+                                                  (4096, 1024, 1024, True, 1)])
+def test_gemm_bf16x3_big_body(L, orient, M, N, K, grouped, splits):
+    """Compensated bf16 (PKC_PREC_BF16X3) on the 128x128 tile body (head and tail bf16 images in
+    LDS, 3 MFMAs per product: lo*hi, hi*lo, hi*hi): standalone (>= 160 tiles) and grouped (>= 32
+    tiles, K >= 1024) launches, every operand orientation (row-major, m-contiguous PAIR staging),
+    ragged edges, split-K slabs.  Against the fp64 product of the unrounded operands at ~2^-16
+    relative per product, and well inside plain bf16's error."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    akc, bkc = {"nt": (1, 1), "nn": (1, 0), "tn": (0, 0)}[orient]
+    Ast = A if akc else A.t().contiguous()
+    Bst = B if bkc else B.t().contiguous()
+    Ad, Bd = Ast.to(DEV), Bst.to(DEV)
+    assert L.lib().pkc_gemm_grouped_tile(3, akc, bkc, M, N, K, L.ptr(Ad), Ast.shape[1], L.ptr(Bd),
+                                         Bst.shape[1]) == 128
+    Cd = torch.full((splits, M, N), float("nan"), device=DEV)
+    if grouped:
+        pr = L.GemmProblem(a_kcontig=akc, b_kcontig=bkc, M=M, N=N, K=K, splits=splits,
+                           A=Ad.data_ptr(), lda=Ast.shape[1], B=Bd.data_ptr(), ldb=Bst.shape[1],
+                           C=Cd.data_ptr(), ldc=N, slab_stride=M * N)
+        L.call("pkc_gemm_grouped", 3, C.byref(pr), 1, _s())
+    else:
+        L.call("pkc_gemm", 3, akc, bkc, M, N, K, L.ptr(Ad), Ast.shape[1], L.ptr(Bd), Bst.shape[1],
+               L.ptr(Cd), N, splits, M * N, _s())
+    out = Cd.sum(0).cpu().double()
+    exact = A.double() @ B.double().t()
+    e3 = (out - exact).abs().max().item()
+    assert e3 <= _tol(3, K), (e3, _tol(3, K))
+    # plain bf16's error on a row block (the full fp64 bf16 product is slow on the CPU)
+    eb = ((A[:256].bfloat16().double() @ B.bfloat16().double().t()) - exact[:256]).abs().max().item()
+    assert e3 < 0.05 * eb, (e3, eb)
+
+
 @pytest.mark.parametrize("prec", [0, 2, 3])
 def test_gemm_grouped(L, prec):
     """Several matmuls of different orientation / shape / split count in one launch."""
