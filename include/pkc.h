@@ -22,8 +22,9 @@ extern "C" {
  * 1: rounds 1-3; 2: pkc_logsoftmax_bwd, and the structs as they stand after round 3 (which appended
  * pkc_dense_bwd_args.dz_scratch without a bump); 3: pkc_opt_seg (direct PKC_OP_OPTIM);
  * 4: PKC_PREC_BF16X3; 5: pkc_rnn_args.step_bf16 and its bf16 operand copies;
- * 6: pkc_bn_bwd_epi, pkc_gemm_bnbwd_ok, pkc_dense_bwd_pre. */
-#define PKC_ABI_VERSION 6
+ * 6: pkc_bn_bwd_epi, pkc_gemm_bnbwd_ok, pkc_dense_bwd_pre;
+ * 7: pkc_src_digest, pkc_gemm_grouped_tile, pkc_rnn_args.persist_* (persistent liGRU time loops). */
+#define PKC_ABI_VERSION 7
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
@@ -438,6 +439,17 @@ typedef struct {
    * Cell state, gates, h and every other quantity stay fp32.  0: exact-fp32 products. */
   int step_bf16;
   void* hs_h; const void* U_h[4]; void* ut_h; void* dgates_h;
+  /* Persistent time loops (liGRU with bf16 step products and a block-sparse U, H <= 576): the
+   * whole forward (and BPTT) time loop of a layer in ONE launch of ceil(B2 / rows_per_wg)
+   * workgroups, each owning its batch rows for all T steps with the layer's nonzero U (U^T)
+   * blocks held in registers and LDS as MFMA operands and h_{t-1} (dgates_t) in LDS — no per-step
+   * launch, no cross-workgroup hand-off (rows are independent).  persist_fwd / persist_bwd:
+   * [nwaves][nslots] int32 fragment plans (pkc_rnn_persist_geometry): bits 0-7 the output tile
+   * (16 units; BPTT: 16 columns k), 8-15 the 32-wide contraction block + 1 (0 = none), bit 16 the
+   * tile's last fragment, bit 17 valid; each tile's fragments in one wave.  persist_kb = the
+   * forward plan's nslots.
+   * NULL (or a layer outside these limits): the per-step launches. */
+  const int32_t* persist_fwd; const int32_t* persist_bwd; int persist_kb;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
 /* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that
@@ -455,6 +467,11 @@ int pkc_pattern_mask(const float* W, int rows, int cols, const float* patterns, 
 int pkc_seq_gather(const float* feats, int64_t ld_feats, int F, const int32_t* labels, int nlab,
                    const int64_t* beg, const int32_t* len, const int32_t* left, int B, int max_len,
                    float* x_out, int32_t* lab_out, void* stream);
+/* Geometry of the persistent liGRU loops' plan tables (pkc_rnn_args.persist_*): waves per
+ * workgroup, fragment slots per wave of the forward plan (= persist_kb) and of the BPTT plan,
+ * batch rows per workgroup, largest H. */
+int pkc_rnn_persist_geometry(int* nwaves, int* nslots_fwd, int* nslots_bwd, int* rows_per_wg,
+                             int* hmax);
 int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream);
 int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream);
 

@@ -1247,6 +1247,12 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
    : a->H <= 1024 ? FN<G, CELL, 64>(__VA_ARGS__)                     \
    : FN<G, CELL, 128>(__VA_ARGS__))
 
+// Persistent liGRU time loops (pkc_rnn_persist.hip): one launch per layer and direction of the
+// whole forward / BPTT loop, for block-sparse U in bf16 step mode (pkc_rnn_args.persist_*)
+bool rnn_persist_ok(const pkc_rnn_args* a, bool bwd);
+int rnn_persist_fwd(const pkc_rnn_args* a, hipStream_t s);
+int rnn_persist_bwd(const pkc_rnn_args* a, hipStream_t s);
+
 #ifdef PKC_RNN_FWD
 template <int G, int CELL>
 static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
@@ -1260,6 +1266,9 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   if (a->train && a->drop_p > 0.f) {
     hipLaunchKernelGGL(rnn_drop_mask_kernel, dim3(64), dim3(256), 0, s, *a, B2);
     PKC_LAUNCH_CHECK("pkc_rnn_fwd drop mask");
+  }
+  if constexpr (CELL == PKC_CELL_LIGRU) {
+    if (rnn_persist_ok(a, false)) return rnn_persist_fwd(a, s);
   }
   if constexpr (!two_phase(CELL) && G > 1) {
     if (a->kmap_fwd) {
@@ -1275,6 +1284,19 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
 #ifdef PKC_RNN_BWD
 template <int G, int CELL>
 static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
+  if constexpr (CELL == PKC_CELL_LIGRU) {
+    if (rnn_persist_ok(a, true)) {
+      const int H = a->H;
+      hipLaunchKernelGGL(rnn_transpose_u, dim3((H + 31) / 32, (H + 31) / 32, G), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
+      PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
+      int st = rnn_persist_bwd(a, s);
+      if (st) return st;
+      hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
+      PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
+      return PKC_OK;
+    }
+  }
   if constexpr (!two_phase(CELL) && G > 1) {
     if (a->kmap_bwd) {
       if (a->kmap_s_bwd == 16) return bwd_impl_s<G, CELL, 16, true>(a, dpre, s);

@@ -1,0 +1,397 @@
+// pkc_rnn_persist.hip — persistent time loops of a block-sparse liGRU layer in bf16 step mode
+// (north_star: "recurrent time-step loops fused per wavefront"; the per-step form of the same
+// arithmetic is pkc_rnn_impl.h rnn_fwd_mm / rnn_bwd_mm + rnn_bwd_epi).
+//
+// Reference: liGRU neural_networks.py:1573-1584 (z = sig(wz + Uz h); hc = act(wh + Uh h) * drop;
+// h = z h + (1 - z) hc), both directions as one 2B-row batch (:1536-1538).  The recurrence couples
+// the units of a row, never two rows: row r's h_t needs only row r's h_{t-1}.  So the whole T-step
+// loop of a layer runs as ONE launch of ceil(B2 / RPW) workgroups, each owning RPW rows for every
+// step, with no cross-workgroup hand-off at all:
+//   * the layer's nonzero U blocks (C3's HCGS masks keep ~175 of the 648 blocks of 16 units x 32
+//     k per gate) are loaded ONCE: the first NFR fragments of each wave as registers (B operands
+//     of v_mfma_f32_16x16x32_bf16), the rest into LDS;
+//   * h_{t-1} of the workgroup's rows is the A operand, a bf16 image in LDS (double-buffered by
+//     step parity) whose batch rows sit at MFMA rows 0, 4, 8, 12, so the C layout (row 4 q + i in
+//     lane group q) puts batch row q's result in register 0 of lane group q: every lane carries a
+//     live element out of the chain;
+//   * per step: each wave runs its fragment list (whole output tiles, balanced over the waves by
+//     the host), flushing each finished tile's products to LDS; barrier; the cell update spread
+//     over all threads (gates / h / y stores, the next A image); barrier.
+// The per-step form pays a launch boundary and a cross-XCD fetch of h_{t-1} every step (~5 us for
+// C3); here a step is the MFMA chains, two LDS passes and two workgroup barriers.
+// The BPTT loop is the same with U^T fragments (output tile = 16 columns k, contraction = units j
+// of both gates summed in one chain) and the dgates_t images as A operands: dh_{t-1} =
+// sum_g dgates_g U_g, then the liGRU gate gradients of step t-1 (gate_grads / bwd_step_epi).
+// Numerics: the bf16 step mode's (bf16 h / dgates / U operands, fp32 accumulation and cell math);
+// only the order of the fp32 block sums differs from the per-step kernels.
+//
+// Plan tables (host, pkc.engine): per wave NF int32 entries, bits 0-7 output tile, 8-15 block + 1
+// (0: none — a tile with no nonzero block still flushes its zeros), bit 16 flush (the tile's last
+// fragment), bit 17 valid.
+#define PKC_RNN_PERSIST
+#include "pkc_rnn_impl.h"
+
+namespace pkc {
+namespace persist {
+
+constexpr int NW = 8, NT = 64 * NW;     // two waves per SIMD
+constexpr int RPW = 4;                  // batch rows per workgroup
+// fragment slots per wave (plan width) and how many of them are register-resident (the rest,
+// NF - NFR per wave, in LDS): the forward holds 2 x 4 VGPRs per slot and fewer live epilogue
+// values than the BPTT, which needs five prefetched inputs per element
+constexpr int FNF = 26, FNFR = 18;
+constexpr int BNF = 24, BNFR = 16;
+constexpr int HMAX = 576;               // H <= HMAX (36 tiles of 16)
+// row stride of the bf16 A images (elements): 16-byte rows at dword offsets 0, 48, 32, 16 mod 64
+// banks for the 4 live rows, so an A-fragment read (4 rows x 4 lane groups x 16 B) is conflict-free
+constexpr int HP = 608;
+constexpr int IMG = RPW * HP;           // one A image (bf16 elements)
+constexpr int EPT = (RPW * HMAX + NT - 1) / NT;   // epilogue elements per thread
+constexpr int FRAG = 64 * 16;           // bytes of one B fragment (64 lanes x 8 bf16)
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
+
+__device__ __forceinline__ bf8 zero8() {
+  bf8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+  return v;
+}
+
+// 8 bf16 of a row at k0 .. k0+7 (zero past kmax / when !ok); rows of even length: 4-byte pairs
+__device__ __forceinline__ bf8 load8(const __bf16* row, bool ok, int k0, int kmax) {
+  bf8 v;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const bool in = ok && k0 + j < kmax;
+    const bf2 x = *reinterpret_cast<const bf2*>(row + (in ? k0 + j : 0));
+    v[j] = in ? x[0] : (__bf16)0.f;
+    v[j + 1] = in ? x[1] : (__bf16)0.f;
+  }
+  return v;
+}
+
+// A fragment of 32-wide block kb: lane (MFMA row c, lane group q) holds k = 32 kb + 8 q .. + 7;
+// MFMA rows 4 i are batch row i of the image, the other rows zero
+__device__ __forceinline__ bf8 a_frag(const __bf16* img, int c, int q, int kb) {
+  if ((c & 3) == 0) return *reinterpret_cast<const bf8*>(img + (c >> 2) * HP + 32 * kb + 8 * q);
+  return zero8();
+}
+
+__device__ __forceinline__ int pl_tile(int e) { return e & 255; }
+__device__ __forceinline__ int pl_blk(int e) { return ((e >> 8) & 255) - 1; }
+__device__ __forceinline__ bool pl_flush(int e) { return (e >> 16) & 1; }
+__device__ __forceinline__ bool pl_valid(int e) { return (e >> 17) & 1; }
+
+// The B fragments of one wave's plan: slots < NFR into registers, the rest into the wave's LDS
+// region (lane-linear 16-byte pieces: conflict-free reads).  src(g, tile, c) = the row of U_h (fwd:
+// unit row, k contiguous) or U^T (bwd: k row, j contiguous) that lane column c reads.
+template <int NF, int NFR>
+struct Frags {
+  static constexpr int NFL = NF - NFR;
+  bf8 r[NFR][2];
+  // slot f, gate g: registers (f < NFR; f is a compile-time index after unrolling) or LDS
+  __device__ __forceinline__ void put(char* ufl, int w, int lane, int f, int g, const bf8& v) {
+    if (f < NFR) r[f < NFR ? f : 0][g] = v;
+    else *reinterpret_cast<bf8*>(ufl + ((w * NFL + (f - NFR)) * 2 + g) * FRAG + 16 * lane) = v;
+  }
+  __device__ __forceinline__ bf8 get(const char* ufl, int w, int lane, int f, int g) const {
+    if (f < NFR) return r[f < NFR ? f : 0][g];
+    return *reinterpret_cast<const bf8*>(ufl + ((w * NFL + (f - NFR)) * 2 + g) * FRAG + 16 * lane);
+  }
+};
+
+// ----------------------------------------------------------------------------------- forward
+__global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
+  constexpr int NF = FNF, NFR = FNFR;
+  using Fr = Frags<NF, NFR>;
+  __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];   // LDS fragments
+  __shared__ __attribute__((aligned(16))) __bf16 hl[2 * IMG];           // A: h_{t-1} (2 steps)
+  __shared__ float accl[2][RPW][HMAX];                                  // the step's products
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int r0 = blockIdx.x * RPW, nr = min(RPW, B2 - r0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int64_t TBH = (int64_t)T * a.B * H, TB2H = (int64_t)T * B2 * H;
+  for (int i = tid; i < IMG; i += NT) reinterpret_cast<uint32_t*>(hl)[i] = 0u;   // both images
+  int pl[NF];
+  Fr fr;
+#pragma clang loop unroll(full)
+  for (int f = 0; f < NF; ++f) {
+    const int e = __builtin_amdgcn_readfirstlane(a.persist_fwd[w * NF + f]);
+    pl[f] = e;
+    const int kb = pl_valid(e) ? pl_blk(e) : -1;
+    const int unit = pl_tile(e) * 16 + c;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const __bf16* row = reinterpret_cast<const __bf16*>(a.U_h[g]) + (int64_t)(unit < H ? unit : 0) * H;
+      fr.put(ufl, w, lane, f, g, kb >= 0 ? load8(row, unit < H, 32 * kb + 8 * q, H) : zero8());
+    }
+  }
+  // this thread's cell-update elements: the same every step (h_{t-1} and the mask in registers);
+  // 32-bit element offsets (every saved tensor of a layer holds < 2^31 elements: host check) so the
+  // stores take a uniform base + per-lane offset
+  const int B = a.B, D = ix.bidir ? 2 * H : H;
+  int ost[EPT], opre[EPT], oout[EPT], el[EPT];
+  bool rev[EPT];
+  float hp[EPT], mk[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = tid + NT * j;
+    const bool ok = e < nr * H;
+    const int rl = ok ? e / H : 0, u = ok ? e % H : 0, r = r0 + rl;
+    rev[j] = ix.bidir && r >= B;                   // the reversed direction: time T-1-t
+    const int rr = rev[j] ? r - B : r;
+    ost[j] = r * H + u;                            // (t, r, u) of (T, B2, H): + t B2 H
+    opre[j] = rr * H + u;                          // (tt, rr, u) of (T, B, H): + tt B H
+    oout[j] = rr * D + (rev[j] ? H : 0) + u;       // (tt, rr, u) of (T, B, D): + tt B D
+    el[j] = ok ? rl * HP + u : -1;                 // the element in the A image (-1: none)
+    hp[j] = 0.f;                                   // h_init = 0
+    mk[j] = ok ? drop_val(a, r, u, B2) : 0.f;
+  }
+  const float* __restrict__ wpre = a.wpre;
+  float* __restrict__ gates = a.gates;
+  float* __restrict__ hs = a.hs;
+  __bf16* __restrict__ hs_h = reinterpret_cast<__bf16*>(a.hs_h);
+  float* __restrict__ y = a.y;
+  const int BH = B * H, B2H = B2 * H, BD = B * D, iTBH = (int)TBH;
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const __bf16* img = hl + (t & 1) * IMG;
+    // this step's gate pre-activations (independent of the recurrence: in flight during the MFMAs)
+    float wz[EPT], wh[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int pi = (rev[j] ? T - 1 - t : t) * BH + opre[j];
+      wz[j] = el[j] >= 0 ? wpre[pi] : 0.f;
+      wh[j] = el[j] >= 0 ? wpre[iTBH + pi] : 0.f;
+    }
+    f32x4 az = {0.f, 0.f, 0.f, 0.f}, ah = {0.f, 0.f, 0.f, 0.f};
+#pragma clang loop unroll(full)
+    for (int f = 0; f < NF; ++f) {
+      const int e = pl[f];
+      const int kb = pl_valid(e) ? pl_blk(e) : -1;  // wave-uniform
+      if (kb >= 0) {
+        const bf8 av = a_frag(img, c, q, kb);
+        const bf8 bz = fr.get(ufl, w, lane, f, 0), bh = fr.get(ufl, w, lane, f, 1);
+        az = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bz, az, 0, 0, 0);
+        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bh, ah, 0, 0, 0);
+      }
+      if (pl_valid(e) && pl_flush(e)) {              // batch row q, unit 16 tile + c: register 0
+        const int unit = pl_tile(e) * 16 + c;
+        if (unit < H) {
+          accl[0][q][unit] = az[0];
+          accl[1][q][unit] = ah[0];
+        }
+        az = f32x4{0.f, 0.f, 0.f, 0.f};
+        ah = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    __syncthreads();
+    // liGRU cell update (pkc_rnn_impl.h fwd_epi, CELL_LIGRU)
+    __bf16* nimg = hl + ((t + 1) & 1) * IMG;
+    const int tst = t * B2H;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      if (el[j] < 0) continue;
+      const int rl = el[j] / HP, u = el[j] - rl * HP;
+      const float z = sigm(wz[j] + accl[0][rl][u]);
+      const float hcr = act_fwd(a.act, wh[j] + accl[1][rl][u]);
+      const float h = z * hp[j] + (1.f - z) * (hcr * mk[j]);
+      const int si = tst + ost[j];
+      gates[si] = z;
+      gates[(int)TB2H + si] = hcr;
+      hs[si + B2H] = h;                              // hs[t + 1]
+      hs_h[si + B2H] = (__bf16)h;
+      y[(rev[j] ? T - 1 - t : t) * BD + oout[j]] = h;
+      nimg[el[j]] = (__bf16)h;
+      hp[j] = h;
+    }
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------------- BPTT
+__global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
+  constexpr int NF = BNF, NFR = BNFR;
+  using Fr = Frags<NF, NFR>;
+  __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];
+  __shared__ __attribute__((aligned(16))) __bf16 dl[2][2 * IMG];    // [step parity][gate z, h]
+  __shared__ float accl[RPW][HMAX];                                // dh products of the step
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int r0 = blockIdx.x * RPW, nr = min(RPW, B2 - r0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int64_t TB2H = (int64_t)T * B2 * H;
+  const int64_t n = (int64_t)B2 * H;
+  for (int i = tid; i < 2 * IMG; i += NT) reinterpret_cast<uint32_t*>(&dl[0][0])[i] = 0u;
+  // U^T fragments: B[j][k] = U[j][k] with column k = 16 tile + c, rows j = 32 jb + 8 q .. + 7,
+  // contiguous in ut_h[g][k][j]
+  int pl[NF];
+  Fr fr;
+#pragma clang loop unroll(full)
+  for (int f = 0; f < NF; ++f) {
+    const int e = __builtin_amdgcn_readfirstlane(a.persist_bwd[w * NF + f]);
+    pl[f] = e;
+    const int jb = pl_valid(e) ? pl_blk(e) : -1;
+    const int k = pl_tile(e) * 16 + c;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const __bf16* row = reinterpret_cast<const __bf16*>(a.ut_h) + (int64_t)g * H * H +
+                          (int64_t)(k < H ? k : 0) * H;
+      fr.put(ufl, w, lane, f, g, jb >= 0 ? load8(row, k < H, 32 * jb + 8 * q, H) : zero8());
+    }
+  }
+  const int B = a.B, D = ix.bidir ? 2 * H : H;
+  int ost[EPT], oout[EPT], el[EPT];
+  bool rev[EPT];
+  float gc[EPT], mk[EPT];
+  const __bf16* dgh_in = reinterpret_cast<const __bf16*>(a.dgates_h);
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = tid + NT * j;
+    const bool ok = e < nr * H;
+    const int rl = ok ? e / H : 0, k = ok ? e % H : 0, r = r0 + rl;
+    rev[j] = ix.bidir && r >= B;
+    const int rr = rev[j] ? r - B : r;
+    ost[j] = r * H + k;
+    oout[j] = rr * D + (rev[j] ? H : 0) + k;
+    el[j] = ok ? rl * HP + k : -1;
+    // step T-1 (rnn_bwd_init): g_{T-1} in carry slot (T-1-(T-1)) & 1 = 0, and its dgates (bf16)
+    // as the first A images
+    gc[j] = ok ? a.work[ost[j]] : 0.f;
+    mk[j] = ok ? drop_val(a, r, k, B2) : 0.f;
+    if (ok) {
+      const int si = (T - 1) * B2 * H + ost[j];
+      const int par = (T - 1) & 1;
+      dl[par][el[j]] = dgh_in[si];
+      dl[par][IMG + el[j]] = dgh_in[(int)TB2H + si];
+    }
+  }
+  const float* __restrict__ gates = a.gates;
+  const float* __restrict__ hs = a.hs;
+  const float* __restrict__ dy = a.dy;
+  float* __restrict__ dgates = a.dgates;
+  __bf16* __restrict__ dgh = reinterpret_cast<__bf16*>(a.dgates_h);
+  const int B2H = B2 * H, BD = B * D, iTB2H = (int)TB2H;
+  const int dyn = a.dy_nslab > 0 ? a.dy_nslab : 1;
+  const int64_t dys = a.dy_slab_stride;
+  __syncthreads();
+  for (int tt = T - 2; tt >= 0; --tt) {
+    const int t = tt + 1;
+    const __bf16* img = dl[t & 1];
+    const int tst = tt * B2H;
+    float zt[EPT], dyv[EPT], hpv[EPT], ztt[EPT], hct[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const bool ok = el[j] >= 0;
+      const int si = tst + ost[j];
+      zt[j] = ok ? gates[si + B2H] : 0.f;             // z_t (step tt + 1)
+      float dv = 0.f;
+      if (ok) {
+        const int oi = (rev[j] ? T - 1 - tt : tt) * BD + oout[j];
+        for (int sl = 0; sl < dyn; ++sl) dv += dy[(int64_t)sl * dys + oi];
+      }
+      dyv[j] = dv;
+      hpv[j] = ok ? hs[si] : 0.f;                     // h_{tt-1} = hs[tt]
+      ztt[j] = ok ? gates[si] : 0.f;
+      hct[j] = ok ? gates[iTB2H + si] : 0.f;
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma clang loop unroll(full)
+    for (int f = 0; f < NF; ++f) {
+      const int e = pl[f];
+      const int jb = pl_valid(e) ? pl_blk(e) : -1;
+      if (jb >= 0) {
+        const bf8 b0 = fr.get(ufl, w, lane, f, 0), b1 = fr.get(ufl, w, lane, f, 1);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img, c, q, jb), b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img + IMG, c, q, jb), b1, acc, 0, 0, 0);
+      }
+      if (pl_valid(e) && pl_flush(e)) {
+        const int k = pl_tile(e) * 16 + c;
+        if (k < H) accl[q][k] = acc[0];
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    __syncthreads();
+    // bwd_step_epi + gate_grads (CELL_LIGRU) for step tt
+    __bf16* nimg = dl[tt & 1];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      if (el[j] < 0) continue;
+      const int rl = el[j] / HP, k = el[j] - rl * HP;
+      const float dh = accl[rl][k] + gc[j] * zt[j];
+      const float g = dyv[j] + dh;
+      const float z = ztt[j], hcr = hct[j], m = mk[j];
+      const float hc = hcr * m;
+      const float dz = g * (hpv[j] - hc);
+      const float dhc = g * (1.f - z);
+      const float d0 = dz * z * (1.f - z);
+      const float d1 = dhc * m * act_bwd_out(a.act, hcr);
+      const int si = tst + ost[j];
+      dgates[si] = d0;
+      dgates[iTB2H + si] = d1;
+      dgh[si] = (__bf16)d0;
+      dgh[iTB2H + si] = (__bf16)d1;
+      nimg[el[j]] = (__bf16)d0;
+      nimg[IMG + el[j]] = (__bf16)d1;
+      gc[j] = g;
+    }
+    __syncthreads();
+  }
+  // the carry of step 0 where the per-step form leaves it (slot (T-1) & 1)
+  if (T > 1) {
+    const int p0 = (T - 1) & 1;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j)
+      if (el[j] >= 0) a.work[p0 * n + ost[j]] = gc[j];
+  }
+}
+
+}  // namespace persist
+
+bool rnn_persist_ok(const pkc_rnn_args* a, bool bwd) {
+  using namespace persist;
+  const int64_t B2 = a->bidir ? 2 * a->B : a->B;
+  const int64_t D = a->bidir ? 2 * a->H : a->H;
+  if (2 * (int64_t)a->T * B2 * a->H >= (1ll << 31) || (int64_t)a->T * a->B * D >= (1ll << 31))
+    return false;                               // 32-bit element offsets
+  return a->cell == PKC_CELL_LIGRU && a->step_bf16 && (bwd ? a->persist_bwd : a->persist_fwd) &&
+         a->persist_kb == FNF && a->H <= HMAX && a->H % 2 == 0 && !a->ln_gamma && a->qbits <= 0 &&
+         a->hs_h && a->U_h[0] && a->U_h[1] && (!bwd || (a->ut_h && a->dgates_h));
+}
+
+int rnn_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
+  using namespace persist;
+  const int B2 = a->bidir ? 2 * a->B : a->B;
+  hipLaunchKernelGGL(fwd_loop, dim3((B2 + RPW - 1) / RPW), dim3(NT), 0, s, *a);
+  PKC_LAUNCH_CHECK("pkc_rnn_fwd persistent loop");
+  return PKC_OK;
+}
+
+int rnn_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
+  using namespace persist;
+  const int B2 = a->bidir ? 2 * a->B : a->B;
+  hipLaunchKernelGGL(bwd_loop, dim3((B2 + RPW - 1) / RPW), dim3(NT), 0, s, *a);
+  PKC_LAUNCH_CHECK("pkc_rnn_bwd persistent loop");
+  return PKC_OK;
+}
+
+}  // namespace pkc
+
+// plan-table geometry for the host (pkc.engine builds the per-wave fragment lists)
+extern "C" int pkc_rnn_persist_geometry(int* nwaves, int* nslots_fwd, int* nslots_bwd,
+                                        int* rows_per_wg, int* hmax) {
+  using namespace pkc::persist;
+  if (nwaves) *nwaves = NW;
+  if (nslots_fwd) *nslots_fwd = FNF;
+  if (nslots_bwd) *nslots_bwd = BNF;
+  if (rows_per_wg) *rows_per_wg = RPW;
+  if (hmax) *hmax = HMAX;
+  return PKC_OK;
+}

@@ -67,6 +67,9 @@ SEQ_META_SLOTS = 4
 # steps, bf16 matmuls only.
 RNN_BF16 = os.environ.get("PKC_RNN_BF16", "1") != "0"
 RNN_BF16_SPARSE = os.environ.get("PKC_RNN_BF16_SPARSE", "0") != "0"     # block-sparse U too
+# persistent liGRU time loops for block-sparse U in bf16 step mode (pkc_rnn_persist.hip; 0: the
+# per-step launches)
+RNN_PERSIST = os.environ.get("PKC_RNN_PERSIST", "1") != "0"
 SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
@@ -169,6 +172,50 @@ def _f32(n, dev):
 
 def _b(v):
     return str(v).strip().lower() in ("1", "true", "yes", "y", "on", "t")
+
+
+def persist_geometry():
+    """(waves, forward slots, BPTT slots, rows per workgroup, largest H) of the persistent loops."""
+    v = [C.c_int() for _ in range(5)]
+    L.lib().pkc_rnn_persist_geometry(*[C.byref(x) for x in v])
+    return tuple(x.value for x in v)
+
+
+def persist_plans(mask):
+    """Fragment plans of the persistent liGRU loops (pkc_rnn_args.persist_*) for a static U mask
+    (H x H bool, any gate): forward tiles of 16 units x the 32-wide blocks of k they read, BPTT
+    tiles of 16 columns k x the 32-wide blocks of units j; each tile's fragments in one wave, the
+    tiles spread over the waves longest first (LPT) so the per-step MFMA chains are balanced.
+    None when the layer does not fit the kernels' geometry (pkc_rnn_persist_geometry)."""
+    nw, nsf, nsb, _, hmax = persist_geometry()
+    H = mask.shape[0]
+    if H > hmax or H % 2:
+        return None
+    hp = -(-H // 32) * 32
+    mp = np.zeros((hp, hp), dtype=bool)
+    mp[:H, :H] = mask
+    nt = -(-H // 16)
+    fwd = mp.reshape(hp // 16, 16, hp // 32, 32).any(axis=(1, 3))[:nt]       # [unit tile][k blk]
+    bwd = mp.reshape(hp // 32, 32, hp // 16, 16).any(axis=(1, 3)).T[:nt]     # [k tile][j blk]
+    out = []
+    for pres, nslot in ((fwd, nsf), (bwd, nsb)):
+        frags = [np.nonzero(pres[t])[0].tolist() or [-1] for t in range(nt)]
+        load, lists = [0] * nw, [[] for _ in range(nw)]
+        for t in sorted(range(nt), key=lambda t: -len(frags[t])):
+            wv = min(range(nw), key=lambda v: load[v])
+            load[wv] += len(frags[t])
+            lists[wv].append(t)
+        if max(load) > nslot:
+            return None
+        tab = np.zeros((nw, nslot), dtype=np.int32)
+        for wv in range(nw):
+            f = 0
+            for t in sorted(lists[wv]):
+                for i, b in enumerate(frags[t]):
+                    tab[wv, f] = t | ((b + 1) << 8) | ((i == len(frags[t]) - 1) << 16) | (1 << 17)
+                    f += 1
+        out.append(tab.reshape(-1))
+    return out
 
 
 def _splits(M, N, K, cap):
@@ -995,6 +1042,16 @@ class Engine:
 
                 lb["kmap_fwd"], lb["kmap_s_fwd"] = table(fwd, nt)
                 lb["kmap_bwd"], lb["kmap_s_bwd"] = table(bwd, n.G * nb)
+                lb["persist_fwd"] = lb["persist_bwd"] = None
+                if (RNN_PERSIST and n.cell == L.CELL_LIGRU and self.prec == L.PREC_BF16
+                        and lb.get("hs_h") is not None):
+                    union = torch.zeros(H, H, dtype=torch.bool, device=self.dev)
+                    for m in um:
+                        union |= m.detach().reshape(H, H) != 0
+                    plans = persist_plans(union.cpu().numpy())
+                    if plans is not None:
+                        lb["persist_fwd"], lb["persist_bwd"] = (torch.from_numpy(p_).to(self.dev)
+                                                                for p_ in plans)
 
     def _build_optim(self):
         """One pkc_opt_tensor per parameter that receives a gradient (utils.py:1833-1881)."""
@@ -1575,13 +1632,18 @@ class Engine:
             a.kmap_bwd, a.kmap_s_bwd = lb["kmap_bwd"].data_ptr(), lb["kmap_s_bwd"]
         # (block-sparse U keeps the fp32 steps: C3's 16-row tiles over 16-wide blocks measured
         # 16.6 vs 16.1 us per step and layer with bf16 operands, profiles/r04_rnn_bf16_ab.txt)
-        if lb.get("hs_h") is not None and (RNN_BF16_SPARSE or (lb.get("kmap_fwd") is None
-                                                               and lb.get("kmap_bwd") is None)):
+        persist = lb.get("persist_fwd") is not None
+        if lb.get("hs_h") is not None and (RNN_BF16_SPARSE or persist or (
+                lb.get("kmap_fwd") is None and lb.get("kmap_bwd") is None)):
             a.step_bf16 = 1
             a.hs_h, a.ut_h, a.dgates_h = (lb["hs_h"].data_ptr(), lb["ut_h"].data_ptr(),
                                           lb["dgates_h"].data_ptr())
             for g in range(n.G):
                 a.U_h[g] = lb["U_h"].data_ptr() + 2 * g * H * H
+            if persist:
+                a.persist_fwd, a.persist_bwd = (lb["persist_fwd"].data_ptr(),
+                                                lb["persist_bwd"].data_ptr())
+                a.persist_kb = persist_geometry()[1]
         if sp.get("ln"):
             a.ln_gamma, a.ln_beta, a.ln_eps = sp["ln_gamma"].data_ptr(), sp["ln_beta"].data_ptr(), 1e-6
             a.ln_xhat, a.ln_stat = lb["ln_xhat"].data_ptr(), lb["ln_stat"].data_ptr()

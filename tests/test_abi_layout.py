@@ -51,7 +51,8 @@ LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa
                  3: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012",
                  4: "29670d34ec50ca9c1650f053da10b2d570ed9bff4e9d0d22f31b11ca9c53e012",
                  5: "2c453ea47366535096140ab754d5ecfcd019ccecde60defafc6b607b14f5eb2d",
-                 6: "1bcf851b6b8c7c47b5d010bb84ad5bfed004e6061606a15f6e24fda230644bd9"}
+                 6: "1bcf851b6b8c7c47b5d010bb84ad5bfed004e6061606a15f6e24fda230644bd9",
+                 7: "e7c2d5119718927e74e47e4889727b8834bcec21da87a549b5a754e85736ecb5"}
 
 
 def _layout_digest(L):
