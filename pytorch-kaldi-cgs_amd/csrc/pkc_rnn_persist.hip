@@ -79,6 +79,15 @@ __device__ __forceinline__ bf8 a_frag(const __bf16* img, int c, int q, int kb) {
   return zero8();
 }
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding global
+// load and store of the thread (vmcnt), which would stall each step on the previous step's output
+// stores and this step's prefetched pre-activations; the loop exchanges data through LDS alone
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ int pl_tile(int e) { return e & 255; }
 __device__ __forceinline__ int pl_blk(int e) { return ((e >> 8) & 255) - 1; }
 __device__ __forceinline__ bool pl_flush(int e) { return (e >> 16) & 1; }
@@ -190,7 +199,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
         ah = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    __syncthreads();
+    lds_barrier();
     // liGRU cell update (pkc_rnn_impl.h fwd_epi, CELL_LIGRU)
     __bf16* nimg = hl + ((t + 1) & 1) * IMG;
     const int tst = t * B2H;
@@ -210,7 +219,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
       nimg[el[j]] = (__bf16)h;
       hp[j] = h;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -318,7 +327,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
         acc = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    __syncthreads();
+    lds_barrier();
     // bwd_step_epi + gate_grads (CELL_LIGRU) for step tt
     __bf16* nimg = dl[tt & 1];
 #pragma unroll
@@ -342,7 +351,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       nimg[IMG + el[j]] = (__bf16)d1;
       gc[j] = g;
     }
-    __syncthreads();
+    lds_barrier();
   }
   // the carry of step 0 where the per-step form leaves it (slot (T-1) & 1)
   if (T > 1) {

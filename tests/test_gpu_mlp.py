@@ -138,17 +138,22 @@ def test_engine_c1_full_size_vs_oracle(prec):
     (oracle.nets.use_bf16x3_matmuls), and its first step's posteriors also against the fp32 oracle
     at north_star's 1e-4.
 
+    Every step is checked from the SAME starting state: before each oracle step the oracle nets
+    and optimizers take the engine's weights, BatchNorm statistics and optimizer state as they were
+    before the engine ran that step.  (Over several steps this model's training is chaotic at init
+    — RMSprop's first steps are +-4.47 lr sign steps whatever |g| is — so an unsynchronised
+    comparison measures the chaos, not the kernels: round 4 loosened to 0.3 on that.)
+
     Counted, not loosened (tests/flipcheck.py): a ReLU pre-activation within rounding of zero can
     take the other branch on the GPU than in the oracle, and one such element moves its BatchNorm
-    column's whole gradient and every gradient below it.  Each step runs on the GPU first; the
-    oracle then takes the GPU's branch at every ReLU (act_masks) and the elements where its own
-    branch differs are COUNTED per layer (at most 16 per layer and step), each required to be a
-    rounding tie (|pre-activation| <= 1e-4).  Everything else is held tight at every step:
-    posteriors 1e-4 relative, loss 1e-5, err exact, every gradient 1e-4 of its norm; after the 3
-    steps the SGD body's parameters elementwise within 1e-4 of the tensor's scale, the RMSprop
-    heads' too except a counted share (<= 0.1 %) of sign steps (RMSprop's first steps move every
-    element by +-4.47 lr whatever |g| is, so a gradient element within rounding of zero that takes
-    the other sign moves its weight by ~9 lr), each bounded by 2 x 4.48 lr x steps."""
+    column's whole gradient and every gradient below it.  The engine runs each step first; the
+    oracle then takes the engine's branch at every ReLU (act_masks) and the elements where its own
+    branch differs are COUNTED per layer (at most 8 per layer and step), each required to be a
+    rounding tie (|pre-activation| <= 1e-5).  Everything else is held tight at every step:
+    posteriors 1e-4 relative, loss 1e-5, err exact, every gradient 1e-4 of its norm, every updated
+    parameter elementwise within 1e-4 of the tensor's scale — except a counted share (<= 0.1 %)
+    of RMSprop sign steps in the heads (a gradient element within rounding of zero whose sign
+    differs moves its weight by ~9 lr), each bounded by 2 x 4.48 lr."""
     from flipcheck import assert_counted, sign_flips, step_outliers
     from oracle import nets as ON
     from oracle import run as OR
@@ -207,15 +212,24 @@ def test_engine_c1_full_size_vs_oracle(prec):
     head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
     gview = {id(p): getattr(n, key) for n in eng.nodes for (p, key, _m) in n.params()
              if isinstance(key, str)}
-    flips = []
+    flips, report = [], {}
     for s in range(steps):
-        # the GPU step first: its ReLU inputs gamma * x_hat + beta (gamma / beta as the step's
+        # the engine's state before this step -> the oracle's starting state
+        eng.sync_state()
+        start = {a: {k: v.detach().cpu().clone() for k, v in nets[a].state_dict().items()}
+                 for a in nets}
+        ostart = {a: eng.optimizer_state_dict(a) for a in nets}
+        for a in nets:
+            onets[a].load_state_dict(start[a])
+            if s > 0:
+                ooptim[a].load_state_dict(ostart[a])
+        # the engine step first: its ReLU inputs gamma * x_hat + beta (gamma / beta as the step's
         # forward saw them, before its optimizer moves them)
-        gam = [nets["MLP_layers1"].bn[i].weight.detach().clone() for i in range(5)]
-        bet = [nets["MLP_layers1"].bn[i].bias.detach().clone() for i in range(5)]
+        gam = [start["MLP_layers1"]["bn.%d.weight" % i] for i in range(5)]
+        bet = [start["MLP_layers1"]["bn.%d.bias" % i] for i in range(5)]
         eng.train_step()
         loss, err = eng.loss_values()
-        gpre = [(l.xhat[:B * 1024].view(B, 1024) * gam[i] + bet[i]).cpu()
+        gpre = [l.xhat[:B * 1024].view(B, 1024).cpu() * gam[i] + bet[i]
                 for i, l in enumerate(body_layers)]
         pre = []
         outs = oracle_step(onets, ooptim, s, pre, [(g > 0).float() for g in gpre])
@@ -228,7 +242,7 @@ def test_engine_c1_full_size_vs_oracle(prec):
         rel = ((post - ref).abs() / ref.abs().clamp_min(1e-3)).max().item()
         print("%s step %d posterior max rel err %.3g; ReLU branch flips per layer %s (largest "
               "|pre-activation| among them %.3g)" % (prec, s, rel, fl, tie))
-        assert max(fl) <= 16 and tie <= 1e-4, "step %d ReLU branch flips per layer %s, largest " \
+        assert max(fl) <= 8 and tie <= 1e-5, "step %d ReLU branch flips per layer %s, largest " \
             "|pre-activation| %.3g" % (s, fl, tie)
         assert rel < 1e-4, "step %d posterior max rel err %.3g (flips %s)" % (s, rel, flips)
         if s == 0 and x3:
@@ -254,22 +268,23 @@ def test_engine_c1_full_size_vs_oracle(prec):
         assert checked >= 20
         np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-5)
         np.testing.assert_allclose(err, outs["err_final"].item())
-    eng.sync_state()
-    report = {}
-    for a in nets:
-        lr = float(opts[a]["arch_lr"])
-        rms = opts[a]["arch_opt"] == "rmsprop"
-        for k, v in nets[a].state_dict().items():
-            if k.endswith("num_batches_tracked"):
-                continue
-            ref = onets[a].state_dict()[k].double()
-            n, dmax, rest = step_outliers(v.cpu(), ref, 1e-4, max(float(ref.abs().max()), lr))
-            report["%s/%s" % (a, k)] = n
-            assert_counted("%s %s" % (a, k), n, ref.numel(), 1e-3 if rms else 0.0, dmax,
-                           (2 * 4.48 * lr * steps if rms else
-                            1e-4 * max(float(ref.abs().max()), lr)) + 1e-7,
-                           "(ReLU flips per step %s; outliers per tensor %s)" % (flips, report))
-    print("%s parameter outliers (RMSprop sign steps) per tensor: %s" % (prec, report))
+        # the step's updates from the common start
+        eng.sync_state()
+        for a in nets:
+            lr = float(opts[a]["arch_lr"])
+            rms = opts[a]["arch_opt"] == "rmsprop"
+            for k, v in nets[a].state_dict().items():
+                if k.endswith("num_batches_tracked"):
+                    continue
+                ref = onets[a].state_dict()[k].double()
+                scale = max(float(ref.abs().max()), lr)
+                n, dmax, rest = step_outliers(v.cpu(), ref, 1e-4, scale)
+                report["%d %s/%s" % (s, a, k)] = n
+                assert_counted("step %d %s %s" % (s, a, k), n, ref.numel(), 1e-3 if rms else 0.0,
+                               dmax, (2 * 4.48 * lr if rms else 1e-4 * scale) + 1e-7,
+                               "(ReLU flips per step %s)" % flips)
+    print("%s parameter outliers (RMSprop sign steps) per step and tensor: %s" % (
+        prec, {k: v for k, v in report.items() if v}))
 
 
 @pytest.mark.parametrize("prec", ["bf16"])
