@@ -41,6 +41,28 @@ namespace pkc {
 
 constexpr int RT = 256;          // threads per workgroup (4 waves)
 
+// Phase trace (measurement builds only: -DPKC_TRACE, pkc/_build.py build(trace=True)).  PKC_TR(i)
+// drains the workgroup's outstanding memory operations, then wave 0 lane 0 stores the shader clock
+// (s_memtime) as stamp i of its workgroup: per-phase durations of one launch, read back with
+// pkc_trace_read (the last launch of the traced kernel).  Stamps 0 and 7: the constant 100 MHz
+// clock (s_memrealtime) at entry and exit, comparable across workgroups and XCDs.
+#ifdef PKC_TRACE
+constexpr int TRACE_SLOTS = 8, TRACE_WG = 4096;
+__device__ unsigned long long trace_buf[TRACE_WG * TRACE_SLOTS];
+__device__ __forceinline__ void trace_stamp(int i, bool real) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  const unsigned long long v = real ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+  const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (threadIdx.x == 0 && wg < TRACE_WG) {
+    volatile unsigned long long* b = trace_buf;        // a vector store, kept in program order
+    b[wg * TRACE_SLOTS + i] = v;
+  }
+}
+#define PKC_TR(i) ::pkc::trace_stamp((i), (i) == 0 || (i) == 7)
+#else
+#define PKC_TR(i) do { } while (0)
+#endif
+
 __host__ __device__ constexpr int cell_gates(int cell) {
   return cell == PKC_CELL_LSTM ? 4 : cell == PKC_CELL_GRU ? 3 : cell == PKC_CELL_RNN ? 1 : 2;
 }
@@ -644,6 +666,8 @@ template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4,
 __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
   static_assert(!BF || (!QH && PH == 0), "bf16 steps: one-phase cells, no quantised h");
+  PKC_TR(0);
+  PKC_TR(1);
   const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   constexpr int NTH = 64 * NW;
   __shared__ float red[NW * 32 * 17];
@@ -706,6 +730,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
 #pragma unroll
     for (int s = 0; s < S; ++s) vb[s] = 0.f;
   }
+  PKC_TR(2);                        // operands (and the epilogue inputs) in registers
   if constexpr (QH) {
     // each gate's QuantizeLinear re-quantises h in place (q1..q4): gate g's product reads
     // q_{g+1} = Q(q_g) with var_g = max|q_g| over the whole tensor.  With all B2 <= 32 rows in this
@@ -740,6 +765,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
 #pragma unroll
       for (int g = 0; g < 4; ++g) vars[g] = v1;
     }
+    PKC_TR(3);                      // var reduced
     const QParams qp = qparams(vars[0], qscale);
     const bool qon = vars[0] != 0.f;
     // gate g's columns take the product of q_{g+1}: one chain per gate into its own accumulators
@@ -770,7 +796,12 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
   }
   }   // !BF
+#ifdef PKC_TRACE
+  asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));   // the products complete before stamp 4
+#endif
+  PKC_TR(4);
   reduce_tile<NW>(acc0, acc1, red, tile);
+  PKC_TR(5);
   for (int p = threadIdx.x; p < 32 * NU; p += NTH) {
     const int rl = p / NU, ul = p % NU;
     const int r = r0 + rl, j = u0 + ul;
@@ -785,6 +816,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
       else fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
     }
   }
+  PKC_TR(6);
+  PKC_TR(7);
 }
 
 // BPTT step for target tt (t = tt + 1 has its gate gradients): dh = acc + carries, g = dy + dh,
@@ -1359,6 +1392,14 @@ extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
     default: return fwd_impl<4, PKC_CELL_LSTM>(a, S(stream));
   }
 }
+
+#ifdef PKC_TRACE
+// measurement builds only: the forward step kernels' stamps (n <= TRACE_WG * TRACE_SLOTS)
+extern "C" int pkc_trace_read(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pkc::trace_buf), sizeof(unsigned long long) * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #endif  // PKC_RNN_FWD
 #ifdef PKC_RNN_BWD

@@ -48,6 +48,7 @@ constexpr int HP = 608;
 constexpr int IMG = RPW * HP;           // one A image (bf16 elements)
 constexpr int EPT = (RPW * HMAX + NT - 1) / NT;   // epilogue elements per thread
 constexpr int FRAG = 64 * 16;           // bytes of one B fragment (64 lanes x 8 bf16)
+constexpr int SW = 2;                   // plan slots per scheduling window
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
@@ -72,11 +73,13 @@ __device__ __forceinline__ bf8 load8(const __bf16* row, bool ok, int k0, int kma
   return v;
 }
 
-// A fragment of 32-wide block kb: lane (MFMA row c, lane group q) holds k = 32 kb + 8 q .. + 7;
-// MFMA rows 4 i are batch row i of the image, the other rows zero
+// A fragment of 32-wide block kb: lane (MFMA row c, lane group q) holds k = 32 kb + 8 q .. + 7 of
+// batch row c >> 2.  MFMA rows 4 i .. 4 i + 3 all carry batch row i; only row 4 q of each result
+// (register 0 of lane group q) is used, the three duplicates are ignored — so every lane reads
+// (same-address lanes are LDS broadcasts) and the fragment loop stays branch-free: the compiler
+// can issue the next fragments' LDS reads under the current MFMAs
 __device__ __forceinline__ bf8 a_frag(const __bf16* img, int c, int q, int kb) {
-  if ((c & 3) == 0) return *reinterpret_cast<const bf8*>(img + (c >> 2) * HP + 32 * kb + 8 * q);
-  return zero8();
+  return *reinterpret_cast<const bf8*>(img + (c >> 2) * HP + 32 * kb + 8 * q);
 }
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding global
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   using Fr = Frags<NF, NFR>;
   __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];   // LDS fragments
   __shared__ __attribute__((aligned(16))) __bf16 hl[2 * IMG];           // A: h_{t-1} (2 steps)
-  __shared__ float accl[2][RPW][HMAX];                                  // the step's products
+  __shared__ float accl[2][RPW][HMAX + 16];     // the step's products (+16: columns past H)
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2, T = a.T;
   const int r0 = blockIdx.x * RPW, nr = min(RPW, B2 - r0);
@@ -171,65 +174,81 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   for (int t = 0; t < T; ++t) {
     const __bf16* img = hl + (t & 1) * IMG;
     // this step's gate pre-activations (independent of the recurrence: in flight during the MFMAs)
+    // (every lane loads — element 0 for an unused slot — and every lane consumes the values below:
+    // a load under a per-lane branch leaves its register pending on the other path, and the next
+    // step's overwrite would wait for every outstanding memory operation, this step's stores too)
     float wz[EPT], wh[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int pi = (rev[j] ? T - 1 - t : t) * BH + opre[j];
-      wz[j] = el[j] >= 0 ? wpre[pi] : 0.f;
-      wh[j] = el[j] >= 0 ? wpre[iTBH + pi] : 0.f;
+      const int pi = el[j] >= 0 ? (rev[j] ? T - 1 - t : t) * BH + opre[j] : 0;
+      wz[j] = wpre[pi];
+      wh[j] = wpre[iTBH + pi];
     }
     f32x4 az = {0.f, 0.f, 0.f, 0.f}, ah = {0.f, 0.f, 0.f, 0.f};
+    // straight-line over the plan: empty slots multiply zero B fragments (loaded as zeros) with any
+    // A block; a tile's last slot stores its running products (wave-uniform branch; columns past H
+    // to the spill-over slot HMAX + c) and restarts them
 #pragma clang loop unroll(full)
     for (int f = 0; f < NF; ++f) {
       const int e = pl[f];
-      const int kb = pl_valid(e) ? pl_blk(e) : -1;  // wave-uniform
-      if (kb >= 0) {
-        const bf8 av = a_frag(img, c, q, kb);
-        const bf8 bz = fr.get(ufl, w, lane, f, 0), bh = fr.get(ufl, w, lane, f, 1);
-        az = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bz, az, 0, 0, 0);
-        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bh, ah, 0, 0, 0);
+      const int kb = pl_valid(e) ? max(pl_blk(e), 0) : 0;  // wave-uniform
+      const bf8 av = a_frag(img, c, q, kb);
+      az = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, fr.get(ufl, w, lane, f, 0), az, 0, 0, 0);
+      ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, fr.get(ufl, w, lane, f, 1), ah, 0, 0, 0);
+      const bool fl = pl_valid(e) && pl_flush(e);
+      const int unit = pl_tile(e) * 16 + c;
+      const int col = fl && unit < H ? unit : HMAX + c;   // batch row q, unit: register 0
+      if (fl) {
+        accl[0][q][col] = az[0];
+        accl[1][q][col] = ah[0];
       }
-      if (pl_valid(e) && pl_flush(e)) {              // batch row q, unit 16 tile + c: register 0
-        const int unit = pl_tile(e) * 16 + c;
-        if (unit < H) {
-          accl[0][q][unit] = az[0];
-          accl[1][q][unit] = ah[0];
-        }
-        az = f32x4{0.f, 0.f, 0.f, 0.f};
-        ah = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      const f32x4 zero = {0.f, 0.f, 0.f, 0.f};       // restart after a flush (a select: a
+      az = fl ? zero : az;                            // multiply by 0 would turn inf into NaN)
+      ah = fl ? zero : ah;
+      // a scheduling window of SW slots: the next slots' LDS reads overlap these MFMAs, without
+      // the whole plan's reads hoisted to the top (4 VGPRs each)
+      if (f % SW == SW - 1) __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
     // liGRU cell update (pkc_rnn_impl.h fwd_epi, CELL_LIGRU)
     __bf16* nimg = hl + ((t + 1) & 1) * IMG;
     const int tst = t * B2H;
+    // every element's values first, then the stores: vmcnt is one in-order counter for loads and
+    // stores alike, so a load consumed after this step's first stores would wait for those too
+    float zv[EPT], hv[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const bool ok = el[j] >= 0;
+      const int e = ok ? el[j] : 0;
+      const int rl = e / HP, u = e - rl * HP;
+      zv[j] = sigm(wz[j] + accl[0][rl][u]);
+      hv[j] = act_fwd(a.act, wh[j] + accl[1][rl][u]);
+      const float h = zv[j] * hp[j] + (1.f - zv[j]) * (hv[j] * mk[j]);
+      hp[j] = ok ? h : 0.f;                          // (a select: consumed on every lane)
+    }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       if (el[j] < 0) continue;
-      const int rl = el[j] / HP, u = el[j] - rl * HP;
-      const float z = sigm(wz[j] + accl[0][rl][u]);
-      const float hcr = act_fwd(a.act, wh[j] + accl[1][rl][u]);
-      const float h = z * hp[j] + (1.f - z) * (hcr * mk[j]);
       const int si = tst + ost[j];
-      gates[si] = z;
-      gates[(int)TB2H + si] = hcr;
-      hs[si + B2H] = h;                              // hs[t + 1]
-      hs_h[si + B2H] = (__bf16)h;
-      y[(rev[j] ? T - 1 - t : t) * BD + oout[j]] = h;
-      nimg[el[j]] = (__bf16)h;
-      hp[j] = h;
+      gates[si] = zv[j];
+      gates[(int)TB2H + si] = hv[j];
+      hs[si + B2H] = hp[j];                          // hs[t + 1]
+      hs_h[si + B2H] = (__bf16)hp[j];
+      y[(rev[j] ? T - 1 - t : t) * BD + oout[j]] = hp[j];
+      nimg[el[j]] = (__bf16)hp[j];
     }
     lds_barrier();
   }
 }
 
 // ----------------------------------------------------------------------------------- BPTT
+template <bool DY2>                     // DY2: dL/dy in two slabs (one: the common case)
 __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
   constexpr int NF = BNF, NFR = BNFR;
   using Fr = Frags<NF, NFR>;
   __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];
   __shared__ __attribute__((aligned(16))) __bf16 dl[2][2 * IMG];    // [step parity][gate z, h]
-  __shared__ float accl[RPW][HMAX];                                // dh products of the step
+  __shared__ float accl[RPW][HMAX + 16];        // dh products of the step (+16: columns past H)
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2, T = a.T;
   const int r0 = blockIdx.x * RPW, nr = min(RPW, B2 - r0);
@@ -256,9 +275,11 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       fr.put(ufl, w, lane, f, g, jb >= 0 ? load8(row, k < H, 32 * jb + 8 * q, H) : zero8());
     }
   }
-  const int B = a.B, D = ix.bidir ? 2 * H : H;
-  int ost[EPT], oout[EPT], el[EPT];
-  bool rev[EPT];
+  const int B = a.B, D = ix.bidir ? 2 * H : H, BD = B * D;
+  // per element: (t, r, k) offset ost + t B2 H of the saved tensors and ob + tt osg of dL/dy (the
+  // reversed direction runs time backwards) — both 0 for an unused slot, which then reads element
+  // 0 of its step: every lane's addresses without a select or branch in the step loop
+  int ost[EPT], ob[EPT], osg[EPT], el[EPT];
   float gc[EPT], mk[EPT];
   const __bf16* dgh_in = reinterpret_cast<const __bf16*>(a.dgates_h);
 #pragma unroll
@@ -266,10 +287,12 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     const int e = tid + NT * j;
     const bool ok = e < nr * H;
     const int rl = ok ? e / H : 0, k = ok ? e % H : 0, r = r0 + rl;
-    rev[j] = ix.bidir && r >= B;
-    const int rr = rev[j] ? r - B : r;
-    ost[j] = r * H + k;
-    oout[j] = rr * D + (rev[j] ? H : 0) + k;
+    const bool rev = ix.bidir && r >= B;
+    const int rr = rev ? r - B : r;
+    const int oout = rr * D + (rev ? H : 0) + k;
+    ost[j] = ok ? r * H + k : 0;
+    ob[j] = ok ? (rev ? (T - 1) * BD : 0) + oout : 0;
+    osg[j] = ok ? (rev ? -BD : BD) : 0;
     el[j] = ok ? rl * HP + k : -1;
     // step T-1 (rnn_bwd_init): g_{T-1} in carry slot (T-1-(T-1)) & 1 = 0, and its dgates (bf16)
     // as the first A images
@@ -287,69 +310,77 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
   const float* __restrict__ dy = a.dy;
   float* __restrict__ dgates = a.dgates;
   __bf16* __restrict__ dgh = reinterpret_cast<__bf16*>(a.dgates_h);
-  const int B2H = B2 * H, BD = B * D, iTB2H = (int)TB2H;
-  const int dyn = a.dy_nslab > 0 ? a.dy_nslab : 1;
-  const int64_t dys = a.dy_slab_stride;
+  const int B2H = B2 * H, iTB2H = (int)TB2H;
+  const int dys = DY2 ? (int)a.dy_slab_stride : 0;   // < 2^31 (rnn_persist_ok)
+  float zc[EPT];                                // z_{tt+1}, carried from the step before
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) zc[j] = gates[(T - 1) * B2H + ost[j]];
   __syncthreads();
   for (int tt = T - 2; tt >= 0; --tt) {
     const int t = tt + 1;
     const __bf16* img = dl[t & 1];
     const int tst = tt * B2H;
-    float zt[EPT], dyv[EPT], hpv[EPT], ztt[EPT], hct[EPT];
+    float dyv[EPT], hpv[EPT], ztt[EPT], hct[EPT];
+    // (unconditional loads and uses, as the forward's)
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const bool ok = el[j] >= 0;
       const int si = tst + ost[j];
-      zt[j] = ok ? gates[si + B2H] : 0.f;             // z_t (step tt + 1)
-      float dv = 0.f;
-      if (ok) {
-        const int oi = (rev[j] ? T - 1 - tt : tt) * BD + oout[j];
-        for (int sl = 0; sl < dyn; ++sl) dv += dy[(int64_t)sl * dys + oi];
-      }
-      dyv[j] = dv;
-      hpv[j] = ok ? hs[si] : 0.f;                     // h_{tt-1} = hs[tt]
-      ztt[j] = ok ? gates[si] : 0.f;
-      hct[j] = ok ? gates[iTB2H + si] : 0.f;
+      const int oi = ob[j] + tt * osg[j];
+      // one or two slabs (rnn_persist_ok; the engine sums more beforehand)
+      dyv[j] = DY2 ? dy[oi] + dy[dys + oi] : dy[oi];
+      hpv[j] = hs[si];                                // h_{tt-1} = hs[tt]
+      ztt[j] = gates[si];
+      hct[j] = gates[iTB2H + si];
     }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma clang loop unroll(full)
-    for (int f = 0; f < NF; ++f) {
+    for (int f = 0; f < NF; ++f) {              // straight-line, as the forward's
       const int e = pl[f];
-      const int jb = pl_valid(e) ? pl_blk(e) : -1;
-      if (jb >= 0) {
-        const bf8 b0 = fr.get(ufl, w, lane, f, 0), b1 = fr.get(ufl, w, lane, f, 1);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img, c, q, jb), b0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img + IMG, c, q, jb), b1, acc, 0, 0, 0);
-      }
-      if (pl_valid(e) && pl_flush(e)) {
-        const int k = pl_tile(e) * 16 + c;
-        if (k < H) accl[q][k] = acc[0];
-        acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      const int jb = pl_valid(e) ? max(pl_blk(e), 0) : 0;
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img, c, q, jb), fr.get(ufl, w, lane, f, 0),
+                                                    acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img + IMG, c, q, jb),
+                                                    fr.get(ufl, w, lane, f, 1), acc, 0, 0, 0);
+      const bool fl = pl_valid(e) && pl_flush(e);
+      const int k = pl_tile(e) * 16 + c;
+      if (fl) accl[q][k < H ? k : HMAX + c] = acc[0];
+      acc = fl ? f32x4{0.f, 0.f, 0.f, 0.f} : acc;
+      if (f % SW == SW - 1) __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
     // bwd_step_epi + gate_grads (CELL_LIGRU) for step tt
     __bf16* nimg = dl[tt & 1];
+    // values first, then the stores (as the forward's)
+    float d0v[EPT], d1v[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      if (el[j] < 0) continue;
-      const int rl = el[j] / HP, k = el[j] - rl * HP;
-      const float dh = accl[rl][k] + gc[j] * zt[j];
+      const bool ok = el[j] >= 0;
+      const int e = ok ? el[j] : 0;
+      const int rl = e / HP, k = e - rl * HP;
+      const float dh = accl[rl][k] + gc[j] * zc[j];   // z_{tt+1}: the previous step's z
       const float g = dyv[j] + dh;
       const float z = ztt[j], hcr = hct[j], m = mk[j];
       const float hc = hcr * m;
       const float dz = g * (hpv[j] - hc);
       const float dhc = g * (1.f - z);
-      const float d0 = dz * z * (1.f - z);
-      const float d1 = dhc * m * act_bwd_out(a.act, hcr);
+      d0v[j] = dz * z * (1.f - z);
+      d1v[j] = dhc * m * act_bwd_out(a.act, hcr);
+      gc[j] = ok ? g : 0.f;                           // (a select: consumed on every lane)
+      zc[j] = z;
+      // the next step's A images on every lane (an unused slot writes column HP - 1 of row 0, a
+      // padding column no fragment reads): the values are consumed here, ahead of the stores
+      const int ei = ok ? e : HP - 1;
+      nimg[ei] = (__bf16)d0v[j];
+      nimg[IMG + ei] = (__bf16)d1v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      if (el[j] < 0) continue;
       const int si = tst + ost[j];
-      dgates[si] = d0;
-      dgates[iTB2H + si] = d1;
-      dgh[si] = (__bf16)d0;
-      dgh[iTB2H + si] = (__bf16)d1;
-      nimg[el[j]] = (__bf16)d0;
-      nimg[IMG + el[j]] = (__bf16)d1;
-      gc[j] = g;
+      dgates[si] = d0v[j];
+      dgates[iTB2H + si] = d1v[j];
+      dgh[si] = (__bf16)d0v[j];
+      dgh[iTB2H + si] = (__bf16)d1v[j];
     }
     lds_barrier();
   }
@@ -370,6 +401,8 @@ bool rnn_persist_ok(const pkc_rnn_args* a, bool bwd) {
   const int64_t D = a->bidir ? 2 * a->H : a->H;
   if (2 * (int64_t)a->T * B2 * a->H >= (1ll << 31) || (int64_t)a->T * a->B * D >= (1ll << 31))
     return false;                               // 32-bit element offsets
+  if (bwd && (a->dy_nslab > 2 || (a->dy_nslab == 2 && 2 * a->dy_slab_stride >= (1ll << 31))))
+    return false;                               // dL/dy: at most 2 slabs, 32-bit offsets
   return a->cell == PKC_CELL_LIGRU && a->step_bf16 && (bwd ? a->persist_bwd : a->persist_fwd) &&
          a->persist_kb == FNF && a->H <= HMAX && a->H % 2 == 0 && !a->ln_gamma && a->qbits <= 0 &&
          a->hs_h && a->U_h[0] && a->U_h[1] && (!bwd || (a->ut_h && a->dgates_h));
@@ -386,7 +419,10 @@ int rnn_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
 int rnn_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
   using namespace persist;
   const int B2 = a->bidir ? 2 * a->B : a->B;
-  hipLaunchKernelGGL(bwd_loop, dim3((B2 + RPW - 1) / RPW), dim3(NT), 0, s, *a);
+  if (a->dy_nslab > 1)
+    hipLaunchKernelGGL(bwd_loop<true>, dim3((B2 + RPW - 1) / RPW), dim3(NT), 0, s, *a);
+  else
+    hipLaunchKernelGGL(bwd_loop<false>, dim3((B2 + RPW - 1) / RPW), dim3(NT), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd persistent loop");
   return PKC_OK;
 }

@@ -73,12 +73,12 @@ def _deps(src, seen=None):
     return seen
 
 
-def _compile(src):
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+def _compile(src, bdir=BUILD, defs=()):
+    obj = os.path.join(bdir, os.path.basename(src) + ".o")
     newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(d) for d in _deps(src)])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + list(defs) + ["-c", src, "-o", obj]
     if src.endswith(".cpp"):
         cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-x", "c++", "-c",
                src, "-o", obj]
@@ -88,20 +88,29 @@ def _compile(src):
     return obj
 
 
-def build(verbose=False):
-    os.makedirs(BUILD, exist_ok=True)
+# The phase-trace variant (measurement only, never the product): every source built with
+# -DPKC_TRACE into build_trace/ and pkc/libpkc_trace.so, loaded with PKC_LIB=...; the step kernels
+# then record s_memtime stamps per workgroup at their phase boundaries (pkc_rnn_impl.h PKC_TR)
+TRACE_BUILD = os.path.join(TOP, "build_trace")
+TRACE_LIB = os.path.join(PKG, "libpkc_trace.so")
+
+
+def build(verbose=False, trace=False):
+    bdir, lib = (TRACE_BUILD, TRACE_LIB) if trace else (BUILD, LIB)
+    os.makedirs(bdir, exist_ok=True)
     srcs = _sources()
+    defs = ("-DPKC_TRACE",) if trace else ()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
+        objs = list(ex.map(lambda s: _compile(s, bdir, defs), srcs))
     digest = src_digest()
     objs.append(_digest_obj(digest))
-    stamp = os.path.join(BUILD, "libpkc.objs")
+    stamp = os.path.join(bdir, "libpkc.objs")
     listing = "\n".join(objs + [digest])
     same = os.path.exists(stamp) and open(stamp).read() == listing
-    if same and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
-        return LIB
+    if same and os.path.exists(lib) and os.path.getmtime(lib) >= max(os.path.getmtime(o) for o in objs):
+        return lib
     # RCCL: the pkc_dp_* all-reduce entry points for non-Python hosts
-    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", LIB] + objs + [
+    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", lib] + objs + [
         "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -109,10 +118,10 @@ def build(verbose=False):
     with open(stamp, "w") as f:            # a removed source also forces the next relink
         f.write(listing)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    build(verbose=True, trace="--trace" in sys.argv)
     sys.exit(0)

@@ -1,0 +1,62 @@
+"""Phase breakdown of the recurrent forward step kernel (measurement only).
+
+Runs the sequence bench's config on the phase-trace build of libpkc (pkc/libpkc_trace.so, built
+with `python pytorch-kaldi-cgs_amd/pkc/_build.py --trace`; its step kernels stamp s_memtime at
+their phase boundaries, pkc_rnn_impl.h PKC_TR) and prints, over the workgroups of the last traced
+launch, the median duration of every phase in shader-clock cycles and in ns (the cycle counter's
+rate taken from the 100 MHz real-time stamps of the same workgroups).  The stamps drain the
+outstanding memory operations at each boundary, so the phases add up to somewhat more than the
+untraced kernel; their proportions are the point.
+
+Usage: PKC_LIB=pytorch-kaldi-cgs_amd/pkc/libpkc_trace.so python scripts/trace_steps.py --config c5
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+sys.path.insert(0, os.path.join(ROOT, "pytorch-kaldi-cgs_amd"))
+
+PHASES = ["entry", "operand + epilogue-input loads", "var max-abs reduction",
+          "quantise + MFMA chains", "4-wave tile reduction (LDS)", "cell update + stores"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c5")
+    ap.add_argument("--prec", default="fp32")
+    ap.add_argument("--steps", type=int, default=2)
+    a = ap.parse_args()
+    assert "libpkc_trace" in os.environ.get("PKC_LIB", ""), "set PKC_LIB to the trace build"
+    import torch
+    import bench_seq
+    from pkc import _lib as L
+    bench_seq.run(a.config, a.steps, 1, prec=a.prec)
+    torch.cuda.synchronize()
+    n = 4096 * 8
+    buf = (C.c_ulonglong * n)()
+    assert L.lib().pkc_trace_read(buf, n) == 0
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
+    t = t[(t[:, 0] > 0) & (t[:, 7] > 0)]
+    cyc = np.diff(t[:, 1:7], axis=1)                        # phases 1..5 in shader cycles
+    real_ns = (t[:, 7] - t[:, 0]) * 10.0                    # 100 MHz
+    ghz = (t[:, 6] - t[:, 1]) / np.maximum(real_ns, 1)
+    clk = float(np.median(ghz))
+    span_ns = float((t[:, 7].max() - t[:, 0].min()) * 10.0)
+    out = {"config": a.config, "prec": a.prec, "workgroups": int(len(t)),
+           "clock_ghz_median": round(clk, 3), "launch_span_ns": span_ns,
+           "workgroup_ns_median": float(np.median(real_ns)),
+           "phases": {PHASES[i + 1]: {"cycles_median": float(np.median(cyc[:, i])),
+                                      "ns_median": round(float(np.median(cyc[:, i])) / clk, 1),
+                                      "cycles_max": float(cyc[:, i].max())}
+                      for i in range(5)}}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -48,3 +48,24 @@ def assert_counted(name, n, size, frac, max_abs, bound_abs, detail=""):
         name, n, size, allowed, detail)
     assert max_abs <= bound_abs, "%s: an element moved %.3g (> %.3g) %s" % (
         name, max_abs, bound_abs, detail)
+
+
+def optim_state_by_name(sd, net, onet):
+    """A torch.optim state_dict indexed over net.parameters(), re-indexed over onet.parameters()
+    (the oracle class may register its parameters in another order); tensors to the CPU."""
+    names = [n for n, _ in net.named_parameters()]
+    where = {n: i for i, (n, _) in enumerate(onet.named_parameters())}
+    state = {where[names[i]]: {a: (b.detach().cpu().clone() if torch.is_tensor(b) else b)
+                               for a, b in st.items()} for i, st in sd["state"].items()}
+    group = dict(sd["param_groups"][0])
+    group["params"] = list(range(len(where)))
+    return {"state": state, "param_groups": [group]}
+
+
+def resync(nets, onets, opt_sds, oopts):
+    """The oracle's starting state := the GPU side's (parameters, buffers, optimizer state), so a
+    step is compared from a common start and one step's rounding flips do not compound."""
+    for k in nets:
+        onets[k].load_state_dict({n: v.detach().cpu().clone() for n, v in nets[k].state_dict().items()})
+        if opt_sds is not None:
+            oopts[k].load_state_dict(optim_state_by_name(opt_sds[k], nets[k], onets[k]))

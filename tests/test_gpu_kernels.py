@@ -697,7 +697,7 @@ def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
         A, W = A.bfloat16().float(), W.bfloat16().float()
     rows = L.lib().pkc_gemm_colstats_ok(prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K)
     tiles = -(-M // 128) * -(-N // 128)
-    assert rows == (128 if tiles >= (1024 if prec == 0 else 160) and prec != 3 else 64), rows
+    assert rows == (128 if tiles >= (1024 if prec == 0 else 160) else 64), rows
     Cd = torch.full((M, N), float("nan"), device=DEV)
     work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
     L.call("pkc_gemm_colstats", prec, 1, 1, M, N, K, L.ptr(Ad), K, L.ptr(Wd), K, L.ptr(Cd), N,

@@ -135,7 +135,7 @@ def _seq_vs_oracle(body, bf16=False):
 
 
 def _seq_vs_oracle_run(body, bf16):
-    from flipcheck import assert_counted, step_outliers
+    from flipcheck import assert_counted, resync
     import pkc.neural_networks as NN
     from oracle import nets as ON
     from oracle import run as OR
@@ -205,7 +205,13 @@ def _seq_vs_oracle_run(body, bf16):
     rng_e, rng_o = random.Random(7), random.Random(7)
     snt = 0
     post_out = []
+    report = {}
     for step in range(3):
+        # the engine's state before this step -> the oracle's starting state (parameters, BN
+        # statistics, optimizer state): each step is compared from a common start, so a rounding
+        # flip of one step is counted in that step and does not compound through the next ones
+        eng.sync_state()
+        resync(nets, onets, {k: eng.optimizer_state_dict(k) for k in nets} if step else None, oopt)
         batch = eng.next_seq_batch(rng_e)
         begs, blens, lefts, T = batch
         # oracle batch assembly exactly as core.py:183-200
@@ -247,7 +253,15 @@ def _seq_vs_oracle_run(body, bf16):
         else:
             assert rel < 1e-4, "step %d posterior rel err %.3g (%d of %d above 1e-4)" % (
                 step, rel, nout, relm.numel())
-    report = {}
+        _seq_check_update(body, bf16, step, eng, nets, onets, opts, report, post_out)
+    print("%s%s parameter outliers per step and tensor: %s" % (
+        body, " bf16" if bf16 else "", {k: v for k, v in report.items() if v[0]}))
+
+
+def _seq_check_update(body, bf16, step, eng, nets, onets, opts, report, post_out):
+    """The step's parameter updates (and BN running statistics) from the common start."""
+    from flipcheck import assert_counted, step_outliers
+    eng.sync_state()
     for k in nets:
         for name, v in nets[k].state_dict().items():
             if name.endswith("num_batches_tracked"):
@@ -273,19 +287,19 @@ def _seq_vs_oracle_run(body, bf16):
                 scale = float(sd_o[name.replace("running_mean", "running_var")].double().sqrt().max())
             # elementwise within 1e-4 of the tensor's scale, except counted RMSprop sign steps
             # (tests/flipcheck.py): a gradient element within rounding of zero takes the other
-            # sign and moves its weight by ~9 lr per step; each bounded by 2 x 4.48 lr x steps
+            # sign and moves its weight by ~9 lr in the step; each bounded by 2 x 4.48 lr
             lr = float(opts[k]["arch_lr"])
             scale = max(scale, lr)      # (a tensor whose gradient is rounding-level, e.g. ln0's
             # beta in front of bn0, stays within rounding of its init: lr is its scale)
             n, dmax, rest = step_outliers(v.cpu(), ref, 1e-4, scale)
-            report["%s/%s" % (k, name)] = n
+            report["%d %s/%s" % (step, k, name)] = (n, round(dmax / scale, 6))
             sgd = opts[k]["arch_opt"] == "sgd"
             # bf16 mode (SGD): an operand-rounding flip moves a gradient element, and its update,
-            # by ~2^-9 of one product — counted (<= 0.5 %), each within 1e-3 of the scale
+            # by ~2^-9 of one product — counted (<= 0.5 %), each within 1e-3 of the scale;
+            # RMSprop (fp32): a sign step of one step, 2 x 4.48 lr
             frac = (0.005 if bf16 else 0.0) if sgd else 0.02
-            bound = (1e-3 if bf16 else 1e-4) * scale if sgd else 2 * 4.48 * lr * 3
-            assert_counted("%s %s" % (k, name), n, ref.numel(), frac, dmax, bound + 1e-7,
-                           "(outliers per tensor %s; posteriors above 1e-4 per step %s)" % (
-                               report, post_out))
-    print("%s%s parameter outliers (RMSprop sign steps) per tensor: %s" % (
-        body, " bf16" if bf16 else "", report))
+            bound = (1e-3 if bf16 else 1e-4) * scale if sgd else 2 * 4.48 * lr
+            assert_counted("step %d %s %s" % (step, k, name), n, ref.numel(), frac, dmax,
+                           bound + 1e-7, "(outliers, max diff / scale per tensor %s; posteriors "
+                           "above 1e-4 per step %s)" % (
+                               {a: b for a, b in report.items() if b[0]}, post_out))
