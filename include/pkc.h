@@ -23,8 +23,9 @@ extern "C" {
  * pkc_dense_bwd_args.dz_scratch without a bump); 3: pkc_opt_seg (direct PKC_OP_OPTIM);
  * 4: PKC_PREC_BF16X3; 5: pkc_rnn_args.step_bf16 and its bf16 operand copies;
  * 6: pkc_bn_bwd_epi, pkc_gemm_bnbwd_ok, pkc_dense_bwd_pre;
- * 7: pkc_src_digest, pkc_gemm_grouped_tile, pkc_rnn_args.persist_* (persistent liGRU time loops). */
-#define PKC_ABI_VERSION 7
+ * 7: pkc_src_digest, pkc_gemm_grouped_tile, pkc_rnn_args.persist_* (persistent liGRU time loops);
+ * 8: pkc_rnn_args.qh_exact (exact quantised-h step products). */
+#define PKC_ABI_VERSION 8
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
@@ -32,8 +33,8 @@ enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_
  * BF16X3: compensated bf16 — fp32 operands split at staging into a bf16 head and a bf16 tail
  * (a = hi + lo, lo = bf16(a - hi)) and multiplied as hi*hi + hi*lo + lo*hi on the bf16 MFMA with
  * fp32 accumulation: products to ~2^-16 relative (the dropped lo*lo term), i.e. fp32-class
- * results at 3/16 of the exact-fp32 MFMA cost.  The 64x64 tile bodies (pkc_gemm,
- * pkc_gemm_grouped, the 64-row pkc_gemm_colstats) take it; the 128x128 body does not. */
+ * results at 3/16 of the exact-fp32 MFMA cost.  Every tile body takes it (64x64 and 128x128,
+ * pkc_gemm, pkc_gemm_grouped, pkc_gemm_colstats). */
 enum { PKC_PREC_FP32 = 0, PKC_PREC_BF16 = 1, PKC_PREC_BF16IN = 2, PKC_PREC_BF16X3 = 3 };
 /* neural_networks.py:54-78 act_fun */
 enum { PKC_ACT_LINEAR = 0, PKC_ACT_RELU = 1, PKC_ACT_TANH = 2, PKC_ACT_SIGMOID = 3,
@@ -450,6 +451,15 @@ typedef struct {
    * forward plan's nslots.
    * NULL (or a layer outside these limits): the per-step launches. */
   const int32_t* persist_fwd; const int32_t* persist_bwd; int persist_kb;
+  /* Exact quantised-h step products (qbits > 0, step_bf16 = 0): the caller guarantees U[g] lies on
+   * a weight grid of <= 8 bits (m / 2^(b-1), |m| <= 2^(b-1): exact in bf16) and passes its bf16
+   * copies in U_h[g].  The forward step then writes the grid integers k of q_g (|k| <= 2^(qbits-1))
+   * as two exact bf16 parts and evaluates U q_g = var 2^-(qbits-1) U k on the bf16 MFMA with fp32
+   * accumulation (exact integer sums up to H = 512): the fp32 products to within their own
+   * rounding.  Each step leaves its per-wave max|h| partials in work (two slots by step parity,
+   * at most 2 x H floats; work's 8 x B2 x H hold them) for the next step's var.
+   * 0: the exact-fp32 chain. */
+  int qh_exact;
 } pkc_rnn_args;
 int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream);
 /* out = q1..q_reps (reps consecutive n-float tensors) of the in-place input quantisation that

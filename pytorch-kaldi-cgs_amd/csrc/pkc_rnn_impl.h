@@ -444,7 +444,8 @@ __device__ __forceinline__ void tile_blocks(const int32_t* row, int* blk) {
 
 // Sum the four waves' 32x16 partial tiles (MFMA C layout: col = lane & 15, row = 4*(lane>>4)+i)
 // into tile[32][17]; red is [4][32][17] scratch.  Ends with a barrier.
-template <int NW = 4>
+// R16: 16-row tiles (acc1 unused): rows 0..15 only.
+template <int NW = 4, bool R16 = false>
 __device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1, float* red,
                                             float* tile) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -453,10 +454,10 @@ __device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     rw[(4 * q + i) * 17 + c] = acc0[i];
-    rw[(16 + 4 * q + i) * 17 + c] = acc1[i];
+    if constexpr (!R16) rw[(16 + 4 * q + i) * 17 + c] = acc1[i];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 32 * 16; e += 64 * NW) {
+  for (int e = threadIdx.x; e < (R16 ? 16 : 32) * 16; e += 64 * NW) {
     const int r = e >> 4, cc = e & 15;
     const int o = r * 17 + cc;
     float v = (red[o] + red[32 * 17 + o]) + (red[2 * 32 * 17 + o] + red[3 * 32 * 17 + o]);
@@ -539,6 +540,33 @@ __device__ __forceinline__ void mfma_chain_h(const rbf16x8* va, const rbf16x8* v
   }
 }
 
+// The quantised strip in place (q = Q(x), as qin) and the grid integers k = sign(x) ceil(|x| / var
+// 2^(b-1)) of it as bf16 pairs kh = trunc(k / 256), kl = k - 256 kh (both exact, |kh| <= 128,
+// |kl| <= 255): the operands of the exact quantised-h products (rnn_fwd_mm QX)
+template <bool FAST, int S>
+__device__ __forceinline__ void qsplit_strip(float* v, const QParams& p, rbf16x8* kh, rbf16x8* kl) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const float x = v[s];
+    float m;
+    if constexpr (FAST) {
+      float q = x * p.rcp_s;
+      const float e = __builtin_fmaf(-q, p.var_s, x);
+      q = __builtin_fmaf(e, p.rcp_s, q);
+      m = ceilf(fabsf(q));
+      v[s] = copysignf(m * p.var_s, x);
+    } else {
+      m = ceilf(fabsf(x / p.var) * p.scale);
+      const float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+      v[s] = m * p.iscale * p.var * sg;
+    }
+    const float k = copysignf(m, x);
+    const float hi = truncf(k * (1.f / 256.f));
+    kh[s / 8][s % 8] = (__bf16)hi;
+    kl[s / 8][s % 8] = (__bf16)__builtin_fmaf(-256.f, hi, k);
+  }
+}
+
 // ------------------------------------------------------------------------------- forward step
 // The cell update's inputs at (r, j) that do not depend on this step's products: the gate
 // pre-activations W x (+BN), h_{t-1}, c_{t-1} (LSTM) and the dropout mask.  rnn_fwd_mm requests
@@ -566,7 +594,7 @@ __device__ __forceinline__ EpiIn epi_load(const pkc_rnn_args& a, const RnnIdx& i
 
 // Cell update of step t at (r, j) from the recurrent products acc[g] = (U_g h_{t-1})[r][j].
 template <int CELL, bool QH, bool BF>
-__device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
+__device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
                                         int j, const float* acc, const float* vars, float qscale,
                                         const EpiIn& e) {
   const int H = a.H;
@@ -600,13 +628,13 @@ __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix,
     a.gates[si] = z;
     a.gates[TB2H + si] = rg;
     a.rh[si] = rg * hp;
-    return;
+    return 0.f;
   } else if constexpr (CELL == PKC_CELL_MINGRU) {
     // phase 1 of a minimalGRU step: update gate and z*h (the input of Uh)
     const float z = sigm(e.w[0] + acc[0]);
     a.gates[si] = z;
     a.rh[si] = z * hp;
-    return;
+    return 0.f;
   } else if constexpr (CELL == PKC_CELL_RNN) {
     const float hcr = act_fwd(a.act, e.w[0] + acc[0]);
     h = hcr * m;
@@ -636,6 +664,7 @@ __device__ __forceinline__ void fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix,
   if constexpr (BF)   // the next step's bf16 operand (step_bf16: every step runs a BF instance)
     reinterpret_cast<__bf16*>(a.hs_h)[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = (__bf16)h;
   a.y[ix.out(t, r, j)] = h;
+  return h;
 }
 
 // phase 2 of a GRU / minimalGRU step: h = z*h_{t-1} + (1-z)*act(wh + Uh (r|z)*h_{t-1})*drop
@@ -661,10 +690,17 @@ __device__ __forceinline__ void cand_epi(const pkc_rnn_args& a, const RnnIdx& ix
 // NW waves (4: 256 threads, or 8: the contraction in 32 strips of S — half the operand loads per
 // lane and half the MFMA chain per wave, for the long-H layers whose step is load-latency-bound)
 // BF: bf16 step product (step_bf16: hs_h / U_h operands, mfma_chain_h)
+// QX (quantised h, pkc_rnn_args.qh_exact): U is on an 8-bit grid (m / 128, |m| <= 128: exact in
+// bf16, U_h) and q_g = RN(k var_s) with integers |k| <= 2^15, so U q_g = var_s U k up to the one
+// rounding of each q: k = 256 kh + kl (|kh| <= 128, |kl| <= 255, both exact in bf16) and the two
+// bf16 MFMA chains over (kh, U_h) and (kl, U_h) sum integer multiples of 2^-7 in fp32 (exactly up
+// to H = 512, fp32-rounded beyond) — the products of the fp32 chain to within its own rounding, at
+// 1/16 of its MFMA issue per chain
 template <int NG, int CELL, int PH, int S, bool QH, bool SP = false, int NW = 4, bool R16 = false,
-          bool BF = false>
+          bool BF = false, bool QX = false>
 __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int vw) {
   static_assert(NW == 4 || !SP, "block-sparse tables are laid out for 16 strips");
+  static_assert(!QX || (QH && !SP && !BF && S % 8 == 0), "exact quantised-h products: dense QH");
   static_assert(!BF || (!QH && PH == 0), "bf16 steps: one-phase cells, no quantised h");
   PKC_TR(0);
   PKC_TR(1);
@@ -692,6 +728,17 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   }
   float vars[4] = {0.f, 0.f, 0.f, 0.f};
   const float qscale = QH ? ldexpf(1.f, a.qbits - 1) : 1.f;
+  // QX: var = max|h_{t-1}| from the previous step's per-wave partials (a.work, two slots by step
+  // parity, EW per workgroup), read beside the operand strips — no block reduction
+  constexpr int EW = ((R16 ? 16 : 32) * NU + 63) / 64;   // waves holding epilogue elements
+  const int npart = (int)(gridDim.x * gridDim.y) * EW;
+  float pmax = 0.f;
+  if constexpr (QX) {
+    if (t > 0) {
+      const float* part = a.work + ((t - 1) & 1) * npart;
+      for (int i = lane; i < npart; i += 64) pmax = fmaxf(pmax, part[i]);
+    }
+  }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   if constexpr (BF) {
     const __bf16* srch = reinterpret_cast<const __bf16*>(a.hs_h) + (int64_t)t * B2 * H;
@@ -712,7 +759,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     }
     mfma_chain_h<S, R16>(ha, hb, hu, acc0, acc1);
   } else {
-  float va[S], vb[S], vu[S];
+  float va[S], vb[S], vu[QX ? 1 : S];
+  rbf16x8 hu[QX ? S / 8 : 1];
   if constexpr (SP) {
     static_assert(!QH && PH == 0, "block-sparse U: no quantised h, one-phase cells");
     int blk[S / 16];
@@ -724,7 +772,12 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     const int kb = (w * 4 + q) * S;
     load_strip<S>(src + (int64_t)(ra < B2 ? ra : 0) * H, ra < B2, kb, H, vw, va);
     if constexpr (!R16) load_strip<S>(src + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, vw, vb);
-    load_strip<S>(pu, u < H, kb, H, vw, vu);
+    if constexpr (QX) {
+      const __bf16* puh = reinterpret_cast<const __bf16*>(a.U_h[gi]) + (int64_t)(u < H ? u : 0) * H;
+      load_strip_h<S>(puh, u < H, kb, H, vw == 4 && H % 8 == 0, hu);
+    } else {
+      load_strip<S>(pu, u < H, kb, H, vw, vu);
+    }
   }
   if constexpr (R16) {
 #pragma unroll
@@ -743,7 +796,11 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     // <= var (monotone rounding of ceil(.) / 2^(b-1) <= 1), so var_{g+1} = max|q_{g+1}| = var_g.
     // (NW waves x 4 lane groups x S = H: with 8 waves each holds half a 4-wave strip)
     __shared__ float qred[2 * NW];
-    {
+    if constexpr (QX) {
+      const float v1 = warp_max(pmax);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) vars[g] = v1;
+    } else {
       float mx = -INFINITY, mn = INFINITY;
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -773,15 +830,51 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
     // accumulator — the same sums as masking the other gates' U columns to zero, without the
     // per-gate mask pass (S selects per lane per gate)
     f32x4 ag0[NG], ag1[NG];
+    bool fixed = false;           // QX, 4 gates: q3 == q2 on every element of this wave's strips
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if (qon) {
-        if (qp.fast) qin_strips<true, S, R16>(va, vb, qp);
-        else qin_strips<false, S, R16>(va, vb, qp);
-      }
       ag0[g] = f32x4{0.f, 0.f, 0.f, 0.f};
       ag1[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mfma_chain<S, R16>(va, vb, vu, ag0[g], ag1[g]);
+      if constexpr (QX) {
+        if (g >= 2 && fixed) {    // then q4 = Q(q3) = q3 = q2: gates 2 and 3 repeat gate 1's sums
+          ag0[g] = ag0[NG > 1 ? 1 : 0];
+          ag1[g] = ag1[NG > 1 ? 1 : 0];
+        } else if (qon) {
+          rbf16x8 ah[S / 8], al[S / 8], bh[R16 ? 1 : S / 8], bl[R16 ? 1 : S / 8];
+          if (qp.fast) qsplit_strip<true, S>(va, qp, ah, al);
+          else qsplit_strip<false, S>(va, qp, ah, al);
+          if constexpr (!R16) {
+            if (qp.fast) qsplit_strip<true, S>(vb, qp, bh, bl);
+            else qsplit_strip<false, S>(vb, qp, bh, bl);
+          }
+          f32x4 h0 = ag0[g], h1 = ag1[g], l0 = ag0[g], l1 = ag1[g];
+          mfma_chain_h<S, R16>(ah, bh, hu, h0, h1);
+          mfma_chain_h<S, R16>(al, bl, hu, l0, l1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ag0[g][i] = __builtin_fmaf(256.f, h0[i], l0[i]) * qp.var_s;
+            if constexpr (!R16) ag1[g][i] = __builtin_fmaf(256.f, h1[i], l1[i]) * qp.var_s;
+          }
+          if (NG == 4 && g == 1) {
+            // Q is idempotent on most grid values (k var_s divides back to k), but the rounding
+            // of k var_s can push one to k + 1 once: test the third call on this wave's strips
+            bool eq = true;
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2) {
+              eq = eq && (qp.fast ? qin<true>(va[s2], qp) : qin<false>(va[s2], qp)) == va[s2];
+              if constexpr (!R16)
+                eq = eq && (qp.fast ? qin<true>(vb[s2], qp) : qin<false>(vb[s2], qp)) == vb[s2];
+            }
+            fixed = __all(eq);
+          }
+        }
+      } else {
+        if (qon) {
+          if (qp.fast) qin_strips<true, S, R16>(va, vb, qp);
+          else qin_strips<false, S, R16>(va, vb, qp);
+        }
+        mfma_chain<S, R16>(va, vb, vu, ag0[g], ag1[g]);
+      }
     }
     acc0 = ag0[0];
     acc1 = ag1[0];
@@ -800,8 +893,9 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));   // the products complete before stamp 4
 #endif
   PKC_TR(4);
-  reduce_tile<NW>(acc0, acc1, red, tile);
+  reduce_tile<NW, R16>(acc0, acc1, red, tile);
   PKC_TR(5);
+  float hmax = 0.f;               // QX: max|h| over this thread's elements
   for (int p = threadIdx.x; p < 32 * NU; p += NTH) {
     const int rl = p / NU, ul = p % NU;
     const int r = r0 + rl, j = u0 + ul;
@@ -812,8 +906,16 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < NG; ++g) acc[g] = tile[rl * 17 + g * NU + ul];
-      if constexpr (PF) fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, pre);
-      else fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
+      float h;
+      if constexpr (PF) h = fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, pre);
+      else h = fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
+      if constexpr (QX) hmax = fmaxf(hmax, fabsf(h));
+    }
+  }
+  if constexpr (QX) {             // this step's max|h| partials, one per epilogue wave
+    if (w < EW) {
+      const float m = warp_max(hmax);
+      if (lane == 0) a.work[(t & 1) * npart + (blockIdx.x + gridDim.x * blockIdx.y) * EW + w] = m;
     }
   }
   PKC_TR(6);
@@ -1107,12 +1209,25 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
           else
             hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true, 4, true>), g16, dim3(RT), 0, s,
                                *a, t, vw);
-        } else if (a->qbits > 0 && qh_eight_waves(S))
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), g16,
-                             dim3(2 * RT), 0, s, *a, t, vw);
-        else if (a->qbits > 0)
-          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), g16, dim3(RT), 0, s,
-                             *a, t, vw);
+        } else if (a->qbits > 0 && qh_eight_waves(S)) {
+          bool done = false;
+          if constexpr (CELL == PKC_CELL_LSTM && (S / 2) % 8 == 0)
+            if ((done = a->qh_exact != 0))
+              hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true, false, true>),
+                                 g16, dim3(2 * RT), 0, s, *a, t, vw);
+          if (!done)
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, true, false, 8, true>), g16,
+                               dim3(2 * RT), 0, s, *a, t, vw);
+        } else if (a->qbits > 0) {
+          bool done = false;
+          if constexpr (CELL == PKC_CELL_LSTM && S % 8 == 0)
+            if ((done = a->qh_exact != 0))
+              hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true, false, true>), g16,
+                                 dim3(RT), 0, s, *a, t, vw);
+          if (!done)
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, true>), g16, dim3(RT), 0,
+                               s, *a, t, vw);
+        }
         else if (eight_waves(S))
           hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8, true>), g16,
                              dim3(2 * RT), 0, s, *a, t, vw);
@@ -1125,8 +1240,15 @@ static int fwd_impl_s(const pkc_rnn_args* a, hipStream_t s) {
                              dim3(RT), 0, s, *a, t, vw);
         else
           hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, false, true>), g1, dim3(RT), 0, s, *a, t, vw);
-      } else if (a->qbits > 0)
-        hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
+      } else if (a->qbits > 0) {
+        bool done = false;
+        if constexpr (CELL == PKC_CELL_LSTM && S % 8 == 0)
+          if ((done = a->qh_exact != 0))
+            hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true, false, 4, false, false, true>), g1,
+                               dim3(RT), 0, s, *a, t, vw);
+        if (!done)
+          hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S, true>), g1, dim3(RT), 0, s, *a, t, vw);
+      }
       else if (eight_waves(S))
         hipLaunchKernelGGL((rnn_fwd_mm<G, CELL, 0, S / 2, false, false, 8>), g1, dim3(2 * RT), 0, s,
                            *a, t, vw);
@@ -1366,6 +1488,11 @@ static int check(const pkc_rnn_args* a, bool bwd) {
     PKC_CHECK_ARG(a->hs_h, "pkc_rnn: bf16 steps need hs_h");
     for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U_h[g], "pkc_rnn: bf16 steps need U_h[%d]", g);
     if (bwd) PKC_CHECK_ARG(a->ut_h && a->dgates_h, "pkc_rnn_bwd: bf16 steps need ut_h, dgates_h");
+  }
+  if (a->qh_exact) {
+    PKC_CHECK_ARG(a->qbits > 0 && a->qbits <= 16 && !a->step_bf16 && a->work,
+                  "pkc_rnn: qh_exact needs quantised h (qbits <= 16), fp32 step products and work");
+    for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U_h[g], "pkc_rnn: qh_exact needs U_h[%d]", g);
   }
   if (a->kmap_fwd || a->kmap_bwd) {
     PKC_CHECK_ARG((a->cell == PKC_CELL_LIGRU || a->cell == PKC_CELL_LSTM) && a->qbits <= 0,

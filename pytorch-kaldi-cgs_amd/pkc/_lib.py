@@ -9,7 +9,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
-ABI_VERSION = 7         # include/pkc.h PKC_ABI_VERSION
+ABI_VERSION = 8         # include/pkc.h PKC_ABI_VERSION
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 PREC_FP32, PREC_BF16, PREC_BF16IN, PREC_BF16X3 = 0, 1, 2, 3
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
@@ -79,7 +79,8 @@ class RnnArgs(C.Structure):
                 ("ln_stat", vp), ("ln_g", vp), ("ln_dgamma", vp), ("ln_dbeta", vp),
                 ("kmap_fwd", vp), ("kmap_bwd", vp), ("kmap_s_fwd", C.c_int), ("kmap_s_bwd", C.c_int),
                 ("step_bf16", C.c_int), ("hs_h", vp), ("U_h", vp * 4), ("ut_h", vp), ("dgates_h", vp),
-                ("persist_fwd", vp), ("persist_bwd", vp), ("persist_kb", C.c_int)]
+                ("persist_fwd", vp), ("persist_bwd", vp), ("persist_kb", C.c_int),
+                ("qh_exact", C.c_int)]
 
 
 class GemmProblem(C.Structure):

@@ -70,6 +70,10 @@ RNN_BF16_SPARSE = os.environ.get("PKC_RNN_BF16_SPARSE", "0") != "0"     # block-
 # persistent liGRU time loops for block-sparse U in bf16 step mode (pkc_rnn_persist.hip; 0: the
 # per-step launches)
 RNN_PERSIST = os.environ.get("PKC_RNN_PERSIST", "1") != "0"
+# quantised-h LSTM steps with U on an 8-bit (or coarser) weight grid (C5): the step products as
+# exact integer sums on the bf16 MFMA (pkc_rnn_args.qh_exact) in every precision — the fp32
+# products to within their own rounding; 0: the exact-fp32 chain
+RNN_QH_EXACT = os.environ.get("PKC_RNN_QH_EXACT", "1") != "0"
 SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
@@ -934,6 +938,8 @@ class Engine:
                               xw_h=torch.zeros(M * K, dtype=bf, device=dev))
             if sp["ibits"]:
                 lb["hq"] = _f32((T + 1) * B2 * H, dev)      # q4(h_{t-1}) per step
+                if RNN_QH_EXACT and 0 < sp["qbits"] <= 8:    # exact bf16 copies of the grid U
+                    lb["U_hq"] = torch.zeros(G * H * H, dtype=torch.bfloat16, device=dev)
                 if n.lbuf:                                   # layers >= 1: q1..qG of y_{l-1}
                     lb["xq"] = _f32(G * M * K, dev)
                     lb["qwork"] = _f32(256, dev)
@@ -1644,6 +1650,10 @@ class Engine:
                 a.persist_fwd, a.persist_bwd = (lb["persist_fwd"].data_ptr(),
                                                 lb["persist_bwd"].data_ptr())
                 a.persist_kb = persist_geometry()[1]
+        if lb.get("U_hq") is not None:
+            a.qh_exact = 1
+            for g in range(n.G):
+                a.U_h[g] = lb["U_hq"].data_ptr() + 2 * g * H * H
         if sp.get("ln"):
             a.ln_gamma, a.ln_beta, a.ln_eps = sp["ln_gamma"].data_ptr(), sp["ln_beta"].data_ptr(), 1e-6
             a.ln_xhat, a.ln_stat = lb["ln_xhat"].data_ptr(), lb["ln_stat"].data_ptr()
@@ -1716,7 +1726,7 @@ class Engine:
                 self._k("rnn_bn_fwd H=%d" % H, 0, 4.0 * M * H * (sf + 2), "pkc_dense_fwd",
                         C.byref(a), ptr(lb["work"]), s)
             ra = self._rnn_args(n, li, train, T)
-            if ra.step_bf16:                  # this step's U (after the last update) as bf16
+            if ra.step_bf16 or ra.qh_exact:   # this step's U (after the last update) as bf16
                 for g in range(n.G):
                     self._k("cast_bf16 U", 0, 6.0 * H * H, "pkc_cast_bf16", ptr(n.wq(li, "U", g)),
                             C.c_void_p(ra.U_h[g]), H * H, s)
