@@ -538,6 +538,19 @@ def main():
     sweep = {}
     if rank == 0 and world == 1 and not args.no_batch_sweep:
         sweep = batch_sweep(prec)
+        if args.prec == "bf16" and not args.no_fp32:
+            # the reference-precision modes at the large batches: exact fp32 and compensated bf16
+            # (fp32-class products on the bf16 MFMA), with the first-step posterior error of each
+            # batch against the oracle (north_star: 1e-4)
+            by = {"bf16": sweep}
+            for name, pr in (("fp32", _lib.PREC_FP32), ("bf16x3", _lib.PREC_BF16X3)):
+                by[name] = batch_sweep(pr)
+                torch.cuda.empty_cache()
+            by["bf16x3_over_fp32"] = {b: round(by["bf16x3"][b] / by["fp32"][b], 3) for b in by["fp32"]}
+            if not args.no_cpu_baseline:
+                by["bf16x3_posterior_max_rel_err"] = {
+                    b: parity_leg(_lib.PREC_BF16X3, int(b))["posterior_max_rel_err"] for b in by["fp32"]}
+            extra["batch_sweep_by_prec"] = by
     seq = {}
     if rank == 0 and world == 1 and not args.no_seq_configs:
         # BASELINE configs C3-C5: C3 (the largest single-GPU config) measured like the headline,
