@@ -800,3 +800,60 @@ def test_engine_eager_adam_segs_bounded():
     assert len(eng._seg_keep) == n0, (n0, len(eng._seg_keep))
     loss, _ = eng.loss_values()
     assert np.isfinite(loss)
+
+
+@pytest.mark.parametrize("variant", ["sgd_rmsprop", "momentum_adam", "quant_odd"])
+def test_opt_direct_form_matches_map_form(variant):
+    """the direct PKC_OP_OPTIM form (pkc_opt_seg runs in the launch arguments,
+    PKC_OPT_DIRECT=1, the default) against the chunk-map form on the same model and data, 3 steps,
+    bit-identical parameters, BatchNorm statistics and optimizer state.  Covers SGD without momentum
+    (no s1 buffer) + RMSprop, SGD with momentum + Adam, and 8-bit quantised weights (qout written
+    through the segments) with odd-sized, not 16-byte-aligned tensors (layers 1000 / 517 / 33 /
+    1023 / 999 units), whose launches also exceed PKC_OPT_SEGS_MAX segments and fall back to the
+    map."""
+    import pkc.engine as E
+    from pkc.engine import Engine, parse_model
+    cfg = c1_config()
+    body = cfg["architecture1"]
+    if variant == "momentum_adam":
+        body.update(opt_momentum="0.9")
+        for sec in ("architecture2", "architecture3"):
+            cfg[sec].update(arch_opt="adam", opt_betas="0.9,0.999", opt_eps="1e-8",
+                            opt_amsgrad="False")
+    if variant == "quant_odd":
+        body.update(dnn_lay="1000,517,33,1023,999", mlp_quant="True")
+    dims = (("architecture1", 440), ("architecture2", int(body["dnn_lay"].split(",")[-1])),
+            ("architecture3", int(body["dnn_lay"].split(",")[-1])))
+    B = 128
+    rs = np.random.RandomState(9)
+    X = torch.from_numpy(rs.randn(B * 4, 440).astype(np.float32)).to(DEV)
+    lab = torch.from_numpy(np.stack([rs.randint(0, 1928, B * 4), rs.randint(0, 48, B * 4)], 1)
+                           .astype(np.int32)).to(DEV)
+    states = {}
+    for direct in (True, False):
+        nets, opts = build_nets(cfg, dims)
+        for n in nets.values():
+            n.to(DEV).train()
+        old = E.OPT_DIRECT
+        E.OPT_DIRECT = direct
+        try:
+            eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fmllr": (0, 440)},
+                         ["lab_cd", "lab_mono"], batch=B, seed=3)
+            eng.bind_chunk(X, lab, B * 4)
+            for _ in range(3):
+                eng.train_step()
+            torch.cuda.synchronize()
+            eng.sync_state()
+        finally:
+            E.OPT_DIRECT = old
+        st = {}
+        for a, net in nets.items():
+            for k, v in net.state_dict().items():
+                st["%s/%s" % (a, k)] = v.detach().cpu().clone()
+            for pi, d in eng.optimizer_state_dict(a)["state"].items():
+                for k, v in d.items():
+                    st["%s/opt%d/%s" % (a, pi, k)] = torch.as_tensor(v).cpu().clone()
+        states[direct] = st
+    assert states[True].keys() == states[False].keys()
+    for k in states[True]:
+        assert torch.equal(states[True][k], states[False][k]), k
