@@ -86,3 +86,16 @@ def test_persistent_ligru_bptt_matches_per_step_short():
     rel = ((pp - ps).abs() / ps.abs().clamp_min(1e-3)).max().item()
     print("T <= 8: posterior max rel diff %.3g, flat gradient rel diff %.3g" % (rel, gerr))
     assert rel < 1e-3 and gerr < 1e-3, (rel, gerr)
+
+
+def test_persistent_ligru_very_short_sentences():
+    """Edge lengths: padded batches of T = 1..3 steps (the BPTT loop then runs 0-2 steps and the
+    carry hand-off at its end is skipped or taken) — forward and gradients as the per-step form."""
+    used_p, out_p, _ = _run(True, steps=2, lo=1, hi=4)
+    used_s, out_s, _ = _run(False, steps=2, lo=1, hi=4)
+    assert all(used_p) and not any(used_s)
+    for s, ((pp, gp, lp), (ps, gs, ls)) in enumerate(zip(out_p, out_s)):
+        gerr = (gp - gs).norm().item() / gs.norm().item()
+        rel = ((pp - ps).abs() / ps.abs().clamp_min(1e-3)).max().item()
+        print("T <= 3 step %d: posterior max rel diff %.3g, flat gradient rel diff %.3g" % (s, rel, gerr))
+        assert rel < 1e-3 and gerr < 1e-3, (s, rel, gerr)

@@ -1,7 +1,8 @@
 """Sequence training steps replayed from captured graphs (Engine.capture on a sequence model: one
 graph per padded length T, captured at its first batch) against the same steps issued eagerly:
 bit-identical losses, posteriors and trained parameters, for liGRU + HCGS (block-sparse U), LSTM,
-bidirectional LSTM and LSTM with 8-bit weights / 16-bit inputs.  The batch metadata reaches the
+bidirectional LSTM and LSTM with 8-bit weights / 16-bit inputs (exact quantised-h products), and
+in bf16 mode liGRU + HCGS (the persistent time loops) and the bidirectional LSTM (bf16 steps).  The batch metadata reaches the
 device through the pinned ring (no host synchronisation per batch), and a batch's data-parallel
 frame weight follows the batch it belongs to (SeqBatch.index)."""
 import copy
@@ -37,10 +38,14 @@ def _build(body):
     return cfg, nets, opts
 
 
-@pytest.mark.parametrize("body", ["ligru_hcgs_sparse", "lstm", "lstm_bidir", "lstm_quant"])
+@pytest.mark.parametrize("body", ["ligru_hcgs_sparse", "lstm", "lstm_bidir", "lstm_quant",
+                                  "ligru_hcgs_sparse:bf16", "lstm_bidir:bf16"])
 def test_seq_graph_replay_equals_eager(body):
     import pkc.engine as E
+    from pkc import _lib as L
     from pkc.engine import Engine, parse_model
+    body, _, mode = body.partition(":")
+    prec = L.PREC_BF16 if mode == "bf16" else L.PREC_FP32
     cfg, nets0, opts = _build(body)
     F, B = 20, 4
     rs = np.random.RandomState(0)
@@ -57,7 +62,11 @@ def test_seq_graph_replay_equals_eager(body):
         for graphs in (False, True):
             nets = copy.deepcopy(nets0)
             eng = Engine(nets, opts, parse_model(cfg["model"]["model"]), {"fea": (0, F)},
-                         ["lab_cd", "lab_mono"], batch=B, max_len=16, seed=1)
+                         ["lab_cd", "lab_mono"], batch=B, max_len=16, seed=1, prec=prec)
+            if mode == "bf16" and body.startswith("ligru"):
+                assert all(lb.get("persist_fwd") is not None for lb in eng.nodes[0].lbuf)
+            if body == "lstm_quant":
+                assert all(lb.get("U_hq") is not None for lb in eng.nodes[0].lbuf)
             if graphs:
                 assert eng.capture()
             eng.bind_chunk(X, lab, end[-1], end_index=end)
