@@ -91,6 +91,34 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Phase trace (PKC_TRACE measurement builds only): wave `lane 0` of workgroup 0 accumulates the
+// shader-clock cycles of each step phase over the loop — 0 fragment loop, 1 wait at the products
+// barrier, 2 cell-update values, 3 store issue, 4 wait at the step-end barrier — read back with
+// pkc_trace_read_persist ([fwd, bwd][wave][8]: the five sums, then T).  The stamps sit where the
+// loop already drains the LDS counter.
+#ifdef PKC_TRACE
+__device__ unsigned long long ptrace_buf[2 * NW * 8];
+#define PTR_DECL unsigned long long pt_acc[5] = {0, 0, 0, 0, 0}, pt_last = 0
+#define PTR_MARK(i)                                                     \
+  do {                                                                  \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();       \
+    if ((i) > 0) pt_acc[(i) - 1] += now_ - pt_last;                     \
+    pt_last = now_;                                                     \
+  } while (0)
+#define PTR_STORE(k)                                                    \
+  do {                                                                  \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                   \
+      volatile unsigned long long* b_ = ptrace_buf + ((k) * NW + (threadIdx.x >> 6)) * 8; \
+      for (int i_ = 0; i_ < 5; ++i_) b_[i_] = pt_acc[i_];               \
+      b_[5] = (unsigned long long)T;                                    \
+    }                                                                   \
+  } while (0)
+#else
+#define PTR_DECL do { } while (0)
+#define PTR_MARK(i) do { } while (0)
+#define PTR_STORE(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ int pl_tile(int e) { return e & 255; }
 __device__ __forceinline__ int pl_blk(int e) { return ((e >> 8) & 255) - 1; }
 __device__ __forceinline__ bool pl_flush(int e) { return (e >> 16) & 1; }
@@ -171,7 +199,9 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   float* __restrict__ y = a.y;
   const int BH = B * H, B2H = B2 * H, BD = B * D, iTBH = (int)TBH;
   __syncthreads();
+  PTR_DECL;
   for (int t = 0; t < T; ++t) {
+    PTR_MARK(0);
     const __bf16* img = hl + (t & 1) * IMG;
     // this step's gate pre-activations (independent of the recurrence: in flight during the MFMAs)
     // (every lane loads — element 0 for an unused slot — and every lane consumes the values below:
@@ -209,7 +239,9 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
       // the whole plan's reads hoisted to the top (4 VGPRs each)
       if (f % SW == SW - 1) __builtin_amdgcn_sched_barrier(0);
     }
+    PTR_MARK(1);
     lds_barrier();
+    PTR_MARK(2);
     // liGRU cell update (pkc_rnn_impl.h fwd_epi, CELL_LIGRU)
     __bf16* nimg = hl + ((t + 1) & 1) * IMG;
     const int tst = t * B2H;
@@ -226,6 +258,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
       const float h = zv[j] * hp[j] + (1.f - zv[j]) * (hv[j] * mk[j]);
       hp[j] = ok ? h : 0.f;                          // (a select: consumed on every lane)
     }
+    PTR_MARK(3);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       if (el[j] < 0) continue;
@@ -237,8 +270,11 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
       y[(rev[j] ? T - 1 - t : t) * BD + oout[j]] = hp[j];
       nimg[el[j]] = (__bf16)hp[j];
     }
+    PTR_MARK(4);
     lds_barrier();
+    PTR_MARK(5);
   }
+  PTR_STORE(0);
 }
 
 // ----------------------------------------------------------------------------------- BPTT
@@ -316,7 +352,9 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
 #pragma unroll
   for (int j = 0; j < EPT; ++j) zc[j] = gates[(T - 1) * B2H + ost[j]];
   __syncthreads();
+  PTR_DECL;
   for (int tt = T - 2; tt >= 0; --tt) {
+    PTR_MARK(0);
     const int t = tt + 1;
     const __bf16* img = dl[t & 1];
     const int tst = tt * B2H;
@@ -347,7 +385,9 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       acc = fl ? f32x4{0.f, 0.f, 0.f, 0.f} : acc;
       if (f % SW == SW - 1) __builtin_amdgcn_sched_barrier(0);
     }
+    PTR_MARK(1);
     lds_barrier();
+    PTR_MARK(2);
     // bwd_step_epi + gate_grads (CELL_LIGRU) for step tt
     __bf16* nimg = dl[tt & 1];
     // values first, then the stores (as the forward's)
@@ -373,6 +413,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       nimg[ei] = (__bf16)d0v[j];
       nimg[IMG + ei] = (__bf16)d1v[j];
     }
+    PTR_MARK(3);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       if (el[j] < 0) continue;
@@ -382,8 +423,11 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       dgh[si] = (__bf16)d0v[j];
       dgh[iTB2H + si] = (__bf16)d1v[j];
     }
+    PTR_MARK(4);
     lds_barrier();
+    PTR_MARK(5);
   }
+  PTR_STORE(1);
   // the carry of step 0 where the per-step form leaves it (slot (T-1) & 1)
   if (T > 1) {
     const int p0 = (T - 1) & 1;
@@ -440,3 +484,12 @@ extern "C" int pkc_rnn_persist_geometry(int* nwaves, int* nslots_fwd, int* nslot
   if (hmax) *hmax = HMAX;
   return PKC_OK;
 }
+
+#ifdef PKC_TRACE
+// measurement builds only: the persistent loops' per-wave phase sums (n <= 2 * 8 * 8)
+extern "C" int pkc_trace_read_persist(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pkc::persist::ptrace_buf),
+                             sizeof(unsigned long long) * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -185,6 +185,48 @@ def persist_geometry():
     return tuple(x.value for x in v)
 
 
+def _balance(sizes, nw):
+    """Tiles -> waves minimising the largest per-wave fragment count (the step's MFMA chain is the
+    slowest wave's): longest-processing-time first, then moves and swaps off the fullest wave while
+    they lower it (deterministic).  C3's BPTT plans: 23-24 -> 22 slots on the fullest wave."""
+    load, asg = [0] * nw, [0] * len(sizes)
+    for t in sorted(range(len(sizes)), key=lambda t: (-sizes[t], t)):
+        v = min(range(nw), key=lambda v: (load[v], v))
+        load[v] += sizes[t]
+        asg[t] = v
+    for _ in range(4 * len(sizes)):
+        mx = max(load)
+        src = load.index(mx)
+        mine = [t for t in range(len(sizes)) if asg[t] == src]
+        done = False
+        for t in mine:                                  # a move that lowers the maximum
+            for v in range(nw):
+                if v != src and load[v] + sizes[t] < mx:
+                    load[src] -= sizes[t]
+                    load[v] += sizes[t]
+                    asg[t] = v
+                    done = True
+                    break
+            if done:
+                break
+        if not done:                                    # or a swap with a smaller tile
+            for t in mine:
+                for u in range(len(sizes)):
+                    v = asg[u]
+                    d = sizes[t] - sizes[u]
+                    if v != src and d > 0 and load[v] + d < mx:
+                        load[src] -= d
+                        load[v] += d
+                        asg[t], asg[u] = v, src
+                        done = True
+                        break
+                if done:
+                    break
+        if not done:
+            break
+    return asg
+
+
 def persist_plans(mask):
     """Fragment plans of the persistent liGRU loops (pkc_rnn_args.persist_*) for a static U mask
     (H x H bool, any gate): forward tiles of 16 units x the 32-wide blocks of k they read, BPTT
@@ -204,11 +246,9 @@ def persist_plans(mask):
     out = []
     for pres, nslot in ((fwd, nsf), (bwd, nsb)):
         frags = [np.nonzero(pres[t])[0].tolist() or [-1] for t in range(nt)]
-        load, lists = [0] * nw, [[] for _ in range(nw)]
-        for t in sorted(range(nt), key=lambda t: -len(frags[t])):
-            wv = min(range(nw), key=lambda v: load[v])
-            load[wv] += len(frags[t])
-            lists[wv].append(t)
+        asg = _balance([len(f) for f in frags], nw)
+        lists = [[t for t in range(nt) if asg[t] == wv] for wv in range(nw)]
+        load = [sum(len(frags[t]) for t in lst) for lst in lists]
         if max(load) > nslot:
             return None
         tab = np.zeros((nw, nslot), dtype=np.int32)

@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--config", default="c5")
     ap.add_argument("--prec", default="fp32")
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--persist", action="store_true",
+                    help="the persistent liGRU loops' per-wave phase sums instead (C3, bf16)")
     a = ap.parse_args()
+    if a.persist:
+        return persist(a)
     assert "libpkc_trace" in os.environ.get("PKC_LIB", ""), "set PKC_LIB to the trace build"
     import torch
     import bench_seq
@@ -55,6 +59,34 @@ def main():
                                       "ns_median": round(float(np.median(cyc[:, i])) / clk, 1),
                                       "cycles_max": float(cyc[:, i].max())}
                       for i in range(5)}}
+    print(json.dumps(out, indent=1))
+
+
+PPHASES = ["fragment loop (MFMAs)", "products barrier wait", "cell-update values",
+           "store issue", "step-end barrier wait"]
+
+
+def persist(a):
+    """Per step and wave (workgroup 0 of the last forward / BPTT loop launched): cycles of each
+    phase, averaged over the loop's steps."""
+    import torch
+    import bench_seq
+    from pkc import _lib as L
+    bench_seq.run(a.config, a.steps, 1, prec=a.prec)
+    torch.cuda.synchronize()
+    n = 2 * 8 * 8
+    buf = (C.c_ulonglong * n)()
+    assert L.lib().pkc_trace_read_persist(buf, n) == 0
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(2, 8, 8).astype(np.int64)
+    out = {"config": a.config, "prec": a.prec}
+    for k, name in enumerate(("forward loop", "BPTT loop")):
+        T = int(t[k, 0, 5])
+        steps = T if k == 0 else max(T - 1, 1)
+        per = t[k, :, :5] / float(steps)
+        out[name] = {"T": T, "cycles_per_step_by_wave": {
+            PPHASES[i]: [round(float(v), 1) for v in per[:, i]] for i in range(5)},
+            "cycles_per_step_wave_mean": {PPHASES[i]: round(float(per[:, i].mean()), 1)
+                                          for i in range(5)}}
     print(json.dumps(out, indent=1))
 
 
