@@ -14,9 +14,12 @@
 //     step parity) whose batch rows sit at MFMA rows 0, 4, 8, 12, so the C layout (row 4 q + i in
 //     lane group q) puts batch row q's result in register 0 of lane group q: every lane carries a
 //     live element out of the chain;
-//   * per step: each wave runs its fragment list (whole output tiles, balanced over the waves by
-//     the host), flushing each finished tile's products to LDS; barrier; the cell update spread
-//     over all threads (gates / h / y stores, the next A image); barrier.
+//   * per step: each wave runs its fragment list (the fragments dealt to the waves in equal runs
+//     by the host; a tile cut between two waves flushes its second part into a spill-over tile),
+//     storing each finished tile's products to LDS, with the next slot's operands read under the
+//     current slot's MFMAs; barrier; the cell update spread over all threads (adding a cut tile's
+//     spill-over; gates / h / y stores, the next A image); barrier.  (LDS float atomics for the
+//     cut tiles measured 2x slower steps than these plain stores.)
 // The per-step form pays a launch boundary and a cross-XCD fetch of h_{t-1} every step (~5 us for
 // C3); here a step is the MFMA chains, two LDS passes and two workgroup barriers.
 // The BPTT loop is the same with U^T fragments (output tile = 16 columns k, contraction = units j
@@ -25,9 +28,9 @@
 // Numerics: the bf16 step mode's (bf16 h / dgates / U operands, fp32 accumulation and cell math);
 // only the order of the fp32 block sums differs from the per-step kernels.
 //
-// Plan tables (host, pkc.engine): per wave NF int32 entries, bits 0-7 output tile, 8-15 block + 1
-// (0: none — a tile with no nonzero block still flushes its zeros), bit 16 flush (the tile's last
-// fragment), bit 17 valid.
+// Plan tables (host, pkc.engine.persist_plans): per wave NF int32 entries, bits 0-7 output tile,
+// 8-15 block + 1, bit 16 flush (the last fragment of this wave's part of the tile), bit 17 valid,
+// bit 18 the flush of a cut tile's second part, 19-21 its spill-over tile.
 #define PKC_RNN_PERSIST
 #include "pkc_rnn_impl.h"
 
@@ -36,11 +39,11 @@ namespace persist {
 
 constexpr int NW = 8, NT = 64 * NW;     // two waves per SIMD
 constexpr int RPW = 4;                  // batch rows per workgroup
-// fragment slots per wave (plan width) and how many of them are register-resident (the rest,
-// NF - NFR per wave, in LDS): the forward holds 2 x 4 VGPRs per slot and fewer live epilogue
-// values than the BPTT, which needs five prefetched inputs per element
-constexpr int FNF = 26, FNFR = 18;
-constexpr int BNF = 24, BNFR = 16;
+// fragment slots per wave (plan width: ceil(fragments / 8) <= NF, C3: 22) and how many of them
+// are register-resident (the rest, NF - NFR per wave, in LDS); 16 register slots leave room for
+// the one-slot operand look-ahead
+constexpr int FNF = 23, FNFR = 16;
+constexpr int BNF = 22, BNFR = 14;
 constexpr int HMAX = 576;               // H <= HMAX (36 tiles of 16)
 // row stride of the bf16 A images (elements): 16-byte rows at dword offsets 0, 48, 32, 16 mod 64
 // banks for the 4 live rows, so an A-fragment read (4 rows x 4 lane groups x 16 B) is conflict-free
@@ -48,7 +51,6 @@ constexpr int HP = 608;
 constexpr int IMG = RPW * HP;           // one A image (bf16 elements)
 constexpr int EPT = (RPW * HMAX + NT - 1) / NT;   // epilogue elements per thread
 constexpr int FRAG = 64 * 16;           // bytes of one B fragment (64 lanes x 8 bf16)
-constexpr int SW = 2;                   // plan slots per scheduling window
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
@@ -123,6 +125,39 @@ __device__ __forceinline__ int pl_tile(int e) { return e & 255; }
 __device__ __forceinline__ int pl_blk(int e) { return ((e >> 8) & 255) - 1; }
 __device__ __forceinline__ bool pl_flush(int e) { return (e >> 16) & 1; }
 __device__ __forceinline__ bool pl_valid(int e) { return (e >> 17) & 1; }
+__device__ __forceinline__ bool pl_spill(int e) { return (e >> 18) & 1; }
+__device__ __forceinline__ int pl_sidx(int e) { return (e >> 19) & 7; }
+constexpr int NTILE = HMAX / 16;        // output tiles of a layer
+// product-tile row: H columns, 16 for tile columns past H, then NW spill-over tiles of 16
+constexpr int XCOL = HMAX + 16, AW = XCOL + NW * 16;
+// el: an element's A-image position (bits 0-15) and its tile's spill-over index + 1 (bits 16-19)
+__device__ __forceinline__ int el_pos(int el) { return el & 0xFFFF; }
+__device__ __forceinline__ int el_spill(int el) { return (el >> 16) - 1; }
+// the slot's 32-wide A block (block 0 for an empty slot: any block, its B fragments are zeros)
+__device__ __forceinline__ int slot_blk(int e) { return pl_valid(e) ? max(pl_blk(e), 0) : 0; }
+
+// A cell-update element's offsets, from its A-image position el (row rl = el / HP, unit u) — an
+// unused slot (el < 0) takes element 0 of the workgroup's first row (valid addresses, unused
+// values).  Recomputed where used (a few integer ops) rather than held in registers through the
+// fragment loop: the opaque copy keeps the compiler from hoisting them out of the time loop.
+struct ElemOff {
+  int ost;    // (t, r, u) of (T, B2, H): + t B2 H
+  int opre;   // (tt, rr, u) of (T, B, H): + tt B H
+  int oout;   // (tt, rr, u) of (T, B, D): + tt B D
+  bool rev;   // the reversed direction (rows >= B): time T-1-t
+};
+__device__ __forceinline__ ElemOff elem_off(int el, int r0, int H, int B, int D, bool bidir) {
+  int e = el < 0 ? 0 : el_pos(el);
+  asm volatile("" : "+v"(e));
+  const int rl = e / HP, u = e - rl * HP, r = r0 + rl;
+  ElemOff o;
+  o.rev = bidir && r >= B;
+  const int rr = o.rev ? r - B : r;
+  o.ost = r * H + u;
+  o.opre = rr * H + u;
+  o.oout = rr * D + (o.rev ? H : 0) + u;
+  return o;
+}
 
 // The B fragments of one wave's plan: slots < NFR into registers, the rest into the wave's LDS
 // region (lane-linear 16-byte pieces: conflict-free reads).  src(g, tile, c) = the row of U_h (fwd:
@@ -148,7 +183,8 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   using Fr = Frags<NF, NFR>;
   __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];   // LDS fragments
   __shared__ __attribute__((aligned(16))) __bf16 hl[2 * IMG];           // A: h_{t-1} (2 steps)
-  __shared__ float accl[2][RPW][HMAX + 16];     // the step's products (+16: columns past H)
+  __shared__ float accl[2][RPW][AW];            // the step's products (see AW)
+  __shared__ int tspill[NTILE];                  // tile -> its spill-over tile (-1: not cut)
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2, T = a.T;
   const int r0 = blockIdx.x * RPW, nr = min(RPW, B2 - r0);
@@ -175,20 +211,23 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   // 32-bit element offsets (every saved tensor of a layer holds < 2^31 elements: host check) so the
   // stores take a uniform base + per-lane offset
   const int B = a.B, D = ix.bidir ? 2 * H : H;
-  int ost[EPT], opre[EPT], oout[EPT], el[EPT];
-  bool rev[EPT];
+  // tiles without a fragment keep zero products; the spill-over map from the plans
+  for (int i = tid; i < 2 * RPW * AW; i += NT) (&accl[0][0][0])[i] = 0.f;
+  for (int i = tid; i < NTILE; i += NT) tspill[i] = -1;
+  __syncthreads();
+  if (lane == 0)
+    for (int f = 0; f < NF; ++f)
+      if (pl_valid(pl[f]) && pl_flush(pl[f]) && pl_spill(pl[f])) tspill[pl_tile(pl[f])] = pl_sidx(pl[f]);
+  __syncthreads();
+  int el[EPT];
   float hp[EPT], mk[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = tid + NT * j;
     const bool ok = e < nr * H;
     const int rl = ok ? e / H : 0, u = ok ? e % H : 0, r = r0 + rl;
-    rev[j] = ix.bidir && r >= B;                   // the reversed direction: time T-1-t
-    const int rr = rev[j] ? r - B : r;
-    ost[j] = r * H + u;                            // (t, r, u) of (T, B2, H): + t B2 H
-    opre[j] = rr * H + u;                          // (tt, rr, u) of (T, B, H): + tt B H
-    oout[j] = rr * D + (rev[j] ? H : 0) + u;       // (tt, rr, u) of (T, B, D): + tt B D
-    el[j] = ok ? rl * HP + u : -1;                 // the element in the A image (-1: none)
+    // the element in the A image and its tile's spill-over (-1: none)
+    el[j] = ok ? (rl * HP + u) | ((tspill[u >> 4] + 1) << 16) : -1;
     hp[j] = 0.f;                                   // h_init = 0
     mk[j] = ok ? drop_val(a, r, u, B2) : 0.f;
   }
@@ -198,7 +237,6 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   __bf16* __restrict__ hs_h = reinterpret_cast<__bf16*>(a.hs_h);
   float* __restrict__ y = a.y;
   const int BH = B * H, B2H = B2 * H, BD = B * D, iTBH = (int)TBH;
-  __syncthreads();
   PTR_DECL;
   for (int t = 0; t < T; ++t) {
     PTR_MARK(0);
@@ -210,24 +248,32 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
     float wz[EPT], wh[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int pi = el[j] >= 0 ? (rev[j] ? T - 1 - t : t) * BH + opre[j] : 0;
+      const ElemOff o = elem_off(el[j], r0, H, B, D, ix.bidir);
+      const int pi = el[j] >= 0 ? (o.rev ? T - 1 - t : t) * BH + o.opre : 0;
       wz[j] = wpre[pi];
       wh[j] = wpre[iTBH + pi];
     }
     f32x4 az = {0.f, 0.f, 0.f, 0.f}, ah = {0.f, 0.f, 0.f, 0.f};
-    // straight-line over the plan: empty slots multiply zero B fragments (loaded as zeros) with any
-    // A block; a tile's last slot stores its running products (wave-uniform branch; columns past H
-    // to the spill-over slot HMAX + c) and restarts them
+    // straight-line over the plan (empty slots multiply zero B fragments); slot f + 1's operands
+    // (the A fragment, and B from LDS past the register slots) are read before slot f's MFMAs, so
+    // their LDS latency overlaps the chain
+    bf8 av = a_frag(img, c, q, slot_blk(pl[0]));
+    bf8 bz = fr.get(ufl, w, lane, 0, 0), bh = fr.get(ufl, w, lane, 0, 1);
 #pragma clang loop unroll(full)
     for (int f = 0; f < NF; ++f) {
       const int e = pl[f];
-      const int kb = pl_valid(e) ? max(pl_blk(e), 0) : 0;  // wave-uniform
-      const bf8 av = a_frag(img, c, q, kb);
-      az = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, fr.get(ufl, w, lane, f, 0), az, 0, 0, 0);
-      ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, fr.get(ufl, w, lane, f, 1), ah, 0, 0, 0);
+      const int fn = f + 1 < NF ? f + 1 : f;
+      const bf8 an = a_frag(img, c, q, slot_blk(pl[fn]));
+      const bf8 bzn = fr.get(ufl, w, lane, fn, 0), bhn = fr.get(ufl, w, lane, fn, 1);
+      az = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bz, az, 0, 0, 0);
+      ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bh, ah, 0, 0, 0);
+      av = an;
+      bz = bzn;
+      bh = bhn;
       const bool fl = pl_valid(e) && pl_flush(e);
       const int unit = pl_tile(e) * 16 + c;
-      const int col = fl && unit < H ? unit : HMAX + c;   // batch row q, unit: register 0
+      // batch row q, unit: register 0; a cut tile's second part to its spill-over tile
+      const int col = pl_spill(e) ? XCOL + 16 * pl_sidx(e) + c : (unit < H ? unit : HMAX + c);
       if (fl) {
         accl[0][q][col] = az[0];
         accl[1][q][col] = ah[0];
@@ -235,9 +281,9 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
       const f32x4 zero = {0.f, 0.f, 0.f, 0.f};       // restart after a flush (a select: a
       az = fl ? zero : az;                            // multiply by 0 would turn inf into NaN)
       ah = fl ? zero : ah;
-      // a scheduling window of SW slots: the next slots' LDS reads overlap these MFMAs, without
-      // the whole plan's reads hoisted to the top (4 VGPRs each)
-      if (f % SW == SW - 1) __builtin_amdgcn_sched_barrier(0);
+      // one slot per scheduling window: the look-ahead above is the overlap, and no later slot's
+      // reads are hoisted here (4 VGPRs each)
+      __builtin_amdgcn_sched_barrier(0);
     }
     PTR_MARK(1);
     lds_barrier();
@@ -251,10 +297,12 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const bool ok = el[j] >= 0;
-      const int e = ok ? el[j] : 0;
+      const int e = ok ? el_pos(el[j]) : 0;
       const int rl = e / HP, u = e - rl * HP;
-      zv[j] = sigm(wz[j] + accl[0][rl][u]);
-      hv[j] = act_fwd(a.act, wh[j] + accl[1][rl][u]);
+      const int sp = ok ? el_spill(el[j]) : -1, xc = XCOL + 16 * (sp < 0 ? 0 : sp) + (u & 15);
+      const float xz = accl[0][rl][xc], xh = accl[1][rl][xc];     // (selects, no branch)
+      zv[j] = sigm(wz[j] + (accl[0][rl][u] + (sp < 0 ? 0.f : xz)));
+      hv[j] = act_fwd(a.act, wh[j] + (accl[1][rl][u] + (sp < 0 ? 0.f : xh)));
       const float h = zv[j] * hp[j] + (1.f - zv[j]) * (hv[j] * mk[j]);
       hp[j] = ok ? h : 0.f;                          // (a select: consumed on every lane)
     }
@@ -262,13 +310,14 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       if (el[j] < 0) continue;
-      const int si = tst + ost[j];
+      const ElemOff o = elem_off(el[j], r0, H, B, D, ix.bidir);
+      const int si = tst + o.ost;
       gates[si] = zv[j];
       gates[(int)TB2H + si] = hv[j];
       hs[si + B2H] = hp[j];                          // hs[t + 1]
       hs_h[si + B2H] = (__bf16)hp[j];
-      y[(rev[j] ? T - 1 - t : t) * BD + oout[j]] = hp[j];
-      nimg[el[j]] = (__bf16)hp[j];
+      y[(o.rev ? T - 1 - t : t) * BD + o.oout] = hp[j];
+      nimg[el_pos(el[j])] = (__bf16)hp[j];
     }
     PTR_MARK(4);
     lds_barrier();
@@ -284,7 +333,8 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
   using Fr = Frags<NF, NFR>;
   __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];
   __shared__ __attribute__((aligned(16))) __bf16 dl[2][2 * IMG];    // [step parity][gate z, h]
-  __shared__ float accl[RPW][HMAX + 16];        // dh products of the step (+16: columns past H)
+  __shared__ float accl[RPW][AW];               // dh products of the step (see AW)
+  __shared__ int tspill[NTILE];                  // tile -> its spill-over tile (-1: not cut)
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2, T = a.T;
   const int r0 = blockIdx.x * RPW, nr = min(RPW, B2 - r0);
@@ -312,10 +362,17 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     }
   }
   const int B = a.B, D = ix.bidir ? 2 * H : H, BD = B * D;
-  // per element: (t, r, k) offset ost + t B2 H of the saved tensors and ob + tt osg of dL/dy (the
-  // reversed direction runs time backwards) — both 0 for an unused slot, which then reads element
-  // 0 of its step: every lane's addresses without a select or branch in the step loop
-  int ost[EPT], ob[EPT], osg[EPT], el[EPT];
+  // per element: its A-image position (elem_off gives the offsets where they are used); an unused
+  // slot reads element 0 of the workgroup's first row: every lane's addresses without a select
+  // or branch in the step loop
+  for (int i = tid; i < RPW * AW; i += NT) (&accl[0][0])[i] = 0.f;   // tiles without fragments
+  for (int i = tid; i < NTILE; i += NT) tspill[i] = -1;
+  __syncthreads();
+  if (lane == 0)
+    for (int f = 0; f < NF; ++f)
+      if (pl_valid(pl[f]) && pl_flush(pl[f]) && pl_spill(pl[f])) tspill[pl_tile(pl[f])] = pl_sidx(pl[f]);
+  __syncthreads();
+  int el[EPT];
   float gc[EPT], mk[EPT];
   const __bf16* dgh_in = reinterpret_cast<const __bf16*>(a.dgates_h);
 #pragma unroll
@@ -323,22 +380,17 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     const int e = tid + NT * j;
     const bool ok = e < nr * H;
     const int rl = ok ? e / H : 0, k = ok ? e % H : 0, r = r0 + rl;
-    const bool rev = ix.bidir && r >= B;
-    const int rr = rev ? r - B : r;
-    const int oout = rr * D + (rev ? H : 0) + k;
-    ost[j] = ok ? r * H + k : 0;
-    ob[j] = ok ? (rev ? (T - 1) * BD : 0) + oout : 0;
-    osg[j] = ok ? (rev ? -BD : BD) : 0;
-    el[j] = ok ? rl * HP + k : -1;
+    el[j] = ok ? (rl * HP + k) | ((tspill[k >> 4] + 1) << 16) : -1;
+    const int ostj = r * H + k;
     // step T-1 (rnn_bwd_init): g_{T-1} in carry slot (T-1-(T-1)) & 1 = 0, and its dgates (bf16)
     // as the first A images
-    gc[j] = ok ? a.work[ost[j]] : 0.f;
+    gc[j] = ok ? a.work[ostj] : 0.f;
     mk[j] = ok ? drop_val(a, r, k, B2) : 0.f;
     if (ok) {
-      const int si = (T - 1) * B2 * H + ost[j];
+      const int si = (T - 1) * B2 * H + ostj;
       const int par = (T - 1) & 1;
-      dl[par][el[j]] = dgh_in[si];
-      dl[par][IMG + el[j]] = dgh_in[(int)TB2H + si];
+      dl[par][el_pos(el[j])] = dgh_in[si];
+      dl[par][IMG + el_pos(el[j])] = dgh_in[(int)TB2H + si];
     }
   }
   const float* __restrict__ gates = a.gates;
@@ -350,7 +402,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
   const int dys = DY2 ? (int)a.dy_slab_stride : 0;   // < 2^31 (rnn_persist_ok)
   float zc[EPT];                                // z_{tt+1}, carried from the step before
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) zc[j] = gates[(T - 1) * B2H + ost[j]];
+  for (int j = 0; j < EPT; ++j) zc[j] = gates[(T - 1) * B2H + elem_off(el[j], r0, H, B, D, ix.bidir).ost];
   __syncthreads();
   PTR_DECL;
   for (int tt = T - 2; tt >= 0; --tt) {
@@ -362,8 +414,9 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     // (unconditional loads and uses, as the forward's)
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int si = tst + ost[j];
-      const int oi = ob[j] + tt * osg[j];
+      const ElemOff o = elem_off(el[j], r0, H, B, D, ix.bidir);
+      const int si = tst + o.ost;
+      const int oi = (o.rev ? T - 1 - tt : tt) * BD + o.oout;
       // one or two slabs (rnn_persist_ok; the engine sums more beforehand)
       dyv[j] = DY2 ? dy[oi] + dy[dys + oi] : dy[oi];
       hpv[j] = hs[si];                                // h_{tt-1} = hs[tt]
@@ -371,19 +424,26 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       hct[j] = gates[iTB2H + si];
     }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // operand look-ahead by half a slot (the BPTT holds more per-element state than the forward
+    // and has two A images): gate 1's operands of slot f are read under gate 0's MFMA, gate 0's of
+    // slot f + 1 under gate 1's
+    bf8 a0 = a_frag(img, c, q, slot_blk(pl[0])), b0 = fr.get(ufl, w, lane, 0, 0);
 #pragma clang loop unroll(full)
-    for (int f = 0; f < NF; ++f) {              // straight-line, as the forward's
+    for (int f = 0; f < NF; ++f) {
       const int e = pl[f];
-      const int jb = pl_valid(e) ? max(pl_blk(e), 0) : 0;
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img, c, q, jb), fr.get(ufl, w, lane, f, 0),
-                                                    acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_frag(img + IMG, c, q, jb),
-                                                    fr.get(ufl, w, lane, f, 1), acc, 0, 0, 0);
+      const int fn = f + 1 < NF ? f + 1 : f;
+      const bf8 a1 = a_frag(img + IMG, c, q, slot_blk(e)), b1 = fr.get(ufl, w, lane, f, 1);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+      const bf8 a0n = a_frag(img, c, q, slot_blk(pl[fn])), b0n = fr.get(ufl, w, lane, fn, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+      a0 = a0n;
+      b0 = b0n;
       const bool fl = pl_valid(e) && pl_flush(e);
       const int k = pl_tile(e) * 16 + c;
-      if (fl) accl[q][k < H ? k : HMAX + c] = acc[0];
+      if (fl)   // (a cut tile's second part to its spill-over tile)
+        accl[q][pl_spill(e) ? XCOL + 16 * pl_sidx(e) + c : (k < H ? k : HMAX + c)] = acc[0];
       acc = fl ? f32x4{0.f, 0.f, 0.f, 0.f} : acc;
-      if (f % SW == SW - 1) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     PTR_MARK(1);
     lds_barrier();
@@ -395,9 +455,11 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const bool ok = el[j] >= 0;
-      const int e = ok ? el[j] : 0;
+      const int e = ok ? el_pos(el[j]) : 0;
       const int rl = e / HP, k = e - rl * HP;
-      const float dh = accl[rl][k] + gc[j] * zc[j];   // z_{tt+1}: the previous step's z
+      const int sp = ok ? el_spill(el[j]) : -1;
+      const float xd = accl[rl][XCOL + 16 * (sp < 0 ? 0 : sp) + (k & 15)];
+      const float dh = (accl[rl][k] + (sp < 0 ? 0.f : xd)) + gc[j] * zc[j];   // z_{tt+1}: previous
       const float g = dyv[j] + dh;
       const float z = ztt[j], hcr = hct[j], m = mk[j];
       const float hc = hcr * m;
@@ -417,7 +479,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       if (el[j] < 0) continue;
-      const int si = tst + ost[j];
+      const int si = tst + elem_off(el[j], r0, H, B, D, ix.bidir).ost;
       dgates[si] = d0v[j];
       dgates[iTB2H + si] = d1v[j];
       dgh[si] = (__bf16)d0v[j];
@@ -433,7 +495,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     const int p0 = (T - 1) & 1;
 #pragma unroll
     for (int j = 0; j < EPT; ++j)
-      if (el[j] >= 0) a.work[p0 * n + ost[j]] = gc[j];
+      if (el[j] >= 0) a.work[p0 * n + elem_off(el[j], r0, H, B, D, ix.bidir).ost] = gc[j];
   }
 }
 

@@ -185,54 +185,15 @@ def persist_geometry():
     return tuple(x.value for x in v)
 
 
-def _balance(sizes, nw):
-    """Tiles -> waves minimising the largest per-wave fragment count (the step's MFMA chain is the
-    slowest wave's): longest-processing-time first, then moves and swaps off the fullest wave while
-    they lower it (deterministic).  C3's BPTT plans: 23-24 -> 22 slots on the fullest wave."""
-    load, asg = [0] * nw, [0] * len(sizes)
-    for t in sorted(range(len(sizes)), key=lambda t: (-sizes[t], t)):
-        v = min(range(nw), key=lambda v: (load[v], v))
-        load[v] += sizes[t]
-        asg[t] = v
-    for _ in range(4 * len(sizes)):
-        mx = max(load)
-        src = load.index(mx)
-        mine = [t for t in range(len(sizes)) if asg[t] == src]
-        done = False
-        for t in mine:                                  # a move that lowers the maximum
-            for v in range(nw):
-                if v != src and load[v] + sizes[t] < mx:
-                    load[src] -= sizes[t]
-                    load[v] += sizes[t]
-                    asg[t] = v
-                    done = True
-                    break
-            if done:
-                break
-        if not done:                                    # or a swap with a smaller tile
-            for t in mine:
-                for u in range(len(sizes)):
-                    v = asg[u]
-                    d = sizes[t] - sizes[u]
-                    if v != src and d > 0 and load[v] + d < mx:
-                        load[src] -= d
-                        load[v] += d
-                        asg[t], asg[u] = v, src
-                        done = True
-                        break
-                if done:
-                    break
-        if not done:
-            break
-    return asg
-
-
 def persist_plans(mask):
     """Fragment plans of the persistent liGRU loops (pkc_rnn_args.persist_*) for a static U mask
     (H x H bool, any gate): forward tiles of 16 units x the 32-wide blocks of k they read, BPTT
-    tiles of 16 columns k x the 32-wide blocks of units j; each tile's fragments in one wave, the
-    tiles spread over the waves longest first (LPT) so the per-step MFMA chains are balanced.
-    None when the layer does not fit the kernels' geometry (pkc_rnn_persist_geometry)."""
+    tiles of 16 columns k x the 32-wide blocks of units j.  The fragments, tile by tile, are dealt
+    to the waves in runs of ceil(total / waves), so every wave's per-step MFMA chain has the same
+    length; a tile cut between two waves flushes from both, the second part into a spill-over tile
+    (bit 18, its index in bits 19-21) that the cell update adds.  Tiles without a nonzero block take
+    no slot (their products are zero).  None when the layer does not fit
+    (pkc_rnn_persist_geometry)."""
     nw, nsf, nsb, _, hmax = persist_geometry()
     H = mask.shape[0]
     if H > hmax or H % 2:
@@ -245,19 +206,24 @@ def persist_plans(mask):
     bwd = mp.reshape(hp // 32, 32, hp // 16, 16).any(axis=(1, 3)).T[:nt]     # [k tile][j blk]
     out = []
     for pres, nslot in ((fwd, nsf), (bwd, nsb)):
-        frags = [np.nonzero(pres[t])[0].tolist() or [-1] for t in range(nt)]
-        asg = _balance([len(f) for f in frags], nw)
-        lists = [[t for t in range(nt) if asg[t] == wv] for wv in range(nw)]
-        load = [sum(len(frags[t]) for t in lst) for lst in lists]
-        if max(load) > nslot:
+        blocks = [np.nonzero(pres[t])[0].tolist() for t in range(nt)]
+        seq = [(t, b) for t in range(nt) for b in blocks[t]]
+        # a run at least one tile long: a tile is cut at most once (two parts)
+        run = max(1, -(-len(seq) // nw), max(len(b) for b in blocks))
+        if run > nslot:
             return None
         tab = np.zeros((nw, nslot), dtype=np.int32)
-        for wv in range(nw):
-            f = 0
-            for t in sorted(lists[wv]):
-                for i, b in enumerate(frags[t]):
-                    tab[wv, f] = t | ((b + 1) << 8) | ((i == len(frags[t]) - 1) << 16) | (1 << 17)
-                    f += 1
+        nsplit, first_wave = 0, {}
+        for i, (t, b) in enumerate(seq):
+            wv, f = divmod(i, run)
+            first_wave.setdefault(t, wv)
+            last = i + 1 == len(seq) or seq[i + 1][0] != t or (i + 1) % run == 0
+            ent = t | ((b + 1) << 8) | (int(last) << 16) | (1 << 17)
+            if last and wv != first_wave[t]:         # the second part of a cut tile: its own slot
+                ent |= (1 << 18) | (nsplit << 19)
+                nsplit += 1
+            tab[wv, f] = ent
+        assert nsplit < nw
         out.append(tab.reshape(-1))
     return out
 
