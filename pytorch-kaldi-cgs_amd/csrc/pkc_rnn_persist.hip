@@ -49,11 +49,15 @@ constexpr int HMAX = 576;               // H <= HMAX (36 tiles of 16)
 // banks for the 4 live rows, so an A-fragment read (4 rows x 4 lane groups x 16 B) is conflict-free
 constexpr int HP = 608;
 constexpr int IMG = RPW * HP;           // one A image (bf16 elements)
-constexpr int EPT = (RPW * HMAX + NT - 1) / NT;   // epilogue elements per thread
+// the cell update works on pairs of adjacent units (H is even): 8-byte loads and stores, 4-byte
+// bf16 pairs — half the memory instructions of one element per lane
+constexpr int PPT = (RPW * HMAX / 2 + NT - 1) / NT;   // epilogue unit pairs per thread
+constexpr int EPT = 2 * PPT;                          // epilogue elements per thread
 constexpr int FRAG = 64 * 16;           // bytes of one B fragment (64 lanes x 8 bf16)
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
+typedef __attribute__((ext_vector_type(2))) float fl2;
 
 __device__ __forceinline__ bf8 zero8() {
   bf8 v;
@@ -219,17 +223,18 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
     for (int f = 0; f < NF; ++f)
       if (pl_valid(pl[f]) && pl_flush(pl[f]) && pl_spill(pl[f])) tspill[pl_tile(pl[f])] = pl_sidx(pl[f]);
   __syncthreads();
-  int el[EPT];
+  int el[PPT];                                    // per pair: its first unit (see el_pos)
   float hp[EPT], mk[EPT];
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = tid + NT * j;
+  for (int j = 0; j < PPT; ++j) {
+    const int e = 2 * (tid + NT * j);              // the pair's first element (u even)
     const bool ok = e < nr * H;
     const int rl = ok ? e / H : 0, u = ok ? e % H : 0, r = r0 + rl;
-    // the element in the A image and its tile's spill-over (-1: none)
+    // the pair in the A image and its tile's spill-over (-1: none)
     el[j] = ok ? (rl * HP + u) | ((tspill[u >> 4] + 1) << 16) : -1;
-    hp[j] = 0.f;                                   // h_init = 0
-    mk[j] = ok ? drop_val(a, r, u, B2) : 0.f;
+    hp[2 * j] = hp[2 * j + 1] = 0.f;               // h_init = 0
+    mk[2 * j] = ok ? drop_val(a, r, u, B2) : 0.f;
+    mk[2 * j + 1] = ok ? drop_val(a, r, u + 1, B2) : 0.f;
   }
   const float* __restrict__ wpre = a.wpre;
   float* __restrict__ gates = a.gates;
@@ -245,13 +250,13 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
     // (every lane loads — element 0 for an unused slot — and every lane consumes the values below:
     // a load under a per-lane branch leaves its register pending on the other path, and the next
     // step's overwrite would wait for every outstanding memory operation, this step's stores too)
-    float wz[EPT], wh[EPT];
+    fl2 wz[PPT], wh[PPT];
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
       const ElemOff o = elem_off(el[j], r0, H, B, D, ix.bidir);
-      const int pi = el[j] >= 0 ? (o.rev ? T - 1 - t : t) * BH + o.opre : 0;
-      wz[j] = wpre[pi];
-      wh[j] = wpre[iTBH + pi];
+      const int pi = el[j] >= 0 ? (o.rev ? T - 1 - t : t) * BH + o.opre : 0;   // even
+      wz[j] = *reinterpret_cast<const fl2*>(wpre + pi);
+      wh[j] = *reinterpret_cast<const fl2*>(wpre + iTBH + pi);
     }
     f32x4 az = {0.f, 0.f, 0.f, 0.f}, ah = {0.f, 0.f, 0.f, 0.f};
     // straight-line over the plan (empty slots multiply zero B fragments); slot f + 1's operands
@@ -293,31 +298,40 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
     const int tst = t * B2H;
     // every element's values first, then the stores: vmcnt is one in-order counter for loads and
     // stores alike, so a load consumed after this step's first stores would wait for those too
-    float zv[EPT], hv[EPT];
+    fl2 zv[PPT], hv[PPT];
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
       const bool ok = el[j] >= 0;
       const int e = ok ? el_pos(el[j]) : 0;
       const int rl = e / HP, u = e - rl * HP;
       const int sp = ok ? el_spill(el[j]) : -1, xc = XCOL + 16 * (sp < 0 ? 0 : sp) + (u & 15);
-      const float xz = accl[0][rl][xc], xh = accl[1][rl][xc];     // (selects, no branch)
-      zv[j] = sigm(wz[j] + (accl[0][rl][u] + (sp < 0 ? 0.f : xz)));
-      hv[j] = act_fwd(a.act, wh[j] + (accl[1][rl][u] + (sp < 0 ? 0.f : xh)));
-      const float h = zv[j] * hp[j] + (1.f - zv[j]) * (hv[j] * mk[j]);
-      hp[j] = ok ? h : 0.f;                          // (a select: consumed on every lane)
+      const fl2 xz = *reinterpret_cast<const fl2*>(&accl[0][rl][xc]);    // (selects, no branch)
+      const fl2 xh = *reinterpret_cast<const fl2*>(&accl[1][rl][xc]);
+      const fl2 pz = *reinterpret_cast<const fl2*>(&accl[0][rl][u]);
+      const fl2 ph = *reinterpret_cast<const fl2*>(&accl[1][rl][u]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = 2 * j + i;
+        zv[j][i] = sigm(wz[j][i] + (pz[i] + (sp < 0 ? 0.f : xz[i])));
+        hv[j][i] = act_fwd(a.act, wh[j][i] + (ph[i] + (sp < 0 ? 0.f : xh[i])));
+        const float h = zv[j][i] * hp[k] + (1.f - zv[j][i]) * (hv[j][i] * mk[k]);
+        hp[k] = ok ? h : 0.f;                        // (a select: consumed on every lane)
+      }
     }
     PTR_MARK(3);
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
       if (el[j] < 0) continue;
       const ElemOff o = elem_off(el[j], r0, H, B, D, ix.bidir);
-      const int si = tst + o.ost;
-      gates[si] = zv[j];
-      gates[(int)TB2H + si] = hv[j];
-      hs[si + B2H] = hp[j];                          // hs[t + 1]
-      hs_h[si + B2H] = (__bf16)hp[j];
-      y[(o.rev ? T - 1 - t : t) * BD + o.oout] = hp[j];
-      nimg[el_pos(el[j])] = (__bf16)hp[j];
+      const int si = tst + o.ost;                    // even: every offset below is
+      const fl2 h2 = {hp[2 * j], hp[2 * j + 1]};
+      const bf2 hb = {(__bf16)h2[0], (__bf16)h2[1]};
+      *reinterpret_cast<fl2*>(gates + si) = zv[j];
+      *reinterpret_cast<fl2*>(gates + (int)TB2H + si) = hv[j];
+      *reinterpret_cast<fl2*>(hs + si + B2H) = h2;   // hs[t + 1]
+      *reinterpret_cast<bf2*>(hs_h + si + B2H) = hb;
+      *reinterpret_cast<fl2*>(y + (o.rev ? T - 1 - t : t) * BD + o.oout) = h2;
+      *reinterpret_cast<bf2*>(nimg + el_pos(el[j])) = hb;
     }
     PTR_MARK(4);
     lds_barrier();
@@ -372,25 +386,29 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     for (int f = 0; f < NF; ++f)
       if (pl_valid(pl[f]) && pl_flush(pl[f]) && pl_spill(pl[f])) tspill[pl_tile(pl[f])] = pl_sidx(pl[f]);
   __syncthreads();
-  int el[EPT];
+  int el[PPT];                                   // per unit pair (as the forward's)
   float gc[EPT], mk[EPT];
   const __bf16* dgh_in = reinterpret_cast<const __bf16*>(a.dgates_h);
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = tid + NT * j;
+  for (int j = 0; j < PPT; ++j) {
+    const int e = 2 * (tid + NT * j);
     const bool ok = e < nr * H;
     const int rl = ok ? e / H : 0, k = ok ? e % H : 0, r = r0 + rl;
     el[j] = ok ? (rl * HP + k) | ((tspill[k >> 4] + 1) << 16) : -1;
     const int ostj = r * H + k;
     // step T-1 (rnn_bwd_init): g_{T-1} in carry slot (T-1-(T-1)) & 1 = 0, and its dgates (bf16)
     // as the first A images
-    gc[j] = ok ? a.work[ostj] : 0.f;
-    mk[j] = ok ? drop_val(a, r, k, B2) : 0.f;
+    const fl2 g2 = *reinterpret_cast<const fl2*>(a.work + ostj);
+    gc[2 * j] = ok ? g2[0] : 0.f;
+    gc[2 * j + 1] = ok ? g2[1] : 0.f;
+    mk[2 * j] = ok ? drop_val(a, r, k, B2) : 0.f;
+    mk[2 * j + 1] = ok ? drop_val(a, r, k + 1, B2) : 0.f;
     if (ok) {
       const int si = (T - 1) * B2 * H + ostj;
       const int par = (T - 1) & 1;
-      dl[par][el_pos(el[j])] = dgh_in[si];
-      dl[par][IMG + el_pos(el[j])] = dgh_in[(int)TB2H + si];
+      *reinterpret_cast<bf2*>(&dl[par][el_pos(el[j])]) = *reinterpret_cast<const bf2*>(dgh_in + si);
+      *reinterpret_cast<bf2*>(&dl[par][IMG + el_pos(el[j])]) =
+          *reinterpret_cast<const bf2*>(dgh_in + (int)TB2H + si);
     }
   }
   const float* __restrict__ gates = a.gates;
@@ -402,7 +420,12 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
   const int dys = DY2 ? (int)a.dy_slab_stride : 0;   // < 2^31 (rnn_persist_ok)
   float zc[EPT];                                // z_{tt+1}, carried from the step before
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) zc[j] = gates[(T - 1) * B2H + elem_off(el[j], r0, H, B, D, ix.bidir).ost];
+  for (int j = 0; j < PPT; ++j) {
+    const fl2 z2 = *reinterpret_cast<const fl2*>(
+        gates + (T - 1) * B2H + elem_off(el[j], r0, H, B, D, ix.bidir).ost);
+    zc[2 * j] = z2[0];
+    zc[2 * j + 1] = z2[1];
+  }
   __syncthreads();
   PTR_DECL;
   for (int tt = T - 2; tt >= 0; --tt) {
@@ -410,18 +433,19 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     const int t = tt + 1;
     const __bf16* img = dl[t & 1];
     const int tst = tt * B2H;
-    float dyv[EPT], hpv[EPT], ztt[EPT], hct[EPT];
-    // (unconditional loads and uses, as the forward's)
+    fl2 dyv[PPT], hpv[PPT], ztt[PPT], hct[PPT];
+    // (unconditional loads and uses, as the forward's; every offset is even)
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
       const ElemOff o = elem_off(el[j], r0, H, B, D, ix.bidir);
       const int si = tst + o.ost;
       const int oi = (o.rev ? T - 1 - tt : tt) * BD + o.oout;
       // one or two slabs (rnn_persist_ok; the engine sums more beforehand)
-      dyv[j] = DY2 ? dy[oi] + dy[dys + oi] : dy[oi];
-      hpv[j] = hs[si];                                // h_{tt-1} = hs[tt]
-      ztt[j] = gates[si];
-      hct[j] = gates[iTB2H + si];
+      const fl2 d0 = *reinterpret_cast<const fl2*>(dy + oi);
+      dyv[j] = DY2 ? d0 + *reinterpret_cast<const fl2*>(dy + dys + oi) : d0;
+      hpv[j] = *reinterpret_cast<const fl2*>(hs + si);     // h_{tt-1} = hs[tt]
+      ztt[j] = *reinterpret_cast<const fl2*>(gates + si);
+      hct[j] = *reinterpret_cast<const fl2*>(gates + iTB2H + si);
     }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     // operand look-ahead by half a slot (the BPTT holds more per-element state than the forward
@@ -451,39 +475,44 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
     // bwd_step_epi + gate_grads (CELL_LIGRU) for step tt
     __bf16* nimg = dl[tt & 1];
     // values first, then the stores (as the forward's)
-    float d0v[EPT], d1v[EPT];
+    fl2 d0v[PPT], d1v[PPT];
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
       const bool ok = el[j] >= 0;
       const int e = ok ? el_pos(el[j]) : 0;
       const int rl = e / HP, k = e - rl * HP;
       const int sp = ok ? el_spill(el[j]) : -1;
-      const float xd = accl[rl][XCOL + 16 * (sp < 0 ? 0 : sp) + (k & 15)];
-      const float dh = (accl[rl][k] + (sp < 0 ? 0.f : xd)) + gc[j] * zc[j];   // z_{tt+1}: previous
-      const float g = dyv[j] + dh;
-      const float z = ztt[j], hcr = hct[j], m = mk[j];
-      const float hc = hcr * m;
-      const float dz = g * (hpv[j] - hc);
-      const float dhc = g * (1.f - z);
-      d0v[j] = dz * z * (1.f - z);
-      d1v[j] = dhc * m * act_bwd_out(a.act, hcr);
-      gc[j] = ok ? g : 0.f;                           // (a select: consumed on every lane)
-      zc[j] = z;
-      // the next step's A images on every lane (an unused slot writes column HP - 1 of row 0, a
-      // padding column no fragment reads): the values are consumed here, ahead of the stores
-      const int ei = ok ? e : HP - 1;
-      nimg[ei] = (__bf16)d0v[j];
-      nimg[IMG + ei] = (__bf16)d1v[j];
+      const fl2 xd = *reinterpret_cast<const fl2*>(&accl[rl][XCOL + 16 * (sp < 0 ? 0 : sp) + (k & 15)]);
+      const fl2 pd = *reinterpret_cast<const fl2*>(&accl[rl][k]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kk = 2 * j + i;
+        const float dh = (pd[i] + (sp < 0 ? 0.f : xd[i])) + gc[kk] * zc[kk];   // z_{tt+1}: previous
+        const float g = dyv[j][i] + dh;
+        const float z = ztt[j][i], hcr = hct[j][i], m = mk[kk];
+        const float hc = hcr * m;
+        const float dz = g * (hpv[j][i] - hc);
+        const float dhc = g * (1.f - z);
+        d0v[j][i] = dz * z * (1.f - z);
+        d1v[j][i] = dhc * m * act_bwd_out(a.act, hcr);
+        gc[kk] = ok ? g : 0.f;                        // (a select: consumed on every lane)
+        zc[kk] = z;
+      }
+      // the next step's A images on every lane (an unused slot writes columns HP - 2, HP - 1 of
+      // row 0, padding no fragment reads): the values are consumed here, ahead of the stores
+      const int ei = ok ? e : HP - 2;
+      *reinterpret_cast<bf2*>(nimg + ei) = bf2{(__bf16)d0v[j][0], (__bf16)d0v[j][1]};
+      *reinterpret_cast<bf2*>(nimg + IMG + ei) = bf2{(__bf16)d1v[j][0], (__bf16)d1v[j][1]};
     }
     PTR_MARK(3);
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
+    for (int j = 0; j < PPT; ++j) {
       if (el[j] < 0) continue;
       const int si = tst + elem_off(el[j], r0, H, B, D, ix.bidir).ost;
-      dgates[si] = d0v[j];
-      dgates[iTB2H + si] = d1v[j];
-      dgh[si] = (__bf16)d0v[j];
-      dgh[iTB2H + si] = (__bf16)d1v[j];
+      *reinterpret_cast<fl2*>(dgates + si) = d0v[j];
+      *reinterpret_cast<fl2*>(dgates + iTB2H + si) = d1v[j];
+      *reinterpret_cast<bf2*>(dgh + si) = bf2{(__bf16)d0v[j][0], (__bf16)d0v[j][1]};
+      *reinterpret_cast<bf2*>(dgh + iTB2H + si) = bf2{(__bf16)d1v[j][0], (__bf16)d1v[j][1]};
     }
     PTR_MARK(4);
     lds_barrier();
@@ -494,8 +523,10 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
   if (T > 1) {
     const int p0 = (T - 1) & 1;
 #pragma unroll
-    for (int j = 0; j < EPT; ++j)
-      if (el[j] >= 0) a.work[p0 * n + elem_off(el[j], r0, H, B, D, ix.bidir).ost] = gc[j];
+    for (int j = 0; j < PPT; ++j)
+      if (el[j] >= 0)
+        *reinterpret_cast<fl2*>(a.work + p0 * n + elem_off(el[j], r0, H, B, D, ix.bidir).ost) =
+            fl2{gc[2 * j], gc[2 * j + 1]};
   }
 }
 
