@@ -447,8 +447,9 @@ typedef struct {
    * launch, no cross-workgroup hand-off (rows are independent).  persist_fwd / persist_bwd:
    * [nwaves][nslots] int32 fragment plans (pkc_rnn_persist_geometry): bits 0-7 the output tile
    * (16 units; BPTT: 16 columns k), 8-15 the 32-wide contraction block + 1 (0 = none), bit 16 the
-   * tile's last fragment, bit 17 valid; each tile's fragments in one wave.  persist_kb = the
-   * forward plan's nslots.
+   * last fragment of this wave's part of the tile, bit 17 valid, bit 18 set on that flush when
+   * the part is the second of a tile cut between two waves, bits 19-21 its spill-over tile index
+   * (distinct per cut tile, < nwaves - 1).  persist_kb = the forward plan's nslots.
    * NULL (or a layer outside these limits): the per-step launches. */
   const int32_t* persist_fwd; const int32_t* persist_bwd; int persist_kb;
   /* Exact quantised-h step products (qbits > 0, step_bf16 = 0): the caller guarantees U[g] lies on

@@ -759,6 +759,8 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
       if constexpr (!R16) load_strip_h<S>(srch + (int64_t)(rb < B2 ? rb : 0) * H, rb < B2, kb, H, v8, hb);
       load_strip_h<S>(puh, u < H, kb, H, v8, hu);
     }
+    PKC_TR(2);                      // operands (and the epilogue inputs) in registers
+    PKC_TR(3);
     mfma_chain_h<S, R16>(ha, hb, hu, acc0, acc1);
   } else {
   float va[S], vb[S], vu[QX ? 1 : S];

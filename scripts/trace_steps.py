@@ -47,6 +47,8 @@ def main():
     assert L.lib().pkc_trace_read(buf, n) == 0
     t = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
     t = t[(t[:, 0] > 0) & (t[:, 7] > 0)]
+    if not (t[:, 3] > 0).any():         # no quantised-h phase (stamp 3): an empty phase
+        t[:, 3] = t[:, 2]
     cyc = np.diff(t[:, 1:7], axis=1)                        # phases 1..5 in shader cycles
     real_ns = (t[:, 7] - t[:, 0]) * 10.0                    # 100 MHz
     ghz = (t[:, 6] - t[:, 1]) / np.maximum(real_ns, 1)
