@@ -618,14 +618,19 @@ def test_engine_split_dw_large_batch(mode):
     assert t0 == pytest.approx(t1, rel=1e-6)
     err = (g1 - g0).abs().max().item()
     assert err <= 1e-5 * g0.abs().max().item(), "split-K dW gradient max abs diff %.3g" % err
+    from flipcheck import assert_counted, step_outliers
+    outliers = {}
     for k in u0:
         if u0[k].norm().item() == 0.0:
             continue
-        # SGD steps follow the gradient (1e-5); RMSprop's first step is lr * sign(g), so a
-        # gradient within rounding of zero that flips sign moves by 2 lr: a few elements
-        d = (u1[k] - u0[k]).norm().item()
-        assert d <= 1e-2 * u0[k].norm().item(), "%s update: rel diff %.3g" % (
-            k, d / u0[k].norm().item())
+        # SGD steps follow the gradient: elementwise within 1e-4 of the update's scale.  RMSprop's
+        # first step is lr * sign(g), so a gradient within rounding of zero that flips sign moves
+        # by 2 lr: counted (<= 0.1 % of the tensor), each at most twice the largest step
+        scale = float(u0[k].abs().max())
+        n, dmax, _ = step_outliers(u1[k], u0[k], 1e-4, scale)
+        outliers[k] = n
+        assert_counted(k, n, u0[k].numel(), 1e-3, dmax, 2 * scale + 1e-12,
+                       "(update outliers per tensor %s)" % {a: b for a, b in outliers.items() if b})
 
 
 @pytest.mark.parametrize("B,mode", [(128, "eager"), (128, "graph"), (1024, "eager")])
