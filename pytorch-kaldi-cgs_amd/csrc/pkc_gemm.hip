@@ -960,6 +960,15 @@ static bool big_enabled() {
   }();
   return on != 0;
 }
+// compensated-bf16 problems of grouped launches on the 128x128 body (PKC_X3_GROUPED_BIG=0: the
+// 64x64 body, whose grouped instances keep several workgroups per CU)
+static bool x3_grouped_big() {
+  static const int on = [] {
+    const char* v = getenv("PKC_X3_GROUPED_BIG");
+    return v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
 
 }  // namespace pkc
 
@@ -1042,8 +1051,9 @@ extern "C" int pkc_gemm_grouped_tile(int prec, int a_kcontig, int b_kcontig, int
                                      const void* A, int64_t lda, const void* B, int64_t ldb) {
   using namespace pkc;
   if (M <= 0 || N <= 0 || K <= 0 || lda <= 0 || ldb <= 0) return 64;
-  return big_enabled() && big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb,
-                                        BIG_MIN_TILES_GROUPED, BIG_MIN_K_GROUPED) ? 128 : 64;
+  return big_enabled() && (prec != PKC_PREC_BF16X3 || x3_grouped_big()) &&
+                 big::eligible(prec, a_kcontig, b_kcontig, M, N, K, A, lda, B, ldb,
+                               BIG_MIN_TILES_GROUPED, BIG_MIN_K_GROUPED) ? 128 : 64;
 }
 
 // rows per partial block pkc_gemm_colstats writes for this shape: 128 (the 128x128 tile body),
@@ -1212,7 +1222,8 @@ extern "C" int pkc_gemm_grouped(int prec, const pkc_gemm_problem* probs, int n, 
     const bool vec = ((uintptr_t)q.A % 16 == 0) && ((uintptr_t)q.B % 16 == 0) && q.lda % e == 0 &&
                      q.ldb % e == 0 && (q.a_kcontig ? q.K % e == 0 : q.M % e == 0) &&
                      (q.b_kcontig ? q.K % e == 0 : q.N % e == 0);
-    const bool bigp = !any_sparse && big_enabled() && big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
+    const bool bigp = !any_sparse && big_enabled() && (prec != PKC_PREC_BF16X3 || x3_grouped_big()) &&
+                      big::eligible(prec, q.a_kcontig, q.b_kcontig, q.M, q.N, q.K,
                                                      q.A, q.lda, q.B, q.ldb, BIG_MIN_TILES_GROUPED,
                                                      BIG_MIN_K_GROUPED);
     any_big |= bigp;
