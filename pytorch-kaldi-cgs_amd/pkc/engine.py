@@ -75,6 +75,9 @@ RNN_PERSIST = os.environ.get("PKC_RNN_PERSIST", "1") != "0"
 # products to within their own rounding; 0: the exact-fp32 chain
 RNN_QH_EXACT = os.environ.get("PKC_RNN_QH_EXACT", "1") != "0"
 SEQ_GRAPHS = int(os.environ.get("PKC_SEQ_GRAPHS", "512"))
+# a padded length T is captured at its SEQ_CAPTURE_AFTER-th batch (eager before): real chunks have
+# many one-off lengths, and a capture costs more than an eager step
+SEQ_CAPTURE_AFTER = max(1, int(os.environ.get("PKC_SEQ_CAPTURE_AFTER", "2")))
 # split-K dW at large frame batches (M >= this many rows): a 1024x1024 dW has only 64 128x128
 # tiles, one per CU on a quarter of the chip, each a 4096-deep chain at B = 4096 (81 us); split
 # 4 ways into slabs (29 us) that a slab-sum operation of the next grouped launch adds into the
@@ -1270,8 +1273,9 @@ class Engine:
         assert feats.dtype == torch.float32 and labels.dtype == torch.int32
         assert feats.shape[1] >= self.F and labels.shape[1] == self.nlab
         key = (feats.data_ptr(), feats.stride(0), labels.data_ptr())
-        if self.seq_graphs and key != getattr(self, "_chunk_key", None):
+        if self.seq_graphs is not None and key != getattr(self, "_chunk_key", None):
             self.seq_graphs.clear()            # the captured gathers read the old chunk
+            self.seq_seen = {}
         self._chunk_key = key
         self.chunk_feats, self.chunk_labels = feats, labels
         if self.seq:
@@ -2382,7 +2386,8 @@ class Engine:
                 # row of the global batch, not the mean of unequal batch means
                 self.grad_scale = float(self.frame_scales[getattr(batch, "index", self.batch_i)])
             self._upload_seq_meta(batch)
-            if self.seq_graphs is not None and allreduce is None and self.frame_scales is None:
+            if (self.seq_graphs is not None and allreduce is None and self.frame_scales is None
+                    and self._seq_seen(batch)):
                 self._seq_graph(batch).replay()
             else:
                 self._train_step_kernels(allreduce, batch)
@@ -2501,6 +2506,16 @@ class Engine:
         if self.opt_entries and not self.static_opt and self.graph is None:
             self._upload_opt_desc(step_inc=1)
 
+    def _seq_seen(self, batch):
+        """Whether this batch's padded length has a graph or has now been seen SEQ_CAPTURE_AFTER
+        times (counted per chunk, with the graphs)."""
+        T = int(batch[3])
+        if T in self.seq_graphs:
+            return True
+        n = self.seq_seen.get(T, 0) + 1
+        self.seq_seen[T] = n
+        return n >= SEQ_CAPTURE_AFTER
+
     def _seq_graph(self, batch):
         """The captured training step of a sentence batch of padded length T (captured on first
         use, kept in an LRU of SEQ_GRAPHS): every launch of the step — gather, recurrent time
@@ -2536,6 +2551,7 @@ class Engine:
             if not self.static_opt or self.sync_bn is not None or self.external:
                 return False
             self.seq_graphs, self.seq_pool, self.seq_captures = {}, torch.cuda.graph_pool_handle(), 0
+            self.seq_seen = {}
             return True
         if not self.static_opt or self.sync_bn is not None:
             return False             # SyncBN: collectives inside the forward / backward, eager

@@ -148,6 +148,8 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32", g
     eng, nets, B = build(cfg_name, rank=rank, world=world, prec=prec)
     cap_s = None
     if graphs:
+        import pkc.engine as E
+        E.SEQ_CAPTURE_AFTER = 1           # the capture pass below sees each timed T once
         assert world == 1 and eng.capture()
     rng = random.Random(7)
     # sample the batches across the length-sorted chunk (short and long sentences alike)

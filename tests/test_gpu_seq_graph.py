@@ -49,7 +49,8 @@ def test_seq_graph_replay_equals_eager(body):
     cfg, nets0, opts = _build(body)
     F, B = 20, 4
     rs = np.random.RandomState(0)
-    # 4 batches of 4 sentences whose longest are 12, 9, 12, 9: two captures, two replays
+    # 4 batches of 4 sentences whose longest are 12, 9, 12, 9: each length eager at its first
+    # batch, captured and replayed at its second (SEQ_CAPTURE_AFTER = 2)
     lens = np.array([5, 7, 12, 9, 6, 9, 8, 9, 12, 12, 10, 5, 7, 9, 9, 6])
     end = np.cumsum(lens)
     X = torch.from_numpy(rs.randn(end[-1], F).astype(np.float32)).to(DEV)
