@@ -73,6 +73,14 @@ __host__ __device__ constexpr bool two_phase(int cell) {
 }
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// The gates of the bf16 step mode (step_bf16: bf16 operands, ~2^-9 each): the hardware exp and
+// reciprocal (about 2 ulp) instead of expf's range reduction and an IEEE division.  Every step of
+// that mode uses it — the per-step kernels and the persistent loops alike.
+__device__ __forceinline__ float sigm_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+template <bool BF>
+__device__ __forceinline__ float sigm_mode(float x) { return BF ? sigm_fast(x) : sigm(x); }
 
 struct RnnIdx {
   int T, B, B2, H;
@@ -642,16 +650,16 @@ __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix
     h = hcr * m;
     a.gates[si] = hcr;
   } else if constexpr (CELL == PKC_CELL_LIGRU) {
-    const float z = sigm(e.w[0] + acc[0]);
+    const float z = sigm_mode<BF>(e.w[0] + acc[0]);
     const float hcr = act_fwd(a.act, e.w[1] + acc[1]);
     h = z * hp + (1.f - z) * (hcr * m);
     a.gates[si] = z;
     a.gates[TB2H + si] = hcr;
   } else {
     // LSTM gates (f, i, o, c); cs[t] = c_{t-1}
-    const float f = sigm(e.w[0] + acc[0]);
-    const float i = sigm(e.w[1] + acc[1]);
-    const float o = sigm(e.w[2] + acc[2]);
+    const float f = sigm_mode<BF>(e.w[0] + acc[0]);
+    const float i = sigm_mode<BF>(e.w[1] + acc[1]);
+    const float o = sigm_mode<BF>(e.w[2] + acc[2]);
     const float cc = act_fwd(a.act, e.w[3] + acc[3]);
     const float cp = e.cp;
     const float c = i * cc * m + f * cp;

@@ -42,7 +42,7 @@ constexpr int RPW = 4;                  // batch rows per workgroup
 // fragment slots per wave (plan width: ceil(fragments / 8) <= NF, C3: 22) and how many of them
 // are register-resident (the rest, NF - NFR per wave, in LDS); 16 register slots leave room for
 // the one-slot operand look-ahead
-constexpr int FNF = 23, FNFR = 16;
+constexpr int FNF = 23, FNFR = 15;
 constexpr int BNF = 22, BNFR = 14;
 constexpr int HMAX = 576;               // H <= HMAX (36 tiles of 16)
 // row stride of the bf16 A images (elements): 16-byte rows at dword offsets 0, 48, 32, 16 mod 64
@@ -186,7 +186,9 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   constexpr int NF = FNF, NFR = FNFR;
   using Fr = Frags<NF, NFR>;
   __shared__ __attribute__((aligned(16))) char ufl[NW * Fr::NFL * 2 * FRAG];   // LDS fragments
-  __shared__ __attribute__((aligned(16))) __bf16 hl[2 * IMG];           // A: h_{t-1} (2 steps)
+  // A: h_{t-1}, one image: the cell update rewrites it after the products barrier (every read of
+  // the step is done) and the next step reads it after the step-end barrier
+  __shared__ __attribute__((aligned(16))) __bf16 hl[IMG];
   __shared__ float accl[2][RPW][AW];            // the step's products (see AW)
   __shared__ int tspill[NTILE];                  // tile -> its spill-over tile (-1: not cut)
   const RnnIdx ix = mkidx(a);
@@ -196,7 +198,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int64_t TBH = (int64_t)T * a.B * H, TB2H = (int64_t)T * B2 * H;
-  for (int i = tid; i < IMG; i += NT) reinterpret_cast<uint32_t*>(hl)[i] = 0u;   // both images
+  for (int i = tid; i < IMG / 2; i += NT) reinterpret_cast<uint32_t*>(hl)[i] = 0u;
   int pl[NF];
   Fr fr;
 #pragma clang loop unroll(full)
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
   PTR_DECL;
   for (int t = 0; t < T; ++t) {
     PTR_MARK(0);
-    const __bf16* img = hl + (t & 1) * IMG;
+    const __bf16* img = hl;
     // this step's gate pre-activations (independent of the recurrence: in flight during the MFMAs)
     // (every lane loads — element 0 for an unused slot — and every lane consumes the values below:
     // a load under a per-lane branch leaves its register pending on the other path, and the next
@@ -262,17 +264,19 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
     // straight-line over the plan (empty slots multiply zero B fragments); slot f + 1's operands
     // (the A fragment, and B from LDS past the register slots) are read before slot f's MFMAs, so
     // their LDS latency overlaps the chain
-    bf8 av = a_frag(img, c, q, slot_blk(pl[0]));
+    // (A fragments two slots ahead: they are the reads every slot makes)
+    bf8 av = a_frag(img, c, q, slot_blk(pl[0])), av1 = a_frag(img, c, q, slot_blk(pl[NF > 1 ? 1 : 0]));
     bf8 bz = fr.get(ufl, w, lane, 0, 0), bh = fr.get(ufl, w, lane, 0, 1);
 #pragma clang loop unroll(full)
     for (int f = 0; f < NF; ++f) {
       const int e = pl[f];
-      const int fn = f + 1 < NF ? f + 1 : f;
-      const bf8 an = a_frag(img, c, q, slot_blk(pl[fn]));
+      const int fn = f + 1 < NF ? f + 1 : f, fn2 = f + 2 < NF ? f + 2 : f;
+      const bf8 an2 = a_frag(img, c, q, slot_blk(pl[fn2]));
       const bf8 bzn = fr.get(ufl, w, lane, fn, 0), bhn = fr.get(ufl, w, lane, fn, 1);
       az = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bz, az, 0, 0, 0);
       ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bh, ah, 0, 0, 0);
-      av = an;
+      av = av1;
+      av1 = an2;
       bz = bzn;
       bh = bhn;
       const bool fl = pl_valid(e) && pl_flush(e);
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
     lds_barrier();
     PTR_MARK(2);
     // liGRU cell update (pkc_rnn_impl.h fwd_epi, CELL_LIGRU)
-    __bf16* nimg = hl + ((t + 1) & 1) * IMG;
+    __bf16* nimg = hl;
     const int tst = t * B2H;
     // every element's values first, then the stores: vmcnt is one in-order counter for loads and
     // stores alike, so a load consumed after this step's first stores would wait for those too
@@ -312,7 +316,7 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int k = 2 * j + i;
-        zv[j][i] = sigm(wz[j][i] + (pz[i] + (sp < 0 ? 0.f : xz[i])));
+        zv[j][i] = sigm_fast(wz[j][i] + (pz[i] + (sp < 0 ? 0.f : xz[i])));   // (bf16 mode)
         hv[j][i] = act_fwd(a.act, wh[j][i] + (ph[i] + (sp < 0 ? 0.f : xh[i])));
         const float h = zv[j][i] * hp[k] + (1.f - zv[j][i]) * (hv[j][i] * mk[k]);
         hp[k] = ok ? h : 0.f;                        // (a select: consumed on every lane)
