@@ -450,32 +450,48 @@ __device__ __forceinline__ void tile_blocks(const int32_t* row, int* blk) {
   }
 }
 
-// Sum the four waves' 32x16 partial tiles (MFMA C layout: col = lane & 15, row = 4*(lane>>4)+i)
-// into tile[32][17]; red is [4][32][17] scratch.  Ends with a barrier.
+// The NW waves' 32x16 partial tiles of a K-split step product (MFMA C layout: column lane & 15,
+// row 4 (lane >> 4) + i) go to red[NW][32][RED_ROW], column c at slot `col`; one barrier.  Each
+// consumer then sums the NW partials of its own element(s) (red_sum / red_sum4) straight into its
+// epilogue: no reduced tile, no second LDS pass, no second barrier (same-box A/B: C3 fp32, C4,
+// C5 1-2% per step·layer).  The sums keep one order, (w0 + w1) + (w2 + w3) [+ ((w4 + w5) +
+// (w6 + w7))], so every element is the fp32 value the former two-pass reduction produced.  Rows
+// of RED_ROW = 20 floats keep 4-slot groups 16-byte aligned.
 // R16: 16-row tiles (acc1 unused): rows 0..15 only.
-template <int NW = 4, bool R16 = false>
-__device__ __forceinline__ void reduce_tile(const f32x4& acc0, const f32x4& acc1, float* red,
-                                            float* tile) {
+constexpr int RED_ROW = 20;
+template <int NW, bool R16 = false>
+__device__ __forceinline__ void stage_partials(const f32x4& acc0, const f32x4& acc1, float* red,
+                                               int col) {
+  static_assert(NW % 4 == 0, "partials are summed in fours");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = lane & 15, q = lane >> 4;
-  float* rw = red + w * 32 * 17;
+  const int q = lane >> 4;
+  float* rw = red + w * 32 * RED_ROW;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    rw[(4 * q + i) * 17 + c] = acc0[i];
-    if constexpr (!R16) rw[(16 + 4 * q + i) * 17 + c] = acc1[i];
+    rw[(4 * q + i) * RED_ROW + col] = acc0[i];
+    if constexpr (!R16) rw[(16 + 4 * q + i) * RED_ROW + col] = acc1[i];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < (R16 ? 16 : 32) * 16; e += 64 * NW) {
-    const int r = e >> 4, cc = e & 15;
-    const int o = r * 17 + cc;
-    float v = (red[o] + red[32 * 17 + o]) + (red[2 * 32 * 17 + o] + red[3 * 32 * 17 + o]);
+}
+template <int NW>
+__device__ __forceinline__ float red_sum(const float* red, int o) {
+  constexpr int P = 32 * RED_ROW;
+  float v = (red[o] + red[P + o]) + (red[2 * P + o] + red[3 * P + o]);
 #pragma unroll
-    for (int w4 = 4; w4 < NW; w4 += 4)
-      v += (red[w4 * 32 * 17 + o] + red[(w4 + 1) * 32 * 17 + o]) +
-           (red[(w4 + 2) * 32 * 17 + o] + red[(w4 + 3) * 32 * 17 + o]);
-    tile[o] = v;
-  }
-  __syncthreads();
+  for (int w4 = 4; w4 < NW; w4 += 4)
+    v += (red[w4 * P + o] + red[(w4 + 1) * P + o]) + (red[(w4 + 2) * P + o] + red[(w4 + 3) * P + o]);
+  return v;
+}
+// four consecutive slots (o % 4 == 0): 16-byte LDS reads, the same order per slot as red_sum
+template <int NW>
+__device__ __forceinline__ float4 red_sum4(const float* red, int o) {
+  constexpr int P = 32 * RED_ROW;
+  auto ld = [&](int w4) { return *reinterpret_cast<const float4*>(red + w4 * P + o); };
+  auto add = [](float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); };
+  float4 v = add(add(ld(0), ld(1)), add(ld(2), ld(3)));
+#pragma unroll
+  for (int w4 = 4; w4 < NW; w4 += 4) v = add(v, add(add(ld(w4), ld(w4 + 1)), add(ld(w4 + 2), ld(w4 + 3))));
+  return v;
 }
 
 // R16: the tile has only its first 16 rows (2B <= 16: C3, C5), the second chain is skipped
@@ -716,8 +732,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   PKC_TR(1);
   const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   constexpr int NTH = 64 * NW;
-  __shared__ float red[NW * 32 * 17];
-  __shared__ float tile[32 * 17];
+  __shared__ __attribute__((aligned(16))) float red[NW * 32 * RED_ROW];
   constexpr int NU = 16 / NG;
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2;
@@ -905,19 +920,27 @@ __global__ __launch_bounds__(64 * NW) void rnn_fwd_mm(pkc_rnn_args a, int t, int
   asm volatile("" ::"v"(acc0[0]), "v"(acc1[0]));   // the products complete before stamp 4
 #endif
   PKC_TR(4);
-  reduce_tile<NW, R16>(acc0, acc1, red, tile);
+  // column c holds gate gi of unit u: staged at slot NG * (c % NU) + gi, so a unit's gates are
+  // adjacent (one 16-byte read per wave partial for the LSTM)
+  stage_partials<NW, R16>(acc0, acc1, red, NG * (c % NU) + gi);
   PKC_TR(5);
   float hmax = 0.f;               // QX: max|h| over this thread's elements
   for (int p = threadIdx.x; p < 32 * NU; p += NTH) {
     const int rl = p / NU, ul = p % NU;
     const int r = r0 + rl, j = u0 + ul;
     if ((R16 && rl >= 16) || r >= B2 || j >= H) continue;
+    const int o = rl * RED_ROW + NG * ul;
     if constexpr (PH == 1) {
-      cand_epi<cand_gate(CELL)>(a, ix, t, r, j, tile[rl * 17 + ul]);
+      cand_epi<cand_gate(CELL)>(a, ix, t, r, j, red_sum<NW>(red, o));
     } else {
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (NG == 4) {
+        const float4 s = red_sum4<NW>(red, o);
+        acc[0] = s.x; acc[1] = s.y; acc[2] = s.z; acc[3] = s.w;
+      } else {
 #pragma unroll
-      for (int g = 0; g < NG; ++g) acc[g] = tile[rl * 17 + g * NU + ul];
+        for (int g = 0; g < NG; ++g) acc[g] = red_sum<NW>(red, o + g);
+      }
       float h;
       if constexpr (PF) h = fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, pre);
       else h = fwd_epi<CELL, QH, BF>(a, ix, t, r, j, acc, vars, qscale, epi_load<CELL, NG>(a, ix, t, r, j));
@@ -999,8 +1022,7 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   static_assert(!BF || MODE <= 1, "bf16 steps: one-phase cells");
   const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   constexpr int NTH = 64 * NW;
-  __shared__ float red[NW * 32 * 17];
-  __shared__ float tile[32 * 17];
+  __shared__ __attribute__((aligned(16))) float red[NW * 32 * RED_ROW];
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1048,13 +1070,13 @@ __global__ __launch_bounds__(64 * NW) void rnn_bwd_mm(pkc_rnn_args a, int t, int
   }
   mfma_chain<S, R16>(va, vb, vu, acc0, acc1);
   }   // !BF
-  reduce_tile<NW>(acc0, acc1, red, tile);
+  stage_partials<NW, R16>(acc0, acc1, red, c);
   const int64_t n = (int64_t)B2 * H;
   for (int p = threadIdx.x; p < 32 * 16; p += NTH) {
     const int rl = p >> 4, kl = p & 15;
     const int r = r0 + rl, kk = k0 + kl;
     if ((R16 && rl >= 16) || r >= B2 || kk >= H) continue;
-    const float v = tile[rl * 17 + kl];
+    const float v = red_sum<NW>(red, rl * RED_ROW + kl);
     if constexpr (MODE == 0) a.work[(4 + bz) * n + (int64_t)r * H + kk] = v;
     else if constexpr (MODE == 1) bwd_step_epi<G, CELL, BF ? 1 : 0>(a, ix, t - 1, r, kk, v);
     else rh_epi<CELL>(a, ix, t, r, kk, v);
