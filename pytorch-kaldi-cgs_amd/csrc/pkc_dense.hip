@@ -443,21 +443,33 @@ __device__ __forceinline__ void f4set(float4& v, int j, float x) {
   if (j == 0) v.x = x; else if (j == 1) v.y = x; else if (j == 2) v.z = x; else v.w = x;
 }
 
-// column-sum of a float4 (4 columns) over the 64 row-groups of the workgroup; all threads get it
-template <int G>
-__device__ __forceinline__ float4 colsum_rows(float4 v, float4* red) {
+// column-sums of K float4 (4 columns each) over the 64 row-groups of the workgroup; all threads
+// get them.  red: K * 4 G float4 of LDS that no earlier exchange of the kernel reads, so one
+// barrier per exchange (the form with a barrier before the writes as well, reusing one buffer,
+// cost two; the sums are the same, operation for operation)
+template <int G, int K>
+__device__ __forceinline__ void colsum_rows(float4 (&v)[K], float4* red) {
 #pragma unroll
   for (int o = G; o < 64; o <<= 1) {
-    v.x += __shfl_xor(v.x, o, 64);
-    v.y += __shfl_xor(v.y, o, 64);
-    v.z += __shfl_xor(v.z, o, 64);
-    v.w += __shfl_xor(v.w, o, 64);
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      v[q].x += __shfl_xor(v[q].x, o, 64);
+      v[q].y += __shfl_xor(v[q].y, o, 64);
+      v[q].z += __shfl_xor(v[q].z, o, 64);
+      v[q].w += __shfl_xor(v[q].w, o, 64);
+    }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c4 = threadIdx.x % G;
+  if (lane < G) {
+#pragma unroll
+    for (int q = 0; q < K; ++q) red[q * 4 * G + wave * G + lane] = v[q];
+  }
   __syncthreads();
-  if (lane < G) red[wave * G + lane] = v;
-  __syncthreads();
-  return f4add(f4add(red[c4], red[G + c4]), f4add(red[2 * G + c4], red[3 * G + c4]));
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    const float4* r = red + q * 4 * G;
+    v[q] = f4add(f4add(r[c4], r[G + c4]), f4add(r[2 * G + c4], r[3 * G + c4]));
+  }
 }
 
 template <int NS, int RI, int G>
@@ -488,7 +500,7 @@ __device__ __forceinline__ void load_slabs(const float* __restrict__ base, int64
 template <int NS, int RI, int G, int XM>
 __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args a) {
   constexpr int FC = 4 * G, RG = FT / G;
-  __shared__ float4 red[4 * G];
+  __shared__ float4 red[2 * 4 * G];        // the mean's exchange, then the variance's
   const int c4 = threadIdx.x % G, rg = threadIdx.x / G;
   const int c = col_group<XM>(blockIdx.x, gridDim.x, FC) * FC + c4 * 4;
   const bool cok = c < a.N;
@@ -516,7 +528,11 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
     float4 sum = z[0];
 #pragma unroll
     for (int i = 1; i < RI; ++i) sum = f4add(sum, z[i]);
-    sum = colsum_rows<G>(sum, red);
+    {
+      float4 v[1] = {sum};
+      colsum_rows<G, 1>(v, red);
+      sum = v[0];
+    }
     const float inv = 1.f / (float)M;
     mean = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
     float4 m2 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -528,7 +544,11 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
         m2 = f4add(m2, make_float4(dx * dx, dy * dy, dz * dz, dw * dw));
       }
     }
-    m2 = colsum_rows<G>(m2, red);
+    {
+      float4 v[1] = {m2};
+      colsum_rows<G, 1>(v, red + 4 * G);
+      m2 = v[0];
+    }
     const float4 var = make_float4(m2.x * inv, m2.y * inv, m2.z * inv, m2.w * inv);
     invstd = make_float4(1.f / sqrtf(var.x + a.eps), 1.f / sqrtf(var.y + a.eps),
                          1.f / sqrtf(var.z + a.eps), 1.f / sqrtf(var.w + a.eps));
@@ -601,7 +621,7 @@ __global__ __launch_bounds__(FT) void dense_fwd_small_kernel(pkc_dense_fwd_args 
 template <int NS, int RI, int G, int XM>
 __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args a) {
   constexpr int FC = 4 * G, RG = FT / G;
-  __shared__ float4 red[4 * G];
+  __shared__ float4 red[2 * 4 * G];        // sum dy and sum dy xhat in one exchange
   const int c4 = threadIdx.x % G, rg = threadIdx.x / G;
   const int c = col_group<XM>(blockIdx.x, gridDim.x, FC) * FC + c4 * 4;
   const bool cok = c < a.N;
@@ -649,8 +669,12 @@ __global__ __launch_bounds__(FT) void dense_bwd_small_kernel(pkc_dense_bwd_args 
     sdyx = f4add(sdyx, make_float4(dy[i].x * xh[i].x, dy[i].y * xh[i].y, dy[i].z * xh[i].z,
                                    dy[i].w * xh[i].w));
   }
-  sdy = colsum_rows<G>(sdy, red);
-  sdyx = colsum_rows<G>(sdyx, red);
+  {
+    float4 v[2] = {sdy, sdyx};
+    colsum_rows<G, 2>(v, red);
+    sdy = v[0];
+    sdyx = v[1];
+  }
   if (!cok) return;
   if (rg == 0) {
     if (bn) {
