@@ -293,21 +293,41 @@ def time_steps(eng, steps, warmup, allreduce=None, world=1):
     return dt
 
 
-def mfma_profile(name):
-    """MFMA utilisation of a configuration from its committed rocprofv3 counter pass
-    (scripts/gpu.sh mfma -> profiles/r*_mfma_<name>.json, scripts/mfma_summary.py: busy cycles over
-    the SIMD cycles the kernels had), MFMA-flop weighted over the kernels; None without one."""
+REC_KERNELS = ("rnn_fwd_mm", "rnn_bwd_mm", "persist::")   # the recurrences' step / loop kernels
+
+
+def mfma_profile(name, prec="fp32"):
+    """MFMA figures of a configuration from its committed rocprofv3 counter pass at `prec`
+    (scripts/gpu.sh mfma -> profiles/r*_mfma_<name>[_bf16].json, scripts/mfma_summary.py); None
+    without one.  "all_kernels": busy-cycle utilisation, MFMA-flop weighted over the kernels whose
+    counter window is trustworthy (the large projection / weight-gradient GEMMs dominate it);
+    "recurrent": the serial recurrence's own kernels (per-step launches or persistent loops) —
+    their MFMA flops over their time, against the dense peak of the pass's dtype."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_%s.json" % name)), reverse=True):
+    suffix = "" if prec == "fp32" else "_" + prec
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_%s%s.json" % (name, suffix))),
+                    reverse=True):
         try:
             rows = json.load(open(f))
+            out = {"source": os.path.relpath(f, ROOT), "prec": prec}
             fl = sum(r["mfma_gflop"] for r in rows if r.get("mfma_util_pct") is not None)
-            if fl <= 0:
-                continue
-            u = sum(r["mfma_util_pct"] * r["mfma_gflop"] for r in rows
-                    if r.get("mfma_util_pct") is not None) / fl
-            return {"mfma_util_pct": round(u, 2), "source": os.path.relpath(f, ROOT)}
-        except (OSError, ValueError, KeyError, TypeError):
+            if fl > 0:
+                out["all_kernels"] = {"mfma_util_pct": round(sum(
+                    r["mfma_util_pct"] * r["mfma_gflop"] for r in rows
+                    if r.get("mfma_util_pct") is not None) / fl, 2), "weighting": "mfma flops"}
+            rec = [r for r in rows if any(k in r["kernel"] for k in REC_KERNELS)]
+            if rec:
+                gf = sum(r["mfma_gflop"] for r in rec)
+                sec = sum(r["mfma_gflop"] / r["tflops"] * 1e-3 for r in rec if r.get("tflops"))
+                tf = gf / sec * 1e-3 if sec > 0 else None
+                peak = MFMA_PEAK_TFLOPS["bf16" if rows and rec[0].get("mfma_dtype") == "bf16"
+                                        else "fp32"]
+                out["recurrent"] = {"tflops": round(tf, 2) if tf else None,
+                                    "pct_of_peak": round(100 * tf / peak, 3) if tf else None,
+                                    "kernels": sorted({r["kernel"].split("(")[0] for r in rec})}
+            if len(out) > 2:
+                return out
+        except (OSError, ValueError, KeyError, TypeError, ZeroDivisionError):
             continue
     return None
 
@@ -330,9 +350,12 @@ def seq_entry(name, steps, warmup, with_cpu, cpu_seconds, prec="fp32"):
                        "note": "algorithmic flops (W, U scaled by mask density, heads; x3 for "
                                "training) over padded rows / measured step time; the recurrence "
                                "is serial-latency-bound: see us_per_time_step_per_layer_fwd_bwd"}
-    prof = mfma_profile(name)
+    prof = mfma_profile(name, prec)
     if prof:
         out["roofline"]["mfma_util"] = prof
+    # first-step posterior error of this mode at the config's layer sizes against the fp32 oracle
+    # (after the timed region; the oracle is the checker, never the thing timed)
+    out.update(bench_seq.parity(name, prec=prec))
     if with_cpu:
         out["cpu_baseline"] = bench_seq.cpu_baseline(name, seconds=cpu_seconds)
     return out

@@ -25,7 +25,7 @@ extern "C" {
  * 6: pkc_bn_bwd_epi, pkc_gemm_bnbwd_ok, pkc_dense_bwd_pre;
  * 7: pkc_src_digest, pkc_gemm_grouped_tile, pkc_rnn_args.persist_* (persistent liGRU time loops);
  * 8: pkc_rnn_args.qh_exact (exact quantised-h step products). */
-#define PKC_ABI_VERSION 8
+#define PKC_ABI_VERSION 9
 
 enum { PKC_OK = 0, PKC_ERR_ARG = -1, PKC_ERR_HIP = -2, PKC_ERR_IO = -3, PKC_ERR_UNSUPPORTED = -4 };
 /* FP32: exact fp32 MFMA (parity); BF16: fp32 operands rounded to bf16 for the MFMA;
@@ -365,6 +365,14 @@ int pkc_cw_stats(const float* raw, int64_t N, int D, int L, int R, double* mean,
 int64_t pkc_cw_stats_work_size(int64_t N, int D, int L, int R);
 int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, const double* mean,
                  const double* std, const int64_t* perm, float* out, int64_t ld_out, void* stream);
+/* One feature stream of a multi-stream chunk (data_io.py:184-263, ABI 9): expanded rows
+ * row0 + perm[j] (row0 + j without perm), j < nrows, of this stream's own expansion and statistics
+ * — the rows the reference keeps after trimming every stream to the widest context window
+ * (row0 = cw_left_max - L, nrows = N - cw_left_max - cw_right_max) — written to out (the stream's
+ * first column in the chunk matrix) with row stride ld_out (the chunk's width). */
+int pkc_cw_apply_rows(const float* raw, int64_t N, int D, int L, int R, const double* mean,
+                      const double* std, const int64_t* perm, int64_t row0, int64_t nrows,
+                      float* out, int64_t ld_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Kaldi feature front-end (replaces the `apply-cmvn ... | add-deltas ...` stages of the fea_opts

@@ -56,6 +56,8 @@ def _reg_norm(nets, op, lam):
 def forward_model(lines, nets, seq, fea_cols, lab_cols, inp, max_len=0, batch=0, forward_out=None):
     """utils.py:1884-2050.  seq: {arch: bool}; fea_cols: {fea: (c0, c1)}; lab_cols: {lab: col}."""
     outs = {}
+    for fea, (c0, c1) in fea_cols.items():         # utils.py:1891-1896: input features first
+        outs[fea] = inp[..., c0:c1]
     for out_name, op, a, b in lines:
         if op == "compute":
             if b in fea_cols:

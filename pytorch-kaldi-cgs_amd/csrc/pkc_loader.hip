@@ -54,15 +54,15 @@ __global__ void cw_finalize_kernel(const double* work, int P, int C, int64_t Nou
   else stdv[col] = sqrt(s / (double)Nout);
 }
 
+// output row j of nrows: the expanded row row0 + perm[j] (row0 + j without perm)
 __global__ __launch_bounds__(256) void cw_apply_kernel(const float* raw, int64_t N, int D, int L,
                                                        int R, const double* mean, const double* stdv,
-                                                       const int64_t* perm, float* out,
-                                                       int64_t ld_out) {
+                                                       const int64_t* perm, int64_t row0,
+                                                       int64_t nrows, float* out, int64_t ld_out) {
   const int C = D * (L + R + 1);
-  const int64_t Nout = N - L - R;
   const int64_t row = blockIdx.y;  // output row
-  if (row >= Nout) return;
-  const int64_t src_row = perm ? perm[row] : row;
+  if (row >= nrows) return;
+  const int64_t src_row = row0 + (perm ? perm[row] : row);
   for (int col = blockIdx.x * 256 + threadIdx.x; col < C; col += gridDim.x * 256) {
     const int b = col / D, d = col % D;
     const double v = (double)raw[cw_src(src_row, b, L, N) * D + d];
@@ -128,8 +128,29 @@ extern "C" int pkc_cw_apply(const float* raw, int64_t N, int D, int L, int R, co
   PKC_CHECK_ARG(Nout < 2147483647LL, "pkc_cw_apply: chunk too large");
   dim3 grid((C + 255) / 256, (unsigned)Nout);
   hipLaunchKernelGGL(cw_apply_kernel, grid, dim3(256), 0, S(stream), raw, N, D, L, R, mean, stdv,
-                     perm, out, ld_out);
+                     perm, (int64_t)0, Nout, out, ld_out);
   PKC_LAUNCH_CHECK("pkc_cw_apply");
+  return PKC_OK;
+}
+
+// One feature stream of a multi-stream chunk (data_io.py:184-263): rows row0 .. row0 + nrows - 1
+// of the stream's own expansion (its context window, its chunk statistics — np.roll wrap-around
+// over the stream's N rows included), i.e. the rows the reference keeps after trimming every stream
+// to the widest window (row0 = cw_left_max - L), written into its column range of the chunk
+// matrix (out = the range's first column, ld_out = the chunk's width), optionally permuted.
+extern "C" int pkc_cw_apply_rows(const float* raw, int64_t N, int D, int L, int R,
+                                 const double* mean, const double* stdv, const int64_t* perm,
+                                 int64_t row0, int64_t nrows, float* out, int64_t ld_out,
+                                 void* stream) {
+  using namespace pkc;
+  const int C = D * (L + R + 1);
+  PKC_CHECK_ARG(raw && mean && stdv && out && N > L + R && ld_out >= C && row0 >= 0 && nrows > 0 &&
+                    row0 + nrows <= N - L - R && nrows < 2147483647LL,
+                "pkc_cw_apply_rows: bad arguments");
+  dim3 grid((C + 255) / 256, (unsigned)nrows);
+  hipLaunchKernelGGL(cw_apply_kernel, grid, dim3(256), 0, S(stream), raw, N, D, L, R, mean, stdv,
+                     perm, row0, nrows, out, ld_out);
+  PKC_LAUNCH_CHECK("pkc_cw_apply_rows");
   return PKC_OK;
 }
 

@@ -1,6 +1,10 @@
 // pkc_rnn_impl.h — the serial time loops of the recurrent layers (forward and BPTT).
-// Compiled as two translation units (pkc_rnn_fwd.hip: PKC_RNN_FWD, pkc_rnn_bwd.hip: PKC_RNN_BWD)
-// that build in parallel; each instantiates only its direction's step kernels.
+// Compiled as six translation units that build in parallel: the direction (PKC_RNN_FWD /
+// PKC_RNN_BWD) times the cell family (PKC_RNN_PART 0: LSTM + the extern "C" dispatch,
+// pkc_rnn_{fwd,bwd}.hip; 1: liGRU, pkc_rnn_{fwd,bwd}_ligru.hip; 2: GRU / minimalGRU / RNN,
+// pkc_rnn_{fwd,bwd}_gru.hip).  Each instantiates only its own step kernels; every kernel and helper
+// has internal linkage (an unnamed namespace), so the translation units share nothing but the
+// entry points declared below.
 //
 // Reference: liGRU  neural_networks.py:1573-1584 (z = sig(wz+Uz h); hc = act(wh+Uh h)*drop;
 //                   h = z*h + (1-z)*hc), shared-weight bidirectional rows via cat/flip
@@ -37,7 +41,25 @@
 #pragma once
 #include "pkc_common.h"
 
+#ifndef PKC_RNN_PART
+#define PKC_RNN_PART 0
+#endif
+
 namespace pkc {
+
+// the per-cell-family time loops (one translation unit each, see above)
+int rnn_fwd_lstm(const pkc_rnn_args* a, hipStream_t s);
+int rnn_fwd_ligru(const pkc_rnn_args* a, hipStream_t s);
+int rnn_fwd_gru(const pkc_rnn_args* a, hipStream_t s);
+int rnn_fwd_mingru(const pkc_rnn_args* a, hipStream_t s);
+int rnn_fwd_rnn(const pkc_rnn_args* a, hipStream_t s);
+int rnn_bwd_lstm(const pkc_rnn_args* a, float* dpre, hipStream_t s);
+int rnn_bwd_ligru(const pkc_rnn_args* a, float* dpre, hipStream_t s);
+int rnn_bwd_gru(const pkc_rnn_args* a, float* dpre, hipStream_t s);
+int rnn_bwd_mingru(const pkc_rnn_args* a, float* dpre, hipStream_t s);
+int rnn_bwd_rnn(const pkc_rnn_args* a, float* dpre, hipStream_t s);
+
+namespace {
 
 constexpr int RT = 256;          // threads per workgroup (4 waves)
 
@@ -1438,11 +1460,15 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
    : a->H <= 1024 ? FN<G, CELL, 64>(__VA_ARGS__)                     \
    : FN<G, CELL, 128>(__VA_ARGS__))
 
+}  // namespace
+
 // Persistent liGRU time loops (pkc_rnn_persist.hip): one launch per layer and direction of the
 // whole forward / BPTT loop, for block-sparse U in bf16 step mode (pkc_rnn_args.persist_*)
 bool rnn_persist_ok(const pkc_rnn_args* a, bool bwd);
 int rnn_persist_fwd(const pkc_rnn_args* a, hipStream_t s);
 int rnn_persist_bwd(const pkc_rnn_args* a, hipStream_t s);
+
+namespace {
 
 #ifdef PKC_RNN_FWD
 template <int G, int CELL>
@@ -1499,7 +1525,7 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
 }
 
 #endif  // PKC_RNN_BWD
-static int check(const pkc_rnn_args* a, bool bwd) {
+[[maybe_unused]] int check(const pkc_rnn_args* a, bool bwd) {
   PKC_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->H > 0 && a->H <= 2048, "pkc_rnn: bad shape (H <= 2048)");
   PKC_CHECK_ARG(a->cell >= PKC_CELL_LIGRU && a->cell <= PKC_CELL_RNN, "pkc_rnn: bad cell %d", a->cell);
   PKC_CHECK_ARG(!two_phase(a->cell) || (a->rh && a->qbits <= 0),
@@ -1526,8 +1552,13 @@ static int check(const pkc_rnn_args* a, bool bwd) {
     if (bwd) PKC_CHECK_ARG(a->ut_h && a->dgates_h, "pkc_rnn_bwd: bf16 steps need ut_h, dgates_h");
   }
   if (a->qh_exact) {
-    PKC_CHECK_ARG(a->qbits > 0 && a->qbits <= 16 && !a->step_bf16 && a->work,
-                  "pkc_rnn: qh_exact needs quantised h (qbits <= 16), fp32 step products and work");
+    // (no LayerNorm: the per-wave max|h| partials QX quantises the next step with are recorded
+    // from the cell's h, which rnn_ln_fwd would then rewrite — the reference quantises the LN
+    // output, neural_networks.py:1093-1094)
+    PKC_CHECK_ARG(a->cell == PKC_CELL_LSTM && a->qbits > 0 && a->qbits <= 16 && !a->step_bf16 &&
+                      a->work && !a->ln_gamma,
+                  "pkc_rnn: qh_exact needs an LSTM with quantised h (qbits <= 16), no LayerNorm, "
+                  "fp32 step products and work");
     for (int g = 0; g < G; ++g) PKC_CHECK_ARG(a->U_h[g], "pkc_rnn: qh_exact needs U_h[%d]", g);
   }
   if (a->kmap_fwd || a->kmap_bwd) {
@@ -1540,44 +1571,85 @@ static int check(const pkc_rnn_args* a, bool bwd) {
   return PKC_OK;
 }
 
+}  // namespace
+
+// ---- this translation unit's cell family
+#if defined(PKC_RNN_FWD) && PKC_RNN_PART == 0
+int rnn_fwd_lstm(const pkc_rnn_args* a, hipStream_t s) { return fwd_impl<4, PKC_CELL_LSTM>(a, s); }
+#elif defined(PKC_RNN_FWD) && PKC_RNN_PART == 1
+int rnn_fwd_ligru(const pkc_rnn_args* a, hipStream_t s) { return fwd_impl<2, PKC_CELL_LIGRU>(a, s); }
+#elif defined(PKC_RNN_FWD) && PKC_RNN_PART == 2
+int rnn_fwd_gru(const pkc_rnn_args* a, hipStream_t s) { return fwd_impl<3, PKC_CELL_GRU>(a, s); }
+int rnn_fwd_mingru(const pkc_rnn_args* a, hipStream_t s) { return fwd_impl<2, PKC_CELL_MINGRU>(a, s); }
+int rnn_fwd_rnn(const pkc_rnn_args* a, hipStream_t s) { return fwd_impl<1, PKC_CELL_RNN>(a, s); }
+#endif
+#if defined(PKC_RNN_BWD) && PKC_RNN_PART == 0
+int rnn_bwd_lstm(const pkc_rnn_args* a, float* d, hipStream_t s) { return bwd_impl<4, PKC_CELL_LSTM>(a, d, s); }
+#elif defined(PKC_RNN_BWD) && PKC_RNN_PART == 1
+int rnn_bwd_ligru(const pkc_rnn_args* a, float* d, hipStream_t s) { return bwd_impl<2, PKC_CELL_LIGRU>(a, d, s); }
+#elif defined(PKC_RNN_BWD) && PKC_RNN_PART == 2
+int rnn_bwd_gru(const pkc_rnn_args* a, float* d, hipStream_t s) { return bwd_impl<3, PKC_CELL_GRU>(a, d, s); }
+int rnn_bwd_mingru(const pkc_rnn_args* a, float* d, hipStream_t s) { return bwd_impl<2, PKC_CELL_MINGRU>(a, d, s); }
+int rnn_bwd_rnn(const pkc_rnn_args* a, float* d, hipStream_t s) { return bwd_impl<1, PKC_CELL_RNN>(a, d, s); }
+#endif
 }  // namespace pkc
 
-#ifdef PKC_RNN_FWD
-extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
-  using namespace pkc;
-  int st = check(a, false);
-  if (st) return st;
-  switch (a->cell) {
-    case PKC_CELL_LIGRU: return fwd_impl<2, PKC_CELL_LIGRU>(a, S(stream));
-    case PKC_CELL_GRU: return fwd_impl<3, PKC_CELL_GRU>(a, S(stream));
-    case PKC_CELL_MINGRU: return fwd_impl<2, PKC_CELL_MINGRU>(a, S(stream));
-    case PKC_CELL_RNN: return fwd_impl<1, PKC_CELL_RNN>(a, S(stream));
-    default: return fwd_impl<4, PKC_CELL_LSTM>(a, S(stream));
-  }
-}
-
-#ifdef PKC_TRACE
-// measurement builds only: the forward step kernels' stamps (n <= TRACE_WG * TRACE_SLOTS)
-extern "C" int pkc_trace_read(unsigned long long* host, int n) {
+#if defined(PKC_TRACE) && defined(PKC_RNN_FWD)
+// measurement builds: this part's forward step-kernel stamps (pkc_trace_read merges the parts)
+#define PKC_RNN_TRACE_NAME2(p) pkc_trace_read_fwd##p
+#define PKC_RNN_TRACE_NAME(p) PKC_RNN_TRACE_NAME2(p)
+extern "C" int PKC_RNN_TRACE_NAME(PKC_RNN_PART)(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(pkc::trace_buf), sizeof(unsigned long long) * n, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
 
-#endif  // PKC_RNN_FWD
-#ifdef PKC_RNN_BWD
+#if defined(PKC_RNN_FWD) && PKC_RNN_PART == 0
+extern "C" int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream) {
+  using namespace pkc;
+  int st = check(a, false);
+  if (st) return st;
+  switch (a->cell) {
+    case PKC_CELL_LIGRU: return rnn_fwd_ligru(a, S(stream));
+    case PKC_CELL_GRU: return rnn_fwd_gru(a, S(stream));
+    case PKC_CELL_MINGRU: return rnn_fwd_mingru(a, S(stream));
+    case PKC_CELL_RNN: return rnn_fwd_rnn(a, S(stream));
+    default: return rnn_fwd_lstm(a, S(stream));
+  }
+}
+
+#ifdef PKC_TRACE
+extern "C" int pkc_trace_read_fwd0(unsigned long long* host, int n);
+extern "C" int pkc_trace_read_fwd1(unsigned long long* host, int n);
+extern "C" int pkc_trace_read_fwd2(unsigned long long* host, int n);
+// measurement builds only: the forward step kernels' stamps (n <= TRACE_WG * TRACE_SLOTS) — the
+// three parts' buffers merged (a part whose kernels did not run left zeros)
+extern "C" int pkc_trace_read(unsigned long long* host, int n) {
+  if (pkc_trace_read_fwd0(host, n)) return -1;
+  unsigned long long* tmp = new unsigned long long[n];
+  int st = 0;
+  for (int p = 1; p <= 2 && !st; ++p) {
+    st = p == 1 ? pkc_trace_read_fwd1(tmp, n) : pkc_trace_read_fwd2(tmp, n);
+    for (int i = 0; i < n && !st; ++i) host[i] = host[i] > tmp[i] ? host[i] : tmp[i];
+  }
+  delete[] tmp;
+  return st;
+}
+#endif
+
+#endif
+#if defined(PKC_RNN_BWD) && PKC_RNN_PART == 0
 extern "C" int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream) {
   using namespace pkc;
   int st = check(a, true);
   if (st) return st;
   PKC_CHECK_ARG(dpre, "pkc_rnn_bwd: null dpre");
   switch (a->cell) {
-    case PKC_CELL_LIGRU: return bwd_impl<2, PKC_CELL_LIGRU>(a, dpre, S(stream));
-    case PKC_CELL_GRU: return bwd_impl<3, PKC_CELL_GRU>(a, dpre, S(stream));
-    case PKC_CELL_MINGRU: return bwd_impl<2, PKC_CELL_MINGRU>(a, dpre, S(stream));
-    case PKC_CELL_RNN: return bwd_impl<1, PKC_CELL_RNN>(a, dpre, S(stream));
-    default: return bwd_impl<4, PKC_CELL_LSTM>(a, dpre, S(stream));
+    case PKC_CELL_LIGRU: return rnn_bwd_ligru(a, dpre, S(stream));
+    case PKC_CELL_GRU: return rnn_bwd_gru(a, dpre, S(stream));
+    case PKC_CELL_MINGRU: return rnn_bwd_mingru(a, dpre, S(stream));
+    case PKC_CELL_RNN: return rnn_bwd_rnn(a, dpre, S(stream));
+    default: return rnn_bwd_lstm(a, dpre, S(stream));
   }
 }
-
-#endif  // PKC_RNN_BWD
+#endif

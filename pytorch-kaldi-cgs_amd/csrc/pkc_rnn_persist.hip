@@ -134,6 +134,13 @@ __device__ __forceinline__ int pl_sidx(int e) { return (e >> 19) & 7; }
 constexpr int NTILE = HMAX / 16;        // output tiles of a layer
 // product-tile row: H columns, 16 for tile columns past H, then NW spill-over tiles of 16
 constexpr int XCOL = HMAX + 16, AW = XCOL + NW * 16;
+// static LDS of the two loops against gfx950's 160 KiB per workgroup (the BPTT sits
+// within 1.6 KB of it; any growth must fail here, not as a link error of the whole library)
+constexpr int LDS_LIMIT = 160 * 1024;
+constexpr int FWD_LDS = NW * (FNF - FNFR) * 2 * FRAG + IMG * 2 + 2 * RPW * AW * 4 + NTILE * 4;
+constexpr int BWD_LDS = NW * (BNF - BNFR) * 2 * FRAG + 2 * 2 * IMG * 2 + RPW * AW * 4 + NTILE * 4;
+static_assert(FWD_LDS <= LDS_LIMIT, "persistent forward loop: static LDS over 160 KiB");
+static_assert(BWD_LDS <= LDS_LIMIT, "persistent BPTT loop: static LDS over 160 KiB");
 // el: an element's A-image position (bits 0-15) and its tile's spill-over index + 1 (bits 16-19)
 __device__ __forceinline__ int el_pos(int el) { return el & 0xFFFF; }
 __device__ __forceinline__ int el_spill(int el) { return (el >> 16) - 1; }

@@ -9,7 +9,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PKC_LIB", os.path.join(_HERE, "libpkc.so"))
 
-ABI_VERSION = 8         # include/pkc.h PKC_ABI_VERSION
+ABI_VERSION = 9         # include/pkc.h PKC_ABI_VERSION
 PKC_OK, PKC_ERR_ARG, PKC_ERR_HIP, PKC_ERR_IO, PKC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 PREC_FP32, PREC_BF16, PREC_BF16IN, PREC_BF16X3 = 0, 1, 2, 3
 ACT = {"linear": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "htanh": 4, "leaky_relu": 5, "elu": 6}
@@ -162,6 +162,8 @@ _SIGS = {
     "pkc_cw_stats": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]),
     "pkc_cw_stats_work_size": (i64, [i64, C.c_int, C.c_int, C.c_int]),
     "pkc_cw_apply": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, i64, vp]),
+    "pkc_cw_apply_rows": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, i64, i64, vp,
+                                    i64, vp]),
     "pkc_feat_frontend": (C.c_int, [vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, C.c_int, vp, C.c_int,
                                     C.c_int, vp, vp]),
     "pkc_ark_write_mat": (C.c_int, [C.c_char_p, C.c_int, C.c_char_p, i64, i64, vp]),

@@ -115,10 +115,6 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
     max_seq = {"train": int(config["batches"].get("max_seq_length_train", "-1")),
                "valid": int(config["batches"].get("max_seq_length_valid", "-1"))}.get(to_do, -1)
     fea_dict, lab_dict, arch_dict = dict_fea_lab_arch(config)
-    if len(fea_dict) != 1:
-        raise NotImplementedError("pkc chunk preparation handles one feature stream per model")
-    (fname, fd), = fea_dict.items()
-    fea, frontend = _read_features(fd[1], fd[2], output_folder)
     labs, lab_names = [], []
     if not fea_only:
         for lname, ld in lab_dict.items():
@@ -126,17 +122,23 @@ def read_lab_fea(cfg_file, fea_only, shared_list, output_folder):
             lab_names.append(lname)
     seq = any(a[2] for a in arch_dict.values())
     rng = np.random if (not seq and to_do != "forward") else None
-    # sort / split the utterances and start the pinned-memory upload on a side stream here, in
-    # the loader thread, so it overlaps the current chunk's training.  The GPU half of load_chunk
-    # (context window, normalisation, frame shuffle) is item 5's finish(): run_nn calls it where the
-    # reference's thread shuffles (after the model init draws), keeping np.random's draw order
-    staged = D.stage_chunk(fea, labs, max_seq, frontend=frontend)
-    L, R = int(fd[3]), int(fd[4])
-    data_set = D.PendingChunk(staged, labs, lab_names, L, R, max_seq, rng, fname)
-    c0, c1 = data_set.fea_cols[fname]
-    fea_dict[fname] = fea_dict[fname][:5] + [c0, c1, c1 - c0]        # data_io.py:225-228
+    # every feature stream (data_io.py:184-263: fea_dict order) sorted / split and its pinned-memory
+    # upload started on a side stream here, in the loader thread, so it overlaps the current chunk's
+    # training.  The GPU half of load_chunk (context windows, normalisation, stream stacking, frame
+    # shuffle) is item 5's finish(): run_nn calls it where the reference's thread shuffles (after
+    # the model init draws), keeping np.random's draw order
+    streams = []
+    for fname, fd in fea_dict.items():
+        fea, frontend = _read_features(fd[1], fd[2], output_folder)
+        staged = D.stage_chunk(fea, labs, max_seq, frontend=frontend)
+        streams.append((staged, int(fd[3]), int(fd[4]), fname))
+    data_set = D.PendingChunk(streams, labs, lab_names, max_seq, rng)
+    for fname in fea_dict:
+        c0, c1 = data_set.fea_cols[fname]
+        fea_dict[fname] = fea_dict[fname][:5] + [c0, c1, c1 - c0]    # data_io.py:225-240
+    c_end = max(c1 for _, c1 in data_set.fea_cols.values())
     for i, ln in enumerate(lab_names):
-        lab_dict[ln] = lab_dict[ln][:3] + [c1 + i]                     # data_io.py:259-261
+        lab_dict[ln] = lab_dict[ln][:3] + [c_end + i]                 # data_io.py:259-261
     # data_io.py:277-282: [data_name, data_end_index, fea_dict, lab_dict, arch_dict, data_set]
     shared_list.extend([data_set.names, data_set.end_index, fea_dict, lab_dict, arch_dict, data_set])
 
@@ -152,6 +154,8 @@ def model_init(config, arch_dict, fea_dims, to_do):
     nns = {}
     out_dims = dict(fea_dims)
     for out, op, a, b in parse_model(config["model"]["model"]):
+        if op == "concatenate":                          # utils.py:1805-1809
+            out_dims[out] = out_dims[a] + out_dims[b]
         if op != "compute":
             continue
         sec = arch_dict[a][0]

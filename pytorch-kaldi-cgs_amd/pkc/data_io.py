@@ -266,24 +266,29 @@ def trim_end_index(end_index, left, right):
 
 class PendingChunk(Chunk):
     """Item 5 of read_lab_fea's shared list: a chunk whose utterances are sorted / split and whose
-    raw frames are uploading (StagedChunk); the GPU half of load_chunk (context window, chunk
-    normalisation, label shift, frame shuffle) runs on finish() — which run_nn calls where the
-    reference's loader thread shuffles, so the np.random draws keep the reference's order — or on
-    first use of the device tensors."""
+    raw frames are uploading (StagedChunk, one per feature stream); the GPU half of load_chunk
+    (context windows, chunk normalisation, label shift, stream stacking, frame shuffle) runs on
+    finish() — which run_nn calls where the reference's loader thread shuffles, so the np.random
+    draws keep the reference's order — or on first use of the device tensors.
 
-    def __init__(self, staged, labs, lab_names, left, right, max_seq, shuffle_rng, fea_name):
-        self._pending = (staged, labs, list(lab_names), left, right, max_seq, shuffle_rng, fea_name)
-        N, D = staged.shape
-        Cc = D * (left + right + 1)
-        super().__init__(staged.names, trim_end_index(staged.end_index, left, right), None, None,
-                         {fea_name: (0, Cc)}, list(lab_names))
+    streams: [(StagedChunk, cw_left, cw_right, fea_name)] in fea_dict order (data_io.py:184)."""
+
+    def __init__(self, streams, labs, lab_names, max_seq, shuffle_rng):
+        self._pending = (streams, labs, list(lab_names), max_seq, shuffle_rng)
+        Lm, Rm = max(l for _, l, _, _ in streams), max(r for _, _, r, _ in streams)
+        cols, c = {}, 0
+        for st, l, r, fname in streams:
+            w = st.shape[1] * (l + r + 1)
+            cols[fname] = (c, c + w)
+            c += w
+        super().__init__(streams[0][0].names, trim_end_index(streams[0][0].end_index, Lm, Rm), None,
+                         None, cols, list(lab_names))
 
     def finish(self):
         if self._pending is not None:
-            staged, labs, lab_names, L, R, max_seq, rng, fname = self._pending
+            streams, labs, lab_names, max_seq, rng = self._pending
             self._pending = None
-            ch = prepare_chunk(None, labs, lab_names, L, R, max_seq, shuffle_rng=rng, fea_name=fname,
-                               staged=staged)
+            ch = prepare_streams(streams, lab_names, shuffle_rng=rng)
             self._feats, self._labels = ch.feats, ch.labels
         return self
 
@@ -398,15 +403,39 @@ def prepare_chunk(fea, labs, lab_names, left, right, max_sequence_length, shuffl
     staged: the StagedChunk of these utterances when the loader thread already uploaded them."""
     if staged is None:
         staged = stage_chunk(fea, labs, max_sequence_length, device, frontend=frontend)
-    names, lab_arrays, end_index = staged.names, staged.lab_arrays, staged.end_index
-    N, D = staged.shape
-    Nout = N - left - right
-    end_index = trim_end_index(end_index, left, right)
-    Cc = D * (left + right + 1)
+    return prepare_streams([(staged, left, right, fea_name)], lab_names, shuffle_rng=shuffle_rng,
+                           device=device)
+
+
+def prepare_streams(streams, lab_names, shuffle_rng=None, device="cuda"):
+    """data_io.read_lab_fea over K feature streams (data_io.py:184-282), each a StagedChunk of the
+    same utterances with its own context window: every stream is expanded and z-normalised over its
+    OWN chunk (load_chunk, :121-145), then trimmed to the widest window — rows
+    [cw_left_max - L, N - L - R - (cw_right_max - R)) of its expansion (:216-219) — and
+    column-stacked in stream order (:235-240); the labels are the first stream's (:232-233), shifted
+    by their chunk minimum and trimmed alike; one frame shuffle permutes the stacked rows
+    (:269-270).  Each stream is written straight into its column range of one chunk matrix in HBM
+    (pkc_cw_apply_rows)."""
+    st0 = streams[0][0]
+    names, lab_arrays, end_index = st0.names, st0.lab_arrays, st0.end_index
+    N = st0.shape[0]
+    for st, _, _, fname in streams[1:]:
+        # data_io.py:244-253: the same sentences and end indexes in every stream
+        if list(st.names) != list(names) or st.shape[0] != N or \
+                not np.array_equal(np.asarray(st.end_index), np.asarray(end_index)):
+            raise ValueError("feature stream %s: different sentence ids or lengths than %s (the "
+                             "reference stops on this, data_io.py:244-253)" % (fname, streams[0][3]))
+    Lm, Rm = max(l for _, l, _, _ in streams), max(r for _, _, r, _ in streams)
+    Nout = N - Lm - Rm
+    if Nout <= 0:
+        raise ValueError("chunk of %d frames is shorter than the context window" % N)
+    end_index = trim_end_index(end_index, Lm, Rm)
+    widths = [st.shape[1] * (l + r + 1) for st, l, r, _ in streams]
+    Ctot = int(sum(widths))
     lab_cols = []
-    for la in lab_arrays:                      # data_io.py:137-141
+    for la in lab_arrays:                      # data_io.py:137-141, then the trim of :216
         la = la - la.min()
-        lab_cols.append(la[left:N - right] if right > 0 else la[left:])
+        lab_cols.append(la[Lm:N - Rm])
     labels = np.stack(lab_cols, 1).astype(np.int32) if lab_cols else np.zeros((Nout, 0), np.int32)
     perm = None
     if shuffle_rng is not None:                # same draws as shuffling the (Nout, C) matrix rows
@@ -414,18 +443,24 @@ def prepare_chunk(fea, labs, lab_names, left, right, max_sequence_length, shuffl
         shuffle_rng.shuffle(perm)
         labels = labels[perm]
     dev = torch.device(device)
-    torch.cuda.current_stream(dev).wait_event(staged.done)
-    raw_d = staged.raw_d
-    raw_d.record_stream(torch.cuda.current_stream(dev))
-    mean = torch.empty(Cc, dtype=torch.float64, device=dev)
-    std = torch.empty(Cc, dtype=torch.float64, device=dev)
-    work = torch.empty(int(L.lib().pkc_cw_stats_work_size(N, D, left, right)), dtype=torch.float64,
-                       device=dev)
-    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    call("pkc_cw_stats", ptr(raw_d), N, D, left, right, ptr(mean), ptr(std), ptr(work), s)
-    feats = torch.empty(Nout, Cc, dtype=torch.float32, device=dev)
+    cur = torch.cuda.current_stream(dev)
+    s = C.c_void_p(cur.cuda_stream)
+    feats = torch.empty(Nout, Ctot, dtype=torch.float32, device=dev)
     perm_d = torch.from_numpy(perm).to(dev) if perm is not None else None
-    call("pkc_cw_apply", ptr(raw_d), N, D, left, right, ptr(mean), ptr(std), ptr(perm_d), ptr(feats),
-         Cc, s)
+    fea_cols, c0 = {}, 0
+    for (st, left, right, fname), w in zip(streams, widths):
+        cur.wait_event(st.done)
+        raw_d = st.raw_d
+        raw_d.record_stream(cur)
+        D = st.shape[1]
+        mean = torch.empty(w, dtype=torch.float64, device=dev)
+        std = torch.empty(w, dtype=torch.float64, device=dev)
+        work = torch.empty(int(L.lib().pkc_cw_stats_work_size(N, D, left, right)),
+                           dtype=torch.float64, device=dev)
+        call("pkc_cw_stats", ptr(raw_d), N, D, left, right, ptr(mean), ptr(std), ptr(work), s)
+        call("pkc_cw_apply_rows", ptr(raw_d), N, D, left, right, ptr(mean), ptr(std), ptr(perm_d),
+             Lm - left, Nout, C.c_void_p(feats.data_ptr() + 4 * c0), Ctot, s)
+        fea_cols[fname] = (c0, c0 + w)
+        c0 += w
     labels_d = torch.from_numpy(np.ascontiguousarray(labels)).to(dev)
-    return Chunk(names, end_index, feats, labels_d, {fea_name: (0, Cc)}, list(lab_names))
+    return Chunk(names, end_index, feats, labels_d, fea_cols, list(lab_names))

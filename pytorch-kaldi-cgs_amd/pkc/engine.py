@@ -163,6 +163,24 @@ class RegTerm:
         return items, bstart
 
 
+def resolve_concat(lines, fea_cols):
+    """[model] concatenate(a, b) (utils.py:2014-2016: torch.cat along the feature axis) of feature
+    streams — or of earlier such concatenations — whose column ranges are adjacent in the chunk
+    matrix: read_lab_fea stacks the streams in fea_dict order (data_io.py:235-240), which is the
+    order the [model] first names them, so the result is the column range spanning both, a
+    zero-copy view of the chunk.  Returns fea_cols with those names added."""
+    cols = dict(fea_cols)
+    for out, op, a, b in lines:
+        if op != "concatenate":
+            continue
+        if a in cols and b in cols and cols[a][1] == cols[b][0]:
+            cols[out] = (cols[a][0], cols[b][1])
+        else:
+            raise NotImplementedError("concatenate(%s,%s): only adjacent feature streams (a column "
+                                      "range of the chunk) are on the pkc path" % (a, b))
+    return cols
+
+
 class SeqBatch(tuple):
     """(begin rows, lengths, left pads, T) of one sentence batch, plus .index: the batch's
     position in the bound chunk (its data-parallel frame weight, Engine.frame_scales)."""
@@ -535,6 +553,7 @@ class Engine:
                     raise NotImplementedError("sync_bn: %s has an input BatchNorm (per-rank "
                                               "statistics)" % a)
         self.prof = None                       # profile mode: list of per-launch events
+        fea_cols = resolve_concat(lines, fea_cols)
         self.F = max(c1 for _, c1 in fea_cols.values())
         self.fea_cols = fea_cols
         self.lab_names = list(lab_names)
@@ -548,6 +567,8 @@ class Engine:
         self.T = self.max_len
         self.drop_keep_in = drop_keep_in or {}
         self.rnn_drop_in = rnn_drop_in or {}
+        # the step form is fixed when the engine is built (module switches read once, here)
+        self.rnn_bf16_sparse = RNN_BF16_SPARSE
         self._build_graph()
         self._alloc()
         self._build_masks()
@@ -583,8 +604,9 @@ class Engine:
             else:
                 raise ValueError("input %s of %s is neither a feature nor a produced output" % (b, a))
             if getattr(net, "seq_model", False):
-                if src[0] != "fea":
-                    raise NotImplementedError("%s: a recurrent arch must read a feature stream" % a)
+                # (src may be a feed-forward node over the T*B rows, e.g. the MLP_layers_first ->
+                # liGRU of TIMIT_mfcc_fbank_fmllr_liGRU_best.cfg: its gradient is the recurrent
+                # layer 0's dX slabs, handed over in _rec_bwd)
                 # input LayerNorm / BatchNorm over the T*B rows (neural_networks.py:1511-1516 ...)
                 for i, spec in enumerate(net.input_norm_specs() if hasattr(net, "input_norm_specs")
                                          else []):
@@ -597,6 +619,8 @@ class Engine:
                 node = RecNode(a, net, K)
                 node.src = src
                 if src[0] == "node":
+                    if getattr(src[1], "rec_consumer", None) is not None:
+                        raise NotImplementedError("%s: read by two recurrent archs" % src[1].name)
                     src[1].rec_consumer = node      # its gradient: the rec layer-0 dX slabs
                 self.nodes.append(node)
                 produced[out] = node
@@ -684,10 +708,14 @@ class Engine:
                     term = RegTerm(op, b, 0, params)
                 term.masks = masks
                 scal[out] = {term: 1.0}
-            elif op == "compute":
+            elif op in ("compute", "concatenate"):     # (concatenate: resolve_concat)
                 continue
             else:
                 raise NotImplementedError("[model] operation %s is not on the pkc path" % op)
+        for n in self.nodes:
+            if getattr(n, "rec_consumer", None) is not None and n.consumers:
+                # its gradient would be the recurrent dX slabs AND the other consumers' slabs
+                raise NotImplementedError("%s: read by a recurrent arch and by other archs" % n.name)
         self.produced = produced
         self.heads = [l for l in self.nodes if l.head]
         if self.train and "loss_final" not in scal and not self.external:
@@ -947,7 +975,10 @@ class Engine:
                               xw_h=torch.zeros(M * K, dtype=bf, device=dev))
             if sp["ibits"]:
                 lb["hq"] = _f32((T + 1) * B2 * H, dev)      # q4(h_{t-1}) per step
-                if RNN_QH_EXACT and 0 < sp["qbits"] <= 8:    # exact bf16 copies of the grid U
+                # exact bf16 copies of the grid U (QX path: LSTM, h on <= 16 bits, no LayerNorm —
+                # the max|h| partials it quantises with are the cell's h before an LN rewrite)
+                if (RNN_QH_EXACT and 0 < sp["qbits"] <= 8 and sp["ibits"] <= 16
+                        and not sp.get("ln") and n.cell == L.CELL_LSTM):
                     lb["U_hq"] = torch.zeros(G * H * H, dtype=torch.bfloat16, device=dev)
                 if n.lbuf:                                   # layers >= 1: q1..qG of y_{l-1}
                     lb["xq"] = _f32(G * M * K, dev)
@@ -1649,7 +1680,7 @@ class Engine:
         # (block-sparse U keeps the fp32 steps: C3's 16-row tiles over 16-wide blocks measured
         # 16.6 vs 16.1 us per step and layer with bf16 operands, profiles/r04_rnn_bf16_ab.txt)
         persist = lb.get("persist_fwd") is not None
-        if lb.get("hs_h") is not None and (RNN_BF16_SPARSE or persist or (
+        if lb.get("hs_h") is not None and (self.rnn_bf16_sparse or persist or (
                 lb.get("kmap_fwd") is None and lb.get("kmap_bwd") is None)):
             a.step_bf16 = 1
             a.hs_h, a.ut_h, a.dgates_h = (lb["hs_h"].data_ptr(), lb["ut_h"].data_ptr(),
@@ -1674,6 +1705,28 @@ class Engine:
                 a.ln_dgamma = lb["ln_pg"].data_ptr()
                 a.ln_dbeta = lb["ln_pg"].data_ptr() + 4 * H
         return a
+
+    def rec_forms(self):
+        """{arch.layer: form} — which implementation each recurrent layer's time loops take:
+        "persistent" (pkc_rnn_persist.hip, one launch per loop), "bf16 steps" / "fp32 steps" (one
+        launch per time step, bf16 or exact-fp32 step products), with "block-sparse U" (kmap
+        tables) and "exact quantised-h" (QX) qualifiers.  A cfg that falls back from the
+        persistent loops (a fragment plan too long, H > 576, ...) shows it here."""
+        out = {}
+        for n in self.nodes:
+            if not n.rec:
+                continue
+            for li in range(len(n.layers)):
+                a = self._rnn_args(n, li, True, self.max_len)
+                lb = n.lbuf[li]
+                persist = a.persist_fwd is not None and a.persist_fwd != 0
+                f = "persistent" if persist else ("bf16 steps" if a.step_bf16 else "fp32 steps")
+                if not persist and lb.get("kmap_fwd") is not None:
+                    f += ", block-sparse U"
+                if a.qh_exact:
+                    f += ", exact quantised-h"
+                out["%s.%d" % (n.arch, li)] = f
+        return out
 
     def _rec_inputs(self, n, li):
         """[(ptr, ld)] per gate of layer li's GEMM input, and the dW operand (final version)."""
@@ -1991,13 +2044,18 @@ class Engine:
         M, T = self.M, self.T
         gs = getattr(n, "gsrc", None)
         if gs is not None:                   # external mode: the caller's output gradient
-            dy_ptr, dy_ns, dy_stride = gs[0].data_ptr(), gs[1], gs[2]
+            dy_t, dy_ns, dy_stride = gs[0], gs[1], gs[2]
         else:
-            dy_ptr, dy_ns = n.gslab.data_ptr(), n.sb
+            dy_t, dy_ns = n.gslab, n.sb
             dy_stride = M * n.N
+        dy_ptr = dy_t.data_ptr()
+        # tests: where each layer's dL/dy slabs sit (tests/test_gpu_steps.py re-reads them)
+        trace = getattr(self, "rec_dy_trace", None)
         for li in reversed(range(len(n.layers))):
             sp, lb = n.layers[li], n.lbuf[li]
             H, K = lb["H"], lb["K"]
+            if trace is not None:
+                trace[(n.arch, li)] = (dy_t, dy_ns, dy_stride)
             ra = self._rnn_args(n, li, True, T)
             if dy_ns > 1 and n.dysum is not None:
                 self._rec_slab_sum_ptr(dy_ptr, dy_ns, M * lb["D"], dy_stride, n.dysum, s)
@@ -2064,7 +2122,8 @@ class Engine:
                 self._gemms(dxp + sums, s)
             if on_layer is not None:
                 on_layer(li)
-            dy_ptr, dy_ns, dy_stride = lb["dx"].data_ptr(), nx, M * K
+            dy_t, dy_ns, dy_stride = lb["dx"], nx, M * K
+            dy_ptr = dy_t.data_ptr()
             if li == 0 and n.src[0] == "node":
                 n.src[1].gsrc = (lb["dx"], nx, M * K)   # input norm: gradient = these dX slabs
             elif li == 0 and self.want_dx:           # external mode: dL/dx of the caller's input
@@ -2866,6 +2925,7 @@ class ForwardRunner:
     batch, BatchNorm with running statistics, no dropout, posteriors normalised by the log prior."""
 
     def __init__(self, nets, lines, fea_cols, forward_outs, max_rows=4096):
+        fea_cols = resolve_concat(lines, fea_cols)
         self.lines, self.fea_cols, self.outs = lines, fea_cols, forward_outs
         self.nets = nets
         self.max_rows = max_rows

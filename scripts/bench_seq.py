@@ -207,6 +207,83 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32", g
             "alg_gflop_per_step": flops / steps / 1e9}
 
 
+def parity(cfg_name, prec="fp32", seed=2234, lo=12, hi=20):
+    """First-step posterior error of a configuration at its full layer sizes (BASELINE metric:
+    "posterior max-abs-err vs ref"): the engine's first training step at `prec` on one batch of B
+    sentences of U[lo, hi] frames (short, so the oracle's eager CPU loop takes seconds), same
+    initial weights, same injected recurrent dropout masks and left padding, against the oracle
+    (the reference's algorithm in fp32 on the CPU).  The oracle is the checker here only."""
+    import pkc.neural_networks as NN
+    from oracle import nets as ON
+    from oracle import run as OR
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    cls, ropts, B = rec_opts(cfg_name)
+    cfg = configparser.ConfigParser()
+    cfg["a1"] = dict(ropts, arch_name="rnn", **OPT)
+    head = dict(dnn_use_laynorm_inp="False", dnn_use_batchnorm_inp="False", arch_name="head",
+                dnn_lay="1928", dnn_drop="0.0", dnn_use_batchnorm="False", dnn_use_laynorm="False",
+                dnn_act="softmax", **dict(OPT, arch_lr="0.0004"))
+    cfg["a2"] = head
+    cfg["a3"] = dict(head, arch_name="mono", dnn_lay="48")
+    model = ("o1=compute(rnn,fea)\no2=compute(head,o1)\no3=compute(mono,o1)\n"
+             "lm=cost_nll(o3,lab_mono)\nlmw=mult_constant(lm,1.0)\nlc=cost_nll(o2,lab_cd)\n"
+             "loss_final=sum(lc,lmw)\nerr_final=cost_err(o2,lab_cd)")
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    rnn = getattr(NN, cls)(cfg["a1"], 440)
+    orn = getattr(ON, cls)(cfg["a1"], 440)
+    orn.load_state_dict(rnn.state_dict())
+    if cfg_name == "c5":
+        pset = np.load(os.path.join(ROOT, "tests", "golden", "quant.npz"),
+                       allow_pickle=False)["pattern_set"].reshape(16, 8, 8)
+        rnn.pattern_kernels = orn.pattern_kernels = pset
+    nets = {"rnn": rnn, "head": NN.MLP(cfg["a2"], rnn.out_dim), "mono": NN.MLP(cfg["a3"], rnn.out_dim)}
+    onets = {"rnn": orn, "head": ON.MLP(cfg["a2"], rnn.out_dim), "mono": ON.MLP(cfg["a3"], rnn.out_dim)}
+    for k in ("head", "mono"):
+        onets[k].load_state_dict(nets[k].state_dict())
+    opts = {"rnn": cfg["a1"], "head": cfg["a2"], "mono": cfg["a3"]}
+    for k in nets:
+        nets[k].cuda().train()
+        onets[k].train()
+    rs = np.random.RandomState(seed)
+    lens = np.sort(rs.randint(lo, hi + 1, size=B))
+    end = np.cumsum(lens)
+    X = rs.randn(end[-1], 440).astype(np.float32)
+    lab = np.stack([rs.randint(0, 1928, end[-1]), rs.randint(0, 48, end[-1])], 1).astype(np.int32)
+    specs = rnn.layer_specs()
+    R = 2 * B if specs[0]["bidir"] else B
+    masks = {("rnn", li): torch.from_numpy((rs.rand(R, sp["H"]) > 0.2).astype(np.float32))
+             for li, sp in enumerate(specs)}
+    eng = Engine(nets, opts, parse_model(model), {"fea": (0, 440)}, ["lab_cd", "lab_mono"],
+                 batch=B, max_len=int(lens.max()), seed=1,
+                 prec=L.PREC_BF16 if prec == "bf16" else L.PREC_FP32,
+                 rnn_drop_in={k: v.cuda() for k, v in masks.items()})
+    eng.bind_chunk(torch.from_numpy(X).cuda(), torch.from_numpy(lab).cuda(), end[-1], end_index=end)
+    batch = eng.next_seq_batch(random.Random(7))
+    _, _, lefts, T = batch
+    inp = torch.zeros(T, B, 442)
+    for k in range(B):                              # core.py:183-200, the engine's left pads
+        n, b0, left = int(lens[k]), int(end[k] - lens[k]), int(lefts[k])
+        inp[left:left + n, k, :440] = torch.from_numpy(X[b0:b0 + n])
+        inp[left:left + n, k, 440:] = torch.from_numpy(lab[b0:b0 + n].astype(np.float32))
+    eng.train_step(batch=batch)
+    post = eng.head_output("o2").cpu().double()
+    f = orn.forward
+    orn.forward = lambda x, _f=f: _f(x, drop_masks=[masks[("rnn", i)] for i in range(len(specs))])
+    outs = OR.forward_model(OR.parse_model(model), onets, {"rnn": True, "head": False, "mono": False},
+                            {"fea": (0, 440)}, {"lab_cd": 440, "lab_mono": 441}, inp, T, B)
+    orn.forward = f
+    ref = outs["o2"].detach().double()
+    d = (post - ref).abs()
+    del eng
+    torch.cuda.empty_cache()
+    return {"posterior_max_abs_err": float(d.max()),
+            "posterior_max_rel_err": float((d / ref.abs().clamp_min(1e-3)).max()),
+            "posterior_ref": "oracle fp32 (reference algorithm), first training step, %d layers at "
+                             "full size, B=%d sentences, T=%d" % (len(specs), B, T)}
+
+
 def gpu_like_T(cfg_name, seed=5):
     """A padded batch length drawn like the GPU's: the longest of B sentence lengths from the
     config's distribution (U[150, 450]; C5 U[100, 200])."""

@@ -27,6 +27,12 @@
 #   treeab      same-box A/B of this tree against the tree in AB_TREE (a built worktree, default
 #               _bis_r4): scripts/bench_seq.py $PKC_ARGS in each, two alternating rounds
 #                                                             -> gpurun_out/treeab.txt
+#   seq2        scripts/bench_seq.py in fp32 and in bf16 mode   -> gpurun_out/seq_fp32.log, seq_bf16.log
+#   seq_prof2   bench_seq under rocprofv3 in fp32 and bf16 mode -> gpurun_out/prof_seq/{fp32,bf16}_kernel_stats.csv
+#   trace       phase trace of the step kernels / persistent loops (libpkc_trace.so, built with
+#               `python pytorch-kaldi-cgs_amd/pkc/_build.py --trace`): scripts/trace_steps.py
+#               $TRACE_ARGS (e.g. "--config c3 --prec bf16 --persist") -> gpurun_out/trace.json
+#   b_sweep     bench.py at B = 1024 / 4096 in fp32, bf16x3 and bf16   -> gpurun_out/b_sweep.txt
 #   round       tests smoke bench bench_prof pmc
 #
 # Extra arguments for a recipe's python command: PKC_ARGS="..." (bench, seq, kprof).
@@ -126,7 +132,7 @@ r_mfma() {
     python3 scripts/mfma_summary.py /tmp/mfma$c > gpurun_out/mfma/$c.json
   done
   # the sequence configs' bf16 performance mode (bf16 projections and step products)
-  for c in c3 c4; do
+  for c in c3 c4 c5; do
     timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d /tmp/mfmab$c -o p -- python3 scripts/bench_seq.py \
       --configs $c --steps 2 --warmup 1 --prec bf16 > gpurun_out/mfma/${c}_bf16.log 2>&1
     ok $? mfma_${c}_bf16
@@ -193,6 +199,43 @@ r_ab() {
     grep -E '^\{|^ *[a-z0-9].*(TF/s|us)' gpurun_out/ab_run.log | sed "s|^|$AB_VAR=$v  |" | cut -c1-400 >> gpurun_out/ab.txt
   done; done
   cat gpurun_out/ab.txt
+}
+
+r_seq2() {
+  for P in fp32 bf16; do
+    timeout -k 10 600 python -u scripts/bench_seq.py --prec $P $A > gpurun_out/seq_$P.log 2>&1
+    ok $? seq_$P
+    grep '^{' gpurun_out/seq_$P.log | cut -c1-400
+  done
+}
+
+r_seq_prof2() {
+  mkdir -p gpurun_out/prof_seq
+  for P in fp32 bf16; do
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pseq$P -o run \
+      -- python3 scripts/bench_seq.py --steps 6 --warmup 2 --prec $P $A > gpurun_out/prof_seq/$P.log 2>&1
+    ok $? seq_prof_$P
+    cp "$(find /tmp/pseq$P -name '*kernel_stats.csv' -print -quit)" gpurun_out/prof_seq/${P}_kernel_stats.csv
+    head -8 gpurun_out/prof_seq/${P}_kernel_stats.csv | cut -c1-160
+  done
+}
+
+r_trace() {
+  PKC_LIB=$GRAFT_REPO_ROOT/pytorch-kaldi-cgs_amd/pkc/libpkc_trace.so timeout -k 10 300 \
+    python -u scripts/trace_steps.py ${TRACE_ARGS:-} > gpurun_out/trace.json 2> gpurun_out/trace.err
+  ok $? trace
+  tr -d '\n' < gpurun_out/trace.json | cut -c1-1200; echo
+}
+
+r_b_sweep() {
+  : > gpurun_out/b_sweep.txt
+  for P in fp32 bf16x3 bf16; do for B in 1024 4096; do
+    timeout -k 10 300 python -u bench.py --batch $B --prec $P --steps 150 --warmup 10 --no-cpu-baseline \
+      --no-batch-sweep --no-fp32 --no-seq-configs > gpurun_out/b_run.log 2>&1
+    ok $? "bench B=$B $P"
+    grep '^{' gpurun_out/b_run.log | cut -c1-160 | sed "s|^|B=$B $P  |" >> gpurun_out/b_sweep.txt
+  done; done
+  cat gpurun_out/b_sweep.txt
 }
 
 [ $# -gt 0 ] || { sed -n 2,30p "$0"; exit 2; }

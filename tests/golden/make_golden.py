@@ -137,6 +137,68 @@ def gen_loader():
     np.savez_compressed(os.path.join(OUT, "loader.npz"), **out)
 
 
+# multi-stream chunks (data_io.py:184-263): three feature streams of different widths and context
+# windows (the TIMIT_mfcc_fbank_fmllr_liGRU_best.cfg shape), column-stacked after a per-stream
+# trim to the widest window, labels (cd + mono) after all features
+MULTI_STREAMS = (("mfcc", 13, 2, 1), ("fbank", 23, 0, 0), ("fmllr", 40, 5, 3))
+
+
+def gen_loader_multi():
+    out = {}
+    rs = np.random.RandomState(12)
+    names, fea0, cd, mono = synth_utts(rs, 6, 9, 30, cd_min=2)
+    streams = {}
+    for name, dim, _, _ in MULTI_STREAMS:
+        streams[name] = {k: (rs.normal(0, 1, size=(len(v), dim)) * (1 + 0.1 * dim) +
+                             rs.normal(0, 0.5, size=(1, dim))).astype(np.float32)
+                         for k, v in fea0.items()}
+        pack_dict("fea_" + name, streams[name], out)
+    pack_dict("cd", cd, out)
+    pack_dict("mono", mono, out)
+
+    def fake_read_mat_ark(spec, output_folder):
+        name = next(n for n, _, _, _ in MULTI_STREAMS if "feats_%s.scp" % n in spec)
+        for k, v in streams[name].items():
+            yield k, v
+
+    def fake_read_vec_int_ark(spec, output_folder):
+        src = mono if "phones" in spec else cd
+        for k, v in src.items():
+            yield k, v
+
+    data_io.read_mat_ark = fake_read_mat_ark
+    data_io.read_vec_int_ark = fake_read_vec_int_ark
+    cfg = configparser.ConfigParser()
+    cfg["exp"] = {"to_do": "train", "seed": "2234"}
+    cfg["batches"] = {"max_seq_length_train": "1000"}
+    cfg["data_chunk"] = {
+        "fea": "\n".join("fea_name=%s\nfea_lst=feats_%s.scp\nfea_opts=\ncw_left=%d\ncw_right=%d\n"
+                         % (n, n, l, r) for n, _, l, r in MULTI_STREAMS),
+        "lab": "lab_name=lab_cd\nlab_folder=alidir\nlab_opts=ali-to-pdf\n\n"
+               "lab_name=lab_mono\nlab_folder=alidir\nlab_opts=ali-to-phones --per-frame=true\n"}
+    cfg["architecture1"] = {"arch_name": "MLP_layers1", "arch_seq_model": "False"}
+    cfg["model"] = {"model": "conc1=concatenate(mfcc,fbank)\nconc2=concatenate(conc1,fmllr)\n"
+                             "out_dnn1=compute(MLP_layers1,conc2)\n"
+                             "loss_cd=cost_nll(out_dnn1,lab_cd)\nloss_mono=cost_nll(out_dnn1,lab_mono)"}
+    cfg_path = os.path.join(_TMP, "chunk_multi.cfg")
+    for seq, tag in ((False, "nonseq"), (True, "seq")):
+        cfg["architecture1"]["arch_seq_model"] = str(seq)
+        with open(cfg_path, "w") as f:
+            cfg.write(f)
+        np.random.seed(2234)
+        shared = []
+        data_io.read_lab_fea(cfg_path, False, shared, _TMP)
+        out["rlf_%s_names" % tag] = np.array(shared[0])
+        out["rlf_%s_end" % tag] = np.asarray(shared[1])
+        out["rlf_%s_data" % tag] = shared[5].astype(np.float32)
+        out["rlf_%s_feacols" % tag] = np.array([shared[2][n][5:8] for n, _, _, _ in MULTI_STREAMS],
+                                               dtype=np.int64)
+        out["rlf_%s_labcols" % tag] = np.array([shared[3]["lab_cd"][3], shared[3]["lab_mono"][3]])
+    out["streams"] = np.array([[d, l, r] for _, d, l, r in MULTI_STREAMS], dtype=np.int64)
+    out["stream_names"] = np.array([n for n, _, _, _ in MULTI_STREAMS])
+    np.savez_compressed(os.path.join(OUT, "loader_multi.npz"), **out)
+
+
 # ----------------------------------------------------------------------------------------------
 # G2: HCGS masks (hcgs.conn_mat + cgs_base.conn_mat), seeded global np.random
 # ----------------------------------------------------------------------------------------------
@@ -541,9 +603,11 @@ if __name__ == "__main__":
             kind, _, v = a.partition(":")
             {"mlp": gen_mlp, "ghcgs": lambda _v: gen_ghcgs(), "gru": lambda _v: gen_gru(),
              "cm": lambda _v: gen_cm(), "run_nn": gen_run_nn,
-             "kmeans": lambda _v: gen_kmeans(), "text_ark": lambda _v: gen_text_ark()}[kind](v)
+             "kmeans": lambda _v: gen_kmeans(), "text_ark": lambda _v: gen_text_ark(),
+             "loader_multi": lambda _v: gen_loader_multi()}[kind](v)
         sys.exit(0)
     gen_loader()
+    gen_loader_multi()
     gen_hcgs()
     gen_ghcgs()
     gen_quant()

@@ -53,7 +53,8 @@ LAYOUT_DIGEST = {2: "aff881268bdfc4a5ffb16199eb028e3b1bdaaa98595e969dfe4d7a2fbfa
                  5: "2c453ea47366535096140ab754d5ecfcd019ccecde60defafc6b607b14f5eb2d",
                  6: "1bcf851b6b8c7c47b5d010bb84ad5bfed004e6061606a15f6e24fda230644bd9",
                  7: "e7c2d5119718927e74e47e4889727b8834bcec21da87a549b5a754e85736ecb5",
-                 8: "9e28b5a7ec480789bbdddbba246843db7d0589d5f3d0eb7cc95c8c98bcc8cc2f"}
+                 8: "9e28b5a7ec480789bbdddbba246843db7d0589d5f3d0eb7cc95c8c98bcc8cc2f",
+                 9: "9e28b5a7ec480789bbdddbba246843db7d0589d5f3d0eb7cc95c8c98bcc8cc2f"}
 
 
 def _layout_digest(L):

@@ -171,6 +171,128 @@ def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta
     return eng
 
 
+def run_config_bf16(name, steps=2, persist=True):
+    """The bf16 performance mode (Engine prec PKC_PREC_BF16: bf16 projections, heads, weight
+    gradients and step products — C3 through the persistent time loops) at the full layer sizes
+    against the oracle run with exactly that rounding (oracle.nets.use_bf16_rec_matmuls /
+    use_bf16_matmuls), SGD (as tests/test_gpu_seq.py's bf16 tests: RMSprop turns rounding noise of
+    near-zero gradients into full-size sign steps), every step from a common start
+    (flipcheck.resync).  Only the fp32 summation order differs in front of the bf16 roundings; a
+    last-bit difference there moves one operand by 2^-9 and what it reaches is counted:
+    posteriors above 1e-4 relative <= 1 % (none above 1e-3), parameter updates outside 1e-4 of the
+    tensor's scale <= 0.5 % (none beyond 1e-3)."""
+    import pkc.engine as E
+    from flipcheck import assert_counted, resync, step_outliers
+    from oracle import nets as ON
+    from oracle import run as OR
+    from pkc import _lib as L
+    from pkc.engine import Engine, parse_model
+    nets, onets, opts, model, B = build_pair(name)
+    sgd = dict(arch_opt="sgd", arch_lr="0.08", opt_momentum="0.0", opt_dampening="0.0",
+               opt_nesterov="False")
+    for k in opts:
+        opts[k].update(sgd)
+    ON.use_bf16_rec_matmuls(onets["rnn"], steps=True)
+    for k in ("head", "mono"):
+        ON.use_bf16_matmuls(onets[k])
+    for k in nets:
+        nets[k].to(DEV).train()
+        onets[k].train()
+    F = 440
+    rs = np.random.RandomState(17)
+    lens = np.sort(rs.randint(12, 21, size=B * steps))
+    end = np.cumsum(lens)
+    X = rs.randn(end[-1], F).astype(np.float32)
+    lab = np.stack([rs.randint(0, 1928, end[-1]), rs.randint(0, 48, end[-1])], 1).astype(np.int32)
+    specs = nets["rnn"].layer_specs()
+    bid = 2 if specs[0]["bidir"] else 1
+    masks = {("rnn", li): torch.from_numpy((rs.rand(bid * B, sp["H"]) > 0.2).astype(np.float32))
+             for li, sp in enumerate(specs)}
+    old = (E.RNN_PERSIST, E.RNN_BF16_SPARSE)
+    # (without the persistent loops C3's block-sparse U takes the per-step bf16 kernels)
+    E.RNN_PERSIST, E.RNN_BF16_SPARSE = persist, not persist
+    try:
+        eng = Engine(nets, opts, parse_model(model), {"fea": (0, F)}, ["lab_cd", "lab_mono"],
+                     batch=B, max_len=int(lens.max()), seed=1, prec=L.PREC_BF16,
+                     rnn_drop_in={k: v.to(DEV) for k, v in masks.items()})
+    finally:
+        E.RNN_PERSIST, E.RNN_BF16_SPARSE = old
+    lbufs = eng.nodes[0].lbuf
+    assert all(lb.get("hs_h") is not None for lb in lbufs), "bf16 step products not taken"
+    if name == "c3":
+        assert all((lb.get("persist_fwd") is not None) == persist for lb in lbufs), \
+            "persistent loops %s" % ("not taken" if persist else "taken")
+    eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), end[-1], end_index=end)
+    oopt = {k: ON.make_optimizer(onets[k].parameters(), opts[k]) for k in onets}
+    lines = OR.parse_model(model)
+    rng_e, rng_o = random.Random(7), random.Random(7)
+    snt = 0
+    posts, report = [], {}
+    for step in range(steps):
+        eng.sync_state()
+        resync(nets, onets, {k: eng.optimizer_state_dict(k) for k in nets} if step else None, oopt)
+        batch = eng.next_seq_batch(rng_e)
+        begs, blens, lefts, T = batch
+        inp = torch.zeros(T, B, F + 2)
+        for k in range(B):                          # core.py:183-200
+            n = int(lens[snt])
+            left = rng_o.randint(0, T - n)
+            b0 = int(end[snt] - n)
+            inp[left:left + n, k, :F] = torch.from_numpy(X[b0:b0 + n])
+            inp[left:left + n, k, F:] = torch.from_numpy(lab[b0:b0 + n].astype(np.float32))
+            assert left == lefts[k]
+            snt += 1
+        body = onets["rnn"]
+        f = body.forward
+        body.forward = lambda x, _f=f: _f(x, drop_masks=[masks[("rnn", i)] for i in range(len(specs))])
+        outs = OR.train_step(lines, onets, oopt, {"rnn": True, "head": False, "mono": False},
+                             {"fea": (0, F)}, {"lab_cd": F, "lab_mono": F + 1}, inp, T, B)
+        body.forward = f
+        eng.train_step(batch=batch)
+        loss, _ = eng.loss_values()
+        np.testing.assert_allclose(loss, outs["loss_final"].item(), rtol=1e-3)
+        post = eng.head_output("o2").cpu()
+        ref = outs["o2"].detach()
+        relm = (post - ref).abs() / ref.abs().clamp_min(1e-3)
+        rel = relm.max().item()
+        nout = int((relm > 1e-4).sum().item())
+        posts.append((nout, round(rel, 6)))
+        assert_counted("%s bf16 step %d posteriors" % (name, step), nout, relm.numel(), 0.01, rel,
+                       1e-3, "(max rel err %.3g; per step %s)" % (rel, posts))
+        eng.sync_state()
+        sd_o = onets["rnn"].state_dict()
+        for k in nets:
+            osd = onets[k].state_dict()
+            for pname, v in nets[k].state_dict().items():
+                if pname.endswith("num_batches_tracked"):
+                    continue
+                r = osd[pname].double()
+                parts = pname.split(".")
+                if k == "rnn" and name == "c3" and pname.endswith("weight") and \
+                        parts[0] in ("wh", "wz", "uh", "uz"):
+                    r = r * sd_o[("hcgsx" if parts[0][0] == "w" else "hcgsh") + ".%s.mask" % parts[1]].double()
+                scale = max(float(r.abs().max()), 0.08)
+                n, dmax, _ = step_outliers(v.cpu(), r, 1e-4, scale)
+                report["%d %s/%s" % (step, k, pname)] = (n, round(dmax / scale, 6))
+                assert_counted("%s bf16 step %d %s %s" % (name, step, k, pname), n, r.numel(), 0.005,
+                               dmax, 1e-3 * scale + 1e-7, "(outliers per tensor %s)" % (
+                                   {a: b for a, b in report.items() if b[0]}))
+    print("%s bf16 (persistent=%s): posteriors above 1e-4 per step (count, max rel) %s; parameter "
+          "outliers %s" % (name, persist, posts, {a: b for a, b in report.items() if b[0]}))
+
+
+def test_c3_ligru_hcgs_full_size_bf16():
+    run_config_bf16("c3")
+
+
+def test_c3_ligru_hcgs_full_size_bf16_per_step():
+    run_config_bf16("c3", persist=False)
+
+
+def test_c4_lstm_bidir_full_size_bf16():
+    run_config_bf16("c4")
+
+
 @pytest.mark.parametrize("sparse", ["force", "off"])
 def test_c3_ligru_hcgs_full_size(sparse):
     run_config("c3", sparse=sparse)

@@ -78,6 +78,15 @@ def make_cfg(body):
                          lstm_bidir="False", skip_regularization="False", guided_hcgs="True",
                          apply_guided_hcgs=str(body == "lstm_ghcgs_apply"), hcgsx_block="8",
                          hcgsx_sparse="50", hcgsh_block="8,4", hcgsh_sparse="75,50", **opt)
+    elif body in ("lstm_quant", "lstm_quant_ln"):
+        # 8-bit weights + 16-bit quantised inputs and h (quantized_modules.py:99-119, 182-222);
+        # _ln: LayerNorm of h too (:1093-1094), whose OUTPUT is what the next step quantises — the
+        # exact integer step products (QX, whose max|h| partials are the cell's h) must stay off
+        cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
+                         lstm_bidir="False", lstm_quant="True", lstm_quant_inp="True",
+                         param_quant="8,8", inp_quant="16",
+                         lstm_use_laynorm="True,True" if body == "lstm_quant_ln" else "False,False",
+                         **opt)
     elif body == "lstm_prune":     # magnitude pruning every forward (neural_networks.py:886-1005)
         cfg["a1"] = dict(LSTM_DEF, arch_name="rnn", lstm_lay="32,24", lstm_drop="0.2,0.2",
                          lstm_bidir="False", lstm_prune="True", lstm_prune_perc="60,40", **opt)
@@ -103,9 +112,12 @@ def make_cfg(body):
                                   "lstm_gl", "lstm_ghcgs_l1", "lstm_ghcgs_apply", "gru", "mingru",
                                   "rnn", "lstm_ln", "gru_ln", "gru_nobn", "lstm_ln_bn",
                                   "ligru_inpnorm", "lstm_bninp", "gru_lninp", "mingru_inpnorm",
-                                  "ligru_hcgs_sparse"])
+                                  "ligru_hcgs_sparse", "lstm_quant", "lstm_quant_ln"])
 def test_seq_engine_vs_oracle(body):
     _seq_vs_oracle(body)
+
+
+QUANT_BODIES = ("lstm_quant", "lstm_quant_ln")
 
 
 @pytest.mark.parametrize("body", ["ligru_hcgs", "lstm", "lstm_bidir", "gru", "ligru", "rnn",
@@ -142,11 +154,12 @@ def _seq_vs_oracle_run(body, bf16):
     from pkc import _lib as L
     from pkc.engine import Engine, parse_model
     cfg = make_cfg(body)
-    if bf16:
+    if bf16 or body in QUANT_BODIES:
         # SGD: RMSprop's first steps are sign steps of 4.47 lr whatever |g| is, so the bf16
-        # operand-rounding noise of a near-zero gradient element becomes a full-size step either
-        # way and later steps compare chaos, not kernels (the fp32 tests keep RMSprop; the
-        # optimizer is not what this test checks)
+        # operand-rounding noise (quantised bodies: the one-quantum moves of the 16-bit input
+        # grid) of a near-zero gradient element becomes a full-size step either way and later
+        # steps compare chaos, not kernels (the fp32 tests keep RMSprop; the optimizer is not
+        # what this test checks)
         for sec in ("a1", "a2", "a3"):
             cfg[sec].update(arch_opt="sgd", arch_lr="0.08", opt_momentum="0.0",
                             opt_dampening="0.0", opt_nesterov="False")
@@ -165,7 +178,7 @@ def _seq_vs_oracle_run(body, bf16):
                 "rnn": "RNN", "lstm_ln": "LSTM", "gru_ln": "GRU", "gru_nobn": "GRU",
                 "lstm_ln_bn": "LSTM", "ligru_inpnorm": "liGRU", "lstm_bninp": "LSTM",
                 "gru_lninp": "GRU", "mingru_inpnorm": "minimalGRU",
-                "ligru_hcgs_sparse": "liGRU"}[body]
+                "ligru_hcgs_sparse": "liGRU", "lstm_quant": "LSTM", "lstm_quant_ln": "LSTM"}[body]
                if sec == "a1" else "MLP")
         nets[o["arch_name"]] = getattr(NN, cls)(o, inp)
         onets[o["arch_name"]] = getattr(ON, cls)(o, inp)
@@ -197,8 +210,15 @@ def _seq_vs_oracle_run(body, bf16):
                      rnn_drop_in={k: v.to(DEV) for k, v in masks.items()})
     finally:
         E.RNN_SPARSE = old_sparse
+    lbufs = next(n for n in eng.nodes if n.rec).lbuf
     if body.endswith("_sparse"):
-        assert all(lb["kmap_fwd"] is not None for lb in eng.nodes[0].lbuf)
+        assert all(lb["kmap_fwd"] is not None for lb in lbufs)
+    if bf16 and body == "ligru_hcgs":    # the persistent time loops (pkc_rnn_persist.hip) run
+        assert all(lb.get("persist_fwd") is not None and lb.get("persist_bwd") is not None
+                   for lb in lbufs), "persistent loops not taken"
+    if body in QUANT_BODIES:             # exact quantised-h products only without LayerNorm
+        qx = [lb.get("U_hq") is not None for lb in lbufs]
+        assert qx == [body == "lstm_quant"] * len(lbufs), qx
     eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), end[-1], end_index=end)
     oopt = {k: ON.make_optimizer(onets[k].parameters(), opts[k]) for k in onets}
     lines = OR.parse_model(cfg["model"]["model"])
@@ -245,8 +265,9 @@ def _seq_vs_oracle_run(body, bf16):
         post_out.append(nout)
         print("%s%s step %d posterior rel err %.3g, %d of %d above 1e-4" % (
             body, " bf16" if bf16 else "", step, rel, nout, relm.numel()))
-        if bf16:
-            # a last-bit fp32 difference in front of a bf16 rounding moves that operand by 2^-9:
+        if bf16 or body in QUANT_BODIES:
+            # a last-bit fp32 difference in front of a bf16 rounding moves that operand by 2^-9
+            # (16-bit quantised h: in front of a ceil() grid step, one element by max|h| / 2^15):
             # the posteriors it moves past 1e-4 are counted (<= 1 %), none past 1e-3
             assert_counted("step %d posteriors" % step, nout, relm.numel(), 0.01, rel, 1e-3,
                            "(max rel err %.3g)" % rel)
@@ -297,8 +318,9 @@ def _seq_check_update(body, bf16, step, eng, nets, onets, opts, report, post_out
             # bf16 mode (SGD): an operand-rounding flip moves a gradient element, and its update,
             # by ~2^-9 of one product — counted (<= 0.5 %), each within 1e-3 of the scale;
             # RMSprop (fp32): a sign step of one step, 2 x 4.48 lr
-            frac = (0.005 if bf16 else 0.0) if sgd else 0.02
-            bound = (1e-3 if bf16 else 1e-4) * scale if sgd else 2 * 4.48 * lr
+            noisy = bf16 or body in QUANT_BODIES
+            frac = (0.005 if noisy else 0.0) if sgd else 0.02
+            bound = (1e-3 if noisy else 1e-4) * scale if sgd else 2 * 4.48 * lr
             assert_counted("step %d %s %s" % (step, k, name), n, ref.numel(), frac, dmax,
                            bound + 1e-7, "(outliers, max diff / scale per tensor %s; posteriors "
                            "above 1e-4 per step %s)" % (

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.lib()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.pkc_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.pkc_abi_version() == _lib.ABI_VERSION == 9
 
 
 def test_gemm_split_policy():
