@@ -170,6 +170,18 @@ int pkc_dense_fwd(const pkc_dense_fwd_args* a, float* work, void* stream);
  * (pkc_gemm_colstats: 128): merges them (Chan, fixed order) and applies — the same outputs with
  * the statistics summed in that blocking. */
 int pkc_dense_fwd_pre(const pkc_dense_fwd_args* a, float* work, int part_rows, void* stream);
+/* A BatchNorm'd layer's matmul AND epilogue in one launch at M <= 128 rows (the reference's
+ * batch_size_train; ABI 9): z = A W^T (A: M x K, lda; W: N x K, ldw; both k-contiguous), then
+ * exactly pkc_dense_fwd's epilogue on z + bias (a->zslab / nslab / slab_stride are not read).
+ * Each workgroup owns a 128-row x 16-column strip over the full contraction, so the BatchNorm
+ * column statistics need nothing from other workgroups.  prec: PKC_PREC_BF16IN (A, W bf16) or
+ * PKC_PREC_BF16 (fp32, rounded to bf16 on load: identical results); fp32 accumulation.
+ * pkc_dense_gemm_fwd_ok: 1 when the shape / precision / alignment is supported (N % 16 == 0,
+ * K % 8 == 0, lda and ldw multiples of 8, A and W 16-byte aligned). */
+int pkc_dense_gemm_fwd_ok(int prec, int M, int N, int K, const void* A, int64_t lda, const void* W,
+                          int64_t ldw);
+int pkc_dense_gemm_fwd(int prec, const void* A, int64_t lda, const void* W, int64_t ldw, int K,
+                       const pkc_dense_fwd_args* a, void* stream);
 /* floats of device workspace pkc_dense_fwd / pkc_dense_bwd need (per-16-row column partials) */
 int64_t pkc_dense_work_size(int M, int N);
 

@@ -161,6 +161,9 @@ _SIGS = {
     "pkc_cast_bf16": (C.c_int, [vp, vp, i64, vp]),
     "pkc_cw_stats": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]),
     "pkc_cw_stats_work_size": (i64, [i64, C.c_int, C.c_int, C.c_int]),
+    "pkc_dense_gemm_fwd_ok": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, vp, i64, vp, i64]),
+    "pkc_dense_gemm_fwd": (C.c_int, [C.c_int, vp, i64, vp, i64, C.c_int, C.POINTER(DenseFwdArgs),
+                                     vp]),
     "pkc_cw_apply": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, i64, vp]),
     "pkc_cw_apply_rows": (C.c_int, [vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, i64, i64, vp,
                                     i64, vp]),

@@ -108,6 +108,9 @@ REC_DW_SPLITS = int(os.environ.get("PKC_REC_DW_SPLITS", "4"))
 REC_WGRAD_BF16 = os.environ.get("PKC_REC_WGRAD_BF16", "1") != "0"
 # workgroups a layer's grouped weight-gradient launch aims at before it splits the contraction
 REC_WG_TARGET = int(os.environ.get("PKC_REC_WG_TARGET", "512"))
+# B <= 128 bf16 MLP layers: matmul + BatchNorm / activation / dropout in one launch
+# (pkc_dense_gemm_fwd; 0: split-K matmul + pkc_dense_fwd, A/B)
+FUSED_FWD = os.environ.get("PKC_FUSED_FWD", "1") != "0"
 # recurrent layers: sum the output-gradient slabs before the BPTT loop (0: per step, A/B)
 REC_DY_PRESUM = os.environ.get("PKC_REC_DY_PRESUM", "1") != "0"
 
@@ -1545,6 +1548,8 @@ class Engine:
     def _dense_fwd(self, n, s, train):
         self._quant_chain(n, s)
         prob = self._fwd_problem(n)
+        if self._fused_fwd(n, prob, s, train):
+            return
         if train and self._colstats_fwd(n, prob, s):
             return
         self._gemms([prob], s)
@@ -1613,22 +1618,7 @@ class Engine:
             self._k("nll_fused N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_nll_fused",
                     C.byref(a), s)
             return
-        keep_in = self.drop_keep_in.get(n.name)
-        a = L.DenseFwdArgs(
-            M=M, N=n.N, nslab=sf, zslab=zp, slab_stride=zs, bias=bias,
-            norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if n.bn else L.NORM_NONE,
-            gamma=n.gamma.data_ptr(), beta=n.beta.data_ptr(),
-            running_mean=n.rm.data_ptr(), running_var=n.rv.data_ptr(),
-            momentum=0.05, eps=1e-5, save_mean=n.save_mean.data_ptr(),
-            save_invstd=n.save_invstd.data_ptr(), act=L.ACT[n.act],
-            drop_p=n.drop if train else 0.0, seed=self.seed,
-            step_ctr=self.ctr.data_ptr(), stream_id=zlib.crc32(n.name.encode()),
-            keep_in=keep_in.data_ptr() if keep_in is not None else None,
-            keep_out=n.keep.data_ptr() if (n.keep is not None and train) else None,
-            xhat=n.xhat.data_ptr(), count_n=0,
-            out=None if (train and getattr(n, "f32_dead", False)
-                         and getattr(n, "bn_states", None) is None) else n.out.data_ptr(),
-            out_bf16=n.out_h.data_ptr() if n.out_h is not None else None)
+        a = self._dense_fwd_args(n, train, zp, sf, zs, bias)
         if train and n.bn and getattr(n, "bn_states", None) is not None:
             # SyncBN: this rank's column state into its row of bn_states, all-reduce (gather),
             # merge + apply
@@ -1646,6 +1636,52 @@ class Engine:
             return
         self._k("dense_fwd N=%d" % n.N, 0, 4.0 * M * n.N * (sf + 2), "pkc_dense_fwd",
                 C.byref(a), ptr(n.work), s)
+
+    def _dense_fwd_args(self, n, train, zp, sf, zs, bias):
+        """pkc_dense_fwd_args of a dense layer's epilogue (BN / act / dropout)."""
+        M = self.M
+        keep_in = self.drop_keep_in.get(n.name)
+        return L.DenseFwdArgs(
+            M=M, N=n.N, nslab=sf, zslab=zp, slab_stride=zs, bias=bias,
+            norm=(L.NORM_BN_TRAIN if train else L.NORM_BN_EVAL) if n.bn else L.NORM_NONE,
+            gamma=n.gamma.data_ptr(), beta=n.beta.data_ptr(),
+            running_mean=n.rm.data_ptr(), running_var=n.rv.data_ptr(),
+            momentum=0.05, eps=1e-5, save_mean=n.save_mean.data_ptr(),
+            save_invstd=n.save_invstd.data_ptr(), act=L.ACT[n.act],
+            drop_p=n.drop if train else 0.0, seed=self.seed,
+            step_ctr=self.ctr.data_ptr(), stream_id=zlib.crc32(n.name.encode()),
+            keep_in=keep_in.data_ptr() if keep_in is not None else None,
+            keep_out=n.keep.data_ptr() if (n.keep is not None and train) else None,
+            xhat=n.xhat.data_ptr(), count_n=0,
+            out=None if (train and getattr(n, "f32_dead", False)
+                         and getattr(n, "bn_states", None) is None) else n.out.data_ptr(),
+            out_bf16=n.out_h.data_ptr() if n.out_h is not None else None)
+
+    def _fused_fwd(self, n, prob, s, train, riding=()):
+        """A BatchNorm'd hidden layer at M <= 128 rows with bf16 products: matmul and epilogue in
+        ONE launch (pkc_dense_gemm_fwd: each workgroup a 128 x 16 column strip over the full
+        contraction, so its BatchNorm statistics are local) instead of a split-K matmul writing
+        slabs + the pkc_dense_fwd launch.  Returns False when not taken (exact-fp32 / compensated
+        precisions, block-sparse W, LayerNorm, SyncBN, operations riding in the forward launch)."""
+        if not (FUSED_FWD and self.prec == L.PREC_BF16 and self.M <= 128 and not n.head
+                and n.W is not None and not n.ln and not riding
+                and getattr(n, "bn_states", None) is None):
+            return False
+        lab, fl, nb, p = prob[:4]
+        if p.ktiles:
+            return False
+        prec = L.PREC_BF16
+        if len(prob) > 4 and prob[4] is not None:
+            prec, (nb, p) = L.PREC_BF16IN, prob[4]
+        if not L.lib().pkc_dense_gemm_fwd_ok(prec, p.M, p.N, p.K, C.c_void_p(p.A), p.lda,
+                                             C.c_void_p(p.B), p.ldb):
+            return False
+        n.sf = 1
+        a = self._dense_fwd_args(n, train, None, 1, 0, n.b.data_ptr())
+        self._k("fused_fwd %dx%dx%d" % (p.M, p.N, p.K), fl, nb - 4.0 * p.splits * p.M * p.N +
+                4.0 * p.M * p.N * 2, "pkc_dense_gemm_fwd", prec, C.c_void_p(p.A), p.lda,
+                C.c_void_p(p.B), p.ldb, p.K, C.byref(a), s)
+        return True
 
     def _rnn_args(self, n, li, train, T):
         sp, lb = n.layers[li], n.lbuf[li]
@@ -1828,6 +1864,9 @@ class Engine:
             for g in grp:
                 self._quant_chain(g, s)
             probs = [self._fwd_problem(g) for g in grp]
+            if len(grp) == 1 and self._fused_fwd(n, probs[0], s, train, slots.get(n)):
+                i += 1
+                continue
             if len(grp) == 1 and train and self._colstats_fwd(n, probs[0], s):
                 i += 1
                 continue

@@ -315,6 +315,88 @@ def test_dense_bn_fwd_bwd(L, act, p, M, N, S):
     assert zz.grad.sum(0).abs().max() < 1e-4 * max(1.0, M / 256)
 
 
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+@pytest.mark.parametrize("p", [0.0, 0.15])
+@pytest.mark.parametrize("M,N,K", [(128, 1024, 1024), (128, 1024, 440), (100, 64, 96), (1, 16, 8),
+                                   (128, 48, 1032)])
+def test_dense_gemm_fwd_fused(L, act, p, M, N, K):
+    """pkc_dense_gemm_fwd (matmul + BatchNorm / activation / dropout in one launch, every row of a
+    16-column strip per workgroup) against torch on the bf16-rounded operands: out, xhat, the
+    batch statistics, running statistics, keep mask; the fp32-staged form (PKC_PREC_BF16) equal
+    bit for bit to the bf16-stored one (BF16IN), and both equal to the split-K matmul + pkc_dense_fwd
+    path up to the fp32 summation order of the K-deep products."""
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    bias = torch.randn(N, generator=g) * 0.1
+    gamma = torch.rand(N, generator=g) + 0.5
+    beta = torch.randn(N, generator=g) * 0.1
+    keep = (torch.rand(M, N, generator=g) > p).to(torch.uint8)
+    z = (X.bfloat16().double() @ W.bfloat16().double().t()).float() + bias
+    _, _, _, ref = _bn_ref(z, gamma, beta, act, keep.float(), p) if M > 1 else (None,) * 4
+    d = {k: v.to(DEV) for k, v in dict(X=X, W=W, bias=bias, gamma=gamma, beta=beta,
+                                        keep=keep).items()}
+    outs = {}
+    for prec in (1, 2):                          # PKC_PREC_BF16 (fp32 staged), PKC_PREC_BF16IN
+        Xd, Wd = (d["X"], d["W"]) if prec == 1 else (d["X"].bfloat16(), d["W"].bfloat16())
+        rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+        sm, si = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+        xhat, out = torch.zeros(M, N, device=DEV), torch.zeros(M, N, device=DEV)
+        outh = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        kout = torch.zeros(M, N, dtype=torch.uint8, device=DEV)
+        a_ = L.DenseFwdArgs(M=M, N=N, nslab=1, zslab=None, slab_stride=0, bias=d["bias"].data_ptr(),
+                            norm=L.NORM_BN_TRAIN, gamma=d["gamma"].data_ptr(),
+                            beta=d["beta"].data_ptr(), running_mean=rm.data_ptr(),
+                            running_var=rv.data_ptr(), momentum=0.05, eps=1e-5,
+                            save_mean=sm.data_ptr(), save_invstd=si.data_ptr(), act=L.ACT[act],
+                            drop_p=p, seed=1, step_ctr=None, stream_id=0,
+                            keep_in=d["keep"].data_ptr() if p > 0 else None,
+                            keep_out=kout.data_ptr() if p > 0 else None, xhat=xhat.data_ptr(),
+                            out=out.data_ptr(), out_bf16=outh.data_ptr())
+        assert L.lib().pkc_dense_gemm_fwd_ok(prec, M, N, K, C.c_void_p(Xd.data_ptr()), K,
+                                             C.c_void_p(Wd.data_ptr()), K)
+        L.call("pkc_dense_gemm_fwd", prec, L.ptr(Xd), K, L.ptr(Wd), K, K, C.byref(a_), _s())
+        torch.cuda.synchronize()
+        outs[prec] = [t.cpu() for t in (out, xhat, sm, si, rm, rv, outh.float(), kout)]
+    for a, b in zip(outs[1], outs[2]):
+        assert torch.equal(a, b), "fp32-staged and bf16-stored operands differ"
+    out, xhat, sm, si, rm, rv, outh, kout = outs[2]
+    assert torch.equal(outh, out.bfloat16().float())
+    if p > 0:
+        assert torch.equal(kout, keep)
+    if M == 1:                                   # one row: BatchNorm gives beta, xhat 0
+        assert torch.equal(xhat, torch.zeros_like(xhat))
+        return
+    mu, var = z.double().mean(0), z.double().var(0, unbiased=False)
+    torch.testing.assert_close(sm, mu.float(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(si, (1 / (var + 1e-5).sqrt()).float(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rm, 0.05 * mu.float(), rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(rv, 0.95 + 0.05 * z.var(0, unbiased=True), rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(xhat, ((z.double() - mu) / (var + 1e-5).sqrt()).float(), rtol=1e-4,
+                               atol=2e-5)
+    torch.testing.assert_close(out, ref.detach(), rtol=1e-4, atol=2e-5)
+    # the unfused path (split-K slabs + pkc_dense_fwd) on the same rounded operands
+    splits = L.lib().pkc_gemm_pick_splits(M, N, K)
+    Cd = torch.zeros(splits, M, N, device=DEV)
+    Xb, Wb = d["X"].bfloat16(), d["W"].bfloat16()
+    L.call("pkc_gemm", 2, 1, 1, M, N, K, L.ptr(Xb), K, L.ptr(Wb), K, L.ptr(Cd), N, splits, M * N,
+           _s())
+    rm2, rv2 = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+    sm2, si2 = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+    xhat2, out2 = torch.zeros(M, N, device=DEV), torch.zeros(M, N, device=DEV)
+    a2 = L.DenseFwdArgs(M=M, N=N, nslab=splits, zslab=Cd.data_ptr(), slab_stride=M * N,
+                        bias=d["bias"].data_ptr(), norm=L.NORM_BN_TRAIN, gamma=d["gamma"].data_ptr(),
+                        beta=d["beta"].data_ptr(), running_mean=rm2.data_ptr(),
+                        running_var=rv2.data_ptr(), momentum=0.05, eps=1e-5, save_mean=sm2.data_ptr(),
+                        save_invstd=si2.data_ptr(), act=L.ACT[act], drop_p=p, seed=1, step_ctr=None,
+                        stream_id=0, keep_in=d["keep"].data_ptr() if p > 0 else None, keep_out=None,
+                        xhat=xhat2.data_ptr(), out=out2.data_ptr())
+    work = torch.zeros(L.lib().pkc_dense_work_size(M, N), device=DEV)
+    L.call("pkc_dense_fwd", C.byref(a2), L.ptr(work), _s())
+    torch.testing.assert_close(out, out2.cpu(), rtol=1e-4, atol=2e-5)
+    torch.testing.assert_close(xhat, xhat2.cpu(), rtol=1e-4, atol=2e-5)
+
+
 def test_dense_dropout_rate_and_determinism(L):
     M, N, p = 256, 512, 0.15
     z = torch.randn(1, M, N, device=DEV)
