@@ -109,8 +109,11 @@ REC_WGRAD_BF16 = os.environ.get("PKC_REC_WGRAD_BF16", "1") != "0"
 # workgroups a layer's grouped weight-gradient launch aims at before it splits the contraction
 REC_WG_TARGET = int(os.environ.get("PKC_REC_WG_TARGET", "512"))
 # B <= 128 bf16 MLP layers: matmul + BatchNorm / activation / dropout in one launch
-# (pkc_dense_gemm_fwd; 0: split-K matmul + pkc_dense_fwd, A/B)
-FUSED_FWD = os.environ.get("PKC_FUSED_FWD", "1") != "0"
+# (pkc_dense_gemm_fwd) instead of the split-K matmul + pkc_dense_fwd pair.  Same box, two
+# alternating rounds: C2 0.1429 / 0.1437 ms per step fused against 0.1423 / 0.1423 for the pair
+# (19 vs 24 launches per step): each workgroup of the fused form ingests all 128 rows of the input
+# (256 KB at K = 1024), the pair's split-K tiles 16 KB — off by default (1: on)
+FUSED_FWD = os.environ.get("PKC_FUSED_FWD", "0") != "0"
 # recurrent layers: sum the output-gradient slabs before the BPTT loop (0: per step, A/B)
 REC_DY_PRESUM = os.environ.get("PKC_REC_DY_PRESUM", "1") != "0"
 

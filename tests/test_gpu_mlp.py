@@ -479,8 +479,8 @@ def test_engine_sparsity_vs_oracle(variant):
                                        err_msg="%s %s" % (a, k))
 
 
-@pytest.mark.parametrize("steps", [3])
-def test_engine_c2_bf16_vs_oracle(steps):
+@pytest.mark.parametrize("fused", [False, True])
+def test_engine_c2_bf16_vs_oracle(fused, steps=3):
     """BASELINE C2 (the bench headline): the C1 model at B = 128 with bf16 matmul operands
     (PREC_BF16: every operand of Y = X W^T, dX = dY W, dW = dY^T X rounded to bf16 RNE, fp32
     accumulation, fp32 master weights / BN / loss / optimizer).
@@ -496,7 +496,10 @@ def test_engine_c2_bf16_vs_oracle(steps):
         1 / 2 / 3, and the bf16 oracle against the fp32 oracle by 7.7e-3 / 0.12 / 0.20 (measured on
         the CPU).  Steps 1-2 are therefore held to the bf16-vs-fp32 spread (0.15 relative on the
         log-posteriors) and the loss to 1e-3 relative of both oracles.
+    fused: the hidden layers' forward as ONE launch each (pkc_dense_gemm_fwd, PKC_FUSED_FWD=1)
+    instead of the split-K matmul + BatchNorm pair — same bounds.
     """
+    import pkc.engine as E
     from oracle import nets as ON
     from oracle import run as OR
     from pkc import _lib as L
@@ -539,6 +542,17 @@ def test_engine_c2_bf16_vs_oracle(steps):
                  drop_keep_in={k: v.to(DEV) for k, v in keeps.items()})
     eng.bind_chunk(torch.from_numpy(X).to(DEV), torch.from_numpy(lab).to(DEV), B * steps)
     head = [l for l in eng.layers if l.arch == "MLP_layers2"][-1]
+    old_fused = E.FUSED_FWD
+    E.FUSED_FWD = fused
+    try:
+        _c2_steps(eng, head, refs, steps, B)
+        if fused:
+            assert any("fused_fwd" in p[0] for p in eng.profile_step()), "fused forward not taken"
+    finally:
+        E.FUSED_FWD = old_fused
+
+
+def _c2_steps(eng, head, refs, steps, B):
     for s in range(steps):
         eng.train_step()
         loss, _ = eng.loss_values()

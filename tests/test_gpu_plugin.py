@@ -233,9 +233,9 @@ def test_plugin_c5_lstm_pattern_quant_trains_like_reference():
     where a last-bit difference sits in front of a ceil: posteriors 1e-3 relative, gradients 1e-3
     of the tensor's largest; each step's updates elementwise within 1e-4 of the tensor's scale
     except counted outliers: <= 0.2 % of a weight on another 8-bit grid point (tests/quantcheck.py),
-    and RMSprop's amplification of the gradients' difference near g = 0 (each <= 2 x 4.48 lr, the
-    count printed) — the weights must differ by exactly their gradients' RMSprop updates (fp64
-    recomputation from each side's gradient, 1e-6 of the scale)."""
+    and RMSprop's amplification of the gradients' difference near g = 0 (each <= 2 x 4.48 lr, at
+    most 5 % of a tensor, the counts printed) — the weights must differ by exactly their
+    gradients' RMSprop updates (fp64 recomputation from each side's gradient, 1e-6 of the scale)."""
     from flipcheck import assert_counted, resync, step_outliers
     from oracle import nets as ON
     from oracle import run as OR
@@ -320,9 +320,18 @@ def test_plugin_c5_lstm_pattern_quant_trains_like_reference():
                 notes[tag] = n
                 assert resid <= 1e-6 * scale, "%s: weights differ by %.3g beyond their gradients' " \
                     "RMSprop updates (%d update outliers)" % (tag, resid, n)
-                # (the count of such moves is reported, not bounded: the gradients carry the
-                # tolerance above and the optimizer arithmetic is checked exactly)
-                assert dmax <= 2 * 4.48 * lrk + 1e-7, "%s: a weight moved %.3g" % (tag, dmax)
+                # the count of such moves is the share of gradient elements within the 16-bit
+                # grids' noise of zero, where RMSprop's first-step normaliser turns the sign of the
+                # noise into a full +-4.47 lr step (measured: up to 2.2 % of the heads' weights,
+                # 0.6-1 % of the LSTM matrices, 3.3 % of a 512-wide BatchNorm beta): bounded at
+                # 5 % of the tensor (at least 32 elements), each step at most 2 x 4.48 lr.  Counted
+                # are the moves of at least 5 % of an lr step (from step 1 on the normaliser holds
+                # the first step's g^2, and sub-percent moves of up to ~9 % of a BatchNorm beta's
+                # elements are the gradients' own 1e-3 noise, already held by the residual check)
+                n = int(((dw.abs() > 1e-4 * scale + 1e-7) & (dw.abs() > 0.05 * lrk)).sum())
+                assert_counted(tag + " RMSprop-amplified updates", n, r.numel(),
+                               max(0.05, 32.0 / r.numel()), dmax, 2 * 4.48 * lrk + 1e-7,
+                               "(%d of %d)" % (n, r.numel()))
     for k in nets["rnn"].pattern_mask:
         assert len(nets["rnn"].pattern_mask[k]) == 3
     print("c5 plug-in 8-bit grid flips per step", {a: b for a, b in flips.items() if b})
