@@ -220,6 +220,21 @@ __device__ __forceinline__ float dy_at(const pkc_rnn_args& a, int64_t i) {
   return s;
 }
 
+// LSTM gate gradients of one element from its saved gates (f, i, o, cc), c_t, c_{t-1}, the dropout
+// value m, dL/dh_t = g and the carried dc; returns dc * f, the carry into step t-1 (the per-step
+// kernels and the persistent BPTT loop share this arithmetic)
+__device__ __forceinline__ float lstm_grads(int act, float f, float i, float o, float cc, float c,
+                                            float cp, float m, float g, float dc_carry, float* dgo) {
+#pragma clang fp contract(off)     // (as fwd_epi's LSTM update: the same rounding wherever inlined)
+  const float tc = act_fwd(act, c);
+  const float dc = g * o * act_bwd_out(act, tc) + dc_carry;
+  dgo[0] = dc * cp * f * (1.f - f);
+  dgo[1] = dc * cc * m * i * (1.f - i);
+  dgo[2] = g * tc * o * (1.f - o);
+  dgo[3] = dc * i * m * act_bwd_out(act, cc);
+  return dc * f;
+}
+
 // Gate gradients of step t at (r, k) given the total dL/dh_t = g (and, LSTM, the carried dc).
 template <int CELL>
 __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
@@ -258,13 +273,7 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
     const float cc = a.gates[3 * TB2H + si];
     const float c = a.cs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + k];
     const float cp = a.cs[(int64_t)t * ix.B2 * H + (int64_t)r * H + k];
-    const float tc = act_fwd(a.act, c);
-    const float dc = g * o * act_bwd_out(a.act, tc) + dc_carry;
-    dgo[0] = dc * cp * f * (1.f - f);
-    dgo[1] = dc * cc * m * i * (1.f - i);
-    dgo[2] = g * tc * o * (1.f - o);
-    dgo[3] = dc * i * m * act_bwd_out(a.act, cc);
-    *dc_out = dc * f;            // carried into step t-1
+    *dc_out = lstm_grads(a.act, f, i, o, cc, c, cp, m, g, dc_carry, dgo);
     *g_out = g;
   }
 }
@@ -641,10 +650,13 @@ __device__ __forceinline__ EpiIn epi_load(const pkc_rnn_args& a, const RnnIdx& i
 }
 
 // Cell update of step t at (r, j) from the recurrent products acc[g] = (U_g h_{t-1})[r][j].
-template <int CELL, bool QH, bool BF>
+// PUB (the persistent LSTM loop, pkc_rnn_lstm_persist.hip): h_t is handed to the other
+// workgroups of the launch — its store is an agent-scope write-through (sc1) store — and the
+// LSTM's c_t is returned through c_out (kept in a register for the next step).
+template <int CELL, bool QH, bool BF, bool PUB = false>
 __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
                                         int j, const float* acc, const float* vars, float qscale,
-                                        const EpiIn& e) {
+                                        const EpiIn& e, float* c_out = nullptr) {
   const int H = a.H;
   if constexpr (QH) {
     // the hidden state the reference keeps for step t-1 (hiddens[t-1], and the saved input of the
@@ -694,7 +706,10 @@ __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix
     a.gates[si] = z;
     a.gates[TB2H + si] = hcr;
   } else {
-    // LSTM gates (f, i, o, c); cs[t] = c_{t-1}
+    // LSTM gates (f, i, o, c); cs[t] = c_{t-1}.  No fma contraction here: the per-step kernels and
+    // the persistent loop inline this in different code, where the compiler's contraction choices
+    // differed (i cc m + f c_{t-1}); unfused, both round like the reference's separate ops.
+#pragma clang fp contract(off)
     const float f = sigm_mode<BF>(e.w[0] + acc[0]);
     const float i = sigm_mode<BF>(e.w[1] + acc[1]);
     const float o = sigm_mode<BF>(e.w[2] + acc[2]);
@@ -707,8 +722,14 @@ __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix
     a.gates[TB2H + si] = i;
     a.gates[2 * TB2H + si] = o;
     a.gates[3 * TB2H + si] = cc;
+    if (c_out) *c_out = c;
   }
-  a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+  float* const hsp = a.hs + (int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j;
+  if constexpr (PUB)
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned*)hsp, __float_as_uint(h),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *hsp = h;
   if constexpr (BF)   // the next step's bf16 operand (step_bf16: every step runs a BF instance)
     reinterpret_cast<__bf16*>(a.hs_h)[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = (__bf16)h;
   a.y[ix.out(t, r, j)] = h;
@@ -1467,6 +1488,10 @@ static int bwd_impl_s(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
 bool rnn_persist_ok(const pkc_rnn_args* a, bool bwd);
 int rnn_persist_fwd(const pkc_rnn_args* a, hipStream_t s);
 int rnn_persist_bwd(const pkc_rnn_args* a, hipStream_t s);
+// Persistent, grid-synchronised LSTM loops with quantised h (pkc_rnn_lstm_persist.hip)
+bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd);
+int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s);
+int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s);
 
 namespace {
 
@@ -1486,6 +1511,9 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   }
   if constexpr (CELL == PKC_CELL_LIGRU) {
     if (rnn_persist_ok(a, false)) return rnn_persist_fwd(a, s);
+  }
+  if constexpr (CELL == PKC_CELL_LSTM) {
+    if (rnn_lstm_persist_ok(a, false)) return rnn_lstm_persist_fwd(a, s);
   }
   if constexpr (!two_phase(CELL) && G > 1) {
     if (a->kmap_fwd) {
@@ -1508,6 +1536,19 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
       PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
       int st = rnn_persist_bwd(a, s);
+      if (st) return st;
+      hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
+      PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
+      return PKC_OK;
+    }
+  }
+  if constexpr (CELL == PKC_CELL_LSTM) {
+    if (rnn_lstm_persist_ok(a, true)) {
+      const int H = a->H;
+      hipLaunchKernelGGL(rnn_transpose_u, dim3((H + 31) / 32, (H + 31) / 32, G), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
+      PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
+      int st = rnn_lstm_persist_bwd(a, s);
       if (st) return st;
       hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
       PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");

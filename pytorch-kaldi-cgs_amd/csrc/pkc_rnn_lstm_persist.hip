@@ -1,0 +1,339 @@
+// pkc_rnn_lstm_persist.hip — grid-synchronised persistent time loops of a dense LSTM layer with
+// quantised recurrent input (the C5 family: quantized_modules LSTM, qbits <= 16, U on a weight grid
+// of <= 8 bits, uni-directional, B <= 16 rows; forward H in {512, 768, 1024}, BPTT H = 512).
+// north_star: "recurrent time-step loops fused per wavefront"; the per-step form of the same
+// arithmetic is pkc_rnn_impl.h rnn_fwd_mm (QX) and rnn_bwd_mm + rnn_bwd_epi.
+//
+// Reference: the LSTM step neural_networks.py:1077-1097; the four in-place QuantizeLinear calls on
+// h_{t-1} per step quantized_modules.py:99-119.
+//
+// Unlike the liGRU loops (pkc_rnn_persist.hip: rows are independent, one workgroup owns a row for
+// every step) an LSTM layer's U (4 x H x H) does not fit a workgroup: the units are dealt to
+// H / 16 workgroups, each holding its 16 units' U rows of all four gates (forward; BPTT: its 16
+// columns of U^T) as MFMA operands in registers for the whole loop, and every step hands h_t
+// (BPTT: dgates_t) to every workgroup through memory — the measured alternative to a launch
+// boundary per step (MI355X_MICROARCH.md, persistent-kernel price list):
+//   * payload: stored by its owner with agent-scope write-through (sc1) stores, loaded by every
+//     workgroup with sc1 loads (bypassing the reading CU's L1; nothing else reads it in the launch);
+//   * step barrier: after every storing wave's s_waitcnt vmcnt(0) and a workgroup barrier, one
+//     lane adds 1 to a monotone counter (agent-scope atomic); the next step's readers wait — one
+//     lane polls with relaxed sc1 loads and s_sleep, the other waves at the workgroup barrier — for
+//     NWG x (steps done).  Every spin is bounded: a launch whose peers never arrive sets the
+//     timeout word (counter + 1) and ends;
+//   * the step's inputs that do not depend on the recurrence (W x, dL/dy, saved gates) are
+//     requested before the wait, so they arrive during it.
+// Numerics: bit-identical to the per-step kernels (tests/test_gpu_lstm_persist.py):
+//   forward: the per-step QX kernel's per-wave k-ranges (wave w: [w H / 8, (w + 1) H / 8)), whose
+//     kh / kl x U_h sums are exact integers in any order, the same fmaf(256, hi, lo) x var_s per
+//     wave, the same ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)) across waves, then fwd_epi;
+//   BPTT: per gate the per-step kernel's fp32 16x16x4 MFMA chains over the same lane-group strips
+//     of j, the same sum over the 8 strips, rnn_bwd_epi's (((0 + s0) + s1) + s2) + s3 over the
+//     gates and the shared lstm_grads.
+#define PKC_RNN_PERSIST
+#include "pkc_rnn_impl.h"
+
+namespace pkc {
+namespace lstmp {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+constexpr int UPW = 16;                   // units (BPTT: columns k) per workgroup
+constexpr int ROWS = 16;                  // batch rows of the MFMA tiles (B <= 16)
+constexpr int FNW = 8, FNT = 64 * FNW;    // forward: waves / threads per workgroup
+constexpr int BNW = 16, BNT = 64 * BNW;   // BPTT: 8 strips x 2 gate pairs
+constexpr int BS = 16;                    // BPTT strip per lane group (H = 512: 8 x 4 x 16)
+constexpr unsigned SPIN_MAX = 1u << 25;   // polls (s_sleep 1 each) before a wait gives up
+
+// 8 consecutive floats of a handed-off tensor: sc1 loads (8-byte, agent scope, relaxed)
+__device__ __forceinline__ void ld_pub8(const float* p, float* v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned long long x =
+        __hip_atomic_load((const gu64*)(p + 2 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v[2 * i] = __uint_as_float((unsigned)x);
+    v[2 * i + 1] = __uint_as_float((unsigned)(x >> 32));
+  }
+}
+__device__ __forceinline__ void st_pub(float* p, float v) {
+  __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Workgroup barrier for LDS hand-offs only (no vmcnt drain: loads in flight stay in flight)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// This workgroup's payload of the step is stored: every storing wave drains its stores, then one
+// lane (behind the workgroup barrier) adds the workgroup's arrival
+__device__ __forceinline__ void arrive(unsigned* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until ctr >= target: thread 0 polls, the other waves wait at the barrier it then joins.
+// false on every thread of the workgroup when the wait timed out.
+__device__ __forceinline__ bool wait_ctr(unsigned* ctr, unsigned target, int* abort_lds) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    int ab = 0;
+    while (__hip_atomic_load((gu32*)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > SPIN_MAX) {
+        __hip_atomic_store((gu32*)(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ab = 1;
+        break;
+      }
+    }
+    *abort_lds = ab;
+  }
+  lds_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: loads stay below)
+  return *abort_lds == 0;
+}
+
+// ----------------------------------------------------------------------------------- forward
+// KS: 32-wide k-steps per wave (H = 256 KS).  Workgroup wg owns units [16 wg, 16 wg + 16).
+template <int KS>
+__global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
+  __shared__ float red[FNW][4][ROWS][UPW];     // each wave's four gate tiles of the step
+  __shared__ float xm[FNW];                    // per-wave max|h_{t-1}|
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B = a.B, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int u0 = blockIdx.x * UPW;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B * H, TBH = (int64_t)T * B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  // the wave's U fragments for the whole loop: gate g's tile column c = unit u0 + c, k = kw +
+  // 32 s + 8 q .. + 7 (the per-step kernel's wave w covers the same k-range)
+  const int kw = w * 32 * KS;
+  rbf16x8 ub[4][KS];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      ub[g][s] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.U_h[g]) +
+                                                   (int64_t)(u0 + c) * H + kw + 32 * s + 8 * q);
+  // this thread's cell-update element (row r, unit j): its h, c and dropout value in registers
+  const bool ep = tid < B * UPW;
+  const int r = ep ? tid >> 4 : 0, j = u0 + (tid & 15);
+  float hreg = 0.f, creg = 0.f;                // h_init = c_init = 0
+  const float mreg = drop_val(a, r, j, B);
+  const float qscale = ldexpf(1.f, a.qbits - 1);
+  const float* hrow = a.hs + (int64_t)(c < B ? c : 0) * H + kw + 8 * q;
+  for (int t = 0; t < T; ++t) {
+    // this step's gate pre-activations (independent of the recurrence: in flight during the wait)
+    float wv[4];
+    const int64_t pi = ix.pre(t, r, j);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) wv[g] = a.wpre[g * TBH + pi];
+    if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
+    // h_{t-1} = hs[t]: this lane's MFMA A strips (row c; rows >= B are zeros)
+    float va[8 * KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) ld_pub8(hrow + (int64_t)t * n + 32 * s, va + 8 * s);
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8 * KS; ++s) {
+      va[s] = c < B ? va[s] : 0.f;
+      mx = fmaxf(mx, fabsf(va[s]));
+    }
+    mx = warp_max(mx);
+    if (lane == 0) xm[w] = mx;
+    lds_barrier();
+    // var = max|h_{t-1}| over the whole tensor (the per-step kernel's max over the partials)
+    float var = xm[0];
+#pragma unroll
+    for (int i = 1; i < FNW; ++i) var = fmaxf(var, xm[i]);
+    const QParams qp = qparams(var, qscale);
+    const bool qon = var != 0.f;
+    // gate g reads q_{g+1} = Q(q_g): the strip is re-quantised in place before each gate
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 part = {0.f, 0.f, 0.f, 0.f};
+      if (qon) {
+        rbf16x8 kh[KS], kl[KS];
+        if (qp.fast) qsplit_strip<true, 8 * KS>(va, qp, kh, kl);
+        else qsplit_strip<false, 8 * KS>(va, qp, kh, kl);
+        f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, l0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          h0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh[s], ub[g][s], h0, 0, 0, 0);
+          l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl[s], ub[g][s], l0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[i] = __builtin_fmaf(256.f, h0[i], l0[i]) * qp.var_s;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = part[i];
+    }
+    lds_barrier();
+    if (ep) {
+      const int ul = tid & 15;
+      float acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[v][g][r][ul]; };
+        acc[g] = ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      EpiIn e;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) e.w[g] = wv[g];
+      e.hp = hreg;
+      e.cp = creg;
+      e.m = mreg;
+      const float vars[4] = {var, var, var, var};
+      float cn = 0.f;
+      hreg = fwd_epi<PKC_CELL_LSTM, true, false, true>(a, ix, t, r, j, acc, vars, qscale, e, &cn);
+      creg = cn;
+    }
+    if (t + 1 < T) arrive(ctr);
+  }
+}
+
+// ----------------------------------------------------------------------------------- BPTT
+// dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k;
+// wave W: strip jr = W % 8 of j (the per-step kernel's wave), gates 2 (W / 8) and 2 (W / 8) + 1.
+__global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
+  __shared__ float red[4][8][ROWS][UPW];       // [gate][strip] partial tiles of the step
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B = a.B, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int W = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int jr = W & 7, gp = W >> 3;
+  const int c = lane & 15, q = lane >> 4;
+  const int k0 = blockIdx.x * UPW;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B * H, TB2H = (int64_t)T * B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kb = (jr * 4 + q) * BS;             // this lane group's strip of j
+  // U^T strips (B operand, column k0 + c) of the wave's two gates, for the whole loop
+  float vu[2][BS];
+#pragma unroll
+  for (int gg = 0; gg < 2; ++gg) {
+    const float* pu = a.ut + (int64_t)(2 * gp + gg) * H * H + (int64_t)(k0 + c) * H + kb;
+#pragma unroll
+    for (int s = 0; s < BS; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(pu + s);
+      vu[gg][s] = v.x; vu[gg][s + 1] = v.y; vu[gg][s + 2] = v.z; vu[gg][s + 3] = v.w;
+    }
+  }
+  const bool ep = tid < B * UPW;
+  const int r = ep ? tid >> 4 : 0, k = k0 + (tid & 15);
+  const int64_t e = (int64_t)r * H + k;
+  // the carries of step T-1 (rnn_bwd_init, slot 0) and the dropout value
+  float gcar = a.work[e], dccar = a.work[2 * n + e];
+  const float mreg = drop_val(a, r, k, B);
+  const float* drow = a.dgates + (int64_t)(c < B ? c : 0) * H + kb;
+  for (int tt = T - 2; tt >= 0; --tt) {
+    const int t = tt + 1;
+    // step tt's saved gates, c_tt, c_{tt-1} and dL/dy_tt: in flight during the wait
+    const int64_t si = ix.st(tt, r, k);
+    const float f = a.gates[si], ig = a.gates[TB2H + si], o = a.gates[2 * TB2H + si];
+    const float cc = a.gates[3 * TB2H + si];
+    const float cN = a.cs[(int64_t)(tt + 1) * n + e], cP = a.cs[(int64_t)tt * n + e];
+    const float dyv = dy_at(a, ix.out(tt, r, k));
+    if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
+    // dgates_t strips of the wave's two gates (row c; rows >= B are zeros)
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
+      float va[BS];
+      const float* p = drow + (int64_t)(2 * gp + gg) * TB2H + (int64_t)t * n;
+#pragma unroll
+      for (int s = 0; s < BS; s += 8) ld_pub8(p + s, va + s);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < BS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(c < B ? va[s] : 0.f, vu[gg][s], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[2 * gp + gg][jr][4 * q + i][c] = acc[i];
+    }
+    lds_barrier();
+    if (ep) {
+      const int kl = tid & 15;
+      float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[g][v][r][kl]; };
+        dh += ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      const float g = dyv + dh;                 // bwd_step_epi
+      float dg[4];
+      const float dco = lstm_grads(a.act, f, ig, o, cc, cN, cP, mreg, g, dccar, dg);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) st_pub(a.dgates + q4 * TB2H + si, dg[q4]);
+      gcar = g;
+      dccar = dco;
+    }
+    if (tt > 0) arrive(ctr);
+  }
+  // the carries of step 0 where the per-step form leaves them (slot (T-1) & 1)
+  if (ep && T > 1) {
+    const int p0 = (T - 1) & 1;
+    a.work[p0 * n + e] = gcar;
+    a.work[2 * n + p0 * n + e] = dccar;
+  }
+}
+
+}  // namespace lstmp
+
+bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
+  const char* env = getenv("PKC_RNN_LSTM_PERSIST");   // "0": the per-step launches (A/B, tests)
+  if (env && env[0] == '0') return false;
+  if (!(a->cell == PKC_CELL_LSTM && !a->bidir && a->qh_exact && a->qbits > 0 && !a->step_bf16 &&
+        !a->ln_gamma && !a->kmap_fwd && !a->kmap_bwd && a->work && a->B <= lstmp::ROWS))
+    return false;
+  if ((int64_t)a->T * a->B * a->H * 4 >= (1ll << 31)) return false;
+  if (bwd) return a->H == 512 && a->dgates && a->ut;
+  return a->H % 256 == 0 && a->H >= 512 && a->H <= 1024 && a->U_h[0] && a->U_h[1] && a->U_h[2] &&
+         a->U_h[3] && a->hq;
+}
+
+static int lstm_ctr_reset(const pkc_rnn_args* a, hipStream_t s) {
+  PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * (int64_t)a->B * a->H, 0, 16, s),
+                "pkc_rnn persistent LSTM counters");
+  return PKC_OK;
+}
+
+int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
+  using namespace lstmp;
+  int st = lstm_ctr_reset(a, s);
+  if (st) return st;
+  const dim3 grid(a->H / UPW);
+  switch (a->H / 256) {
+    case 2: hipLaunchKernelGGL(qx_fwd_loop<2>, grid, dim3(FNT), 0, s, *a); break;
+    case 3: hipLaunchKernelGGL(qx_fwd_loop<3>, grid, dim3(FNT), 0, s, *a); break;
+    default: hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a); break;
+  }
+  PKC_LAUNCH_CHECK("pkc_rnn_fwd persistent LSTM loop");
+  return PKC_OK;
+}
+
+int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
+  using namespace lstmp;
+  if (a->T < 2) return PKC_OK;
+  int st = lstm_ctr_reset(a, s);
+  if (st) return st;
+  hipLaunchKernelGGL(bwd_loop, dim3(a->H / UPW), dim3(BNT), 0, s, *a);
+  PKC_LAUNCH_CHECK("pkc_rnn_bwd persistent LSTM loop");
+  return PKC_OK;
+}
+
+}  // namespace pkc
+
+// which time-loop form pkc_rnn_fwd / pkc_rnn_bwd takes for these arguments: 1 the persistent liGRU
+// loops, 2 the persistent LSTM loops, 0 one launch per step
+extern "C" int pkc_rnn_persist_form(const pkc_rnn_args* a, int bwd) {
+  if (!a) return 0;
+  if (a->cell == PKC_CELL_LIGRU && pkc::rnn_persist_ok(a, bwd != 0)) return 1;
+  if (pkc::rnn_lstm_persist_ok(a, bwd != 0)) return 2;
+  return 0;
+}

@@ -122,6 +122,7 @@ _SIGS = {
     "pkc_fakequant_input": (C.c_int, [vp, vp, i64, C.c_int, C.c_int, vp, vp]),
     "pkc_pattern_mask": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp]),
     "pkc_rnn_fwd": (C.c_int, [C.POINTER(RnnArgs), vp]),
+    "pkc_rnn_persist_form": (C.c_int, [C.POINTER(RnnArgs), C.c_int]),
     "pkc_rnn_bwd": (C.c_int, [C.POINTER(RnnArgs), vp, vp]),
     "pkc_seq_gather": (C.c_int, [vp, i64, C.c_int, vp, C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp,
                                  vp]),

@@ -1747,10 +1747,13 @@ class Engine:
 
     def rec_forms(self):
         """{arch.layer: form} — which implementation each recurrent layer's time loops take:
-        "persistent" (pkc_rnn_persist.hip, one launch per loop), "bf16 steps" / "fp32 steps" (one
-        launch per time step, bf16 or exact-fp32 step products), with "block-sparse U" (kmap
-        tables) and "exact quantised-h" (QX) qualifiers.  A cfg that falls back from the
-        persistent loops (a fragment plan too long, H > 576, ...) shows it here."""
+        "persistent" (pkc_rnn_persist.hip, one launch per loop), "persistent grid-synchronised"
+        (pkc_rnn_lstm_persist.hip), "bf16 steps" / "fp32 steps" (one launch per time step, bf16 or
+        exact-fp32 step products), with "block-sparse U" (kmap tables) and "exact quantised-h" (QX)
+        qualifiers; a BPTT that takes another form than its forward is named after a "/".  A cfg
+        that falls back from the persistent loops (a fragment plan too long, H > 576, ...) shows it
+        here (pkc_rnn_persist_form: the library's own decision for these arguments)."""
+        names = {1: "persistent", 2: "persistent grid-synchronised"}
         out = {}
         for n in self.nodes:
             if not n.rec:
@@ -1758,9 +1761,13 @@ class Engine:
             for li in range(len(n.layers)):
                 a = self._rnn_args(n, li, True, self.max_len)
                 lb = n.lbuf[li]
-                persist = a.persist_fwd is not None and a.persist_fwd != 0
-                f = "persistent" if persist else ("bf16 steps" if a.step_bf16 else "fp32 steps")
-                if not persist and lb.get("kmap_fwd") is not None:
+                ff = L.lib().pkc_rnn_persist_form(C.byref(a), 0)
+                fb = L.lib().pkc_rnn_persist_form(C.byref(a), 1)
+                step = "bf16 steps" if a.step_bf16 else "fp32 steps"
+                f = names.get(ff, step)
+                if fb != ff:
+                    f += " / BPTT " + names.get(fb, step)
+                if not ff and lb.get("kmap_fwd") is not None:
                     f += ", block-sparse U"
                 if a.qh_exact:
                     f += ", exact quantised-h"

@@ -1,0 +1,101 @@
+"""The persistent grid-synchronised LSTM loops (csrc/pkc_rnn_lstm_persist.hip) against the per-step
+launches they replace, on the same layer and inputs: every saved forward tensor (h, c, the gates, the
+quantised h, the layer output), the BPTT's gate gradients, the input gradient and every weight
+gradient must be bit-identical — the persistent forward keeps the per-step kernel's per-wave
+contraction ranges (exact integer sums), its per-wave fmaf(256, hi, lo) * var_s and its cross-wave
+summation order; the BPTT keeps the per-step fp32 MFMA chains per gate and strip and both summation
+orders (pkc_rnn_lstm_persist.hip header).  The per-step form itself is pinned to the oracle
+(test_gpu_configs.py::test_c5_lstm_pattern_quant_full_size, test_gpu_quant_step.py), so this makes
+the persistent loops oracle-exact by transitivity.
+
+Sizes: C5's layers (H = 512, B = 12, quantised h of 16 bits, 8-bit U; BASELINE configs[4]) and
+the forward-only shapes H = 768 / 1024.  The hand-off is also exercised under uneven load (a side
+stream of large matmuls running during the loops, MI355X_MICROARCH.md: hand-offs must be tested
+under load), and the timeout word of every launch must stay zero.
+"""
+import configparser
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cases import LSTM_DEF
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(H, T, B, seed, persist, load=False):
+    import pkc.neural_networks as NN
+    from test_gpu_rnn import run_block, dx0
+    os.environ["PKC_RNN_LSTM_PERSIST"] = "1" if persist else "0"
+    try:
+        opts = dict(LSTM_DEF, lstm_lay="%d,%d" % (H, H), lstm_drop="0.2,0.2", lstm_quant="True",
+                    lstm_quant_inp="True")
+        cp = configparser.ConfigParser()
+        cp["s"] = {k: str(v) for k, v in opts.items()}
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        F = 40
+        net = NN.LSTM(cp["s"], F).to("cuda").train()
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(T, B, F, generator=g).cuda()
+        dy = torch.randn(T, B, net.out_dim, generator=g).cuda()
+        side = None
+        if load:                       # uneven load: large matmuls on another stream meanwhile
+            side = torch.cuda.Stream()
+            a = torch.randn(4096, 4096, device="cuda")
+            with torch.cuda.stream(side):
+                for _ in range(12):
+                    a = torch.tanh(a @ a * 1e-3)
+        eng, node, y = run_block(net, x, dy)
+        if side is not None:
+            side.synchronize()
+        forms = eng.rec_forms()
+        out = {"y": y.cpu(), "dx0": dx0(eng, node).cpu(), "grad": eng.gflat.cpu()}
+        for li, lb in enumerate(node.lbuf):
+            n = B * H
+            for k in ("hs", "cs", "gates", "hq", "dgates"):
+                out["%d.%s" % (li, k)] = lb[k].cpu()
+            out["%d.timeout" % li] = lb["rwork"][4 * n:4 * n + 2].view(torch.int32).cpu()
+        return out, forms
+    finally:
+        os.environ.pop("PKC_RNN_LSTM_PERSIST", None)
+
+
+@pytest.mark.parametrize("H,T,B,seed,load", [(512, 40, 12, 1, False), (512, 23, 12, 2, True),
+                                             (512, 9, 7, 3, False), (768, 12, 12, 4, False),
+                                             (1024, 10, 16, 5, False)])
+def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load):
+    ref, forms_ref = _run(H, T, B, seed, False)
+    got, forms = _run(H, T, B, seed, True, load)
+    assert all("persistent" not in f for f in forms_ref.values()), forms_ref
+    want = "persistent grid-synchronised" + ("" if H == 512 else " / BPTT fp32 steps")
+    assert all(f.startswith(want) for f in forms.values()), forms
+    print("H %d T %d B %d forms %s" % (H, T, B, forms))
+    bad = []
+    for k in ref:
+        if k.endswith(".timeout"):
+            # [step counter, timeout word] of the last persistent launch, the BPTT's (32 x (T - 2)
+            # arrivals); with per-step BPTT launches (H != 512) their gate slabs hold these words
+            if H == 512:
+                assert int(got[k][0]) == 32 * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
+                assert int(got[k][1]) == 0, "%s: a persistent loop timed out" % k
+            continue
+        a, b = got[k], ref[k]
+        if not torch.equal(a, b):
+            nd = int((a != b).sum())
+            first = int((a != b).reshape(-1).nonzero()[0])
+            bad.append("%s: %d of %d differ (max %.3g, first at flat %d)" % (
+                k, nd, a.numel(), float((a.double() - b.double()).abs().max()), first))
+    assert not bad, "; ".join(bad)
+    assert float(ref["grad"].abs().max()) > 0
+
+
+def test_lstm_persist_repeatable():
+    """Three back-to-back runs of the same persistent loops: identical outputs (the step counters
+    are re-zeroed per launch; a stale counter would let a workgroup run ahead)."""
+    outs = [_run(512, 17, 12, 7, True)[0] for _ in range(3)]
+    for o in outs[1:]:
+        for k in o:
+            assert torch.equal(o[k], outs[0][k]), k
