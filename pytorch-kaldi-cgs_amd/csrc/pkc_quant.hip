@@ -100,6 +100,58 @@ __global__ void pattern_mask_kernel(const float* W, int R, int Cc, const float* 
   }
 }
 
+// The 8 x 8 form (every pattern_shape the reference cfgs use): one thread per tile, its 64 |W| in
+// registers (lane l reads tile tj0 + l: a row's 64 lanes read 2 KB contiguous), the P <= 32 scores
+// in registers (the generic kernel's indexed score[] array lives in scratch), patterns read
+// uniformly (scalar loads).  The scores sum in the generic kernel's order (a, then b) and the
+// ties select the same patterns: bit-identical masks.
+template <int PMAX>
+__global__ __launch_bounds__(256) void pattern_mask8_kernel(const float* __restrict__ W, int R,
+                                                            int Cc, const float* __restrict__ pat,
+                                                            int P, float* __restrict__ mask) {
+  const int tiles_c = Cc / 8;
+  const int ntiles = (R / 8) * tiles_c;
+  const int tix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tix >= ntiles) return;
+  const int ti = tix / tiles_c, tj = tix % tiles_c;
+  const float* w0 = W + (int64_t)ti * 8 * Cc + tj * 8;
+  float x[64];
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    const float4 u = *reinterpret_cast<const float4*>(w0 + (int64_t)a * Cc);
+    const float4 v = *reinterpret_cast<const float4*>(w0 + (int64_t)a * Cc + 4);
+    x[8 * a + 0] = fabsf(u.x); x[8 * a + 1] = fabsf(u.y); x[8 * a + 2] = fabsf(u.z);
+    x[8 * a + 3] = fabsf(u.w); x[8 * a + 4] = fabsf(v.x); x[8 * a + 5] = fabsf(v.y);
+    x[8 * a + 6] = fabsf(v.z); x[8 * a + 7] = fabsf(v.w);
+  }
+  float score[PMAX];
+  float best = -INFINITY;
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) {
+    float s = 0.f;
+    if (p < P) {
+#pragma unroll
+      for (int e = 0; e < 64; ++e) s += x[e] * pat[p * 64 + e];
+      best = fmaxf(best, s);
+    }
+    score[p] = s;
+  }
+  float* m0 = mask + (int64_t)ti * 8 * Cc + tj * 8;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p) {
+      if (p < P && score[p] >= best) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) m[b] += pat[p * 64 + 8 * a + b];
+      }
+    }
+    *reinterpret_cast<float4*>(m0 + (int64_t)a * Cc) = make_float4(m[0], m[1], m[2], m[3]);
+    *reinterpret_cast<float4*>(m0 + (int64_t)a * Cc + 4) = make_float4(m[4], m[5], m[6], m[7]);
+  }
+}
+
 }  // namespace pkc
 
 extern "C" int pkc_fakequant_weight(const float* w, float* q, int64_t n, int bits, void* stream) {
@@ -147,6 +199,17 @@ extern "C" int pkc_pattern_mask(const float* W, int rows, int cols, const float*
                     cols % pw == 0,
                 "pkc_pattern_mask: bad arguments (rows/cols must be multiples of the pattern)");
   const int ntiles = (rows / ph) * (cols / pw);
+  if (ph == 8 && pw == 8 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)mask & 15) == 0) {
+    const dim3 g((ntiles + 255) / 256);
+    if (P <= 16)
+      hipLaunchKernelGGL(pattern_mask8_kernel<16>, g, dim3(256), 0, S(stream), W, rows, cols, patterns,
+                         P, mask);
+    else
+      hipLaunchKernelGGL(pattern_mask8_kernel<32>, g, dim3(256), 0, S(stream), W, rows, cols, patterns,
+                         P, mask);
+    PKC_LAUNCH_CHECK("pkc_pattern_mask");
+    return PKC_OK;
+  }
   hipLaunchKernelGGL(pattern_mask_kernel, dim3((ntiles + 127) / 128), dim3(128), 0, S(stream), W, rows,
                      cols, patterns, P, ph, pw, mask);
   PKC_LAUNCH_CHECK("pkc_pattern_mask");

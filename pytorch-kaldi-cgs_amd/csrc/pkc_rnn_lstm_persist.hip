@@ -45,15 +45,49 @@ constexpr int BNW = 16, BNT = 64 * BNW;   // BPTT: 8 strips x 2 gate pairs
 constexpr int BS = 16;                    // BPTT strip per lane group (H = 512: 8 x 4 x 16)
 constexpr unsigned SPIN_MAX = 1u << 25;   // polls (s_sleep 1 each) before a wait gives up
 
-// 8 consecutive floats of a handed-off tensor: sc1 loads (8-byte, agent scope, relaxed)
-__device__ __forceinline__ void ld_pub8(const float* p, float* v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const unsigned long long x =
-        __hip_atomic_load((const gu64*)(p + 2 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v[2 * i] = __uint_as_float((unsigned)x);
-    v[2 * i + 1] = __uint_as_float((unsigned)(x >> 32));
-  }
+// Phase trace (PKC_TRACE measurement builds only; scripts/trace_steps.py --lstm-persist): lane 0
+// of every wave of workgroup 0 accumulates the shader-clock cycles of each step phase over the
+// loop ([fwd, bwd][wave][8]: five phase sums, then T), read back with
+// pkc_trace_read_lstm_persist.  Forward phases: wait, h loads + var, quantise + MFMA + partials,
+// cell update + stores, arrive; BPTT: wait, dgates loads + MFMA + partials, gate gradients +
+// stores, arrive.
+#ifdef PKC_TRACE
+__device__ unsigned long long ltrace_buf[2 * BNW * 8];
+#define LTR_DECL unsigned long long lt_acc[5] = {0, 0, 0, 0, 0}, lt_last = 0
+#define LTR_MARK(i)                                                     \
+  do {                                                                  \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();       \
+    if ((i) > 0) lt_acc[(i) - 1] += now_ - lt_last;                     \
+    lt_last = now_;                                                     \
+  } while (0)
+#define LTR_STORE(k)                                                    \
+  do {                                                                  \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                   \
+      volatile unsigned long long* b_ = ltrace_buf + ((k) * BNW + (threadIdx.x >> 6)) * 8; \
+      for (int i_ = 0; i_ < 5; ++i_) b_[i_] = lt_acc[i_];               \
+      b_[5] = (unsigned long long)T;                                    \
+    }                                                                   \
+  } while (0)
+#else
+#define LTR_DECL do { } while (0)
+#define LTR_MARK(i) do { } while (0)
+#define LTR_STORE(k) do { } while (0)
+#endif
+
+// Loads of a handed-off tensor: 16-byte sc1 buffer loads (bypassing this CU's L1; MI355X_MICROARCH
+// visibility table, first row) through a raw descriptor over the tensor; an offset past its range
+// (OOB, the padding rows >= B) reads zeros without a memory access.
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+constexpr unsigned OOB = 0x80000000u;   // >= the descriptors' num_records
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pub_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void ld_pub4(__amdgpu_buffer_rsrc_t r, unsigned off, float* v) {
+  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);   // aux 16: sc1
+  v[0] = __uint_as_float(x[0]);
+  v[1] = __uint_as_float(x[1]);
+  v[2] = __uint_as_float(x[2]);
+  v[3] = __uint_as_float(x[3]);
 }
 __device__ __forceinline__ void st_pub(float* p, float v) {
   __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -127,24 +161,29 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
   float hreg = 0.f, creg = 0.f;                // h_init = c_init = 0
   const float mreg = drop_val(a, r, j, B);
   const float qscale = ldexpf(1.f, a.qbits - 1);
-  const float* hrow = a.hs + (int64_t)(c < B ? c : 0) * H + kw + 8 * q;
+  const __amdgpu_buffer_rsrc_t hsr = pub_rsrc(a.hs);
+  const unsigned hoff = c < B ? 4u * (c * H + kw + 8 * q) : OOB;    // byte offset in hs[t]
+  LTR_DECL;
   for (int t = 0; t < T; ++t) {
+    LTR_MARK(0);
     // this step's gate pre-activations (independent of the recurrence: in flight during the wait)
     float wv[4];
     const int64_t pi = ix.pre(t, r, j);
 #pragma unroll
     for (int g = 0; g < 4; ++g) wv[g] = a.wpre[g * TBH + pi];
     if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
+    LTR_MARK(1);
     // h_{t-1} = hs[t]: this lane's MFMA A strips (row c; rows >= B are zeros)
     float va[8 * KS];
+    const unsigned toff = c < B ? 4u * (unsigned)(t * n) : 0u;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) ld_pub8(hrow + (int64_t)t * n + 32 * s, va + 8 * s);
+    for (int s = 0; s < KS; ++s) {
+      ld_pub4(hsr, hoff + toff + 128 * s, va + 8 * s);
+      ld_pub4(hsr, hoff + toff + 128 * s + 16, va + 8 * s + 4);
+    }
     float mx = 0.f;
 #pragma unroll
-    for (int s = 0; s < 8 * KS; ++s) {
-      va[s] = c < B ? va[s] : 0.f;
-      mx = fmaxf(mx, fabsf(va[s]));
-    }
+    for (int s = 0; s < 8 * KS; ++s) mx = fmaxf(mx, fabsf(va[s]));
     mx = warp_max(mx);
     if (lane == 0) xm[w] = mx;
     lds_barrier();
@@ -154,14 +193,28 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
     for (int i = 1; i < FNW; ++i) var = fmaxf(var, xm[i]);
     const QParams qp = qparams(var, qscale);
     const bool qon = var != 0.f;
-    // gate g reads q_{g+1} = Q(q_g): the strip is re-quantised in place before each gate
+    LTR_MARK(2);
+    // gate g reads q_{g+1} = Q(q_g): the strip is re-quantised in place before each gate.  Q is
+    // idempotent on most grid values, so once Q(q) == q on every element of this wave's strips the
+    // later gates read the same q (the per-step kernel's `fixed` shortcut, taken one gate earlier
+    // here): their integer operands need no second quantisation.  Same values either way.
+    rbf16x8 kh[KS], kl[KS];
+    bool fixed = false;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       f32x4 part = {0.f, 0.f, 0.f, 0.f};
       if (qon) {
-        rbf16x8 kh[KS], kl[KS];
-        if (qp.fast) qsplit_strip<true, 8 * KS>(va, qp, kh, kl);
-        else qsplit_strip<false, 8 * KS>(va, qp, kh, kl);
+        if (!fixed) {
+          if (qp.fast) qsplit_strip<true, 8 * KS>(va, qp, kh, kl);
+          else qsplit_strip<false, 8 * KS>(va, qp, kh, kl);
+          if (g < 3) {
+            bool eq = true;
+#pragma unroll
+            for (int s = 0; s < 8 * KS; ++s)
+              eq = eq && (qp.fast ? qin<true>(va[s], qp) : qin<false>(va[s], qp)) == va[s];
+            fixed = __all(eq);
+          }
+        }
         f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, l0 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -175,6 +228,7 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
       for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = part[i];
     }
     lds_barrier();
+    LTR_MARK(3);
     if (ep) {
       const int ul = tid & 15;
       float acc[4];
@@ -194,8 +248,11 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
       hreg = fwd_epi<PKC_CELL_LSTM, true, false, true>(a, ix, t, r, j, acc, vars, qscale, e, &cn);
       creg = cn;
     }
+    LTR_MARK(4);
     if (t + 1 < T) arrive(ctr);
+    LTR_MARK(5);
   }
+  LTR_STORE(0);
 }
 
 // ----------------------------------------------------------------------------------- BPTT
@@ -232,8 +289,10 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   // the carries of step T-1 (rnn_bwd_init, slot 0) and the dropout value
   float gcar = a.work[e], dccar = a.work[2 * n + e];
   const float mreg = drop_val(a, r, k, B);
-  const float* drow = a.dgates + (int64_t)(c < B ? c : 0) * H + kb;
+  const __amdgpu_buffer_rsrc_t dgr = pub_rsrc(a.dgates);
+  LTR_DECL;
   for (int tt = T - 2; tt >= 0; --tt) {
+    LTR_MARK(0);
     const int t = tt + 1;
     // step tt's saved gates, c_tt, c_{tt-1} and dL/dy_tt: in flight during the wait
     const int64_t si = ix.st(tt, r, k);
@@ -242,21 +301,28 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
     const float cN = a.cs[(int64_t)(tt + 1) * n + e], cP = a.cs[(int64_t)tt * n + e];
     const float dyv = dy_at(a, ix.out(tt, r, k));
     if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
-    // dgates_t strips of the wave's two gates (row c; rows >= B are zeros)
+    LTR_MARK(1);
+    // dgates_t strips of the wave's two gates (row c; rows >= B read zeros), both requested
+    // before the MFMA chains
+    float va[2][BS];
 #pragma unroll
     for (int gg = 0; gg < 2; ++gg) {
-      float va[BS];
-      const float* p = drow + (int64_t)(2 * gp + gg) * TB2H + (int64_t)t * n;
+      const unsigned off =
+          c < B ? 4u * (unsigned)((2 * gp + gg) * TB2H + t * n + (int64_t)c * H + kb) : OOB;
 #pragma unroll
-      for (int s = 0; s < BS; s += 8) ld_pub8(p + s, va + s);
+      for (int s = 0; s < BS; s += 4) ld_pub4(dgr, off + 4 * s, va[gg] + s);
+    }
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < BS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(c < B ? va[s] : 0.f, vu[gg][s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[gg][s], vu[gg][s], acc, 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) red[2 * gp + gg][jr][4 * q + i][c] = acc[i];
     }
     lds_barrier();
+    LTR_MARK(2);
     if (ep) {
       const int kl = tid & 15;
       float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
@@ -273,8 +339,12 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
       gcar = g;
       dccar = dco;
     }
+    LTR_MARK(3);
     if (tt > 0) arrive(ctr);
+    LTR_MARK(4);
+    LTR_MARK(5);
   }
+  LTR_STORE(1);
   // the carries of step 0 where the per-step form leaves them (slot (T-1) & 1)
   if (ep && T > 1) {
     const int p0 = (T - 1) & 1;
@@ -291,7 +361,9 @@ bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
   if (!(a->cell == PKC_CELL_LSTM && !a->bidir && a->qh_exact && a->qbits > 0 && !a->step_bf16 &&
         !a->ln_gamma && !a->kmap_fwd && !a->kmap_bwd && a->work && a->B <= lstmp::ROWS))
     return false;
-  if ((int64_t)a->T * a->B * a->H * 4 >= (1ll << 31)) return false;
+  // byte offsets of the 16-byte payload loads (dgates: G x T x B x H floats) below the
+  // descriptors' 2^31 - 16 range
+  if ((int64_t)a->T * a->B * a->H * 4 * 4 >= (1ll << 31) - 64) return false;
   if (bwd) return a->H == 512 && a->dgates && a->ut;
   return a->H % 256 == 0 && a->H >= 512 && a->H <= 1024 && a->U_h[0] && a->U_h[1] && a->U_h[2] &&
          a->U_h[3] && a->hq;
@@ -328,6 +400,15 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
 }
 
 }  // namespace pkc
+
+#ifdef PKC_TRACE
+// measurement builds only: the persistent LSTM loops' per-wave phase sums (n <= 2 * 16 * 8)
+extern "C" int pkc_trace_read_lstm_persist(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pkc::lstmp::ltrace_buf),
+                             sizeof(unsigned long long) * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // which time-loop form pkc_rnn_fwd / pkc_rnn_bwd takes for these arguments: 1 the persistent liGRU
 // loops, 2 the persistent LSTM loops, 0 one launch per step

@@ -33,9 +33,13 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--persist", action="store_true",
                     help="the persistent liGRU loops' per-wave phase sums instead (C3, bf16)")
+    ap.add_argument("--lstm-persist", action="store_true",
+                    help="the persistent LSTM loops' per-wave phase sums instead (C5)")
     a = ap.parse_args()
     if a.persist:
         return persist(a)
+    if a.lstm_persist:
+        return lstm_persist(a)
     assert "libpkc_trace" in os.environ.get("PKC_LIB", ""), "set PKC_LIB to the trace build"
     import torch
     import bench_seq
@@ -89,6 +93,38 @@ def persist(a):
             PPHASES[i]: [round(float(v), 1) for v in per[:, i]] for i in range(5)},
             "cycles_per_step_wave_mean": {PPHASES[i]: round(float(per[:, i].mean()), 1)
                                           for i in range(5)}}
+    print(json.dumps(out, indent=1))
+
+
+LPHASES = {"forward loop": ["wait for the step's arrivals", "h_{t-1} loads + var",
+                            "quantise + MFMA + partials", "cell update + stores", "arrive"],
+           "BPTT loop": ["wait for the step's arrivals", "dgates loads + MFMA + partials",
+                         "gate gradients + stores", "arrive", "-"]}
+
+
+def lstm_persist(a):
+    """Per step and wave (workgroup 0 of the last persistent LSTM forward / BPTT launch): cycles
+    of each phase averaged over the loop's steps, and ns at the clock measured beside it."""
+    import torch
+    import bench_seq
+    from pkc import _lib as L
+    bench_seq.run(a.config, a.steps, 1, prec=a.prec)
+    torch.cuda.synchronize()
+    n = 2 * 16 * 8
+    buf = (C.c_ulonglong * n)()
+    assert L.lib().pkc_trace_read_lstm_persist(buf, n) == 0
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(2, 16, 8).astype(np.int64)
+    out = {"config": a.config, "prec": a.prec, "clock_ghz_assumed": 2.4}
+    for k, name in enumerate(("forward loop", "BPTT loop")):
+        nw = 8 if k == 0 else 16
+        T = int(t[k, 0, 5])
+        steps = T if k == 0 else max(T - 1, 1)
+        per = t[k, :nw, :5] / float(steps)
+        mean = per.mean(0)
+        out[name] = {"T": T, "waves": nw,
+                     "cycles_per_step_wave_mean": {LPHASES[name][i]: round(float(mean[i]), 1)
+                                                   for i in range(5)},
+                     "cycles_per_step_total": round(float(per.sum(1).mean()), 1)}
     print(json.dumps(out, indent=1))
 
 

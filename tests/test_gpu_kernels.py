@@ -822,3 +822,28 @@ def test_gemm_colstats_dense_fwd_pre(L, M, N, K, prec):
     torch.testing.assert_close(o1, o0, rtol=1e-4, atol=2e-5)
     for u, v in ((rm1, rm0), (rv1, rv0), (sm1, sm0), (si1, si0)):
         torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("R,Cc,P,ph,pw", [(2048, 512, 16, 8, 8), (512, 440, 20, 8, 8),
+                                          (64, 48, 32, 8, 8), (96, 64, 12, 4, 4)])
+def test_pattern_mask_matches_oracle(L, R, Cc, P, ph, pw):
+    """pkc_pattern_mask (sparsity.py:1112-1146; the 8 x 8 register form and the generic kernel)
+    against oracle.masks.apply_patterns, exactly: random tiles, tiles of equal values (every pattern
+    of the same nnz ties: the mask sums the tied patterns) and all-zero tiles (every pattern ties)."""
+    from oracle.masks import apply_patterns
+    from pkc._lib import call, ptr
+    g = torch.Generator().manual_seed(R + Cc + P)
+    W = torch.randn(R, Cc, generator=g)
+    W[:ph, :4 * pw] = 0.5                        # equal-valued tiles
+    W[ph:2 * ph, :2 * pw] = 0.0                  # zero tiles
+    pat = (torch.rand(P, ph, pw, generator=g) < 0.25).float()
+    pat[:, 0, 0] = 1.0                           # every pattern nonempty
+    pat[1] = pat[0]                              # two identical patterns: always tied
+    Wd, pd = W.to(DEV), pat.to(DEV)
+    out = torch.full((R, Cc), -1.0, device=DEV)
+    call("pkc_pattern_mask", ptr(Wd), R, Cc, ptr(pd), P, ph, pw, ptr(out), _s())
+    torch.cuda.synchronize()
+    ref = apply_patterns(W.numpy(), pat.numpy())
+    got = out.cpu().numpy()
+    assert np.array_equal(got, ref), "%d of %d mask values differ" % (int((got != ref).sum()), got.size)
+    assert got.max() >= 2.0                      # ties present
