@@ -129,6 +129,38 @@ __device__ __forceinline__ bool wait_ctr(unsigned* ctr, unsigned target, int* ab
   return *abort_lds == 0;
 }
 
+// The four gates' partial products of this wave's k-range: gate g reads q_{g+1} = Q(q_g), the
+// strip re-quantised in place before each gate.  Q is idempotent on most grid values, so once
+// Q(q) == q on every element of this wave's strips the later gates read the same q (the per-step
+// kernel's `fixed` shortcut, taken one gate earlier here): their integer operands need no second
+// quantisation.  Same values either way.  FAST: qin's form (one instance per launch of the step).
+template <bool FAST, int KS>
+__device__ __forceinline__ void gate_products(float* va, const QParams& qp,
+                                              const rbf16x8 (&ub)[4][KS], f32x4 (&part)[4]) {
+  rbf16x8 kh[KS], kl[KS];
+  bool fixed = false;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    if (!fixed) {
+      qsplit_strip<FAST, 8 * KS>(va, qp, kh, kl);
+      if (g < 3) {
+        bool eq = true;
+#pragma unroll
+        for (int s = 0; s < 8 * KS; ++s) eq &= qin<FAST>(va[s], qp) == va[s];
+        fixed = __all(eq);
+      }
+    }
+    f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, l0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      h0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh[s], ub[g][s], h0, 0, 0, 0);
+      l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl[s], ub[g][s], l0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[g][i] = __builtin_fmaf(256.f, h0[i], l0[i]) * qp.var_s;
+  }
+}
+
 // ----------------------------------------------------------------------------------- forward
 // KS: 32-wide k-steps per wave (H = 256 KS).  Workgroup wg owns units [16 wg, 16 wg + 16).
 template <int KS>
@@ -191,42 +223,21 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
     float var = xm[0];
 #pragma unroll
     for (int i = 1; i < FNW; ++i) var = fmaxf(var, xm[i]);
+    var = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(var)));   // (uniform)
     const QParams qp = qparams(var, qscale);
     const bool qon = var != 0.f;
     LTR_MARK(2);
-    // gate g reads q_{g+1} = Q(q_g): the strip is re-quantised in place before each gate.  Q is
-    // idempotent on most grid values, so once Q(q) == q on every element of this wave's strips the
-    // later gates read the same q (the per-step kernel's `fixed` shortcut, taken one gate earlier
-    // here): their integer operands need no second quantisation.  Same values either way.
-    rbf16x8 kh[KS], kl[KS];
-    bool fixed = false;
+    f32x4 part[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 part = {0.f, 0.f, 0.f, 0.f};
-      if (qon) {
-        if (!fixed) {
-          if (qp.fast) qsplit_strip<true, 8 * KS>(va, qp, kh, kl);
-          else qsplit_strip<false, 8 * KS>(va, qp, kh, kl);
-          if (g < 3) {
-            bool eq = true;
-#pragma unroll
-            for (int s = 0; s < 8 * KS; ++s)
-              eq = eq && (qp.fast ? qin<true>(va[s], qp) : qin<false>(va[s], qp)) == va[s];
-            fixed = __all(eq);
-          }
-        }
-        f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, l0 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          h0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh[s], ub[g][s], h0, 0, 0, 0);
-          l0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl[s], ub[g][s], l0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) part[i] = __builtin_fmaf(256.f, h0[i], l0[i]) * qp.var_s;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = part[i];
+    for (int g = 0; g < 4; ++g) part[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (qon) {                                  // (var is wave-uniform: a scalar branch)
+      if (qp.fast) gate_products<true, KS>(va, qp, ub, part);
+      else gate_products<false, KS>(va, qp, ub, part);
     }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = part[g][i];
     lds_barrier();
     LTR_MARK(3);
     if (ep) {
