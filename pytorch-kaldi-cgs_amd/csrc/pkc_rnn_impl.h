@@ -650,9 +650,9 @@ __device__ __forceinline__ EpiIn epi_load(const pkc_rnn_args& a, const RnnIdx& i
 }
 
 // Cell update of step t at (r, j) from the recurrent products acc[g] = (U_g h_{t-1})[r][j].
-// PUB (the persistent LSTM loop, pkc_rnn_lstm_persist.hip): h_t is handed to the other
-// workgroups of the launch — its store is an agent-scope write-through (sc1) store — and the
-// LSTM's c_t is returned through c_out (kept in a register for the next step).
+// PUB (the persistent LSTM loops, pkc_rnn_lstm_persist.hip): h_t is handed to the other
+// workgroups of the launch, so the caller stores it (hs, and hs_h in bf16 mode) in the hand-off's
+// form; the LSTM's c_t is returned through c_out (kept in a register for the next step).
 template <int CELL, bool QH, bool BF, bool PUB = false>
 __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
                                         int j, const float* acc, const float* vars, float qscale,
@@ -724,14 +724,11 @@ __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix
     a.gates[3 * TB2H + si] = cc;
     if (c_out) *c_out = c;
   }
-  float* const hsp = a.hs + (int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j;
-  if constexpr (PUB)
-    __hip_atomic_store((__attribute__((address_space(1))) unsigned*)hsp, __float_as_uint(h),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *hsp = h;
-  if constexpr (BF)   // the next step's bf16 operand (step_bf16: every step runs a BF instance)
-    reinterpret_cast<__bf16*>(a.hs_h)[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = (__bf16)h;
+  if constexpr (!PUB) {
+    a.hs[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = h;
+    if constexpr (BF)   // the next step's bf16 operand (step_bf16: every step runs a BF instance)
+      reinterpret_cast<__bf16*>(a.hs_h)[(int64_t)(t + 1) * ix.B2 * H + (int64_t)r * H + j] = (__bf16)h;
+  }
   a.y[ix.out(t, r, j)] = h;
   return h;
 }

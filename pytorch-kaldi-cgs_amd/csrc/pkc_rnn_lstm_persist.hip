@@ -79,8 +79,19 @@ __device__ unsigned long long ltrace_buf[2 * BNW * 8];
 // (OOB, the padding rows >= B) reads zeros without a memory access.
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 constexpr unsigned OOB = 0x80000000u;   // >= the descriptors' num_records
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t pub_rsrc(const float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pub_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+// 8 bf16 of a handed-off bf16 tensor (one 16-byte sc1 load; OOB: zeros)
+__device__ __forceinline__ rbf16x8 ld_pub_h8(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(rbf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16));
+}
+// two adjacent bf16 of a handed-off tensor as ONE 4-byte sc1 store (the visibility table's store
+// sizes are 4, 8 and 16 bytes)
+__device__ __forceinline__ void st_pub_h2(void* p, float x0, float x1) {
+  const unsigned b = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x0) |
+                     ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)x1) << 16);
+  __hip_atomic_store((gu32*)p, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void ld_pub4(__amdgpu_buffer_rsrc_t r, unsigned off, float* v) {
   const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);   // aux 16: sc1
@@ -258,6 +269,7 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
       float cn = 0.f;
       hreg = fwd_epi<PKC_CELL_LSTM, true, false, true>(a, ix, t, r, j, acc, vars, qscale, e, &cn);
       creg = cn;
+      st_pub(a.hs + (int64_t)(t + 1) * n + (int64_t)r * H + j, hreg);   // h_t to every workgroup
     }
     LTR_MARK(4);
     if (t + 1 < T) arrive(ctr);
@@ -364,25 +376,245 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   }
 }
 
+// ------------------------------------------------------------- bf16 step mode (C4's LSTM)
+// Dense LSTM with bf16 step products (pkc_rnn_args.step_bf16, no quantised h), B2 <= 32 rows — a
+// bidirectional layer's two directions share U (rows >= B run the reversed time, RnnIdx) —
+// H = 256 KC, KC in {2, 3, 4}.  The per-step bf16 kernels' partition is kept element for element:
+// wave w, lane group q own the contraction strip [(4 w + q) 8 KC, + 8 KC), MFMA i of a chain the 8
+// k at + 8 i, two 16-row chains, the waves' partials summed ((0 + 1) + (2 + 3)) + ((4 + 5) +
+// (6 + 7)); the handed-off operand is the bf16 copy the per-step kernels read (hs_h, dgates_h),
+// stored as pairs of adjacent units.
+constexpr int R32 = 32;
+
+template <int KC>
+__global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a) {
+  __shared__ float red[FNW][4][R32][UPW];       // each wave's four gate tiles (32 rows)
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int u0 = blockIdx.x * UPW;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kb = (4 * w + q) * 8 * KC;
+  rbf16x8 ub[4][KC];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int i = 0; i < KC; ++i)
+      ub[g][i] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.U_h[g]) +
+                                                   (int64_t)(u0 + c) * H + kb + 8 * i);
+  const bool two = B2 > 16;                     // (uniform) the second 16-row chain
+  const int r = tid >> 4, j = u0 + (tid & 15);  // this thread's cell-update element
+  const bool ep = r < B2;
+  const int rr = ep ? r : 0;
+  float hreg = 0.f, creg = 0.f;
+  const float mreg = drop_val(a, rr, j, B2);
+  const __amdgpu_buffer_rsrc_t hr = pub_rsrc(a.hs_h);
+  const unsigned oa = 2u * (c * H + kb), ob = 2u * ((16 + c) * H + kb);
+  const bool ra = c < B2, rb = 16 + c < B2;
+  LTR_DECL;
+  for (int t = 0; t < T; ++t) {
+    LTR_MARK(0);
+    float wv[4];
+    const int64_t pi = ix.pre(t, rr, j);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) wv[g] = a.wpre[g * TBH + pi];
+    if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
+    LTR_MARK(1);
+    // h_{t-1} (bf16, hs_h[t]): the A operands of both row chains (rows >= B2 read zeros)
+    const unsigned to = 2u * (unsigned)(t * n);
+    rbf16x8 ha[KC], hb[KC];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      ha[i] = ld_pub_h8(hr, ra ? oa + to + 16 * i : OOB);
+      hb[i] = ld_pub_h8(hr, two && rb ? ob + to + 16 * i : OOB);
+    }
+    LTR_MARK(2);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[i], ub[g][i], acc0, 0, 0, 0);
+        if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hb[i], ub[g][i], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[w][g][4 * q + i][c] = acc0[i];
+        red[w][g][16 + 4 * q + i][c] = acc1[i];
+      }
+    }
+    lds_barrier();
+    LTR_MARK(3);
+    float h = 0.f;
+    if (ep) {
+      const int ul = tid & 15;
+      float acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[v][g][r][ul]; };
+        acc[g] = ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      EpiIn e;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) e.w[g] = wv[g];
+      e.hp = hreg;
+      e.cp = creg;
+      e.m = mreg;
+      const float vars[4] = {0.f, 0.f, 0.f, 0.f};
+      float cn = 0.f;
+      h = fwd_epi<PKC_CELL_LSTM, false, true, true>(a, ix, t, r, j, acc, vars, 1.f, e, &cn);
+      hreg = h;
+      creg = cn;
+      a.hs[(int64_t)(t + 1) * n + (int64_t)r * H + j] = h;
+    }
+    // the bf16 h_t to every workgroup: units j, j + 1 (lanes l, l ^ 1) in one 4-byte store
+    const float hn = __shfl_xor(h, 1, 64);
+    if (ep && (tid & 1) == 0)
+      st_pub_h2(reinterpret_cast<__bf16*>(a.hs_h) + (int64_t)(t + 1) * n + (int64_t)r * H + j, h, hn);
+    LTR_MARK(4);
+    if (t + 1 < T) arrive(ctr);
+    LTR_MARK(5);
+  }
+  LTR_STORE(0);
+}
+
+// dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k:
+// wave w owns strip w of j for all four gates (the per-step kernel's wave w of each gate's launch)
+template <int KC>
+__global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a) {
+  __shared__ float red[4][FNW][R32][UPW];       // [gate][strip] partial tiles of the step
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int k0 = blockIdx.x * UPW;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B2 * H, TB2H = (int64_t)T * B2 * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kb = (4 * w + q) * 8 * KC;
+  // U^T fragments (ut_h[g][k][j], column k0 + c) of the four gates, for the whole loop
+  rbf16x8 ub[4][KC];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int i = 0; i < KC; ++i)
+      ub[g][i] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.ut_h) +
+                                                   (int64_t)g * H * H + (int64_t)(k0 + c) * H +
+                                                   kb + 8 * i);
+  const bool two = B2 > 16;
+  const int r = tid >> 4, k = k0 + (tid & 15);
+  const bool ep = r < B2;
+  const int rr = ep ? r : 0;
+  const int64_t e = (int64_t)rr * H + k;
+  float gcar = a.work[e], dccar = a.work[2 * n + e];   // step T-1's carries (rnn_bwd_init)
+  const float mreg = drop_val(a, rr, k, B2);
+  const __amdgpu_buffer_rsrc_t dr = pub_rsrc(a.dgates_h);
+  const unsigned oa = 2u * (c * H + kb), ob = 2u * ((16 + c) * H + kb);
+  const bool ra = c < B2, rb = 16 + c < B2;
+  LTR_DECL;
+  for (int tt = T - 2; tt >= 0; --tt) {
+    LTR_MARK(0);
+    const int t = tt + 1;
+    const int64_t si = ix.st(tt, rr, k);
+    const float f = a.gates[si], ig = a.gates[TB2H + si], o = a.gates[2 * TB2H + si];
+    const float cc = a.gates[3 * TB2H + si];
+    const float cN = a.cs[(int64_t)(tt + 1) * n + e], cP = a.cs[(int64_t)tt * n + e];
+    const float dyv = dy_at(a, ix.out(tt, rr, k));
+    if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
+    LTR_MARK(1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const unsigned go = 2u * (unsigned)(g * TB2H + t * n);
+      rbf16x8 ha[KC], hb[KC];
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        ha[i] = ld_pub_h8(dr, ra ? oa + go + 16 * i : OOB);
+        hb[i] = ld_pub_h8(dr, two && rb ? ob + go + 16 * i : OOB);
+      }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[i], ub[g][i], acc0, 0, 0, 0);
+        if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hb[i], ub[g][i], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[g][w][4 * q + i][c] = acc0[i];
+        red[g][w][16 + 4 * q + i][c] = acc1[i];
+      }
+    }
+    lds_barrier();
+    LTR_MARK(2);
+    float dg[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ep) {
+      const int kl = tid & 15;
+      float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[g][v][r][kl]; };
+        dh += ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      const float g = dyv + dh;                 // bwd_step_epi
+      const float dco = lstm_grads(a.act, f, ig, o, cc, cN, cP, mreg, g, dccar, dg);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) a.dgates[q4 * TB2H + si] = dg[q4];
+      gcar = g;
+      dccar = dco;
+    }
+    // the bf16 dgates_tt to every workgroup: columns k, k + 1 (lanes l, l ^ 1) per 4-byte store
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const float dn = __shfl_xor(dg[q4], 1, 64);
+      if (ep && (tid & 1) == 0)
+        st_pub_h2(reinterpret_cast<__bf16*>(a.dgates_h) + q4 * TB2H + si, dg[q4], dn);
+    }
+    LTR_MARK(3);
+    if (tt > 0) arrive(ctr);
+    LTR_MARK(4);
+    LTR_MARK(5);
+  }
+  LTR_STORE(1);
+  if (ep && T > 1) {
+    const int p0 = (T - 1) & 1;
+    a.work[p0 * n + e] = gcar;
+    a.work[2 * n + p0 * n + e] = dccar;
+  }
+}
+
 }  // namespace lstmp
 
 bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
   const char* env = getenv("PKC_RNN_LSTM_PERSIST");   // "0": the per-step launches (A/B, tests)
   if (env && env[0] == '0') return false;
-  if (!(a->cell == PKC_CELL_LSTM && !a->bidir && a->qh_exact && a->qbits > 0 && !a->step_bf16 &&
-        !a->ln_gamma && !a->kmap_fwd && !a->kmap_bwd && a->work && a->B <= lstmp::ROWS))
-    return false;
-  // byte offsets of the 16-byte payload loads (dgates: G x T x B x H floats) below the
+  if (a->cell != PKC_CELL_LSTM || a->ln_gamma || a->kmap_fwd || a->kmap_bwd || !a->work) return false;
+  const int64_t B2 = a->bidir ? 2 * a->B : a->B;
+  // byte offsets of the 16-byte payload loads (dgates: G x T x B2 x H floats) below the
   // descriptors' 2^31 - 16 range
-  if ((int64_t)a->T * a->B * a->H * 4 * 4 >= (1ll << 31) - 64) return false;
-  if (bwd) return a->H == 512 && a->dgates && a->ut;
-  return a->H % 256 == 0 && a->H >= 512 && a->H <= 1024 && a->U_h[0] && a->U_h[1] && a->U_h[2] &&
-         a->U_h[3] && a->hq;
+  if ((int64_t)a->T * B2 * a->H * 4 * 4 >= (1ll << 31) - 64) return false;
+  if (a->qh_exact) {                            // QX: quantised h, fp32 BPTT products
+    if (a->bidir || a->qbits <= 0 || a->step_bf16 || a->B > lstmp::ROWS) return false;
+    if (bwd) return a->H == 512 && a->dgates && a->ut;
+    return a->H % 256 == 0 && a->H >= 512 && a->H <= 1024 && a->U_h[0] && a->U_h[1] &&
+           a->U_h[2] && a->U_h[3] && a->hq;
+  }
+  if (a->step_bf16 && a->qbits <= 0) {          // bf16 step products
+    if (B2 > lstmp::R32 || a->H % 256 || a->H < 512 || a->H > 1024 || !a->hs_h) return false;
+    if (bwd) return a->dgates && a->ut_h && a->dgates_h;
+    return a->U_h[0] && a->U_h[1] && a->U_h[2] && a->U_h[3];
+  }
+  return false;
 }
 
 static int lstm_ctr_reset(const pkc_rnn_args* a, hipStream_t s) {
-  PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * (int64_t)a->B * a->H, 0, 16, s),
-                "pkc_rnn persistent LSTM counters");
+  const int64_t B2 = a->bidir ? 2 * a->B : a->B;
+  PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * B2 * a->H, 0, 16, s), "pkc_rnn persistent LSTM counters");
   return PKC_OK;
 }
 
@@ -391,10 +623,15 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
   const dim3 grid(a->H / UPW);
-  switch (a->H / 256) {
-    case 2: hipLaunchKernelGGL(qx_fwd_loop<2>, grid, dim3(FNT), 0, s, *a); break;
-    case 3: hipLaunchKernelGGL(qx_fwd_loop<3>, grid, dim3(FNT), 0, s, *a); break;
-    default: hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a); break;
+  const int kc = a->H / 256;
+  if (a->qh_exact) {
+    if (kc == 2) hipLaunchKernelGGL(qx_fwd_loop<2>, grid, dim3(FNT), 0, s, *a);
+    else if (kc == 3) hipLaunchKernelGGL(qx_fwd_loop<3>, grid, dim3(FNT), 0, s, *a);
+    else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
+  } else {
+    if (kc == 2) hipLaunchKernelGGL(bf_fwd_loop<2>, grid, dim3(FNT), 0, s, *a);
+    else if (kc == 3) hipLaunchKernelGGL(bf_fwd_loop<3>, grid, dim3(FNT), 0, s, *a);
+    else hipLaunchKernelGGL(bf_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   }
   PKC_LAUNCH_CHECK("pkc_rnn_fwd persistent LSTM loop");
   return PKC_OK;
@@ -405,7 +642,12 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
   if (a->T < 2) return PKC_OK;
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
-  hipLaunchKernelGGL(bwd_loop, dim3(a->H / UPW), dim3(BNT), 0, s, *a);
+  const dim3 grid(a->H / UPW);
+  const int kc = a->H / 256;
+  if (a->qh_exact) hipLaunchKernelGGL(bwd_loop, grid, dim3(BNT), 0, s, *a);
+  else if (kc == 2) hipLaunchKernelGGL(bf_bwd_loop<2>, grid, dim3(FNT), 0, s, *a);
+  else if (kc == 3) hipLaunchKernelGGL(bf_bwd_loop<3>, grid, dim3(FNT), 0, s, *a);
+  else hipLaunchKernelGGL(bf_bwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd persistent LSTM loop");
   return PKC_OK;
 }

@@ -25,13 +25,38 @@ from cases import LSTM_DEF
 pytestmark = pytest.mark.gpu
 
 
-def _run(H, T, B, seed, persist, load=False):
+def _block(net, x, dy, prec):
+    """test_gpu_rnn.run_block with the engine's precision (bf16: the bf16 step products)."""
+    from pkc.engine import Engine
+    T, B, F = x.shape
+    eng = Engine({"rnn": net}, {"rnn": {"arch_opt": "sgd", "arch_lr": "0"}},
+                 [["out", "compute", "rnn", "fea"]], {"fea": (0, F)}, [], batch=B, max_len=T,
+                 train=False, prec=prec)
+    node = eng.nodes[0]
+    eng.T, eng.M = T, T * B
+    eng.x[:T * B * F].copy_(x.reshape(-1))
+    s = eng._stream()
+    eng._rec_fwd(node, s, True)
+    y = node.out[:T * B * node.N].view(T, B, node.N).clone()
+    node.gslab = dy.reshape(-1).contiguous()
+    node.sb = 1
+    eng._rec_bwd(node, s, want_dx0=True)
+    torch.cuda.synchronize()
+    return eng, node, y
+
+
+def _run(H, T, B, seed, persist, load=False, bf16=False, bidir=False):
     import pkc.neural_networks as NN
-    from test_gpu_rnn import run_block, dx0
+    from pkc import _lib as L
+    from test_gpu_rnn import dx0
     os.environ["PKC_RNN_LSTM_PERSIST"] = "1" if persist else "0"
     try:
-        opts = dict(LSTM_DEF, lstm_lay="%d,%d" % (H, H), lstm_drop="0.2,0.2", lstm_quant="True",
-                    lstm_quant_inp="True")
+        if bf16:                       # C4's form: dense, bf16 step products
+            opts = dict(LSTM_DEF, lstm_lay="%d,%d" % (H, H), lstm_drop="0.2,0.2",
+                        lstm_bidir=str(bidir))
+        else:                          # C5's form: quantised h, 8-bit U
+            opts = dict(LSTM_DEF, lstm_lay="%d,%d" % (H, H), lstm_drop="0.2,0.2", lstm_quant="True",
+                        lstm_quant_inp="True")
         cp = configparser.ConfigParser()
         cp["s"] = {k: str(v) for k, v in opts.items()}
         torch.manual_seed(seed)
@@ -48,15 +73,16 @@ def _run(H, T, B, seed, persist, load=False):
             with torch.cuda.stream(side):
                 for _ in range(12):
                     a = torch.tanh(a @ a * 1e-3)
-        eng, node, y = run_block(net, x, dy)
+        eng, node, y = _block(net, x, dy, L.PREC_BF16 if bf16 else L.PREC_FP32)
         if side is not None:
             side.synchronize()
         forms = eng.rec_forms()
         out = {"y": y.cpu(), "dx0": dx0(eng, node).cpu(), "grad": eng.gflat.cpu()}
         for li, lb in enumerate(node.lbuf):
-            n = B * H
-            for k in ("hs", "cs", "gates", "hq", "dgates"):
-                out["%d.%s" % (li, k)] = lb[k].cpu()
+            n = (2 * B if bidir else B) * H
+            for k in ("hs", "cs", "gates", "hq", "dgates", "hs_h", "dgates_h"):
+                if lb.get(k) is not None:
+                    out["%d.%s" % (li, k)] = lb[k].cpu()
             out["%d.timeout" % li] = lb["rwork"][4 * n:4 * n + 2].view(torch.int32).cpu()
         return out, forms
     finally:
@@ -90,6 +116,34 @@ def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load):
                 k, nd, a.numel(), float((a.double() - b.double()).abs().max()), first))
     assert not bad, "; ".join(bad)
     assert float(ref["grad"].abs().max()) > 0
+
+
+@pytest.mark.parametrize("H,T,B,bidir,seed,load", [(1024, 14, 16, True, 11, False),
+                                                   (1024, 9, 16, True, 12, True),
+                                                   (512, 21, 12, False, 13, False),
+                                                   (768, 8, 10, True, 14, False)])
+def test_lstm_persist_bf16_bit_identical_to_steps(H, T, B, bidir, seed, load):
+    """The bf16 step mode's persistent loops (C4's LSTM: 4 x 1024 bidirectional, B = 16, so 32
+    rows per step; and smaller shapes) against the per-step bf16 launches: bit-identical."""
+    ref, forms_ref = _run(H, T, B, seed, False, bf16=True, bidir=bidir)
+    got, forms = _run(H, T, B, seed, True, load, bf16=True, bidir=bidir)
+    assert all("persistent" not in f for f in forms_ref.values()), forms_ref
+    assert all(f.startswith("persistent grid-synchronised") and "/" not in f for f in forms.values()), forms
+    print("bf16 H %d T %d B %d bidir %s forms %s" % (H, T, B, bidir, forms))
+    bad = []
+    n = (2 * B if bidir else B) * H
+    for k in ref:
+        if k.endswith(".timeout"):
+            assert int(got[k][0]) == (H // 16) * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
+            assert int(got[k][1]) == 0, "%s: a persistent loop timed out" % k
+            continue
+        a, b = got[k], ref[k]
+        if not torch.equal(a, b):
+            d = (a != b)
+            bad.append("%s: %d of %d differ (first at flat %d)" % (
+                k, int(d.sum()), a.numel(), int(d.reshape(-1).nonzero()[0])))
+    assert not bad, "; ".join(bad)
+    assert n > 0 and float(ref["grad"].abs().max()) > 0
 
 
 def test_lstm_persist_repeatable():
