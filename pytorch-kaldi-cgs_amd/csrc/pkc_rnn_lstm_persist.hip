@@ -529,20 +529,24 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a) {
     const float dyv = dy_at(a, ix.out(tt, rr, k));
     if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
     LTR_MARK(1);
+    // dgates_t (bf16) of all four gates requested at once: one memory round trip per step
+    rbf16x8 ha[4][KC], hb[4][KC];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const unsigned go = 2u * (unsigned)(g * TB2H + t * n);
-      rbf16x8 ha[KC], hb[KC];
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
-        ha[i] = ld_pub_h8(dr, ra ? oa + go + 16 * i : OOB);
-        hb[i] = ld_pub_h8(dr, two && rb ? ob + go + 16 * i : OOB);
+        ha[g][i] = ld_pub_h8(dr, ra ? oa + go + 16 * i : OOB);
+        hb[g][i] = ld_pub_h8(dr, two && rb ? ob + go + 16 * i : OOB);
       }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[i], ub[g][i], acc0, 0, 0, 0);
-        if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hb[i], ub[g][i], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[g][i], ub[g][i], acc0, 0, 0, 0);
+        if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hb[g][i], ub[g][i], acc1, 0, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

@@ -115,11 +115,17 @@ def lstm_persist(a):
     assert L.lib().pkc_trace_read_lstm_persist(buf, n) == 0
     t = np.frombuffer(buf, dtype=np.uint64).reshape(2, 16, 8).astype(np.int64)
     out = {"config": a.config, "prec": a.prec, "clock_ghz_assumed": 2.4}
+    if a.prec == "bf16":                # the bf16 loops' phases (pkc_rnn_lstm_persist.hip)
+        LPHASES["forward loop"] = ["wait for the step's arrivals", "h_{t-1} load issue",
+                                   "load wait + MFMA + partials", "cell update + stores", "arrive"]
+        LPHASES["BPTT loop"] = ["wait for the step's arrivals", "dgates loads + MFMA + partials",
+                                "gate gradients + stores", "arrive", "-"]
     for k, name in enumerate(("forward loop", "BPTT loop")):
-        nw = 8 if k == 0 else 16
-        T = int(t[k, 0, 5])
+        live = t[k, :, 5] > 0                 # the waves the last launch of that loop stamped
+        nw = int(live.sum())
+        T = int(t[k, live, 5][0]) if nw else 0
         steps = T if k == 0 else max(T - 1, 1)
-        per = t[k, :nw, :5] / float(steps)
+        per = t[k, live, :5] / float(steps)
         mean = per.mean(0)
         out[name] = {"T": T, "waves": nw,
                      "cycles_per_step_wave_mean": {LPHASES[name][i]: round(float(mean[i]), 1)

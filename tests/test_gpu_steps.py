@@ -173,9 +173,15 @@ def test_c3_fp32_per_time_step():
     _check_layers(r, "ligru", "relu", False)
 
 
-def test_c4_bf16_per_time_step():
+@pytest.mark.parametrize("persist", [True, False], ids=["persistent", "per_step"])
+def test_c4_bf16_per_time_step(persist, monkeypatch):
+    """C4 bf16: the persistent grid-synchronised LSTM loops (pkc_rnn_lstm_persist.hip, the
+    default) and the per-step bf16 launches (PKC_RNN_LSTM_PERSIST=0)."""
+    monkeypatch.setenv("PKC_RNN_LSTM_PERSIST", "1" if persist else "0")
     r = _engine("c4", "bf16", lo=30, hi=46)
     assert all(lb.get("hs_h") is not None for lb in r["node"].lbuf)
+    forms = r["eng"].rec_forms()
+    assert all(f.startswith("persistent grid-synchronised") == persist for f in forms.values()), forms
     _check_layers(r, "lstm", "tanh", True)
 
 
