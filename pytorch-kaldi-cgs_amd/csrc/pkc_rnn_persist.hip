@@ -38,7 +38,12 @@ namespace pkc {
 namespace persist {
 
 constexpr int NW = 8, NT = 64 * NW;     // two waves per SIMD
-constexpr int RPW = 4;                  // batch rows per workgroup
+// batch rows per workgroup (1, 2 or 4): the fragment loop is the same for any RPW (every workgroup
+// multiplies all of the layer's U blocks), the cell update and its stores scale with it — one row
+// per workgroup puts B2 workgroups on the loop, each with a quarter of the 4-row form's update
+constexpr int RPW = 1;
+static_assert(RPW == 1 || RPW == 2 || RPW == 4, "rows per workgroup: 1, 2 or 4");
+constexpr int RSH = RPW == 4 ? 2 : (RPW == 2 ? 3 : 4);   // MFMA row c -> batch row c >> RSH
 // fragment slots per wave (plan width: ceil(fragments / 8) <= NF, C3: 22) and how many of them
 // are register-resident (the rest, NF - NFR per wave, in LDS); 16 register slots leave room for
 // the one-slot operand look-ahead
@@ -80,12 +85,13 @@ __device__ __forceinline__ bf8 load8(const __bf16* row, bool ok, int k0, int kma
 }
 
 // A fragment of 32-wide block kb: lane (MFMA row c, lane group q) holds k = 32 kb + 8 q .. + 7 of
-// batch row c >> 2.  MFMA rows 4 i .. 4 i + 3 all carry batch row i; only row 4 q of each result
-// (register 0 of lane group q) is used, the three duplicates are ignored — so every lane reads
+// batch row c >> RSH (RPW = 4: MFMA rows 4 i .. 4 i + 3 all carry batch row i); only row 4 q of
+// each result (register 0 of lane group q, batch row (4 q) >> RSH) is used, the duplicates are
+// ignored — so every lane reads
 // (same-address lanes are LDS broadcasts) and the fragment loop stays branch-free: the compiler
 // can issue the next fragments' LDS reads under the current MFMAs
 __device__ __forceinline__ bf8 a_frag(const __bf16* img, int c, int q, int kb) {
-  return *reinterpret_cast<const bf8*>(img + (c >> 2) * HP + 32 * kb + 8 * q);
+  return *reinterpret_cast<const bf8*>(img + (c >> RSH) * HP + 32 * kb + 8 * q);
 }
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding global
@@ -291,8 +297,8 @@ __global__ __launch_bounds__(NT) void fwd_loop(pkc_rnn_args a) {
       // batch row q, unit: register 0; a cut tile's second part to its spill-over tile
       const int col = pl_spill(e) ? XCOL + 16 * pl_sidx(e) + c : (unit < H ? unit : HMAX + c);
       if (fl) {
-        accl[0][q][col] = az[0];
-        accl[1][q][col] = ah[0];
+        accl[0][(4 * q) >> RSH][col] = az[0];   // (RPW < 4: lane groups of one row write
+        accl[1][(4 * q) >> RSH][col] = ah[0];   // the same value)
       }
       const f32x4 zero = {0.f, 0.f, 0.f, 0.f};       // restart after a flush (a select: a
       az = fl ? zero : az;                            // multiply by 0 would turn inf into NaN)
@@ -476,7 +482,7 @@ __global__ __launch_bounds__(NT) void bwd_loop(pkc_rnn_args a) {
       const bool fl = pl_valid(e) && pl_flush(e);
       const int k = pl_tile(e) * 16 + c;
       if (fl)   // (a cut tile's second part to its spill-over tile)
-        accl[q][pl_spill(e) ? XCOL + 16 * pl_sidx(e) + c : (k < H ? k : HMAX + c)] = acc[0];
+        accl[(4 * q) >> RSH][pl_spill(e) ? XCOL + 16 * pl_sidx(e) + c : (k < H ? k : HMAX + c)] = acc[0];
       acc = fl ? f32x4{0.f, 0.f, 0.f, 0.f} : acc;
       __builtin_amdgcn_sched_barrier(0);
     }
