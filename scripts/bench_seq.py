@@ -36,9 +36,12 @@ OPT = dict(arch_opt="rmsprop", arch_lr="0.0016", opt_momentum="0.0", opt_alpha="
 
 
 def rec_opts(cfg_name):
-    n = {"c3": 4, "c4": 4, "c5": 3, "gru": 4}[cfg_name]
-    if cfg_name in ("c3", "gru"):
-        p = "ligru" if cfg_name == "c3" else "gru"
+    """c3b: C3 with the secondary HCGS setting of SURVEY 8 a13 (blocks [128, 4], sparsity
+    [25, 62.5] %: density ~0.42 instead of C3's 16x masks) — where the persistent loops' fragment
+    plans stop fitting and the layers fall back to the per-step launches (rec_forms)."""
+    n = {"c3": 4, "c3b": 4, "c4": 4, "c5": 3, "gru": 4}[cfg_name]
+    if cfg_name in ("c3", "c3b", "gru"):
+        p = "ligru" if cfg_name != "gru" else "gru"
         d = {p + "_lay": ",".join(["550"] * n), p + "_drop": ",".join(["0.2"] * n),
              p + "_use_laynorm_inp": "False", p + "_use_batchnorm_inp": "False",
              p + "_use_laynorm": ",".join(["False"] * n),
@@ -47,7 +50,10 @@ def rec_opts(cfg_name):
         if cfg_name == "c3":
             d.update(ligru_hcgs="True", hcgsx_block="32,2", hcgsx_sparse="75,75",
                      hcgsh_block="32,2", hcgsh_sparse="75,75")
-        return ("liGRU" if cfg_name == "c3" else "GRU"), d, 8
+        elif cfg_name == "c3b":
+            d.update(ligru_hcgs="True", hcgsx_block="128,4", hcgsx_sparse="25,62.5",
+                     hcgsh_block="128,4", hcgsh_sparse="25,62.5")
+        return ("liGRU" if cfg_name != "gru" else "GRU"), d, 8
     H = "1024" if cfg_name == "c4" else "512"
     d = dict(lstm_lay=",".join([H] * n), lstm_drop=",".join(["0.2"] * n),
              lstm_use_laynorm_inp="False", lstm_use_batchnorm_inp="False",
@@ -204,7 +210,7 @@ def run(cfg_name, steps, warmup, allreduce=None, rank=0, world=1, prec="fp32", g
             "frames_per_s": frames / dt, "ms_per_step": dt * 1e3 / steps,
             "us_per_time_step_per_layer_fwd_bwd": dt * 1e6 / (tsteps * nl),
             "mean_T": tsteps / steps, "alg_tflops_per_s": flops / dt / 1e12,
-            "alg_gflop_per_step": flops / steps / 1e9}
+            "alg_gflop_per_step": flops / steps / 1e9, "rec_forms": eng.rec_forms()}
 
 
 def parity(cfg_name, prec="fp32", seed=2234, lo=12, hi=20):
