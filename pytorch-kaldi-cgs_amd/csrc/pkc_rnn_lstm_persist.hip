@@ -281,6 +281,13 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
 // ----------------------------------------------------------------------------------- BPTT
 // dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k;
 // wave W: strip jr = W % 8 of j (the per-step kernel's wave), gates 2 (W / 8) and 2 (W / 8) + 1.
+// X3: the products in three bf16 parts per dgates element (d = hi + mid + lo exactly, RNE each;
+// U^T on its <= 8-bit grid is exact in bf16) on v_mfma_f32_16x16x32_bf16 with fp32 accumulation —
+// every product exact, the sums rounded in another order than the fp32 16x16x4 chains (not
+// bit-identical to the per-step launches; tests/test_gpu_lstm_persist.py bounds the difference),
+// at 12 instead of 32 MFMA issues per wave and step (the fp32 chains were half of a BPTT step:
+// profiles/r06_lstm_persist_trace_c5.json).  !X3: the per-step kernel's fp32 chains, bit-identical.
+template <bool X3>
 __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   __shared__ float red[4][8][ROWS][UPW];       // [gate][strip] partial tiles of the step
   __shared__ int abort_flag;
@@ -295,16 +302,25 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   const int64_t n = (int64_t)B * H, TB2H = (int64_t)T * B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   const int kb = (jr * 4 + q) * BS;             // this lane group's strip of j
+  // X3: lane group q's 8 j of k-step s at jx + 32 s (the strip's 64 j: 2 bf16 k-steps)
+  const int jx = jr * 4 * BS + 8 * q;
+  const int jl = X3 ? jx : kb;                  // the first of this lane's (two runs of) 8 / 16 j
   // U^T strips (B operand, column k0 + c) of the wave's two gates, for the whole loop
   float vu[2][BS];
+  rbf16x8 uh[2][2];
 #pragma unroll
   for (int gg = 0; gg < 2; ++gg) {
-    const float* pu = a.ut + (int64_t)(2 * gp + gg) * H * H + (int64_t)(k0 + c) * H + kb;
+    const float* pu = a.ut + (int64_t)(2 * gp + gg) * H * H + (int64_t)(k0 + c) * H;
 #pragma unroll
     for (int s = 0; s < BS; s += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(pu + s);
+      const int j = X3 ? jx + 32 * (s / 8) + (s % 8) : kb + s;
+      const float4 v = *reinterpret_cast<const float4*>(pu + j);
       vu[gg][s] = v.x; vu[gg][s + 1] = v.y; vu[gg][s + 2] = v.z; vu[gg][s + 3] = v.w;
     }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) uh[gg][s][i] = (__bf16)vu[gg][8 * s + i];
   }
   const bool ep = tid < B * UPW;
   const int r = ep ? tid >> 4 : 0, k = k0 + (tid & 15);
@@ -331,16 +347,38 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int gg = 0; gg < 2; ++gg) {
       const unsigned off =
-          c < B ? 4u * (unsigned)((2 * gp + gg) * TB2H + t * n + (int64_t)c * H + kb) : OOB;
+          c < B ? 4u * (unsigned)((2 * gp + gg) * TB2H + t * n + (int64_t)c * H + jl) : OOB;
 #pragma unroll
-      for (int s = 0; s < BS; s += 4) ld_pub4(dgr, off + 4 * s, va[gg] + s);
+      for (int s = 0; s < BS; s += 4)
+        ld_pub4(dgr, off + 4 * (X3 ? 32 * (s / 8) + (s % 8) : s), va[gg] + s);
     }
 #pragma unroll
     for (int gg = 0; gg < 2; ++gg) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (X3) {
+        rbf16x8 ph[3][2];                       // hi, mid, lo parts of the two k-steps
 #pragma unroll
-      for (int s = 0; s < BS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[gg][s], vu[gg][s], acc, 0, 0, 0);
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float x = va[gg][8 * s + i];
+            const __bf16 h = (__bf16)x;
+            const float r1 = x - (float)h;
+            const __bf16 m = (__bf16)r1;
+            ph[0][s][i] = h;
+            ph[1][s][i] = m;
+            ph[2][s][i] = (__bf16)(r1 - (float)m);
+          }
+#pragma unroll
+        for (int p = 2; p >= 0; --p)            // small parts first
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[p][s], uh[gg][s], acc, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < BS; ++s)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[gg][s], vu[gg][s], acc, 0, 0, 0);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) red[2 * gp + gg][jr][4 * q + i][c] = acc[i];
     }
@@ -648,7 +686,11 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
   if (st) return st;
   const dim3 grid(a->H / UPW);
   const int kc = a->H / 256;
-  if (a->qh_exact) hipLaunchKernelGGL(bwd_loop, grid, dim3(BNT), 0, s, *a);
+  if (a->qh_exact) {
+    const char* x3 = getenv("PKC_RNN_LSTM_PERSIST_X3");   // "0": the fp32 chains (bit-identical)
+    if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, grid, dim3(BNT), 0, s, *a);
+    else hipLaunchKernelGGL(bwd_loop<true>, grid, dim3(BNT), 0, s, *a);
+  }
   else if (kc == 2) hipLaunchKernelGGL(bf_bwd_loop<2>, grid, dim3(FNT), 0, s, *a);
   else if (kc == 3) hipLaunchKernelGGL(bf_bwd_loop<3>, grid, dim3(FNT), 0, s, *a);
   else hipLaunchKernelGGL(bf_bwd_loop<4>, grid, dim3(FNT), 0, s, *a);

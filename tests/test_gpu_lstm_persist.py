@@ -89,17 +89,28 @@ def _run(H, T, B, seed, persist, load=False, bf16=False, bidir=False):
         os.environ.pop("PKC_RNN_LSTM_PERSIST", None)
 
 
-@pytest.mark.parametrize("H,T,B,seed,load", [(512, 40, 12, 1, False), (512, 23, 12, 2, True),
-                                             (512, 9, 7, 3, False), (768, 12, 12, 4, False),
-                                             (1024, 10, 16, 5, False)])
-def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load):
+BWD_KEYS = ("dgates", "dx0", "grad")      # what the BPTT products feed
+
+
+@pytest.mark.parametrize("H,T,B,seed,load,x3", [(512, 40, 12, 1, False, True),
+                                                (512, 40, 12, 1, False, False),
+                                                (512, 23, 12, 2, True, True),
+                                                (512, 9, 7, 3, False, False),
+                                                (768, 12, 12, 4, False, True),
+                                                (1024, 10, 16, 5, False, True)])
+def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load, x3, monkeypatch):
+    """x3 = False (PKC_RNN_LSTM_PERSIST_X3=0): the BPTT's fp32 16x16x4 chains, every tensor
+    bit-identical.  x3 = True (the default): the BPTT products in three exact bf16 parts — the
+    forward stays bit-identical, what the BPTT feeds (dgates, dx, the weight gradients) differs
+    from the per-step launches only in the fp32 summation order of exact products: bounded at
+    2e-6 of each tensor's largest element (measured in the printout)."""
+    monkeypatch.setenv("PKC_RNN_LSTM_PERSIST_X3", "1" if x3 else "0")
     ref, forms_ref = _run(H, T, B, seed, False)
     got, forms = _run(H, T, B, seed, True, load)
     assert all("persistent" not in f for f in forms_ref.values()), forms_ref
     want = "persistent grid-synchronised" + ("" if H == 512 else " / BPTT fp32 steps")
     assert all(f.startswith(want) for f in forms.values()), forms
-    print("H %d T %d B %d forms %s" % (H, T, B, forms))
-    bad = []
+    bad, rep = [], []
     for k in ref:
         if k.endswith(".timeout"):
             # [step counter, timeout word] of the last persistent launch, the BPTT's (32 x (T - 2)
@@ -109,11 +120,18 @@ def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load):
                 assert int(got[k][1]) == 0, "%s: a persistent loop timed out" % k
             continue
         a, b = got[k], ref[k]
+        if x3 and H == 512 and k.split(".")[-1] in BWD_KEYS:
+            err = float((a.double() - b.double()).abs().max()) / float(b.double().abs().max())
+            rep.append("%s %.2e" % (k, err))
+            if err > 2e-6:
+                bad.append("%s: max |diff| %.3g of max |ref|" % (k, err))
+            continue
         if not torch.equal(a, b):
             nd = int((a != b).sum())
             first = int((a != b).reshape(-1).nonzero()[0])
             bad.append("%s: %d of %d differ (max %.3g, first at flat %d)" % (
                 k, nd, a.numel(), float((a.double() - b.double()).abs().max()), first))
+    print("H %d T %d B %d x3 %s forms %s; BPTT rel. diff: %s" % (H, T, B, x3, forms, ", ".join(rep)))
     assert not bad, "; ".join(bad)
     assert float(ref["grad"].abs().max()) > 0
 
