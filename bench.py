@@ -293,7 +293,7 @@ def time_steps(eng, steps, warmup, allreduce=None, world=1):
     return dt
 
 
-REC_KERNELS = ("rnn_fwd_mm", "rnn_bwd_mm", "persist::")   # the recurrences' step / loop kernels
+REC_KERNELS = ("rnn_fwd_mm", "rnn_bwd_mm", "persist::", "lstmp::")   # the recurrences' step / loop kernels
 
 
 def mfma_profile(name, prec="fp32"):
