@@ -425,7 +425,7 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
 constexpr int R32 = 32;
 
 template <int KC>
-__global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a) {
+__global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
   __shared__ float red[FNW][4][R32][UPW];       // each wave's four gate tiles (32 rows)
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
@@ -437,14 +437,18 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a) {
   const unsigned nwg = gridDim.x;
   const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
-  const int kb = (4 * w + q) * 8 * KC;
+  // lane group q's 8-wide chunk i: the per-step kernels' kb + 8 i with kb = (4 w + q) 8 KC
+  // (co = 0), or 32 w KC + 8 (4 i + q) (co = 1: a row's four lane groups read 64 contiguous bytes
+  // per load instead of four 16-byte pieces 16 KC bytes apart)
+  const int kb = co ? 32 * w * KC + 8 * q : (4 * w + q) * 8 * KC;
+  const int ks = co ? 32 : 8;                   // elements between chunks i and i + 1
   rbf16x8 ub[4][KC];
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int i = 0; i < KC; ++i)
       ub[g][i] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.U_h[g]) +
-                                                   (int64_t)(u0 + c) * H + kb + 8 * i);
+                                                   (int64_t)(u0 + c) * H + kb + ks * i);
   const bool two = B2 > 16;                     // (uniform) the second 16-row chain
   const int r = tid >> 4, j = u0 + (tid & 15);  // this thread's cell-update element
   const bool ep = r < B2;
@@ -468,8 +472,8 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a) {
     rbf16x8 ha[KC], hb[KC];
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
-      ha[i] = ld_pub_h8(hr, ra ? oa + to + 16 * i : OOB);
-      hb[i] = ld_pub_h8(hr, two && rb ? ob + to + 16 * i : OOB);
+      ha[i] = ld_pub_h8(hr, ra ? oa + to + 2 * ks * i : OOB);
+      hb[i] = ld_pub_h8(hr, two && rb ? ob + to + 2 * ks * i : OOB);
     }
     LTR_MARK(2);
 #pragma unroll
@@ -524,7 +528,7 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a) {
 // dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k:
 // wave w owns strip w of j for all four gates (the per-step kernel's wave w of each gate's launch)
 template <int KC>
-__global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a) {
+__global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
   __shared__ float red[4][FNW][R32][UPW];       // [gate][strip] partial tiles of the step
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
@@ -536,7 +540,11 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a) {
   const unsigned nwg = gridDim.x;
   const int64_t n = (int64_t)B2 * H, TB2H = (int64_t)T * B2 * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
-  const int kb = (4 * w + q) * 8 * KC;
+  // lane group q's 8-wide chunk i: the per-step kernels' kb + 8 i with kb = (4 w + q) 8 KC
+  // (co = 0), or 32 w KC + 8 (4 i + q) (co = 1: a row's four lane groups read 64 contiguous bytes
+  // per load instead of four 16-byte pieces 16 KC bytes apart)
+  const int kb = co ? 32 * w * KC + 8 * q : (4 * w + q) * 8 * KC;
+  const int ks = co ? 32 : 8;                   // elements between chunks i and i + 1
   // U^T fragments (ut_h[g][k][j], column k0 + c) of the four gates, for the whole loop
   rbf16x8 ub[4][KC];
 #pragma unroll
@@ -545,7 +553,7 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a) {
     for (int i = 0; i < KC; ++i)
       ub[g][i] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.ut_h) +
                                                    (int64_t)g * H * H + (int64_t)(k0 + c) * H +
-                                                   kb + 8 * i);
+                                                   kb + ks * i);
   const bool two = B2 > 16;
   const int r = tid >> 4, k = k0 + (tid & 15);
   const bool ep = r < B2;
@@ -574,8 +582,8 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a) {
       const unsigned go = 2u * (unsigned)(g * TB2H + t * n);
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
-        ha[g][i] = ld_pub_h8(dr, ra ? oa + go + 16 * i : OOB);
-        hb[g][i] = ld_pub_h8(dr, two && rb ? ob + go + 16 * i : OOB);
+        ha[g][i] = ld_pub_h8(dr, ra ? oa + go + 2 * ks * i : OOB);
+        hb[g][i] = ld_pub_h8(dr, two && rb ? ob + go + 2 * ks * i : OOB);
       }
     }
 #pragma unroll
@@ -654,6 +662,15 @@ bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
   return false;
 }
 
+// bf16 loops' contraction chunking (bf_fwd_loop / bf_bwd_loop `co`): the coalesced chunking by
+// default (C4 bf16 19.9-20.0 vs 20.9-21.0 us per step-layer, same box; the bf16 sums of an
+// element in another grouping: tests/test_gpu_steps.py holds every time step to the oracle), the
+// per-step kernels' chunking with PKC_RNN_LSTM_CO=0 (bit-identical to the per-step launches)
+static int lstm_bf16_coalesced() {
+  const char* v = getenv("PKC_RNN_LSTM_CO");
+  return v && v[0] == '0' ? 0 : 1;
+}
+
 static int lstm_ctr_reset(const pkc_rnn_args* a, hipStream_t s) {
   const int64_t B2 = a->bidir ? 2 * a->B : a->B;
   PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * B2 * a->H, 0, 16, s), "pkc_rnn persistent LSTM counters");
@@ -671,9 +688,10 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     else if (kc == 3) hipLaunchKernelGGL(qx_fwd_loop<3>, grid, dim3(FNT), 0, s, *a);
     else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   } else {
-    if (kc == 2) hipLaunchKernelGGL(bf_fwd_loop<2>, grid, dim3(FNT), 0, s, *a);
-    else if (kc == 3) hipLaunchKernelGGL(bf_fwd_loop<3>, grid, dim3(FNT), 0, s, *a);
-    else hipLaunchKernelGGL(bf_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
+    const int co = lstm_bf16_coalesced();
+    if (kc == 2) hipLaunchKernelGGL(bf_fwd_loop<2>, grid, dim3(FNT), 0, s, *a, co);
+    else if (kc == 3) hipLaunchKernelGGL(bf_fwd_loop<3>, grid, dim3(FNT), 0, s, *a, co);
+    else hipLaunchKernelGGL(bf_fwd_loop<4>, grid, dim3(FNT), 0, s, *a, co);
   }
   PKC_LAUNCH_CHECK("pkc_rnn_fwd persistent LSTM loop");
   return PKC_OK;
@@ -691,9 +709,9 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
     if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, grid, dim3(BNT), 0, s, *a);
     else hipLaunchKernelGGL(bwd_loop<true>, grid, dim3(BNT), 0, s, *a);
   }
-  else if (kc == 2) hipLaunchKernelGGL(bf_bwd_loop<2>, grid, dim3(FNT), 0, s, *a);
-  else if (kc == 3) hipLaunchKernelGGL(bf_bwd_loop<3>, grid, dim3(FNT), 0, s, *a);
-  else hipLaunchKernelGGL(bf_bwd_loop<4>, grid, dim3(FNT), 0, s, *a);
+  else if (kc == 2) hipLaunchKernelGGL(bf_bwd_loop<2>, grid, dim3(FNT), 0, s, *a, lstm_bf16_coalesced());
+  else if (kc == 3) hipLaunchKernelGGL(bf_bwd_loop<3>, grid, dim3(FNT), 0, s, *a, lstm_bf16_coalesced());
+  else hipLaunchKernelGGL(bf_bwd_loop<4>, grid, dim3(FNT), 0, s, *a, lstm_bf16_coalesced());
   PKC_LAUNCH_CHECK("pkc_rnn_bwd persistent LSTM loop");
   return PKC_OK;
 }

@@ -140,9 +140,13 @@ def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load, x3, monkeypatc
                                                    (1024, 9, 16, True, 12, True),
                                                    (512, 21, 12, False, 13, False),
                                                    (768, 8, 10, True, 14, False)])
-def test_lstm_persist_bf16_bit_identical_to_steps(H, T, B, bidir, seed, load):
+def test_lstm_persist_bf16_bit_identical_to_steps(H, T, B, bidir, seed, load, monkeypatch):
     """The bf16 step mode's persistent loops (C4's LSTM: 4 x 1024 bidirectional, B = 16, so 32
-    rows per step; and smaller shapes) against the per-step bf16 launches: bit-identical."""
+    rows per step; and smaller shapes) with the per-step kernels' contraction chunking
+    (PKC_RNN_LSTM_CO=0) against the per-step bf16 launches: bit-identical.  (The default, coalesced
+    chunking sums each element's bf16 products in another grouping; tests/test_gpu_steps.py checks
+    it step by step against the oracle.)"""
+    monkeypatch.setenv("PKC_RNN_LSTM_CO", "0")
     ref, forms_ref = _run(H, T, B, seed, False, bf16=True, bidir=bidir)
     got, forms = _run(H, T, B, seed, True, load, bf16=True, bidir=bidir)
     assert all("persistent" not in f for f in forms_ref.values()), forms_ref
