@@ -1489,6 +1489,10 @@ int rnn_persist_bwd(const pkc_rnn_args* a, hipStream_t s);
 bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd);
 int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s);
 int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s);
+// the liGRU exact-fp32 step mode in the same grid-synchronised form (pkc_rnn_lstm_persist.hip)
+bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd);
+int rnn_ligru_grid_fwd(const pkc_rnn_args* a, hipStream_t s);
+int rnn_ligru_grid_bwd(const pkc_rnn_args* a, hipStream_t s);
 
 namespace {
 
@@ -1508,6 +1512,7 @@ static int fwd_impl(const pkc_rnn_args* a, hipStream_t s) {
   }
   if constexpr (CELL == PKC_CELL_LIGRU) {
     if (rnn_persist_ok(a, false)) return rnn_persist_fwd(a, s);
+    if (rnn_ligru_grid_ok(a, false)) return rnn_ligru_grid_fwd(a, s);
   }
   if constexpr (CELL == PKC_CELL_LSTM) {
     if (rnn_lstm_persist_ok(a, false)) return rnn_lstm_persist_fwd(a, s);
@@ -1533,6 +1538,19 @@ static int bwd_impl(const pkc_rnn_args* a, float* dpre, hipStream_t s) {
       hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
       PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
       int st = rnn_persist_bwd(a, s);
+      if (st) return st;
+      hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
+      PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");
+      return PKC_OK;
+    }
+  }
+  if constexpr (CELL == PKC_CELL_LIGRU) {
+    if (rnn_ligru_grid_ok(a, true)) {
+      const int H = a->H;
+      hipLaunchKernelGGL(rnn_transpose_u, dim3((H + 31) / 32, (H + 31) / 32, G), dim3(256), 0, s, *a);
+      hipLaunchKernelGGL((rnn_bwd_init<G, CELL>), dim3(64), dim3(256), 0, s, *a);
+      PKC_LAUNCH_CHECK("pkc_rnn_bwd init");
+      int st = rnn_ligru_grid_bwd(a, s);
       if (st) return st;
       hipLaunchKernelGGL(rnn_fold_kernel, dim3(1024), dim3(256), 0, s, *a, dpre);
       PKC_LAUNCH_CHECK("pkc_rnn_bwd fold");

@@ -79,8 +79,8 @@ __device__ unsigned long long ltrace_buf[2 * BNW * 8];
 // (OOB, the padding rows >= B) reads zeros without a memory access.
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 constexpr unsigned OOB = 0x80000000u;   // >= the descriptors' num_records
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t pub_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pub_rsrc(const void* base, int bytes = 0x7fffffff) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
 // 8 bf16 of a handed-off bf16 tensor (one 16-byte sc1 load; OOB: zeros)
 __device__ __forceinline__ rbf16x8 ld_pub_h8(__amdgpu_buffer_rsrc_t r, unsigned off) {
@@ -638,6 +638,193 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
   }
 }
 
+// ----------------------------------------------------------- liGRU, exact-fp32 step mode (C3 fp32)
+// The same grid-synchronised form for a liGRU layer whose step products stay fp32 (the parity
+// mode; neural_networks.py:1573-1584): the units (BPTT: columns k) dealt to ceil(H / 16)
+// workgroups of 16 waves, each holding its units' fp32 U rows of both gates (BPTT: Uᵀ columns)
+// as v_mfma_f32_16x16x4_f32 B operands in registers; lane group q of wave w owns the contraction
+// strip [(4 w + q) GK, + GK) (16 x 4 x 12 = 768 >= H; k >= H reads zeros), h_{t-1} / dgates_t
+// handed off as in the LSTM loops (write-through stores, step counter).  B2 <= 16 rows (C3: both
+// directions of B = 8).  The block-sparse U multiplies as dense (its masked entries are exact
+// zeros): the products are the fp32 sums of the per-step block-sparse launches in another order.
+constexpr int GW = 16, GT = 64 * GW;   // waves / threads per workgroup
+constexpr int GK = 12;                 // contraction elements per lane group
+constexpr int GKMAX = 4 * GW * GK;     // 768
+
+// GK consecutive floats of row `row` from k0 of a handed-off (rows x H) matrix at byte offset
+// base: three 16-byte sc1 loads (rows >= nrows: out of range, zeros), elements k >= H zeroed
+__device__ __forceinline__ void ld_strip12(__amdgpu_buffer_rsrc_t r, unsigned base, int row,
+                                           int nrows, int H, int k0, float* v) {
+  const bool ok = row < nrows;
+  const unsigned off = ok ? base + 4u * (unsigned)(row * H + k0) : OOB;
+#pragma unroll
+  for (int m = 0; m < GK / 4; ++m) ld_pub4(r, off + 16 * m, v + 4 * m);
+#pragma unroll
+  for (int s = 0; s < GK; ++s) v[s] = k0 + s < H ? v[s] : 0.f;
+}
+
+__global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
+  __shared__ float red[GW][2][ROWS][UPW];      // each wave's two gate tiles of the step
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int u0 = blockIdx.x * UPW;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kl = (4 * w + q) * GK;
+  // U_g rows of the workgroup's units (B[k][unit] = U_g[unit][k]) over this lane's strip
+  float ub[2][GK];
+  const int uu = u0 + c;
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < GK; ++s)
+      ub[g][s] = uu < H && kl + s < H ? a.U[g][(int64_t)uu * H + kl + s] : 0.f;
+  const int r = tid >> 4, j = u0 + (tid & 15);   // this thread's cell-update element
+  const bool ep = tid < ROWS * UPW && r < B2 && j < H;
+  const int rr = ep ? r : 0, jj = ep ? j : 0;
+  float hreg = 0.f;
+  const float mreg = drop_val(a, rr, jj, B2);
+  // (the descriptor spans hs exactly: a strip's tail past the last row reads zeros, not past it)
+  const __amdgpu_buffer_rsrc_t hr = pub_rsrc(a.hs, (int)(4 * (T + 1) * n));
+  LTR_DECL;
+  for (int t = 0; t < T; ++t) {
+    LTR_MARK(0);
+    float wv[2];
+    const int64_t pi = ix.pre(t, rr, jj);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) wv[g] = a.wpre[g * TBH + pi];
+    if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
+    LTR_MARK(1);
+    float hv[GK];
+    ld_strip12(hr, 4u * (unsigned)(t * n), c, B2, H, kl, hv);
+    LTR_MARK(2);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < GK; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s], ub[g][s], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = acc[i];
+    }
+    lds_barrier();
+    LTR_MARK(3);
+    if (ep) {
+      const int ul = tid & 15;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < GW; ++ww) v += red[ww][g][r][ul];
+        acc[g] = v;
+      }
+      EpiIn e;
+      e.w[0] = wv[0];
+      e.w[1] = wv[1];
+      e.w[2] = e.w[3] = 0.f;
+      e.hp = hreg;
+      e.cp = 0.f;
+      e.m = mreg;
+      const float vars[4] = {0.f, 0.f, 0.f, 0.f};
+      hreg = fwd_epi<PKC_CELL_LIGRU, false, false, true>(a, ix, t, r, j, acc, vars, 1.f, e);
+      st_pub(a.hs + (int64_t)(t + 1) * n + (int64_t)r * H + j, hreg);   // h_t to every workgroup
+    }
+    LTR_MARK(4);
+    if (t + 1 < T) arrive(ctr);
+    LTR_MARK(5);
+  }
+  LTR_STORE(0);
+}
+
+// dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k, then
+// the liGRU gate gradients of step tt (bwd_step_epi + gate_grads, CELL_LIGRU)
+__global__ __launch_bounds__(GT) void lg_bwd_loop(pkc_rnn_args a) {
+  __shared__ float red[GW][2][ROWS][UPW];
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int k0 = blockIdx.x * UPW;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B2 * H, TB2H = (int64_t)T * B2 * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int jl = (4 * w + q) * GK;
+  // Uᵀ columns (B[j][k] = U_g[j][k] = ut[g][k][j]) over this lane's strip of j
+  float ub[2][GK];
+  const int kk = k0 + c;
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int s = 0; s < GK; ++s)
+      ub[g][s] = kk < H && jl + s < H ? a.ut[(int64_t)g * H * H + (int64_t)kk * H + jl + s] : 0.f;
+  const int r = tid >> 4, k = k0 + (tid & 15);
+  const bool ep = tid < ROWS * UPW && r < B2 && k < H;
+  const int rr = ep ? r : 0, ke = ep ? k : 0;
+  const int64_t e = (int64_t)rr * H + ke;
+  float gcar = a.work[e];                       // g_{T-1} (rnn_bwd_init, slot 0)
+  const float mreg = drop_val(a, rr, ke, B2);
+  const __amdgpu_buffer_rsrc_t dgr = pub_rsrc(a.dgates, (int)(4 * 2 * TB2H));
+  LTR_DECL;
+  for (int tt = T - 2; tt >= 0; --tt) {
+    LTR_MARK(0);
+    const int t = tt + 1;
+    // step tt's saved state and dL/dy, z_t of the carry term: in flight during the wait
+    const int64_t si = ix.st(tt, rr, ke);
+    const float z = a.gates[si], hcr = a.gates[TB2H + si];
+    const float hp = a.hs[(int64_t)tt * n + e];
+    const float zt = a.gates[ix.st(t, rr, ke)];
+    const float dyv = dy_at(a, ix.out(tt, rr, ke));
+    if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
+    LTR_MARK(1);
+    float dv[2][GK];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+      ld_strip12(dgr, 4u * (unsigned)(g * TB2H + t * n), c, B2, H, jl, dv[g]);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < GK; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dv[g][s], ub[g][s], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = acc[i];
+    }
+    lds_barrier();
+    LTR_MARK(2);
+    if (ep) {
+      const int kl = tid & 15;
+      float dh = 0.f;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < GW; ++ww) v += red[ww][g][r][kl];
+        dh += v;
+      }
+      dh += gcar * zt;                          // bwd_step_epi: g_t * z_t
+      const float g = dyv + dh;
+      const float hc = hcr * mreg;
+      const float dz = g * (hp - hc);
+      const float dhc = g * (1.f - z);
+      st_pub(a.dgates + si, dz * z * (1.f - z));
+      st_pub(a.dgates + TB2H + si, dhc * mreg * act_bwd_out(a.act, hcr));
+      gcar = g;
+    }
+    LTR_MARK(3);
+    if (tt > 0) arrive(ctr);
+    LTR_MARK(4);
+    LTR_MARK(5);
+  }
+  LTR_STORE(1);
+  if (ep && T > 1) a.work[((T - 1) & 1) * n + e] = gcar;   // step 0's carry where the per-step form leaves it
+}
+
 }  // namespace lstmp
 
 bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
@@ -671,6 +858,18 @@ static int lstm_bf16_coalesced() {
   return v && v[0] == '0' ? 0 : 1;
 }
 
+// liGRU exact-fp32 step mode in the grid-synchronised loops (lg_fwd_loop / lg_bwd_loop)
+bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd) {
+  const char* env = getenv("PKC_RNN_LIGRU_GRID");     // "0": the per-step launches
+  if (env && env[0] == '0') return false;
+  const int64_t B2 = a->bidir ? 2 * a->B : a->B;
+  if (a->cell != PKC_CELL_LIGRU || a->step_bf16 || a->qbits > 0 || a->ln_gamma || !a->work ||
+      B2 > lstmp::ROWS || a->H > lstmp::GKMAX)
+    return false;
+  if ((int64_t)a->T * B2 * a->H * 2 * 4 >= (1ll << 31) - 64) return false;
+  return bwd ? (a->dgates && a->ut) : true;
+}
+
 static int lstm_ctr_reset(const pkc_rnn_args* a, hipStream_t s) {
   const int64_t B2 = a->bidir ? 2 * a->B : a->B;
   PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * B2 * a->H, 0, 16, s), "pkc_rnn persistent LSTM counters");
@@ -694,6 +893,25 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     else hipLaunchKernelGGL(bf_fwd_loop<4>, grid, dim3(FNT), 0, s, *a, co);
   }
   PKC_LAUNCH_CHECK("pkc_rnn_fwd persistent LSTM loop");
+  return PKC_OK;
+}
+
+int rnn_ligru_grid_fwd(const pkc_rnn_args* a, hipStream_t s) {
+  using namespace lstmp;
+  int st = lstm_ctr_reset(a, s);
+  if (st) return st;
+  hipLaunchKernelGGL(lg_fwd_loop, dim3((a->H + UPW - 1) / UPW), dim3(GT), 0, s, *a);
+  PKC_LAUNCH_CHECK("pkc_rnn_fwd grid-synchronised liGRU loop");
+  return PKC_OK;
+}
+
+int rnn_ligru_grid_bwd(const pkc_rnn_args* a, hipStream_t s) {
+  using namespace lstmp;
+  if (a->T < 2) return PKC_OK;
+  int st = lstm_ctr_reset(a, s);
+  if (st) return st;
+  hipLaunchKernelGGL(lg_bwd_loop, dim3((a->H + UPW - 1) / UPW), dim3(GT), 0, s, *a);
+  PKC_LAUNCH_CHECK("pkc_rnn_bwd grid-synchronised liGRU loop");
   return PKC_OK;
 }
 
@@ -732,6 +950,6 @@ extern "C" int pkc_trace_read_lstm_persist(unsigned long long* host, int n) {
 extern "C" int pkc_rnn_persist_form(const pkc_rnn_args* a, int bwd) {
   if (!a) return 0;
   if (a->cell == PKC_CELL_LIGRU && pkc::rnn_persist_ok(a, bwd != 0)) return 1;
-  if (pkc::rnn_lstm_persist_ok(a, bwd != 0)) return 2;
+  if (pkc::rnn_lstm_persist_ok(a, bwd != 0) || pkc::rnn_ligru_grid_ok(a, bwd != 0)) return 2;
   return 0;
 }

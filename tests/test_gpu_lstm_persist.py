@@ -175,3 +175,75 @@ def test_lstm_persist_repeatable():
     for o in outs[1:]:
         for k in o:
             assert torch.equal(o[k], outs[0][k]), k
+
+
+def _run_ligru(H, T, B, seed, grid, hcgs, load=False):
+    import pkc.neural_networks as NN
+    from pkc import _lib as L
+    from cases import LIGRU_DEF
+    from test_gpu_rnn import dx0
+    os.environ["PKC_RNN_LIGRU_GRID"] = "1" if grid else "0"
+    try:
+        opts = dict(LIGRU_DEF, ligru_lay="%d,%d" % (H, H), ligru_drop="0.2,0.2")
+        if hcgs:                       # C3's 16x HCGS masks on W and U
+            opts.update(ligru_hcgs="True", hcgsx_block="32,2", hcgsx_sparse="75,75",
+                        hcgsh_block="32,2", hcgsh_sparse="75,75")
+        cp = configparser.ConfigParser()
+        cp["s"] = {k: str(v) for k, v in opts.items()}
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        F = 40
+        net = NN.liGRU(cp["s"], F).to("cuda").train()
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(T, B, F, generator=g).cuda()
+        dy = torch.randn(T, B, net.out_dim, generator=g).cuda()
+        side = None
+        if load:
+            side = torch.cuda.Stream()
+            a = torch.randn(4096, 4096, device="cuda")
+            with torch.cuda.stream(side):
+                for _ in range(12):
+                    a = torch.tanh(a @ a * 1e-3)
+        eng, node, y = _block(net, x, dy, L.PREC_FP32)
+        if side is not None:
+            side.synchronize()
+        out = {"y": y.cpu(), "dx0": dx0(eng, node).cpu(), "grad": eng.gflat.cpu()}
+        for li, lb in enumerate(node.lbuf):
+            n = 2 * B * H
+            out["%d.hs" % li] = lb["hs"][:(T + 1) * n].cpu()
+            for k in ("gates", "dgates"):
+                out["%d.%s" % (li, k)] = lb[k][:2 * T * n].cpu()
+            out["%d.timeout" % li] = lb["rwork"][4 * n:4 * n + 2].view(torch.int32).cpu()
+        return out, eng.rec_forms()
+    finally:
+        os.environ.pop("PKC_RNN_LIGRU_GRID", None)
+
+
+@pytest.mark.parametrize("H,T,B,hcgs,seed,load", [(550, 40, 8, True, 21, False),
+                                                  (550, 23, 8, True, 22, True),
+                                                  (96, 17, 5, False, 23, False),
+                                                  (768, 9, 8, False, 24, False)])
+def test_ligru_fp32_grid_loops_match_steps(H, T, B, hcgs, seed, load):
+    """The exact-fp32 liGRU step mode (C3 fp32: 4 x 550 bidirectional, B = 8, HCGS U) in the
+    grid-synchronised loops against the per-step launches on the same layer and inputs: the same
+    fp32 products summed in another order (the dense U's masked zeros included), so every tensor
+    within 2e-5 of its largest element over T = 40 steps of two layers (measured values printed);
+    the loops' timeout word stays zero and the last launch saw every arrival."""
+    ref, forms_ref = _run_ligru(H, T, B, seed, False, hcgs)
+    got, forms = _run_ligru(H, T, B, seed, True, hcgs, load)
+    assert all("grid" not in f for f in forms_ref.values()), forms_ref
+    assert all(f.startswith("persistent grid-synchronised") for f in forms.values()), forms
+    rep, bad = [], []
+    nwg = (H + 15) // 16
+    for k in ref:
+        if k.endswith(".timeout"):
+            assert int(got[k][0]) == nwg * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
+            assert int(got[k][1]) == 0, "%s: a loop timed out" % k
+            continue
+        a, b = got[k].double(), ref[k].double()
+        err = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-30)
+        rep.append("%s %.2e" % (k, err))
+        if err > 2e-5:
+            bad.append("%s %.3g" % (k, err))
+    print("liGRU fp32 H %d T %d B %d: %s" % (H, T, B, ", ".join(rep)))
+    assert not bad, bad
