@@ -663,29 +663,30 @@ __device__ __forceinline__ void ld_strip12(__amdgpu_buffer_rsrc_t r, unsigned ba
   for (int s = 0; s < GK; ++s) v[s] = k0 + s < H ? v[s] : 0.f;
 }
 
+// Forward: workgroup wg owns units [8 wg, 8 wg + 8): ONE 16-column MFMA tile holds both gates
+// (column c: gate c / 8, unit 8 wg + c % 8), so a wave runs 12 MFMAs per step, not 24.
+constexpr int LUPW = 8;                // forward units per workgroup
 __global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
-  __shared__ float red[GW][2][ROWS][UPW];      // each wave's two gate tiles of the step
+  __shared__ float red[GW][ROWS][UPW];         // each wave's tile of the step
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2, T = a.T;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
-  const int u0 = blockIdx.x * UPW;
+  const int u0 = blockIdx.x * LUPW;
   const unsigned nwg = gridDim.x;
   const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   const int kl = (4 * w + q) * GK;
-  // U_g rows of the workgroup's units (B[k][unit] = U_g[unit][k]) over this lane's strip
-  float ub[2][GK];
-  const int uu = u0 + c;
+  // B[k][column c] = U_{c / 8}[unit u0 + c % 8][k] over this lane's strip
+  float ub[GK];
+  const int uu = u0 + (c & 7);
+  const float* Ug = a.U[c >> 3];
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int s = 0; s < GK; ++s)
-      ub[g][s] = uu < H && kl + s < H ? a.U[g][(int64_t)uu * H + kl + s] : 0.f;
-  const int r = tid >> 4, j = u0 + (tid & 15);   // this thread's cell-update element
-  const bool ep = tid < ROWS * UPW && r < B2 && j < H;
+  for (int s = 0; s < GK; ++s) ub[s] = uu < H && kl + s < H ? Ug[(int64_t)uu * H + kl + s] : 0.f;
+  const int r = tid >> 3, j = u0 + (tid & 7);    // this thread's cell-update element
+  const bool ep = tid < ROWS * LUPW && r < B2 && j < H;
   const int rr = ep ? r : 0, jj = ep ? j : 0;
   float hreg = 0.f;
   const float mreg = drop_val(a, rr, jj, B2);
@@ -703,25 +704,22 @@ __global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
     float hv[GK];
     ld_strip12(hr, 4u * (unsigned)(t * n), c, B2, H, kl, hv);
     LTR_MARK(2);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < GK; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s], ub[s], acc, 0, 0, 0);
 #pragma unroll
-      for (int s = 0; s < GK; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s], ub[g][s], acc, 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) red[w][g][4 * q + i][c] = acc[i];
-    }
+    for (int i = 0; i < 4; ++i) red[w][4 * q + i][c] = acc[i];
     lds_barrier();
     LTR_MARK(3);
     if (ep) {
-      const int ul = tid & 15;
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      const int ul = tid & 7;
+      float acc2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         float v = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < GW; ++ww) v += red[ww][g][r][ul];
-        acc[g] = v;
+        for (int ww = 0; ww < GW; ++ww) v += red[ww][r][8 * g + ul];
+        acc2[g] = v;
       }
       EpiIn e;
       e.w[0] = wv[0];
@@ -731,7 +729,7 @@ __global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
       e.cp = 0.f;
       e.m = mreg;
       const float vars[4] = {0.f, 0.f, 0.f, 0.f};
-      hreg = fwd_epi<PKC_CELL_LIGRU, false, false, true>(a, ix, t, r, j, acc, vars, 1.f, e);
+      hreg = fwd_epi<PKC_CELL_LIGRU, false, false, true>(a, ix, t, r, j, acc2, vars, 1.f, e);
       st_pub(a.hs + (int64_t)(t + 1) * n + (int64_t)r * H + j, hreg);   // h_t to every workgroup
     }
     LTR_MARK(4);
@@ -900,7 +898,7 @@ int rnn_ligru_grid_fwd(const pkc_rnn_args* a, hipStream_t s) {
   using namespace lstmp;
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
-  hipLaunchKernelGGL(lg_fwd_loop, dim3((a->H + UPW - 1) / UPW), dim3(GT), 0, s, *a);
+  hipLaunchKernelGGL(lg_fwd_loop, dim3((a->H + LUPW - 1) / LUPW), dim3(GT), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_fwd grid-synchronised liGRU loop");
   return PKC_OK;
 }
