@@ -504,12 +504,13 @@ int pkc_seq_gather(const float* feats, int64_t ld_feats, int F, const int32_t* l
 int pkc_rnn_persist_geometry(int* nwaves, int* nslots_fwd, int* nslots_bwd, int* rows_per_wg,
                              int* hmax);
 /* Which time-loop form pkc_rnn_fwd (bwd = 0) / pkc_rnn_bwd (bwd = 1) takes for these arguments:
- * 1 the persistent liGRU loops (persist_* plans above); 2 the persistent grid-synchronised LSTM
- * loops (qh_exact LSTM, uni-directional, B <= 16; forward H in {512, 768, 1024}, BPTT H = 512:
- * the layer's units dealt to H / 16 workgroups that hand h_t / dgates_t to each other every step,
- * bit-identical to the per-step launches; work's floats [4 B H, 4 B H + 4) hold its step counter
- * and timeout word); 0 one launch per time step.  Environment PKC_RNN_LSTM_PERSIST=0 disables
- * form 2. */
+ * 1 the persistent liGRU loops (persist_* plans above); 2 the persistent grid-synchronised loops —
+ * qh_exact LSTM (uni-directional, B <= 16; forward H in {512, 768, 1024}, BPTT H = 512), dense LSTM
+ * in bf16 step mode (B2 <= 32, H in {512, 768, 1024}) and liGRU in exact-fp32 step mode
+ * (B2 <= 16, H <= 768): the layer's units dealt to H / 16 (liGRU forward: H / 8) workgroups that
+ * hand h_t / dgates_t to each other every step; work's floats [4 B2 H, 4 B2 H + 4) hold their step
+ * counter and timeout word; 0 one launch per time step.  Environment: PKC_RNN_LSTM_PERSIST=0 and
+ * PKC_RNN_LIGRU_GRID=0 disable form 2 for LSTM / liGRU. */
 int pkc_rnn_persist_form(const pkc_rnn_args* a, int bwd);
 int pkc_rnn_fwd(const pkc_rnn_args* a, void* stream);
 int pkc_rnn_bwd(const pkc_rnn_args* a, float* dpre, void* stream);
