@@ -235,6 +235,24 @@ __device__ __forceinline__ float lstm_grads(int act, float f, float i, float o, 
   return dc * f;
 }
 
+// liGRU gate gradients of one element from dL/dh_t = g, the saved z and act(a) (hcr), h_{t-1} and
+// the dropout value m (shared by the per-step kernels and the grid-synchronised loops; unfused
+// like lstm_grads)
+__device__ __forceinline__ void ligru_grads(int act, float g, float z, float hcr, float hp, float m,
+                                            float* dgo) {
+#pragma clang fp contract(off)
+  const float hc = hcr * m;
+  const float dz = g * (hp - hc);
+  const float dhc = g * (1.f - z);
+  dgo[0] = dz * z * (1.f - z);
+  dgo[1] = dhc * m * act_bwd_out(act, hcr);   // act' from the post-activation value
+}
+// the liGRU BPTT's carry term: dh + g_t * z_t (unfused)
+__device__ __forceinline__ float ligru_carry(float dh, float gt, float zt) {
+#pragma clang fp contract(off)
+  return dh + gt * zt;
+}
+
 // Gate gradients of step t at (r, k) given the total dL/dh_t = g (and, LSTM, the carried dc).
 template <int CELL>
 __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& ix, int t, int r,
@@ -246,12 +264,7 @@ __device__ __forceinline__ void gate_grads(const pkc_rnn_args& a, const RnnIdx& 
   const float m = drop_val(a, r, k, ix.B2);
   const float hp = a.hs[(int64_t)t * ix.B2 * H + (int64_t)r * H + k];
   if constexpr (CELL == PKC_CELL_LIGRU) {
-    const float z = a.gates[si], hcr = a.gates[TB2H + si];
-    const float hc = hcr * m;
-    const float dz = g * (hp - hc);
-    const float dhc = g * (1.f - z);
-    dgo[0] = dz * z * (1.f - z);
-    dgo[1] = dhc * m * act_bwd_out(a.act, hcr);   // act' from the post-activation value
+    ligru_grads(a.act, g, a.gates[si], a.gates[TB2H + si], hp, m, dgo);
     *g_out = g;
   } else if constexpr (CELL == PKC_CELL_GRU) {
     // dz and da now; dr needs Uh^T da over the whole row (gru_bwd_rh)
@@ -700,6 +713,7 @@ __device__ __forceinline__ float fwd_epi(const pkc_rnn_args& a, const RnnIdx& ix
     h = hcr * m;
     a.gates[si] = hcr;
   } else if constexpr (CELL == PKC_CELL_LIGRU) {
+#pragma clang fp contract(off)     // (as the LSTM branch below: the same rounding wherever inlined)
     const float z = sigm_mode<BF>(e.w[0] + acc[0]);
     const float hcr = act_fwd(a.act, e.w[1] + acc[1]);
     h = z * hp + (1.f - z) * (hcr * m);
@@ -1011,7 +1025,7 @@ __device__ __forceinline__ void bwd_step_epi(const pkc_rnn_args& a, const RnnIdx
   float dh = acc;
   float dc_carry = 0.f;
   if constexpr (CELL == PKC_CELL_LIGRU) {
-    dh += a.work[src * n + e] * a.gates[ix.st(t, r, k)];     // g_t * z_t
+    dh = ligru_carry(dh, a.work[src * n + e], a.gates[ix.st(t, r, k)]);     // + g_t * z_t
   } else if constexpr (CELL == PKC_CELL_GRU) {
     // g_t * z_t + d(rh)_t * r_t  (acc = Uz^T dz_t + Ur^T dr_t)
     dh += a.work[src * n + e] * a.gates[ix.st(t, r, k)] +

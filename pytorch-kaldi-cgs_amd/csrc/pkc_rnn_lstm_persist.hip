@@ -643,16 +643,19 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
 // mode; neural_networks.py:1573-1584): the units (BPTT: columns k) dealt to ceil(H / 16)
 // workgroups of 16 waves, each holding its units' fp32 U rows of both gates (BPTT: Uᵀ columns)
 // as v_mfma_f32_16x16x4_f32 B operands in registers; lane group q of wave w owns the contraction
-// strip [(4 w + q) GK, + GK) (16 x 4 x 12 = 768 >= H; k >= H reads zeros), h_{t-1} / dgates_t
-// handed off as in the LSTM loops (write-through stores, step counter).  B2 <= 16 rows (C3: both
-// directions of B = 8).  The block-sparse U multiplies as dense (its masked entries are exact
-// zeros): the products are the fp32 sums of the per-step block-sparse launches in another order.
+// strip [(4 w + q) GK, + GK) (GK = 16: the per-step 4-wave kernels' strips for H <= 256; k >= H
+// reads zeros), h_{t-1} / dgates_t handed off as in the LSTM loops (write-through stores, step
+// counter).  B2 <= 16 rows (C3: both directions of B = 8).  The waves' partials are summed in the
+// per-step kernels' red_sum order, so for a dense U with H <= 256 (the per-step 4-wave form) the
+// loops are bit-identical to the per-step launches; a block-sparse U multiplies as dense (its
+// masked entries are exact zeros) — the fp32 sums of the per-step block-sparse launches in
+// another order.
 constexpr int GW = 16, GT = 64 * GW;   // waves / threads per workgroup
-constexpr int GK = 12;                 // contraction elements per lane group
-constexpr int GKMAX = 4 * GW * GK;     // 768
+constexpr int GK = 16;                 // contraction elements per lane group
+constexpr int GKMAX = 768;             // largest H (4 GW GK = 1024 covers it)
 
 // GK consecutive floats of row `row` from k0 of a handed-off (rows x H) matrix at byte offset
-// base: three 16-byte sc1 loads (rows >= nrows: out of range, zeros), elements k >= H zeroed
+// base: four 16-byte sc1 loads (rows >= nrows: out of range, zeros), elements k >= H zeroed
 __device__ __forceinline__ void ld_strip12(__amdgpu_buffer_rsrc_t r, unsigned base, int row,
                                            int nrows, int H, int k0, float* v) {
   const bool ok = row < nrows;
@@ -716,9 +719,10 @@ __global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
       float acc2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        float v = 0.f;
+        auto p = [&](int v) { return red[v][r][8 * g + ul]; };
+        float v = (p(0) + p(1)) + (p(2) + p(3));          // red_sum's order
 #pragma unroll
-        for (int ww = 0; ww < GW; ++ww) v += red[ww][r][8 * g + ul];
+        for (int w4 = 4; w4 < GW; w4 += 4) v += (p(w4) + p(w4 + 1)) + (p(w4 + 2) + p(w4 + 3));
         acc2[g] = v;
       }
       EpiIn e;
@@ -797,21 +801,21 @@ __global__ __launch_bounds__(GT) void lg_bwd_loop(pkc_rnn_args a) {
     LTR_MARK(2);
     if (ep) {
       const int kl = tid & 15;
-      float dh = 0.f;
+      float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        float v = 0.f;
+        auto p = [&](int v) { return red[v][g][r][kl]; };
+        float v = (p(0) + p(1)) + (p(2) + p(3));          // red_sum's order
 #pragma unroll
-        for (int ww = 0; ww < GW; ++ww) v += red[ww][g][r][kl];
+        for (int w4 = 4; w4 < GW; w4 += 4) v += (p(w4) + p(w4 + 1)) + (p(w4 + 2) + p(w4 + 3));
         dh += v;
       }
-      dh += gcar * zt;                          // bwd_step_epi: g_t * z_t
+      dh = ligru_carry(dh, gcar, zt);           // bwd_step_epi: + g_t * z_t
       const float g = dyv + dh;
-      const float hc = hcr * mreg;
-      const float dz = g * (hp - hc);
-      const float dhc = g * (1.f - z);
-      st_pub(a.dgates + si, dz * z * (1.f - z));
-      st_pub(a.dgates + TB2H + si, dhc * mreg * act_bwd_out(a.act, hcr));
+      float dg[2];
+      ligru_grads(a.act, g, z, hcr, hp, mreg, dg);
+      st_pub(a.dgates + si, dg[0]);
+      st_pub(a.dgates + TB2H + si, dg[1]);
       gcar = g;
     }
     LTR_MARK(3);

@@ -68,7 +68,8 @@ def build_pair(name, seed=2234, drop=None):
     return nets, onets, opts, model, B
 
 
-def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta_bound=False):
+def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta_bound=False,
+               beta_bound=False):
     import pkc.engine as E
     from oracle import nets as ON
     from oracle import run as OR
@@ -156,10 +157,13 @@ def run_config(name, sparse=None, steps=2, post_tol=1e-4, w_tol=5e-3, quant_beta
                 flips[pname] = nf
             d = (v.cpu().double() - r).norm().item()
             e = d / max(r.norm().item(), 1e-30)
-            if quant_beta_bound and ".bias" in pname and pname.startswith("bn"):
+            if (quant_beta_bound or beta_bound) and ".bias" in pname and pname.startswith("bn"):
                 # gate BatchNorm betas under fake quantisation: their gradients are sums of
                 # quantum-flip noise; RMSprop bounds any such noise step by
-                # lr / sqrt(1 - alpha) = 4.47 lr per step (either sign)
+                # lr / sqrt(1 - alpha) = 4.47 lr per step (either sign).  beta_bound (C3 fp32):
+                # a beta's gradient is a column sum of dgates, many elements of which sit within
+                # fp32 rounding of zero — another summation order (the grid-synchronised loops')
+                # flips their signs, which RMSprop's first steps turn into the same full steps
                 lr = float(opts[k]["arch_lr"])
                 md = (v.cpu().double() - r).abs().max().item()
                 assert md <= 2 * 4.48 * lr * steps, "%s %s max abs diff %.3g" % (name, pname, md)
@@ -295,7 +299,7 @@ def test_c4_lstm_bidir_full_size_bf16():
 
 @pytest.mark.parametrize("sparse", ["force", "off"])
 def test_c3_ligru_hcgs_full_size(sparse):
-    run_config("c3", sparse=sparse)
+    run_config("c3", sparse=sparse, beta_bound=True)
 
 
 def test_c4_lstm_bidir_full_size():

@@ -222,18 +222,23 @@ def _run_ligru(H, T, B, seed, grid, hcgs, load=False):
 @pytest.mark.parametrize("H,T,B,hcgs,seed,load", [(550, 40, 8, True, 21, False),
                                                   (550, 23, 8, True, 22, True),
                                                   (96, 17, 5, False, 23, False),
-                                                  (768, 9, 8, False, 24, False)])
+                                                  (768, 9, 8, False, 24, False),
+                                                  (24, 30, 4, False, 25, False),
+                                                  (24, 2, 4, False, 26, False)])
 def test_ligru_fp32_grid_loops_match_steps(H, T, B, hcgs, seed, load):
     """The exact-fp32 liGRU step mode (C3 fp32: 4 x 550 bidirectional, B = 8, HCGS U) in the
     grid-synchronised loops against the per-step launches on the same layer and inputs: the same
     fp32 products summed in another order (the dense U's masked zeros included), so every tensor
     within 2e-5 of its largest element over T = 40 steps of two layers (measured values printed);
-    the loops' timeout word stays zero and the last launch saw every arrival."""
+    with a dense U and H <= 256 (the per-step launches' 4-wave strips, summed in their order)
+    every tensor is bit-identical; the loops' timeout word stays zero and the last launch saw
+    every arrival."""
     ref, forms_ref = _run_ligru(H, T, B, seed, False, hcgs)
     got, forms = _run_ligru(H, T, B, seed, True, hcgs, load)
     assert all("grid" not in f for f in forms_ref.values()), forms_ref
     assert all(f.startswith("persistent grid-synchronised") for f in forms.values()), forms
     rep, bad = [], []
+    exact = H <= 256 and not hcgs
     nwg = (H + 15) // 16
     for k in ref:
         if k.endswith(".timeout"):
@@ -243,7 +248,7 @@ def test_ligru_fp32_grid_loops_match_steps(H, T, B, hcgs, seed, load):
         a, b = got[k].double(), ref[k].double()
         err = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-30)
         rep.append("%s %.2e" % (k, err))
-        if err > 2e-5:
+        if err > 2e-5 or (exact and not torch.equal(got[k], ref[k])):
             bad.append("%s %.3g" % (k, err))
     print("liGRU fp32 H %d T %d B %d: %s" % (H, T, B, ", ".join(rep)))
     assert not bad, bad
