@@ -643,20 +643,20 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
 // mode; neural_networks.py:1573-1584): the units (BPTT: columns k) dealt to ceil(H / 16)
 // workgroups of 16 waves, each holding its units' fp32 U rows of both gates (BPTT: Uᵀ columns)
 // as v_mfma_f32_16x16x4_f32 B operands in registers; lane group q of wave w owns the contraction
-// strip [(4 w + q) GK, + GK) (GK = 16: the per-step 4-wave kernels' strips for H <= 256; k >= H
-// reads zeros), h_{t-1} / dgates_t handed off as in the LSTM loops (write-through stores, step
-// counter).  B2 <= 16 rows (C3: both directions of B = 8).  The waves' partials are summed in the
-// per-step kernels' red_sum order, so for a dense U with H <= 256 (the per-step 4-wave form) the
-// loops are bit-identical to the per-step launches; a block-sparse U multiplies as dense (its
-// masked entries are exact zeros) — the fp32 sums of the per-step block-sparse launches in
-// another order.
-constexpr int GW = 16, GT = 64 * GW;   // waves / threads per workgroup
-constexpr int GK = 16;                 // contraction elements per lane group
-constexpr int GKMAX = 768;             // largest H (4 GW GK = 1024 covers it)
+// strip [(4 w + q) GK, + GK) (k >= H reads zeros), h_{t-1} / dgates_t handed off as in the LSTM
+// loops (write-through stores, step counter).  B2 <= 16 rows (C3: both directions of B = 8).  The
+// waves' partials are summed in the per-step kernels' red_sum order.  Two shapes: H <= 256 runs
+// the per-step kernels' own 4-wave x 16-element strips (GW = 4, GK = 16), so for a dense U the
+// loops are bit-identical to the per-step launches; 256 < H <= 768 runs 16 waves x 12 elements
+// (C3's H = 550: 12 MFMAs per wave and step, not 16).  A block-sparse U multiplies as dense (its
+// masked entries are exact zeros): the fp32 sums of the per-step block-sparse launches in another
+// order.
+constexpr int GKMAX = 768;             // largest H (16 x 4 x 12)
 
 // GK consecutive floats of row `row` from k0 of a handed-off (rows x H) matrix at byte offset
-// base: four 16-byte sc1 loads (rows >= nrows: out of range, zeros), elements k >= H zeroed
-__device__ __forceinline__ void ld_strip12(__amdgpu_buffer_rsrc_t r, unsigned base, int row,
+// base: GK / 4 16-byte sc1 loads (rows >= nrows: out of range, zeros), elements k >= H zeroed
+template <int GK>
+__device__ __forceinline__ void ld_strip(__amdgpu_buffer_rsrc_t r, unsigned base, int row,
                                            int nrows, int H, int k0, float* v) {
   const bool ok = row < nrows;
   const unsigned off = ok ? base + 4u * (unsigned)(row * H + k0) : OOB;
@@ -669,7 +669,8 @@ __device__ __forceinline__ void ld_strip12(__amdgpu_buffer_rsrc_t r, unsigned ba
 // Forward: workgroup wg owns units [8 wg, 8 wg + 8): ONE 16-column MFMA tile holds both gates
 // (column c: gate c / 8, unit 8 wg + c % 8), so a wave runs 12 MFMAs per step, not 24.
 constexpr int LUPW = 8;                // forward units per workgroup
-__global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
+template <int GW, int GK>
+__global__ __launch_bounds__(64 * GW) void lg_fwd_loop(pkc_rnn_args a) {
   __shared__ float red[GW][ROWS][UPW];         // each wave's tile of the step
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
@@ -705,7 +706,7 @@ __global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
     if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
     LTR_MARK(1);
     float hv[GK];
-    ld_strip12(hr, 4u * (unsigned)(t * n), c, B2, H, kl, hv);
+    ld_strip<GK>(hr, 4u * (unsigned)(t * n), c, B2, H, kl, hv);
     LTR_MARK(2);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -745,7 +746,8 @@ __global__ __launch_bounds__(GT) void lg_fwd_loop(pkc_rnn_args a) {
 
 // dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k, then
 // the liGRU gate gradients of step tt (bwd_step_epi + gate_grads, CELL_LIGRU)
-__global__ __launch_bounds__(GT) void lg_bwd_loop(pkc_rnn_args a) {
+template <int GW, int GK>
+__global__ __launch_bounds__(64 * GW) void lg_bwd_loop(pkc_rnn_args a) {
   __shared__ float red[GW][2][ROWS][UPW];
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
@@ -788,7 +790,7 @@ __global__ __launch_bounds__(GT) void lg_bwd_loop(pkc_rnn_args a) {
     float dv[2][GK];
 #pragma unroll
     for (int g = 0; g < 2; ++g)
-      ld_strip12(dgr, 4u * (unsigned)(g * TB2H + t * n), c, B2, H, jl, dv[g]);
+      ld_strip<GK>(dgr, 4u * (unsigned)(g * TB2H + t * n), c, B2, H, jl, dv[g]);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -902,7 +904,9 @@ int rnn_ligru_grid_fwd(const pkc_rnn_args* a, hipStream_t s) {
   using namespace lstmp;
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
-  hipLaunchKernelGGL(lg_fwd_loop, dim3((a->H + LUPW - 1) / LUPW), dim3(GT), 0, s, *a);
+  const dim3 grid((a->H + LUPW - 1) / LUPW);
+  if (a->H <= 256) hipLaunchKernelGGL((lg_fwd_loop<4, 16>), grid, dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((lg_fwd_loop<16, 12>), grid, dim3(1024), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_fwd grid-synchronised liGRU loop");
   return PKC_OK;
 }
@@ -912,7 +916,9 @@ int rnn_ligru_grid_bwd(const pkc_rnn_args* a, hipStream_t s) {
   if (a->T < 2) return PKC_OK;
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
-  hipLaunchKernelGGL(lg_bwd_loop, dim3((a->H + UPW - 1) / UPW), dim3(GT), 0, s, *a);
+  const dim3 grid((a->H + UPW - 1) / UPW);
+  if (a->H <= 256) hipLaunchKernelGGL((lg_bwd_loop<4, 16>), grid, dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((lg_bwd_loop<16, 12>), grid, dim3(1024), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd grid-synchronised liGRU loop");
   return PKC_OK;
 }
