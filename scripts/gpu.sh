@@ -94,9 +94,14 @@ r_bench_prof() {
   T=$(find /tmp/bprof -name 'bench_kernel_trace.csv' -print -quit)
   S=$(find /tmp/bprof -name 'bench_kernel_stats.csv' -print -quit)
   cp "$S" gpurun_out/bprof/bench_kernel_stats.csv
+  gzip -c "$T" > gpurun_out/bprof/bench_kernel_trace.csv.gz
   # anchor: the heads' NLL launch (once per step; with the deferred tail the gather rides in a
   # grouped launch inside the multi-step graphs): the listing starts there, one whole step long
-  python3 scripts/trace_gaps.py "$T" nll_multi_kernel "<1, true" > gpurun_out/bprof/timeline.txt
+  # (steps holding a standalone batch_gather_kernel are single-step graph replays, not the timed
+  # multi-step graphs: excluded)
+  local NL
+  NL=$(python3 -c "import json,sys; print(round(next(json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')).get('graph_launches_per_step') or 25))" gpurun_out/bprof/bench.log)
+  python3 scripts/trace_gaps.py "$T" nll_multi_kernel "<1, true" batch_gather_kernel "$NL" > gpurun_out/bprof/timeline.txt
   tail -3 gpurun_out/bprof/timeline.txt
 }
 

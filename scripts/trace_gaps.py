@@ -11,6 +11,10 @@ first = sys.argv[2] if len(sys.argv) > 2 else "batch_gather"
 # optional: keep only steps with a kernel whose name contains this (e.g. the bf16 instances, so
 # the fp32 leg of the same bench command is not the one summarised)
 need = sys.argv[3] if len(sys.argv) > 3 else None
+# optional: drop steps holding a kernel whose name contains this (the bench's multi-step graphs
+# run the batch gather inside the first grouped launch; a standalone batch_gather_kernel marks a
+# single-step graph replay — warmup, parity and per-launch probes — or a replay's first step)
+skip = sys.argv[4] if len(sys.argv) > 4 else None
 starts = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
 # the bench's own steps: the most common launch count between consecutive gathers (other
 # workloads in the same trace — batch sweep, sequence configs — have other shapes)
@@ -18,12 +22,15 @@ pairs = list(zip(starts, starts[1:]))
 lens = defaultdict(int)
 for a, b in pairs:
     lens[b - a] += 1
-if need:
-    pairs = [(a, b) for a, b in pairs if any(need in r["Kernel_Name"] for r in rows[a:b])]
+if need or skip:
+    pairs = [(a, b) for a, b in pairs
+             if (not need or any(need in r["Kernel_Name"] for r in rows[a:b]))
+             and not (skip and any(skip in r["Kernel_Name"] for r in rows[a:b]))]
     lens = defaultdict(int)
     for a, b in pairs:
         lens[b - a] += 1
-L = max(lens, key=lens.get)
+# optional: the step's launch count (the bench line's graph_launches_per_step), else the mode
+L = int(sys.argv[5]) if len(sys.argv) > 5 else max(lens, key=lens.get)
 # the graph-replayed steps of the timed region: of the steps with the common shape, the 200
 # shortest from first launch start to last launch end (eager steps of the same command — the
 # parity leg, per-launch cost probes — carry host launch gaps)
