@@ -62,7 +62,7 @@ __device__ unsigned long long ltrace_buf[2 * BNW * 8];
   } while (0)
 #define LTR_STORE(k)                                                    \
   do {                                                                  \
-    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                   \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 63) == 0) { \
       volatile unsigned long long* b_ = ltrace_buf + ((k) * BNW + (threadIdx.x >> 6)) * 8; \
       for (int i_ = 0; i_ < 5; ++i_) b_[i_] = lt_acc[i_];               \
       b_[5] = (unsigned long long)T;                                    \
@@ -422,9 +422,13 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
 // k at + 8 i, two 16-row chains, the waves' partials summed ((0 + 1) + (2 + 3)) + ((4 + 5) +
 // (6 + 7)); the handed-off operand is the bf16 copy the per-step kernels read (hs_h, dgates_h),
 // stored as pairs of adjacent units.
+// RS = 2 (B2 > 16, C4's 32 rows): the rows are split over two workgroups per unit block
+// (blockIdx.y = row half, 2 H / 16 workgroups): each reads and multiplies only its 16 rows of the
+// handed-off operand — half the per-workgroup payload, which bounds the BPTT step (≈ 35 GB/s per
+// CU) — and the elements' sums are unchanged (the two 16-row chains were independent).
 constexpr int R32 = 32;
 
-template <int KC>
+template <int KC, int RS>
 __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
   __shared__ float red[FNW][4][R32][UPW];       // each wave's four gate tiles (32 rows)
   __shared__ int abort_flag;
@@ -434,7 +438,8 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int u0 = blockIdx.x * UPW;
-  const unsigned nwg = gridDim.x;
+  const int y16 = RS == 2 ? 16 * (int)blockIdx.y : 0;   // first row of this workgroup's rows
+  const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   // lane group q's 8-wide chunk i: the per-step kernels' kb + 8 i with kb = (4 w + q) 8 KC
@@ -449,15 +454,15 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
     for (int i = 0; i < KC; ++i)
       ub[g][i] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.U_h[g]) +
                                                    (int64_t)(u0 + c) * H + kb + ks * i);
-  const bool two = B2 > 16;                     // (uniform) the second 16-row chain
-  const int r = tid >> 4, j = u0 + (tid & 15);  // this thread's cell-update element
-  const bool ep = r < B2;
+  const bool two = RS == 1 && B2 > 16;          // (uniform) the second 16-row chain
+  const int r = y16 + (tid >> 4), j = u0 + (tid & 15);   // this thread's cell-update element
+  const bool ep = (RS == 1 || tid < 16 * UPW) && r < B2;
   const int rr = ep ? r : 0;
   float hreg = 0.f, creg = 0.f;
   const float mreg = drop_val(a, rr, j, B2);
   const __amdgpu_buffer_rsrc_t hr = pub_rsrc(a.hs_h);
-  const unsigned oa = 2u * (c * H + kb), ob = 2u * ((16 + c) * H + kb);
-  const bool ra = c < B2, rb = 16 + c < B2;
+  const unsigned oa = 2u * ((y16 + c) * H + kb), ob = 2u * ((16 + c) * H + kb);
+  const bool ra = y16 + c < B2, rb = 16 + c < B2;
   LTR_DECL;
   for (int t = 0; t < T; ++t) {
     LTR_MARK(0);
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
       ha[i] = ld_pub_h8(hr, ra ? oa + to + 2 * ks * i : OOB);
-      hb[i] = ld_pub_h8(hr, two && rb ? ob + to + 2 * ks * i : OOB);
+      if constexpr (RS == 1) hb[i] = ld_pub_h8(hr, two && rb ? ob + to + 2 * ks * i : OOB);
     }
     LTR_MARK(2);
 #pragma unroll
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
       float acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        auto p = [&](int v) { return red[v][g][r][ul]; };
+        auto p = [&](int v) { return red[v][g][r - y16][ul]; };
         acc[g] = ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
       }
       EpiIn e;
@@ -527,7 +532,7 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
 
 // dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k:
 // wave w owns strip w of j for all four gates (the per-step kernel's wave w of each gate's launch)
-template <int KC>
+template <int KC, int RS>
 __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
   __shared__ float red[4][FNW][R32][UPW];       // [gate][strip] partial tiles of the step
   __shared__ int abort_flag;
@@ -537,7 +542,8 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int k0 = blockIdx.x * UPW;
-  const unsigned nwg = gridDim.x;
+  const int y16 = RS == 2 ? 16 * (int)blockIdx.y : 0;   // first row of this workgroup's rows
+  const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TB2H = (int64_t)T * B2 * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   // lane group q's 8-wide chunk i: the per-step kernels' kb + 8 i with kb = (4 w + q) 8 KC
@@ -554,16 +560,16 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
       ub[g][i] = *reinterpret_cast<const rbf16x8*>(reinterpret_cast<const __bf16*>(a.ut_h) +
                                                    (int64_t)g * H * H + (int64_t)(k0 + c) * H +
                                                    kb + ks * i);
-  const bool two = B2 > 16;
-  const int r = tid >> 4, k = k0 + (tid & 15);
-  const bool ep = r < B2;
+  const bool two = RS == 1 && B2 > 16;
+  const int r = y16 + (tid >> 4), k = k0 + (tid & 15);
+  const bool ep = (RS == 1 || tid < 16 * UPW) && r < B2;
   const int rr = ep ? r : 0;
   const int64_t e = (int64_t)rr * H + k;
   float gcar = a.work[e], dccar = a.work[2 * n + e];   // step T-1's carries (rnn_bwd_init)
   const float mreg = drop_val(a, rr, k, B2);
   const __amdgpu_buffer_rsrc_t dr = pub_rsrc(a.dgates_h);
-  const unsigned oa = 2u * (c * H + kb), ob = 2u * ((16 + c) * H + kb);
-  const bool ra = c < B2, rb = 16 + c < B2;
+  const unsigned oa = 2u * ((y16 + c) * H + kb), ob = 2u * ((16 + c) * H + kb);
+  const bool ra = y16 + c < B2, rb = 16 + c < B2;
   LTR_DECL;
   for (int tt = T - 2; tt >= 0; --tt) {
     LTR_MARK(0);
@@ -583,7 +589,7 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
         ha[g][i] = ld_pub_h8(dr, ra ? oa + go + 2 * ks * i : OOB);
-        hb[g][i] = ld_pub_h8(dr, two && rb ? ob + go + 2 * ks * i : OOB);
+        if constexpr (RS == 1) hb[g][i] = ld_pub_h8(dr, two && rb ? ob + go + 2 * ks * i : OOB);
       }
     }
 #pragma unroll
@@ -608,7 +614,7 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
       float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        auto p = [&](int v) { return red[g][v][r][kl]; };
+        auto p = [&](int v) { return red[g][v][r - y16][kl]; };
         dh += ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
       }
       const float g = dyv + dh;                 // bwd_step_epi
@@ -862,6 +868,16 @@ static int lstm_bf16_coalesced() {
   return v && v[0] == '0' ? 0 : 1;
 }
 
+// bf16 loops with more than 16 rows (C4: 2 x 16): the rows split over two workgroups per unit
+// block (RS = 2) by default; PKC_RNN_LSTM_RS=1 keeps both 16-row chains in one workgroup (A/B)
+static bool lstm_bf16_rows_split(const pkc_rnn_args* a) {
+  static const int rs = [] {
+    const char* v = getenv("PKC_RNN_LSTM_RS");
+    return v ? atoi(v) : 2;
+  }();
+  return rs == 2 && (a->bidir ? 2 * a->B : a->B) > 16;
+}
+
 // liGRU exact-fp32 step mode in the grid-synchronised loops (lg_fwd_loop / lg_bwd_loop)
 bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd) {
   const char* env = getenv("PKC_RNN_LIGRU_GRID");     // "0": the per-step launches
@@ -892,9 +908,14 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   } else {
     const int co = lstm_bf16_coalesced();
-    if (kc == 2) hipLaunchKernelGGL(bf_fwd_loop<2>, grid, dim3(FNT), 0, s, *a, co);
-    else if (kc == 3) hipLaunchKernelGGL(bf_fwd_loop<3>, grid, dim3(FNT), 0, s, *a, co);
-    else hipLaunchKernelGGL(bf_fwd_loop<4>, grid, dim3(FNT), 0, s, *a, co);
+    if (lstm_bf16_rows_split(a)) {
+      const dim3 g2(grid.x, 2);
+      if (kc == 2) hipLaunchKernelGGL((bf_fwd_loop<2, 2>), g2, dim3(FNT), 0, s, *a, co);
+      else if (kc == 3) hipLaunchKernelGGL((bf_fwd_loop<3, 2>), g2, dim3(FNT), 0, s, *a, co);
+      else hipLaunchKernelGGL((bf_fwd_loop<4, 2>), g2, dim3(FNT), 0, s, *a, co);
+    } else if (kc == 2) hipLaunchKernelGGL((bf_fwd_loop<2, 1>), grid, dim3(FNT), 0, s, *a, co);
+    else if (kc == 3) hipLaunchKernelGGL((bf_fwd_loop<3, 1>), grid, dim3(FNT), 0, s, *a, co);
+    else hipLaunchKernelGGL((bf_fwd_loop<4, 1>), grid, dim3(FNT), 0, s, *a, co);
   }
   PKC_LAUNCH_CHECK("pkc_rnn_fwd persistent LSTM loop");
   return PKC_OK;
@@ -935,9 +956,17 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
     if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, grid, dim3(BNT), 0, s, *a);
     else hipLaunchKernelGGL(bwd_loop<true>, grid, dim3(BNT), 0, s, *a);
   }
-  else if (kc == 2) hipLaunchKernelGGL(bf_bwd_loop<2>, grid, dim3(FNT), 0, s, *a, lstm_bf16_coalesced());
-  else if (kc == 3) hipLaunchKernelGGL(bf_bwd_loop<3>, grid, dim3(FNT), 0, s, *a, lstm_bf16_coalesced());
-  else hipLaunchKernelGGL(bf_bwd_loop<4>, grid, dim3(FNT), 0, s, *a, lstm_bf16_coalesced());
+  else {
+    const int co = lstm_bf16_coalesced();
+    if (lstm_bf16_rows_split(a)) {
+      const dim3 g2(grid.x, 2);
+      if (kc == 2) hipLaunchKernelGGL((bf_bwd_loop<2, 2>), g2, dim3(FNT), 0, s, *a, co);
+      else if (kc == 3) hipLaunchKernelGGL((bf_bwd_loop<3, 2>), g2, dim3(FNT), 0, s, *a, co);
+      else hipLaunchKernelGGL((bf_bwd_loop<4, 2>), g2, dim3(FNT), 0, s, *a, co);
+    } else if (kc == 2) hipLaunchKernelGGL((bf_bwd_loop<2, 1>), grid, dim3(FNT), 0, s, *a, co);
+    else if (kc == 3) hipLaunchKernelGGL((bf_bwd_loop<3, 1>), grid, dim3(FNT), 0, s, *a, co);
+    else hipLaunchKernelGGL((bf_bwd_loop<4, 1>), grid, dim3(FNT), 0, s, *a, co);
+  }
   PKC_LAUNCH_CHECK("pkc_rnn_bwd persistent LSTM loop");
   return PKC_OK;
 }
