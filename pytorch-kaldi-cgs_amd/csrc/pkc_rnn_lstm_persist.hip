@@ -287,6 +287,9 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
 // bit-identical to the per-step launches; tests/test_gpu_lstm_persist.py bounds the difference),
 // at 12 instead of 32 MFMA issues per wave and step (the fp32 chains were half of a BPTT step:
 // profiles/r06_lstm_persist_trace_c5.json).  !X3: the per-step kernel's fp32 chains, bit-identical.
+// gridDim.y > 1: the B rows split over gridDim.y workgroups per column block (ceil(B / y) rows
+// each, blockIdx.y = row block): each loads only its rows of dgates_t (C5: 48 of 96 KB per step;
+// the payload bounds the step) — the elements' sums are unchanged (rows are independent).
 template <bool X3>
 __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   __shared__ float red[4][8][ROWS][UPW];       // [gate][strip] partial tiles of the step
@@ -298,7 +301,9 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   const int jr = W & 7, gp = W >> 3;
   const int c = lane & 15, q = lane >> 4;
   const int k0 = blockIdx.x * UPW;
-  const unsigned nwg = gridDim.x;
+  const int rb = (B + (int)gridDim.y - 1) / (int)gridDim.y;   // rows per workgroup
+  const int y0 = rb * (int)blockIdx.y;                          // its first row
+  const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B * H, TB2H = (int64_t)T * B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   const int kb = (jr * 4 + q) * BS;             // this lane group's strip of j
@@ -322,9 +327,10 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) uh[gg][s][i] = (__bf16)vu[gg][8 * s + i];
   }
-  const bool ep = tid < B * UPW;
-  const int r = ep ? tid >> 4 : 0, k = k0 + (tid & 15);
+  const bool ep = tid < rb * UPW && y0 + (tid >> 4) < B;
+  const int r = ep ? y0 + (tid >> 4) : 0, k = k0 + (tid & 15);
   const int64_t e = (int64_t)r * H + k;
+  const bool rc = c < rb && y0 + c < B;          // this lane's MFMA row y0 + c is one of ours
   // the carries of step T-1 (rnn_bwd_init, slot 0) and the dropout value
   float gcar = a.work[e], dccar = a.work[2 * n + e];
   const float mreg = drop_val(a, r, k, B);
@@ -347,7 +353,7 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int gg = 0; gg < 2; ++gg) {
       const unsigned off =
-          c < B ? 4u * (unsigned)((2 * gp + gg) * TB2H + t * n + (int64_t)c * H + jl) : OOB;
+          rc ? 4u * (unsigned)((2 * gp + gg) * TB2H + t * n + (int64_t)(y0 + c) * H + jl) : OOB;
 #pragma unroll
       for (int s = 0; s < BS; s += 4)
         ld_pub4(dgr, off + 4 * (X3 ? 32 * (s / 8) + (s % 8) : s), va[gg] + s);
@@ -389,7 +395,7 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
       float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        auto p = [&](int v) { return red[g][v][r][kl]; };
+        auto p = [&](int v) { return red[g][v][r - y0][kl]; };
         dh += ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
       }
       const float g = dyv + dh;                 // bwd_step_epi
@@ -422,10 +428,11 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
 // k at + 8 i, two 16-row chains, the waves' partials summed ((0 + 1) + (2 + 3)) + ((4 + 5) +
 // (6 + 7)); the handed-off operand is the bf16 copy the per-step kernels read (hs_h, dgates_h),
 // stored as pairs of adjacent units.
-// RS = 2 (B2 > 16, C4's 32 rows): the rows are split over two workgroups per unit block
-// (blockIdx.y = row half, 2 H / 16 workgroups): each reads and multiplies only its 16 rows of the
-// handed-off operand — half the per-workgroup payload, which bounds the BPTT step (≈ 35 GB/s per
-// CU) — and the elements' sums are unchanged (the two 16-row chains were independent).
+// RS = 2 / 4 (B2 > 16, C4's 32 rows): the rows are split over RS workgroups per unit block
+// (blockIdx.y = row block of 32 / RS rows, RS H / 16 workgroups): each reads and multiplies only
+// its rows of the handed-off operand (a 16-row MFMA tile, rows past the block reading zeros
+// without a memory access) — 1 / RS of the per-workgroup payload, which bounds the BPTT step
+// (≈ 35 GB/s per CU) — and the elements' sums are unchanged (the row chains were independent).
 constexpr int R32 = 32;
 
 template <int KC, int RS>
@@ -438,7 +445,8 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int u0 = blockIdx.x * UPW;
-  const int y16 = RS == 2 ? 16 * (int)blockIdx.y : 0;   // first row of this workgroup's rows
+  constexpr int RW = RS == 1 ? 32 : 32 / RS;          // rows of this workgroup
+  const int y16 = RW * (int)blockIdx.y;                // its first row
   const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
@@ -456,13 +464,13 @@ __global__ __launch_bounds__(FNT) void bf_fwd_loop(pkc_rnn_args a, int co) {
                                                    (int64_t)(u0 + c) * H + kb + ks * i);
   const bool two = RS == 1 && B2 > 16;          // (uniform) the second 16-row chain
   const int r = y16 + (tid >> 4), j = u0 + (tid & 15);   // this thread's cell-update element
-  const bool ep = (RS == 1 || tid < 16 * UPW) && r < B2;
+  const bool ep = (RS == 1 || tid < RW * UPW) && r < B2;
   const int rr = ep ? r : 0;
   float hreg = 0.f, creg = 0.f;
   const float mreg = drop_val(a, rr, j, B2);
   const __amdgpu_buffer_rsrc_t hr = pub_rsrc(a.hs_h);
   const unsigned oa = 2u * ((y16 + c) * H + kb), ob = 2u * ((16 + c) * H + kb);
-  const bool ra = y16 + c < B2, rb = 16 + c < B2;
+  const bool ra = c < RW && y16 + c < B2, rb = 16 + c < B2;
   LTR_DECL;
   for (int t = 0; t < T; ++t) {
     LTR_MARK(0);
@@ -542,7 +550,8 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int k0 = blockIdx.x * UPW;
-  const int y16 = RS == 2 ? 16 * (int)blockIdx.y : 0;   // first row of this workgroup's rows
+  constexpr int RW = RS == 1 ? 32 : 32 / RS;          // rows of this workgroup
+  const int y16 = RW * (int)blockIdx.y;                // its first row
   const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TB2H = (int64_t)T * B2 * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
@@ -562,14 +571,14 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
                                                    kb + ks * i);
   const bool two = RS == 1 && B2 > 16;
   const int r = y16 + (tid >> 4), k = k0 + (tid & 15);
-  const bool ep = (RS == 1 || tid < 16 * UPW) && r < B2;
+  const bool ep = (RS == 1 || tid < RW * UPW) && r < B2;
   const int rr = ep ? r : 0;
   const int64_t e = (int64_t)rr * H + k;
   float gcar = a.work[e], dccar = a.work[2 * n + e];   // step T-1's carries (rnn_bwd_init)
   const float mreg = drop_val(a, rr, k, B2);
   const __amdgpu_buffer_rsrc_t dr = pub_rsrc(a.dgates_h);
   const unsigned oa = 2u * ((y16 + c) * H + kb), ob = 2u * ((16 + c) * H + kb);
-  const bool ra = y16 + c < B2, rb = 16 + c < B2;
+  const bool ra = c < RW && y16 + c < B2, rb = 16 + c < B2;
   LTR_DECL;
   for (int tt = T - 2; tt >= 0; --tt) {
     LTR_MARK(0);
@@ -868,14 +877,26 @@ static int lstm_bf16_coalesced() {
   return v && v[0] == '0' ? 0 : 1;
 }
 
-// bf16 loops with more than 16 rows (C4: 2 x 16): the rows split over two workgroups per unit
-// block (RS = 2) by default; PKC_RNN_LSTM_RS=1 keeps both 16-row chains in one workgroup (A/B)
-static bool lstm_bf16_rows_split(const pkc_rnn_args* a) {
+// bf16 loops with more than 16 rows (C4: 2 x 16): the workgroups per unit block the rows are
+// split over (PKC_RNN_LSTM_RS = 1, 2 or 4; 1 keeps both 16-row chains in one workgroup)
+static int lstm_bf16_rows_split(const pkc_rnn_args* a) {
   static const int rs = [] {
     const char* v = getenv("PKC_RNN_LSTM_RS");
-    return v ? atoi(v) : 2;
+    const int x = v ? atoi(v) : 2;
+    return x == 1 || x == 4 ? x : 2;
   }();
-  return rs == 2 && (a->bidir ? 2 * a->B : a->B) > 16;
+  return (a->bidir ? 2 * a->B : a->B) > 16 ? rs : 1;
+}
+
+// QX BPTT loop: workgroups per column block the B rows are split over (PKC_RNN_LSTM_QX_RS, default
+// 2 when B > 8; 1: all rows in one workgroup)
+static int lstm_qx_bwd_rows_split(const pkc_rnn_args* a) {
+  static const int rs = [] {
+    const char* v = getenv("PKC_RNN_LSTM_QX_RS");
+    const int x = v ? atoi(v) : 2;
+    return x >= 1 && x <= 4 ? x : 2;
+  }();
+  return a->B > 8 ? rs : 1;
 }
 
 // liGRU exact-fp32 step mode in the grid-synchronised loops (lg_fwd_loop / lg_bwd_loop)
@@ -908,7 +929,13 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   } else {
     const int co = lstm_bf16_coalesced();
-    if (lstm_bf16_rows_split(a)) {
+    const int rs = lstm_bf16_rows_split(a);
+    if (rs == 4) {
+      const dim3 g4(grid.x, 4);
+      if (kc == 2) hipLaunchKernelGGL((bf_fwd_loop<2, 4>), g4, dim3(FNT), 0, s, *a, co);
+      else if (kc == 3) hipLaunchKernelGGL((bf_fwd_loop<3, 4>), g4, dim3(FNT), 0, s, *a, co);
+      else hipLaunchKernelGGL((bf_fwd_loop<4, 4>), g4, dim3(FNT), 0, s, *a, co);
+    } else if (rs == 2) {
       const dim3 g2(grid.x, 2);
       if (kc == 2) hipLaunchKernelGGL((bf_fwd_loop<2, 2>), g2, dim3(FNT), 0, s, *a, co);
       else if (kc == 3) hipLaunchKernelGGL((bf_fwd_loop<3, 2>), g2, dim3(FNT), 0, s, *a, co);
@@ -953,12 +980,19 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
   const int kc = a->H / 256;
   if (a->qh_exact) {
     const char* x3 = getenv("PKC_RNN_LSTM_PERSIST_X3");   // "0": the fp32 chains (bit-identical)
-    if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, grid, dim3(BNT), 0, s, *a);
-    else hipLaunchKernelGGL(bwd_loop<true>, grid, dim3(BNT), 0, s, *a);
+    const dim3 gq(grid.x, lstm_qx_bwd_rows_split(a));
+    if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, gq, dim3(BNT), 0, s, *a);
+    else hipLaunchKernelGGL(bwd_loop<true>, gq, dim3(BNT), 0, s, *a);
   }
   else {
     const int co = lstm_bf16_coalesced();
-    if (lstm_bf16_rows_split(a)) {
+    const int rs = lstm_bf16_rows_split(a);
+    if (rs == 4) {
+      const dim3 g4(grid.x, 4);
+      if (kc == 2) hipLaunchKernelGGL((bf_bwd_loop<2, 4>), g4, dim3(FNT), 0, s, *a, co);
+      else if (kc == 3) hipLaunchKernelGGL((bf_bwd_loop<3, 4>), g4, dim3(FNT), 0, s, *a, co);
+      else hipLaunchKernelGGL((bf_bwd_loop<4, 4>), g4, dim3(FNT), 0, s, *a, co);
+    } else if (rs == 2) {
       const dim3 g2(grid.x, 2);
       if (kc == 2) hipLaunchKernelGGL((bf_bwd_loop<2, 2>), g2, dim3(FNT), 0, s, *a, co);
       else if (kc == 3) hipLaunchKernelGGL((bf_bwd_loop<3, 2>), g2, dim3(FNT), 0, s, *a, co);

@@ -96,6 +96,8 @@ BWD_KEYS = ("dgates", "dx0", "grad")      # what the BPTT products feed
                                                 (512, 40, 12, 1, False, False),
                                                 (512, 23, 12, 2, True, True),
                                                 (512, 9, 7, 3, False, False),
+                                                (512, 11, 9, 6, False, False),
+                                                (512, 13, 16, 7, True, False),
                                                 (768, 12, 12, 4, False, True),
                                                 (1024, 10, 16, 5, False, True)])
 def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load, x3, monkeypatch):
@@ -114,9 +116,11 @@ def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load, x3, monkeypatc
     for k in ref:
         if k.endswith(".timeout"):
             # [step counter, timeout word] of the last persistent launch, the BPTT's (32 x (T - 2)
-            # arrivals); with per-step BPTT launches (H != 512) their gate slabs hold these words
+            # arrivals; B > 8 rows: two row blocks per column block, 64 x (T - 2)); with per-step
+            # BPTT launches (H != 512) their gate slabs hold these words
             if H == 512:
-                assert int(got[k][0]) == 32 * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
+                nwg = 32 * (2 if B > 8 else 1)
+                assert int(got[k][0]) == nwg * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
                 assert int(got[k][1]) == 0, "%s: a persistent loop timed out" % k
             continue
         a, b = got[k], ref[k]
