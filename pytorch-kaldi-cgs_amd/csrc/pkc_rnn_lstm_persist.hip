@@ -683,6 +683,10 @@ __device__ __forceinline__ void ld_strip(__amdgpu_buffer_rsrc_t r, unsigned base
 
 // Forward: workgroup wg owns units [8 wg, 8 wg + 8): ONE 16-column MFMA tile holds both gates
 // (column c: gate c / 8, unit 8 wg + c % 8), so a wave runs 12 MFMAs per step, not 24.
+// Both loops: gridDim.y > 1 splits the B2 rows over that many workgroups per unit (column) block
+// (ceil(B2 / y) rows each, blockIdx.y = row block): each loads only its rows of the handed-off
+// h_{t-1} / dgates_t (MFMA rows past the block read zeros without a memory access); the elements'
+// sums are unchanged (rows are independent).
 constexpr int LUPW = 8;                // forward units per workgroup
 template <int GW, int GK>
 __global__ __launch_bounds__(64 * GW) void lg_fwd_loop(pkc_rnn_args a) {
@@ -694,7 +698,8 @@ __global__ __launch_bounds__(64 * GW) void lg_fwd_loop(pkc_rnn_args a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int u0 = blockIdx.x * LUPW;
-  const unsigned nwg = gridDim.x;
+  const int rb = (B2 + (int)gridDim.y - 1) / (int)gridDim.y, y0 = rb * (int)blockIdx.y;
+  const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   const int kl = (4 * w + q) * GK;
@@ -704,8 +709,8 @@ __global__ __launch_bounds__(64 * GW) void lg_fwd_loop(pkc_rnn_args a) {
   const float* Ug = a.U[c >> 3];
 #pragma unroll
   for (int s = 0; s < GK; ++s) ub[s] = uu < H && kl + s < H ? Ug[(int64_t)uu * H + kl + s] : 0.f;
-  const int r = tid >> 3, j = u0 + (tid & 7);    // this thread's cell-update element
-  const bool ep = tid < ROWS * LUPW && r < B2 && j < H;
+  const int r = y0 + (tid >> 3), j = u0 + (tid & 7);    // this thread's cell-update element
+  const bool ep = tid < rb * LUPW && r < B2 && j < H;
   const int rr = ep ? r : 0, jj = ep ? j : 0;
   float hreg = 0.f;
   const float mreg = drop_val(a, rr, jj, B2);
@@ -721,7 +726,7 @@ __global__ __launch_bounds__(64 * GW) void lg_fwd_loop(pkc_rnn_args a) {
     if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
     LTR_MARK(1);
     float hv[GK];
-    ld_strip<GK>(hr, 4u * (unsigned)(t * n), c, B2, H, kl, hv);
+    ld_strip<GK>(hr, 4u * (unsigned)(t * n), c < rb ? y0 + c : B2, B2, H, kl, hv);
     LTR_MARK(2);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -735,7 +740,7 @@ __global__ __launch_bounds__(64 * GW) void lg_fwd_loop(pkc_rnn_args a) {
       float acc2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        auto p = [&](int v) { return red[v][r][8 * g + ul]; };
+        auto p = [&](int v) { return red[v][r - y0][8 * g + ul]; };
         float v = (p(0) + p(1)) + (p(2) + p(3));          // red_sum's order
 #pragma unroll
         for (int w4 = 4; w4 < GW; w4 += 4) v += (p(w4) + p(w4 + 1)) + (p(w4 + 2) + p(w4 + 3));
@@ -771,7 +776,8 @@ __global__ __launch_bounds__(64 * GW) void lg_bwd_loop(pkc_rnn_args a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int k0 = blockIdx.x * UPW;
-  const unsigned nwg = gridDim.x;
+  const int rb = (B2 + (int)gridDim.y - 1) / (int)gridDim.y, y0 = rb * (int)blockIdx.y;
+  const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TB2H = (int64_t)T * B2 * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   const int jl = (4 * w + q) * GK;
@@ -783,8 +789,8 @@ __global__ __launch_bounds__(64 * GW) void lg_bwd_loop(pkc_rnn_args a) {
 #pragma unroll
     for (int s = 0; s < GK; ++s)
       ub[g][s] = kk < H && jl + s < H ? a.ut[(int64_t)g * H * H + (int64_t)kk * H + jl + s] : 0.f;
-  const int r = tid >> 4, k = k0 + (tid & 15);
-  const bool ep = tid < ROWS * UPW && r < B2 && k < H;
+  const int r = y0 + (tid >> 4), k = k0 + (tid & 15);
+  const bool ep = tid < rb * UPW && r < B2 && k < H;
   const int rr = ep ? r : 0, ke = ep ? k : 0;
   const int64_t e = (int64_t)rr * H + ke;
   float gcar = a.work[e];                       // g_{T-1} (rnn_bwd_init, slot 0)
@@ -805,7 +811,7 @@ __global__ __launch_bounds__(64 * GW) void lg_bwd_loop(pkc_rnn_args a) {
     float dv[2][GK];
 #pragma unroll
     for (int g = 0; g < 2; ++g)
-      ld_strip<GK>(dgr, 4u * (unsigned)(g * TB2H + t * n), c, B2, H, jl, dv[g]);
+      ld_strip<GK>(dgr, 4u * (unsigned)(g * TB2H + t * n), c < rb ? y0 + c : B2, B2, H, jl, dv[g]);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -821,7 +827,7 @@ __global__ __launch_bounds__(64 * GW) void lg_bwd_loop(pkc_rnn_args a) {
       float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        auto p = [&](int v) { return red[v][g][r][kl]; };
+        auto p = [&](int v) { return red[v][g][r - y0][kl]; };
         float v = (p(0) + p(1)) + (p(2) + p(3));          // red_sum's order
 #pragma unroll
         for (int w4 = 4; w4 < GW; w4 += 4) v += (p(w4) + p(w4 + 1)) + (p(w4 + 2) + p(w4 + 3));
@@ -877,6 +883,23 @@ static int lstm_bf16_coalesced() {
   return v && v[0] == '0' ? 0 : 1;
 }
 
+// Compute units of the current device: a grid-synchronised loop needs every workgroup resident at
+// once, and these workgroups (512-1024 threads, large register files) are sized for one per CU, so
+// a row split is only taken while the whole grid still fits one workgroup per CU.
+static int device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return n;
+}
+// the largest of rs, rs / 2, ..., 1 whose grid (base workgroups x split) fits the device
+static int fit_split(int rs, int base) {
+  const int cus = device_cus();
+  while (rs > 1 && base * rs > cus) rs = rs > 2 ? rs - 1 : 1;
+  return rs;
+}
+
 // bf16 loops with more than 16 rows (C4: 2 x 16): the workgroups per unit block the rows are
 // split over (PKC_RNN_LSTM_RS = 1, 2 or 4; 1 keeps both 16-row chains in one workgroup)
 static int lstm_bf16_rows_split(const pkc_rnn_args* a) {
@@ -885,7 +908,9 @@ static int lstm_bf16_rows_split(const pkc_rnn_args* a) {
     const int x = v ? atoi(v) : 2;
     return x == 1 || x == 4 ? x : 2;
   }();
-  return (a->bidir ? 2 * a->B : a->B) > 16 ? rs : 1;
+  if ((a->bidir ? 2 * a->B : a->B) <= 16) return 1;
+  const int r = fit_split(rs, a->H / lstmp::UPW);
+  return r == 3 ? 2 : r;                        // (the bf16 loops take 1, 2 or 4)
 }
 
 // QX BPTT loop: workgroups per column block the B rows are split over (PKC_RNN_LSTM_QX_RS, default
@@ -896,7 +921,7 @@ static int lstm_qx_bwd_rows_split(const pkc_rnn_args* a) {
     const int x = v ? atoi(v) : 2;
     return x >= 1 && x <= 4 ? x : 2;
   }();
-  return a->B > 8 ? rs : 1;
+  return a->B > 8 ? fit_split(rs, a->H / lstmp::UPW) : 1;
 }
 
 // liGRU exact-fp32 step mode in the grid-synchronised loops (lg_fwd_loop / lg_bwd_loop)
@@ -909,6 +934,18 @@ bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd) {
     return false;
   if ((int64_t)a->T * B2 * a->H * 2 * 4 >= (1ll << 31) - 64) return false;
   return bwd ? (a->dgates && a->ut) : true;
+}
+
+// liGRU grid loops: workgroups per unit block the B2 rows are split over (PKC_RNN_LIGRU_GRID_RS,
+// default 2 when B2 > 8; 1: all rows in one workgroup)
+static int ligru_grid_rows_split(const pkc_rnn_args* a) {
+  static const int rs = [] {
+    const char* v = getenv("PKC_RNN_LIGRU_GRID_RS");
+    const int x = v ? atoi(v) : 2;
+    return x >= 1 && x <= 4 ? x : 2;
+  }();
+  // (the forward's unit blocks are the larger grid: ceil(H / 8))
+  return (a->bidir ? 2 * a->B : a->B) > 8 ? fit_split(rs, (a->H + lstmp::LUPW - 1) / lstmp::LUPW) : 1;
 }
 
 static int lstm_ctr_reset(const pkc_rnn_args* a, hipStream_t s) {
@@ -952,7 +989,7 @@ int rnn_ligru_grid_fwd(const pkc_rnn_args* a, hipStream_t s) {
   using namespace lstmp;
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
-  const dim3 grid((a->H + LUPW - 1) / LUPW);
+  const dim3 grid((a->H + LUPW - 1) / LUPW, ligru_grid_rows_split(a));
   if (a->H <= 256) hipLaunchKernelGGL((lg_fwd_loop<4, 16>), grid, dim3(256), 0, s, *a);
   else hipLaunchKernelGGL((lg_fwd_loop<16, 12>), grid, dim3(1024), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_fwd grid-synchronised liGRU loop");
@@ -964,7 +1001,7 @@ int rnn_ligru_grid_bwd(const pkc_rnn_args* a, hipStream_t s) {
   if (a->T < 2) return PKC_OK;
   int st = lstm_ctr_reset(a, s);
   if (st) return st;
-  const dim3 grid((a->H + UPW - 1) / UPW);
+  const dim3 grid((a->H + UPW - 1) / UPW, ligru_grid_rows_split(a));
   if (a->H <= 256) hipLaunchKernelGGL((lg_bwd_loop<4, 16>), grid, dim3(256), 0, s, *a);
   else hipLaunchKernelGGL((lg_bwd_loop<16, 12>), grid, dim3(1024), 0, s, *a);
   PKC_LAUNCH_CHECK("pkc_rnn_bwd grid-synchronised liGRU loop");

@@ -244,7 +244,7 @@ def test_ligru_fp32_grid_loops_match_steps(H, T, B, hcgs, seed, load):
     assert all(f.startswith("persistent grid-synchronised") for f in forms.values()), forms
     rep, bad = [], []
     exact = H <= 256 and not hcgs
-    nwg = (H + 15) // 16
+    nwg = (H + 15) // 16 * (2 if 2 * B > 8 else 1)     # > 8 rows: two row blocks per column block
     for k in ref:
         if k.endswith(".timeout"):
             assert int(got[k][0]) == nwg * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
