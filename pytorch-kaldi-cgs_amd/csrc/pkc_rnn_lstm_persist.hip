@@ -852,10 +852,13 @@ __global__ __launch_bounds__(64 * GW) void lg_bwd_loop(pkc_rnn_args a) {
 
 }  // namespace lstmp
 
+static int device_cus();
+
 bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
   const char* env = getenv("PKC_RNN_LSTM_PERSIST");   // "0": the per-step launches (A/B, tests)
   if (env && env[0] == '0') return false;
   if (a->cell != PKC_CELL_LSTM || a->ln_gamma || a->kmap_fwd || a->kmap_bwd || !a->work) return false;
+  if (a->H / lstmp::UPW > device_cus()) return false;   // (every workgroup resident: one per CU)
   const int64_t B2 = a->bidir ? 2 * a->B : a->B;
   // byte offsets of the 16-byte payload loads (dgates: G x T x B2 x H floats) below the
   // descriptors' 2^31 - 16 range
@@ -933,6 +936,7 @@ bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd) {
       B2 > lstmp::ROWS || a->H > lstmp::GKMAX)
     return false;
   if ((int64_t)a->T * B2 * a->H * 2 * 4 >= (1ll << 31) - 64) return false;
+  if ((a->H + lstmp::LUPW - 1) / lstmp::LUPW > device_cus()) return false;   // (co-residency)
   return bwd ? (a->dgates && a->ut) : true;
 }
 
