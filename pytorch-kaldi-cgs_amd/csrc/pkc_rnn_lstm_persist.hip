@@ -281,6 +281,8 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
 // ----------------------------------------------------------------------------------- BPTT
 // dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the workgroup's 16 columns k;
 // wave W: strip jr = W % 8 of j (the per-step kernel's wave), gates 2 (W / 8) and 2 (W / 8) + 1.
+// SL: the strip per lane group (the per-step 8-wave kernel's S / 2: H / 32).  Bidirectional layers:
+// B2 rows (RnnIdx maps the reversed direction's time).
 // X3: the products in three bf16 parts per dgates element (d = hi + mid + lo exactly, RNE each;
 // U^T on its <= 8-bit grid is exact in bf16) on v_mfma_f32_16x16x32_bf16 with fp32 accumulation —
 // every product exact, the sums rounded in another order than the fp32 16x16x4 chains (not
@@ -290,12 +292,13 @@ __global__ __launch_bounds__(FNT) void qx_fwd_loop(pkc_rnn_args a) {
 // gridDim.y > 1: the B rows split over gridDim.y workgroups per column block (ceil(B / y) rows
 // each, blockIdx.y = row block): each loads only its rows of dgates_t (C5: 48 of 96 KB per step;
 // the payload bounds the step) — the elements' sums are unchanged (rows are independent).
-template <bool X3>
+template <bool X3, int SL = BS>
 __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
+  static_assert(!X3 || SL == 16, "X3: two 8-wide bf16 k-steps per strip");
   __shared__ float red[4][8][ROWS][UPW];       // [gate][strip] partial tiles of the step
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
-  const int H = a.H, B = a.B, T = a.T;
+  const int H = a.H, B = ix.B2, T = a.T;   // (B: the rows, both directions of a bidirectional layer)
   const int tid = threadIdx.x, lane = tid & 63;
   const int W = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int jr = W & 7, gp = W >> 3;
@@ -306,18 +309,18 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
   const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B * H, TB2H = (int64_t)T * B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
-  const int kb = (jr * 4 + q) * BS;             // this lane group's strip of j
+  const int kb = (jr * 4 + q) * SL;             // this lane group's strip of j
   // X3: lane group q's 8 j of k-step s at jx + 32 s (the strip's 64 j: 2 bf16 k-steps)
-  const int jx = jr * 4 * BS + 8 * q;
+  const int jx = jr * 4 * SL + 8 * q;
   const int jl = X3 ? jx : kb;                  // the first of this lane's (two runs of) 8 / 16 j
   // U^T strips (B operand, column k0 + c) of the wave's two gates, for the whole loop
-  float vu[2][BS];
+  float vu[2][SL];
   rbf16x8 uh[2][2];
 #pragma unroll
   for (int gg = 0; gg < 2; ++gg) {
     const float* pu = a.ut + (int64_t)(2 * gp + gg) * H * H + (int64_t)(k0 + c) * H;
 #pragma unroll
-    for (int s = 0; s < BS; s += 4) {
+    for (int s = 0; s < SL; s += 4) {
       const int j = X3 ? jx + 32 * (s / 8) + (s % 8) : kb + s;
       const float4 v = *reinterpret_cast<const float4*>(pu + j);
       vu[gg][s] = v.x; vu[gg][s + 1] = v.y; vu[gg][s + 2] = v.z; vu[gg][s + 3] = v.w;
@@ -349,13 +352,13 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
     LTR_MARK(1);
     // dgates_t strips of the wave's two gates (row c; rows >= B read zeros), both requested
     // before the MFMA chains
-    float va[2][BS];
+    float va[2][SL];
 #pragma unroll
     for (int gg = 0; gg < 2; ++gg) {
       const unsigned off =
           rc ? 4u * (unsigned)((2 * gp + gg) * TB2H + t * n + (int64_t)(y0 + c) * H + jl) : OOB;
 #pragma unroll
-      for (int s = 0; s < BS; s += 4)
+      for (int s = 0; s < SL; s += 4)
         ld_pub4(dgr, off + 4 * (X3 ? 32 * (s / 8) + (s % 8) : s), va[gg] + s);
     }
 #pragma unroll
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(BNT) void bwd_loop(pkc_rnn_args a) {
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ph[p][s], uh[gg][s], acc, 0, 0, 0);
       } else {
 #pragma unroll
-        for (int s = 0; s < BS; ++s)
+        for (int s = 0; s < SL; ++s)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[gg][s], vu[gg][s], acc, 0, 0, 0);
       }
 #pragma unroll
@@ -653,6 +656,218 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
   }
 }
 
+// ------------------------------------------------------------ fp32 step mode (C4 fp32's LSTM)
+// The exact-fp32 step products (no quantised h, no bf16 copies) of a dense LSTM layer, H = 32 SL
+// (512-1024), B2 <= 32 rows, in the per-step 8-wave kernel's tile form: workgroup wg owns units
+// [4 wg, 4 wg + 4) — ONE 16-column tile, column c = gate c / 4 of unit 4 wg + c % 4, as
+// rnn_fwd_mm lays its NG = 4 tile out — over H / 4 workgroups; lane group q of wave w holds U's
+// fp32 strip [(4 w + q) SL, + SL) of its column in registers for the whole loop, the rows' two
+// 16-row chains of v_mfma_f32_16x16x4_f32 run the per-step chain order, the waves' partials are
+// summed in red_sum4's order and fwd_epi updates the cell: bit-identical to the per-step launches.
+// h_t (fp32) is handed off as in the other loops.
+template <int SL>
+__global__ __launch_bounds__(FNT) void f32_fwd_loop(pkc_rnn_args a) {
+  constexpr int NU = 4;                         // units per workgroup (4 gates x 4 = 16 columns)
+  __shared__ float red[FNW][R32][UPW];          // each wave's partial tile (32 rows x 16 columns)
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B2 = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int u0 = blockIdx.x * NU;
+  const unsigned nwg = gridDim.x;
+  const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kb = (4 * w + q) * SL;
+  float ub[SL];
+  {
+    const float* pu = a.U[c / NU] + (int64_t)(u0 + c % NU) * H + kb;
+#pragma unroll
+    for (int s4 = 0; s4 < SL; s4 += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(pu + s4);
+      ub[s4] = v.x; ub[s4 + 1] = v.y; ub[s4 + 2] = v.z; ub[s4 + 3] = v.w;
+    }
+  }
+  const bool two = B2 > 16;                     // (uniform) the second 16-row chain
+  const int r = tid / NU, j = u0 + tid % NU;    // this thread's cell-update element
+  const bool ep = tid < R32 * NU && r < B2;
+  const int rr = ep ? r : 0;
+  float hreg = 0.f, creg = 0.f;
+  const float mreg = drop_val(a, rr, j, B2);
+  const __amdgpu_buffer_rsrc_t hr = pub_rsrc(a.hs);
+  const unsigned oa = 4u * (c * H + kb), ob = 4u * ((16 + c) * H + kb);
+  const bool ra = c < B2, rb = 16 + c < B2;
+  LTR_DECL;
+  for (int t = 0; t < T; ++t) {
+    LTR_MARK(0);
+    float wv[4];
+    const int64_t pi = ix.pre(t, rr, j);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) wv[g] = a.wpre[g * TBH + pi];
+    if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
+    LTR_MARK(1);
+    // h_{t-1} (hs[t]): the A strips of both row chains (rows >= B2 read zeros)
+    const unsigned to = 4u * (unsigned)(t * n);
+    float va[SL], vb[SL];
+#pragma unroll
+    for (int m = 0; m < SL / 4; ++m) ld_pub4(hr, ra ? oa + to + 16 * m : OOB, va + 4 * m);
+    if (two) {
+#pragma unroll
+      for (int m = 0; m < SL / 4; ++m) ld_pub4(hr, rb ? ob + to + 16 * m : OOB, vb + 4 * m);
+    }
+    LTR_MARK(2);
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    if (two) {
+#pragma unroll
+      for (int s2 = 0; s2 < SL; ++s2) {          // mfma_chain's order
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s2], ub[s2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[s2], ub[s2], acc1, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < SL; ++s2)
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s2], ub[s2], acc0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      red[w][4 * q + i][c] = acc0[i];
+      red[w][16 + 4 * q + i][c] = acc1[i];
+    }
+    lds_barrier();
+    LTR_MARK(3);
+    if (ep) {
+      const int ul = tid % NU;
+      float acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[v][r][NU * g + ul]; };
+        acc[g] = ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      EpiIn e;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) e.w[g] = wv[g];
+      e.hp = hreg;
+      e.cp = creg;
+      e.m = mreg;
+      const float vars[4] = {0.f, 0.f, 0.f, 0.f};
+      float cn = 0.f;
+      hreg = fwd_epi<PKC_CELL_LSTM, false, false, true>(a, ix, t, r, j, acc, vars, 1.f, e, &cn);
+      creg = cn;
+      st_pub(a.hs + (int64_t)(t + 1) * n + (int64_t)r * H + j, hreg);   // h_t to every workgroup
+    }
+    LTR_MARK(4);
+    if (t + 1 < T) arrive(ctr);
+    LTR_MARK(5);
+  }
+  LTR_STORE(0);
+}
+
+// BPTT of the same mode: dh_tt[r][k] = sum_g sum_j dgates_g[tt + 1][r][j] U_g[j][k] for the
+// workgroup's 16 columns k and <= 16 rows (blockIdx.y: row block); wave w owns the per-step 8-wave
+// kernel's strip w of j for ALL four gates (U^T strips: 4 SL registers; 16 waves of two gates each
+// would leave 128 registers a wave for 4 SL + 2 SL), each gate's fp32 chain in the per-step order,
+// the gates' dgates_t loaded two at a time (the next gate's strips in flight during a chain), the
+// 8 strips summed as red_sum<8>, the gates as rnn_bwd_epi, then lstm_grads: bit-identical.
+template <int SL>
+__global__ __launch_bounds__(FNT) void f32_bwd_loop(pkc_rnn_args a) {
+  __shared__ float red[4][FNW][ROWS][UPW];      // [gate][strip] partial tiles of the step
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = a.H, B = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int k0 = blockIdx.x * UPW;
+  const int rb = (B + (int)gridDim.y - 1) / (int)gridDim.y;   // rows per workgroup (<= 16)
+  const int y0 = rb * (int)blockIdx.y;
+  const unsigned nwg = gridDim.x * gridDim.y;
+  const int64_t n = (int64_t)B * H, TB2H = (int64_t)T * B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kb = (4 * w + q) * SL;
+  float vu[4][SL];                              // U^T strips (ut[g][k0 + c][kb ..]) of the loop
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float* pu = a.ut + (int64_t)g * H * H + (int64_t)(k0 + c) * H + kb;
+#pragma unroll
+    for (int s4 = 0; s4 < SL; s4 += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(pu + s4);
+      vu[g][s4] = v.x; vu[g][s4 + 1] = v.y; vu[g][s4 + 2] = v.z; vu[g][s4 + 3] = v.w;
+    }
+  }
+  const bool ep = tid < rb * UPW && y0 + (tid >> 4) < B;
+  const int r = ep ? y0 + (tid >> 4) : 0, k = k0 + (tid & 15);
+  const int64_t e = (int64_t)r * H + k;
+  const bool rc = c < rb && y0 + c < B;         // this lane's MFMA row y0 + c is one of ours
+  float gcar = a.work[e], dccar = a.work[2 * n + e];   // step T-1's carries (rnn_bwd_init)
+  const float mreg = drop_val(a, r, k, B);
+  const __amdgpu_buffer_rsrc_t dgr = pub_rsrc(a.dgates);
+  const unsigned lo = 4u * (unsigned)((int64_t)(y0 + c) * H + kb);   // this lane's strip in a slab
+  LTR_DECL;
+  for (int tt = T - 2; tt >= 0; --tt) {
+    LTR_MARK(0);
+    const int t = tt + 1;
+    const int64_t si = ix.st(tt, r, k);
+    const float f = a.gates[si], ig = a.gates[TB2H + si], o = a.gates[2 * TB2H + si];
+    const float cc = a.gates[3 * TB2H + si];
+    const float cN = a.cs[(int64_t)(tt + 1) * n + e], cP = a.cs[(int64_t)tt * n + e];
+    const float dyv = dy_at(a, ix.out(tt, r, k));
+    if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
+    LTR_MARK(1);
+    float va[2][SL];
+    auto ld_gate = [&](int g, float* v) {
+      const unsigned off = 4u * (unsigned)(g * TB2H + t * n) + lo;
+#pragma unroll
+      for (int m = 0; m < SL / 4; ++m) ld_pub4(dgr, rc ? off + 16 * m : OOB, v + 4 * m);
+    };
+    ld_gate(0, va[0]);
+    ld_gate(1, va[1]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < SL; ++s2)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[g & 1][s2], vu[g][s2], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[g][w][4 * q + i][c] = acc[i];
+      if (g + 2 < 4) {
+        // the chain has read its strips: reuse them for gate g + 2 (kept below the chain, so at
+        // most two gates' strips are live)
+        asm volatile("" ::"v"(acc) : "memory");
+        ld_gate(g + 2, va[g & 1]);
+      }
+    }
+    lds_barrier();
+    LTR_MARK(2);
+    if (ep) {
+      const int kl = tid & 15;
+      float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[g][v][r - y0][kl]; };
+        dh += ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      const float g = dyv + dh;                 // bwd_step_epi
+      float dg[4];
+      const float dco = lstm_grads(a.act, f, ig, o, cc, cN, cP, mreg, g, dccar, dg);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) st_pub(a.dgates + q4 * TB2H + si, dg[q4]);
+      gcar = g;
+      dccar = dco;
+    }
+    LTR_MARK(3);
+    if (tt > 0) arrive(ctr);
+    LTR_MARK(4);
+    LTR_MARK(5);
+  }
+  LTR_STORE(1);
+  if (ep && T > 1) {
+    const int p0 = (T - 1) & 1;
+    a.work[p0 * n + e] = gcar;
+    a.work[2 * n + p0 * n + e] = dccar;
+  }
+}
+
 // ----------------------------------------------------------- liGRU, exact-fp32 step mode (C3 fp32)
 // The same grid-synchronised form for a liGRU layer whose step products stay fp32 (the parity
 // mode; neural_networks.py:1573-1584): the units (BPTT: columns k) dealt to ceil(H / 16)
@@ -874,6 +1089,14 @@ bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
     if (bwd) return a->dgates && a->ut_h && a->dgates_h;
     return a->U_h[0] && a->U_h[1] && a->U_h[2] && a->U_h[3];
   }
+  if (a->qbits <= 0) {                          // exact fp32 step products (C4 fp32)
+    const char* f32 = getenv("PKC_RNN_LSTM_F32");   // "0": the per-step launches
+    if (f32 && f32[0] == '0') return false;
+    if (B2 > lstmp::R32 || a->H % 256 || a->H < 512 || a->H > 1024) return false;
+    if (a->H / 4 > device_cus()) return false;  // (the forward: 4 units per workgroup, co-resident)
+    if (bwd) return a->dgates && a->ut;
+    return a->U[0] && a->U[1] && a->U[2] && a->U[3];
+  }
   return false;
 }
 
@@ -940,6 +1163,20 @@ bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd) {
   return bwd ? (a->dgates && a->ut) : true;
 }
 
+// fp32 LSTM BPTT loop: row blocks per column block (each <= 16 rows, the MFMA tile;
+// PKC_RNN_LSTM_F32_RS raises the count, e.g. 4 for 8-row blocks), bounded by co-residency
+static int lstm_f32_bwd_rows_split(const pkc_rnn_args* a, int B2) {
+  static const int rs = [] {
+    const char* v = getenv("PKC_RNN_LSTM_F32_RS");
+    const int x = v ? atoi(v) : 0;
+    return x >= 1 && x <= 4 ? x : 0;
+  }();
+  const int need = (B2 + lstmp::ROWS - 1) / lstmp::ROWS;
+  const int want = rs > need ? rs : need;
+  const int r = fit_split(want, a->H / lstmp::UPW);
+  return r < need ? need : r;
+}
+
 // liGRU grid loops: workgroups per unit block the B2 rows are split over (PKC_RNN_LIGRU_GRID_RS,
 // default 2 when B2 > 8; 1: all rows in one workgroup)
 static int ligru_grid_rows_split(const pkc_rnn_args* a) {
@@ -968,6 +1205,11 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     if (kc == 2) hipLaunchKernelGGL(qx_fwd_loop<2>, grid, dim3(FNT), 0, s, *a);
     else if (kc == 3) hipLaunchKernelGGL(qx_fwd_loop<3>, grid, dim3(FNT), 0, s, *a);
     else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
+  } else if (!a->step_bf16) {                   // exact fp32 step products: 4 units per workgroup
+    const dim3 g4u(a->H / 4);
+    if (kc == 2) hipLaunchKernelGGL(f32_fwd_loop<16>, g4u, dim3(FNT), 0, s, *a);
+    else if (kc == 3) hipLaunchKernelGGL(f32_fwd_loop<24>, g4u, dim3(FNT), 0, s, *a);
+    else hipLaunchKernelGGL(f32_fwd_loop<32>, g4u, dim3(FNT), 0, s, *a);
   } else {
     const int co = lstm_bf16_coalesced();
     const int rs = lstm_bf16_rows_split(a);
@@ -1025,7 +1267,13 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
     if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, gq, dim3(BNT), 0, s, *a);
     else hipLaunchKernelGGL(bwd_loop<true>, gq, dim3(BNT), 0, s, *a);
   }
-  else {
+  else if (!a->step_bf16) {                     // exact fp32: rows in blocks of <= 16
+    const int B2 = a->bidir ? 2 * a->B : a->B;
+    const dim3 gf(grid.x, lstm_f32_bwd_rows_split(a, B2));
+    if (kc == 2) hipLaunchKernelGGL(f32_bwd_loop<16>, gf, dim3(FNT), 0, s, *a);
+    else if (kc == 3) hipLaunchKernelGGL(f32_bwd_loop<24>, gf, dim3(FNT), 0, s, *a);
+    else hipLaunchKernelGGL(f32_bwd_loop<32>, gf, dim3(FNT), 0, s, *a);
+  } else {
     const int co = lstm_bf16_coalesced();
     const int rs = lstm_bf16_rows_split(a);
     if (rs == 4) {

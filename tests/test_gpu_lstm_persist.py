@@ -45,13 +45,13 @@ def _block(net, x, dy, prec):
     return eng, node, y
 
 
-def _run(H, T, B, seed, persist, load=False, bf16=False, bidir=False):
+def _run(H, T, B, seed, persist, load=False, bf16=False, bidir=False, f32=False):
     import pkc.neural_networks as NN
     from pkc import _lib as L
     from test_gpu_rnn import dx0
     os.environ["PKC_RNN_LSTM_PERSIST"] = "1" if persist else "0"
     try:
-        if bf16:                       # C4's form: dense, bf16 step products
+        if bf16 or f32:                # C4's form: dense, bf16 (or exact fp32) step products
             opts = dict(LSTM_DEF, lstm_lay="%d,%d" % (H, H), lstm_drop="0.2,0.2",
                         lstm_bidir=str(bidir))
         else:                          # C5's form: quantised h, 8-bit U
@@ -171,6 +171,37 @@ def test_lstm_persist_bf16_bit_identical_to_steps(H, T, B, bidir, seed, load, mo
                 k, int(d.sum()), a.numel(), int(d.reshape(-1).nonzero()[0])))
     assert not bad, "; ".join(bad)
     assert n > 0 and float(ref["grad"].abs().max()) > 0
+
+
+@pytest.mark.parametrize("H,T,B,bidir,seed,load", [(1024, 10, 16, True, 21, False),
+                                                   (1024, 7, 16, True, 22, True),
+                                                   (512, 15, 12, False, 23, False),
+                                                   (768, 8, 10, True, 24, False)])
+def test_lstm_persist_fp32_bit_identical_to_steps(H, T, B, bidir, seed, load):
+    """The exact-fp32 step mode's loops (C4 fp32: 4 x 1024 bidirectional, B = 16; f32_fwd_loop /
+    f32_bwd_loop) against the per-step fp32 launches: the per-step 8-wave kernels' strips and chain
+    order, red_sum's and rnn_bwd_epi's orders — every tensor bit-identical."""
+    ref, forms_ref = _run(H, T, B, seed, False, f32=True, bidir=bidir)
+    got, forms = _run(H, T, B, seed, True, load, f32=True, bidir=bidir)
+    assert all("persistent" not in f for f in forms_ref.values()), forms_ref
+    assert all(f.startswith("persistent grid-synchronised") and "/" not in f for f in forms.values()), forms
+    print("fp32 H %d T %d B %d bidir %s forms %s" % (H, T, B, bidir, forms))
+    B2 = 2 * B if bidir else B
+    nwg = (H // 16) * ((B2 + 15) // 16)       # the BPTT's column blocks x row blocks of <= 16
+    bad = []
+    for k in ref:
+        if k.endswith(".timeout"):
+            assert int(got[k][0]) == nwg * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
+            assert int(got[k][1]) == 0, "%s: a persistent loop timed out" % k
+            continue
+        a, b = got[k], ref[k]
+        if not torch.equal(a, b):
+            d = (a != b)
+            bad.append("%s: %d of %d differ (first at flat %d, max %.3g)" % (
+                k, int(d.sum()), a.numel(), int(d.reshape(-1).nonzero()[0]),
+                float((a.double() - b.double()).abs().max())))
+    assert not bad, "; ".join(bad)
+    assert float(ref["grad"].abs().max()) > 0
 
 
 def test_lstm_persist_repeatable():
