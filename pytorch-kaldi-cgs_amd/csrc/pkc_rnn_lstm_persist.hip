@@ -659,45 +659,52 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
 // ------------------------------------------------------------ fp32 step mode (C4 fp32's LSTM)
 // The exact-fp32 step products (no quantised h, no bf16 copies) of a dense LSTM layer, H = 32 SL
 // (512-1024), B2 <= 32 rows, in the per-step 8-wave kernel's tile form: workgroup wg owns units
-// [4 wg, 4 wg + 4) — ONE 16-column tile, column c = gate c / 4 of unit 4 wg + c % 4, as
-// rnn_fwd_mm lays its NG = 4 tile out — over H / 4 workgroups; lane group q of wave w holds U's
-// fp32 strip [(4 w + q) SL, + SL) of its column in registers for the whole loop, the rows' two
-// 16-row chains of v_mfma_f32_16x16x4_f32 run the per-step chain order, the waves' partials are
-// summed in red_sum4's order and fwd_epi updates the cell: bit-identical to the per-step launches.
+// [16 wg, 16 wg + 16) as four 16-column tiles (column c of tile tl = gate c / 4 of unit
+// 16 wg + 4 tl + c % 4, as rnn_fwd_mm lays its NG = 4 tile out) and a block of <= 16 rows
+// (blockIdx.y): H / 16 x 2 workgroups for C4.  Lane group q of wave w holds U's fp32 strips
+// [(4 w + q) SL, + SL) of its four columns in registers for the whole loop, each row's chain of
+// v_mfma_f32_16x16x4_f32 runs the per-step order, the waves' partials are summed in red_sum4's
+// order and fwd_epi updates the cell: bit-identical to the per-step launches.  (The first form —
+// one tile per workgroup over H / 4 = 256 workgroups — ran 22 us per step: 256 arrivals on one
+// counter and 256 readers of the whole 128 KB h_{t-1} per step.)
 // h_t (fp32) is handed off as in the other loops.
 template <int SL>
 __global__ __launch_bounds__(FNT) void f32_fwd_loop(pkc_rnn_args a) {
-  constexpr int NU = 4;                         // units per workgroup (4 gates x 4 = 16 columns)
-  __shared__ float red[FNW][R32][UPW];          // each wave's partial tile (32 rows x 16 columns)
+  constexpr int NU = 4, TL = 4;                 // units per tile, tiles (16 units) per workgroup
+  __shared__ float red[FNW][TL][ROWS][UPW];     // each wave's partial tiles (16 rows x 16 columns)
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
   const int H = a.H, B2 = ix.B2, T = a.T;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
-  const int u0 = blockIdx.x * NU;
-  const unsigned nwg = gridDim.x;
+  const int u0 = blockIdx.x * NU * TL;
+  const int rb = (B2 + (int)gridDim.y - 1) / (int)gridDim.y;   // rows per workgroup (<= 16)
+  const int y0 = rb * (int)blockIdx.y;
+  const unsigned nwg = gridDim.x * gridDim.y;
   const int64_t n = (int64_t)B2 * H, TBH = (int64_t)T * a.B * H;
   unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
   const int kb = (4 * w + q) * SL;
-  float ub[SL];
-  {
-    const float* pu = a.U[c / NU] + (int64_t)(u0 + c % NU) * H + kb;
+  // tile tl's column c = gate c / 4 of unit u0 + 4 tl + c % 4 (rnn_fwd_mm's NG = 4 tile layout)
+  float ub[TL][SL];
+#pragma unroll
+  for (int tl = 0; tl < TL; ++tl) {
+    const float* pu = a.U[c / NU] + (int64_t)(u0 + NU * tl + c % NU) * H + kb;
 #pragma unroll
     for (int s4 = 0; s4 < SL; s4 += 4) {
       const float4 v = *reinterpret_cast<const float4*>(pu + s4);
-      ub[s4] = v.x; ub[s4 + 1] = v.y; ub[s4 + 2] = v.z; ub[s4 + 3] = v.w;
+      ub[tl][s4] = v.x; ub[tl][s4 + 1] = v.y; ub[tl][s4 + 2] = v.z; ub[tl][s4 + 3] = v.w;
     }
   }
-  const bool two = B2 > 16;                     // (uniform) the second 16-row chain
-  const int r = tid / NU, j = u0 + tid % NU;    // this thread's cell-update element
-  const bool ep = tid < R32 * NU && r < B2;
+  // this thread's cell-update element: row y0 + tid / 16, unit u0 + tid % 16
+  const int r = y0 + (tid >> 4), j = u0 + (tid & 15);
+  const bool ep = tid < rb * NU * TL && r < B2;
   const int rr = ep ? r : 0;
   float hreg = 0.f, creg = 0.f;
   const float mreg = drop_val(a, rr, j, B2);
   const __amdgpu_buffer_rsrc_t hr = pub_rsrc(a.hs);
-  const unsigned oa = 4u * (c * H + kb), ob = 4u * ((16 + c) * H + kb);
-  const bool ra = c < B2, rb = 16 + c < B2;
+  const bool ra = c < rb && y0 + c < B2;
+  const unsigned oa = 4u * ((y0 + c) * H + kb);
   LTR_DECL;
   for (int t = 0; t < T; ++t) {
     LTR_MARK(0);
@@ -707,41 +714,29 @@ __global__ __launch_bounds__(FNT) void f32_fwd_loop(pkc_rnn_args a) {
     for (int g = 0; g < 4; ++g) wv[g] = a.wpre[g * TBH + pi];
     if (t > 0 && !wait_ctr(ctr, nwg * (unsigned)t, &abort_flag)) return;
     LTR_MARK(1);
-    // h_{t-1} (hs[t]): the A strips of both row chains (rows >= B2 read zeros)
+    // h_{t-1} (hs[t]): this lane's A strip (row y0 + c; rows outside the block read zeros)
     const unsigned to = 4u * (unsigned)(t * n);
-    float va[SL], vb[SL];
+    float va[SL];
 #pragma unroll
     for (int m = 0; m < SL / 4; ++m) ld_pub4(hr, ra ? oa + to + 16 * m : OOB, va + 4 * m);
-    if (two) {
-#pragma unroll
-      for (int m = 0; m < SL / 4; ++m) ld_pub4(hr, rb ? ob + to + 16 * m : OOB, vb + 4 * m);
-    }
     LTR_MARK(2);
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    if (two) {
 #pragma unroll
-      for (int s2 = 0; s2 < SL; ++s2) {          // mfma_chain's order
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s2], ub[s2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[s2], ub[s2], acc1, 0, 0, 0);
-      }
-    } else {
+    for (int tl = 0; tl < TL; ++tl) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s2 = 0; s2 < SL; ++s2)
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s2], ub[s2], acc0, 0, 0, 0);
-    }
+      for (int s2 = 0; s2 < SL; ++s2)             // mfma_chain's order
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s2], ub[tl][s2], acc, 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      red[w][4 * q + i][c] = acc0[i];
-      red[w][16 + 4 * q + i][c] = acc1[i];
+      for (int i = 0; i < 4; ++i) red[w][tl][4 * q + i][c] = acc[i];
     }
     lds_barrier();
     LTR_MARK(3);
     if (ep) {
-      const int ul = tid % NU;
+      const int tl = (tid & 15) / NU, ul = tid % NU;
       float acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        auto p = [&](int v) { return red[v][r][NU * g + ul]; };
+        auto p = [&](int v) { return red[v][tl][r - y0][NU * g + ul]; };
         acc[g] = ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
       }
       EpiIn e;
@@ -1093,7 +1088,7 @@ bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
     const char* f32 = getenv("PKC_RNN_LSTM_F32");   // "0": the per-step launches
     if (f32 && f32[0] == '0') return false;
     if (B2 > lstmp::R32 || a->H % 256 || a->H < 512 || a->H > 1024) return false;
-    if (a->H / 4 > device_cus()) return false;  // (the forward: 4 units per workgroup, co-resident)
+    if (a->H / 16 * ((B2 + 15) / 16) > device_cus()) return false;   // (co-residency)
     if (bwd) return a->dgates && a->ut;
     return a->U[0] && a->U[1] && a->U[2] && a->U[3];
   }
@@ -1206,10 +1201,11 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     else if (kc == 3) hipLaunchKernelGGL(qx_fwd_loop<3>, grid, dim3(FNT), 0, s, *a);
     else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   } else if (!a->step_bf16) {                   // exact fp32 step products: 4 units per workgroup
-    const dim3 g4u(a->H / 4);
-    if (kc == 2) hipLaunchKernelGGL(f32_fwd_loop<16>, g4u, dim3(FNT), 0, s, *a);
-    else if (kc == 3) hipLaunchKernelGGL(f32_fwd_loop<24>, g4u, dim3(FNT), 0, s, *a);
-    else hipLaunchKernelGGL(f32_fwd_loop<32>, g4u, dim3(FNT), 0, s, *a);
+    const int B2 = a->bidir ? 2 * a->B : a->B;
+    const dim3 g16(a->H / 16, lstm_f32_bwd_rows_split(a, B2));   // (the BPTT's row blocks too)
+    if (kc == 2) hipLaunchKernelGGL(f32_fwd_loop<16>, g16, dim3(FNT), 0, s, *a);
+    else if (kc == 3) hipLaunchKernelGGL(f32_fwd_loop<24>, g16, dim3(FNT), 0, s, *a);
+    else hipLaunchKernelGGL(f32_fwd_loop<32>, g16, dim3(FNT), 0, s, *a);
   } else {
     const int co = lstm_bf16_coalesced();
     const int rs = lstm_bf16_rows_split(a);
