@@ -115,7 +115,7 @@ def lstm_persist(a):
     assert L.lib().pkc_trace_read_lstm_persist(buf, n) == 0
     t = np.frombuffer(buf, dtype=np.uint64).reshape(2, 16, 8).astype(np.int64)
     out = {"config": a.config, "prec": a.prec, "clock_ghz_assumed": 2.4}
-    if a.prec == "bf16":                # the bf16 loops' phases (pkc_rnn_lstm_persist.hip)
+    if a.prec == "bf16" or a.config == "c4":   # the bf16 / fp32 dense loops' phases
         LPHASES["forward loop"] = ["wait for the step's arrivals", "h_{t-1} load issue",
                                    "load wait + MFMA + partials", "cell update + stores", "arrive"]
         LPHASES["BPTT loop"] = ["wait for the step's arrivals", "dgates loads + MFMA + partials",
