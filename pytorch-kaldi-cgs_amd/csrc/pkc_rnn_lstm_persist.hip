@@ -863,6 +863,130 @@ __global__ __launch_bounds__(FNT) void f32_bwd_loop(pkc_rnn_args a) {
   }
 }
 
+// The same BPTT with the step's dgates_t staged through LDS (f32_bwd_lds): 8-row blocks
+// (blockIdx.y; 4 H / 16 workgroups for C4), the block's rows of all four gates (4 x 8 x H fp32,
+// 128 KB at H = 1024) loaded in ONE round trip — 16-byte sc1 loads to registers, every lane 16 of
+// them, then written to LDS — instead of f32_bwd_loop's two dependent round trips (its registers
+// hold only two gates' strips beside the four gates' U^T).  The chains read their A strips from
+// LDS: same operands, same order, bit-identical.  LDS rows padded by 4 floats.
+constexpr int LRB = 8;                          // rows per workgroup
+template <int SL>
+__global__ __launch_bounds__(FNT) void f32_bwd_lds(pkc_rnn_args a) {
+  constexpr int H_ = 32 * SL, LS = H_ + 4;       // (H is 32 SL by the dispatch)
+  constexpr int NCH = 4 * LRB * H_ / 4;          // 16-byte chunks of the staged block
+  static_assert(NCH % FNT == 0, "chunks per thread");
+  constexpr int CPT = NCH / FNT;
+  __shared__ __attribute__((aligned(16))) float stg[4 * LRB * LS];
+  __shared__ float red[4][FNW][LRB][UPW];
+  __shared__ int abort_flag;
+  const RnnIdx ix = mkidx(a);
+  const int H = H_, B = ix.B2, T = a.T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int k0 = blockIdx.x * UPW;
+  const int y0 = LRB * (int)blockIdx.y;
+  const unsigned nwg = gridDim.x * gridDim.y;
+  const int64_t n = (int64_t)B * H, TB2H = (int64_t)T * B * H;
+  unsigned* ctr = reinterpret_cast<unsigned*>(a.work + 4 * n);
+  const int kb = (4 * w + q) * SL;
+  float vu[4][SL];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float* pu = a.ut + (int64_t)g * H * H + (int64_t)(k0 + c) * H + kb;
+#pragma unroll
+    for (int s4 = 0; s4 < SL; s4 += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(pu + s4);
+      vu[g][s4] = v.x; vu[g][s4 + 1] = v.y; vu[g][s4 + 2] = v.z; vu[g][s4 + 3] = v.w;
+    }
+  }
+  const bool ep = tid < LRB * UPW && y0 + (tid >> 4) < B;
+  const int r = ep ? y0 + (tid >> 4) : 0, k = k0 + (tid & 15);
+  const int64_t e = (int64_t)r * H + k;
+  float gcar = a.work[e], dccar = a.work[2 * n + e];
+  const float mreg = drop_val(a, r, k, B);
+  const __amdgpu_buffer_rsrc_t dgr = pub_rsrc(a.dgates);
+  // this thread's chunks: chunk i = tid + FNT m -> gate i / (LRB H / 4), row (i / (H / 4)) % LRB,
+  // 4 floats at 4 (i % (H / 4)); rows past B read zeros
+  unsigned goff[CPT];
+  int soff[CPT];
+#pragma unroll
+  for (int m = 0; m < CPT; ++m) {
+    const int i = tid + FNT * m;
+    const int g = i / (LRB * H_ / 4), row = (i / (H_ / 4)) % LRB, k4 = i % (H_ / 4);
+    goff[m] = y0 + row < B ? 4u * (unsigned)(g * TB2H + (int64_t)(y0 + row) * H + 4 * k4) : OOB;
+    soff[m] = (g * LRB + row) * LS + 4 * k4;
+  }
+  const bool rc = c < LRB;                      // MFMA rows >= 8: zeros
+  const float* arow = stg + (c & (LRB - 1)) * LS + kb;
+  LTR_DECL;
+  for (int tt = T - 2; tt >= 0; --tt) {
+    LTR_MARK(0);
+    const int t = tt + 1;
+    const int64_t si = ix.st(tt, r, k);
+    const float f = a.gates[si], ig = a.gates[TB2H + si], o = a.gates[2 * TB2H + si];
+    const float cc = a.gates[3 * TB2H + si];
+    const float cN = a.cs[(int64_t)(tt + 1) * n + e], cP = a.cs[(int64_t)tt * n + e];
+    const float dyv = dy_at(a, ix.out(tt, r, k));
+    if (tt < T - 2 && !wait_ctr(ctr, nwg * (unsigned)(T - 2 - tt), &abort_flag)) return;
+    LTR_MARK(1);
+    const unsigned to = 4u * (unsigned)(t * n);
+    u32x4 st[CPT];
+#pragma unroll
+    for (int m = 0; m < CPT; ++m)
+      st[m] = __builtin_amdgcn_raw_buffer_load_b128(dgr, (int)(goff[m] == OOB ? OOB : goff[m] + to), 0, 16);
+#pragma unroll
+    for (int m = 0; m < CPT; ++m) *reinterpret_cast<u32x4*>(stg + soff[m]) = st[m];
+    lds_barrier();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float va[SL];
+#pragma unroll
+      for (int s4 = 0; s4 < SL; s4 += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(arow + g * LRB * LS + s4);
+        va[s4] = rc ? v.x : 0.f; va[s4 + 1] = rc ? v.y : 0.f;
+        va[s4 + 2] = rc ? v.z : 0.f; va[s4 + 3] = rc ? v.w : 0.f;
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < SL; ++s2)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s2], vu[g][s2], acc, 0, 0, 0);
+      if (q < 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[g][w][4 * q + i][c] = acc[i];
+      }
+    }
+    lds_barrier();
+    LTR_MARK(2);
+    if (ep) {
+      const int kl = tid & 15;
+      float dh = 0.f;                           // rnn_bwd_epi: the gate slabs in order
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        auto p = [&](int v) { return red[g][v][r - y0][kl]; };
+        dh += ((p(0) + p(1)) + (p(2) + p(3))) + ((p(4) + p(5)) + (p(6) + p(7)));
+      }
+      const float g = dyv + dh;                 // bwd_step_epi
+      float dg[4];
+      const float dco = lstm_grads(a.act, f, ig, o, cc, cN, cP, mreg, g, dccar, dg);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) st_pub(a.dgates + q4 * TB2H + si, dg[q4]);
+      gcar = g;
+      dccar = dco;
+    }
+    LTR_MARK(3);
+    if (tt > 0) arrive(ctr);
+    LTR_MARK(4);
+    LTR_MARK(5);
+  }
+  LTR_STORE(1);
+  if (ep && T > 1) {
+    const int p0 = (T - 1) & 1;
+    a.work[p0 * n + e] = gcar;
+    a.work[2 * n + p0 * n + e] = dccar;
+  }
+}
+
 // ----------------------------------------------------------- liGRU, exact-fp32 step mode (C3 fp32)
 // The same grid-synchronised form for a liGRU layer whose step products stay fp32 (the parity
 // mode; neural_networks.py:1573-1584): the units (BPTT: columns k) dealt to ceil(H / 16)
@@ -1172,6 +1296,17 @@ static int lstm_f32_bwd_rows_split(const pkc_rnn_args* a, int B2) {
   return r < need ? need : r;
 }
 
+// fp32 LSTM BPTT with the dgates block staged in LDS (f32_bwd_lds; PKC_RNN_LSTM_F32_LDS=0: the
+// register form f32_bwd_loop), when its 8-row blocks keep the grid at one workgroup per CU
+static bool lstm_f32_bwd_lds(const pkc_rnn_args* a) {
+  static const bool on = [] {
+    const char* v = getenv("PKC_RNN_LSTM_F32_LDS");
+    return !(v && v[0] == '0');
+  }();
+  const int B2 = a->bidir ? 2 * a->B : a->B;
+  return on && a->H / lstmp::UPW * ((B2 + lstmp::LRB - 1) / lstmp::LRB) <= device_cus();
+}
+
 // liGRU grid loops: workgroups per unit block the B2 rows are split over (PKC_RNN_LIGRU_GRID_RS,
 // default 2 when B2 > 8; 1: all rows in one workgroup)
 static int ligru_grid_rows_split(const pkc_rnn_args* a) {
@@ -1262,6 +1397,13 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
     const dim3 gq(grid.x, lstm_qx_bwd_rows_split(a));
     if (x3 && x3[0] == '0') hipLaunchKernelGGL(bwd_loop<false>, gq, dim3(BNT), 0, s, *a);
     else hipLaunchKernelGGL(bwd_loop<true>, gq, dim3(BNT), 0, s, *a);
+  }
+  else if (!a->step_bf16 && lstm_f32_bwd_lds(a)) {   // exact fp32, dgates staged in LDS
+    const int B2 = a->bidir ? 2 * a->B : a->B;
+    const dim3 gl(grid.x, (B2 + LRB - 1) / LRB);
+    if (kc == 2) hipLaunchKernelGGL(f32_bwd_lds<16>, gl, dim3(FNT), 0, s, *a);
+    else if (kc == 3) hipLaunchKernelGGL(f32_bwd_lds<24>, gl, dim3(FNT), 0, s, *a);
+    else hipLaunchKernelGGL(f32_bwd_lds<32>, gl, dim3(FNT), 0, s, *a);
   }
   else if (!a->step_bf16) {                     // exact fp32: rows in blocks of <= 16
     const int B2 = a->bidir ? 2 * a->B : a->B;

@@ -187,7 +187,7 @@ def test_lstm_persist_fp32_bit_identical_to_steps(H, T, B, bidir, seed, load):
     assert all(f.startswith("persistent grid-synchronised") and "/" not in f for f in forms.values()), forms
     print("fp32 H %d T %d B %d bidir %s forms %s" % (H, T, B, bidir, forms))
     B2 = 2 * B if bidir else B
-    nwg = (H // 16) * ((B2 + 15) // 16)       # the BPTT's column blocks x row blocks of <= 16
+    nwg = (H // 16) * ((B2 + 7) // 8)         # the BPTT's column blocks x 8-row blocks (f32_bwd_lds)
     bad = []
     for k in ref:
         if k.endswith(".timeout"):
