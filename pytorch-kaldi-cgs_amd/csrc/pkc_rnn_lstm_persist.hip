@@ -668,9 +668,9 @@ __global__ __launch_bounds__(FNT) void bf_bwd_loop(pkc_rnn_args a, int co) {
 // one tile per workgroup over H / 4 = 256 workgroups — ran 22 us per step: 256 arrivals on one
 // counter and 256 readers of the whole 128 KB h_{t-1} per step.)
 // h_t (fp32) is handed off as in the other loops.
-template <int SL>
+template <int SL, int TL>
 __global__ __launch_bounds__(FNT) void f32_fwd_loop(pkc_rnn_args a) {
-  constexpr int NU = 4, TL = 4;                 // units per tile, tiles (16 units) per workgroup
+  constexpr int NU = 4;                         // units per tile; TL tiles (4 TL units) per workgroup
   __shared__ float red[FNW][TL][ROWS][UPW];     // each wave's partial tiles (16 rows x 16 columns)
   __shared__ int abort_flag;
   const RnnIdx ix = mkidx(a);
@@ -696,8 +696,8 @@ __global__ __launch_bounds__(FNT) void f32_fwd_loop(pkc_rnn_args a) {
       ub[tl][s4] = v.x; ub[tl][s4 + 1] = v.y; ub[tl][s4 + 2] = v.z; ub[tl][s4 + 3] = v.w;
     }
   }
-  // this thread's cell-update element: row y0 + tid / 16, unit u0 + tid % 16
-  const int r = y0 + (tid >> 4), j = u0 + (tid & 15);
+  // this thread's cell-update element: row y0 + tid / (4 TL), unit u0 + tid % (4 TL)
+  const int r = y0 + tid / (NU * TL), j = u0 + tid % (NU * TL);
   const bool ep = tid < rb * NU * TL && r < B2;
   const int rr = ep ? r : 0;
   float hreg = 0.f, creg = 0.f;
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(FNT) void f32_fwd_loop(pkc_rnn_args a) {
     lds_barrier();
     LTR_MARK(3);
     if (ep) {
-      const int tl = (tid & 15) / NU, ul = tid % NU;
+      const int tl = (tid % (NU * TL)) / NU, ul = tid % NU;
       float acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1296,6 +1296,16 @@ static int lstm_f32_bwd_rows_split(const pkc_rnn_args* a, int B2) {
   return r < need ? need : r;
 }
 
+// fp32 LSTM forward loop: 16-column tiles per workgroup (PKC_RNN_LSTM_F32_TL = 2 or 4), 2 only
+// while the grid (H / 8 x row blocks) keeps one workgroup per CU
+static int lstm_f32_fwd_tiles(const pkc_rnn_args* a, int row_blocks) {
+  static const int tl = [] {
+    const char* v = getenv("PKC_RNN_LSTM_F32_TL");
+    return v && atoi(v) == 2 ? 2 : 4;
+  }();
+  return tl == 2 && a->H / 8 * row_blocks <= device_cus() ? 2 : 4;
+}
+
 // fp32 LSTM BPTT with the dgates block staged in LDS (f32_bwd_lds; PKC_RNN_LSTM_F32_LDS=0: the
 // register form f32_bwd_loop), when its 8-row blocks keep the grid at one workgroup per CU
 static bool lstm_f32_bwd_lds(const pkc_rnn_args* a) {
@@ -1337,10 +1347,18 @@ int rnn_lstm_persist_fwd(const pkc_rnn_args* a, hipStream_t s) {
     else hipLaunchKernelGGL(qx_fwd_loop<4>, grid, dim3(FNT), 0, s, *a);
   } else if (!a->step_bf16) {                   // exact fp32 step products: 4 units per workgroup
     const int B2 = a->bidir ? 2 * a->B : a->B;
-    const dim3 g16(a->H / 16, lstm_f32_bwd_rows_split(a, B2));   // (the BPTT's row blocks too)
-    if (kc == 2) hipLaunchKernelGGL(f32_fwd_loop<16>, g16, dim3(FNT), 0, s, *a);
-    else if (kc == 3) hipLaunchKernelGGL(f32_fwd_loop<24>, g16, dim3(FNT), 0, s, *a);
-    else hipLaunchKernelGGL(f32_fwd_loop<32>, g16, dim3(FNT), 0, s, *a);
+    const int ry = lstm_f32_bwd_rows_split(a, B2);              // row blocks of <= 16
+    if (lstm_f32_fwd_tiles(a, ry) == 2) {                        // 8 units per workgroup
+      const dim3 g8(a->H / 8, ry);
+      if (kc == 2) hipLaunchKernelGGL((f32_fwd_loop<16, 2>), g8, dim3(FNT), 0, s, *a);
+      else if (kc == 3) hipLaunchKernelGGL((f32_fwd_loop<24, 2>), g8, dim3(FNT), 0, s, *a);
+      else hipLaunchKernelGGL((f32_fwd_loop<32, 2>), g8, dim3(FNT), 0, s, *a);
+    } else {
+      const dim3 g16(a->H / 16, ry);
+      if (kc == 2) hipLaunchKernelGGL((f32_fwd_loop<16, 4>), g16, dim3(FNT), 0, s, *a);
+      else if (kc == 3) hipLaunchKernelGGL((f32_fwd_loop<24, 4>), g16, dim3(FNT), 0, s, *a);
+      else hipLaunchKernelGGL((f32_fwd_loop<32, 4>), g16, dim3(FNT), 0, s, *a);
+    }
   } else {
     const int co = lstm_bf16_coalesced();
     const int rs = lstm_bf16_rows_split(a);
