@@ -592,6 +592,12 @@ class Engine:
         self.skip_labels = set()
         self.n_launches = 0                    # libpkc launches issued (or captured) so far
         self.graph_launches_per_step = None    # of the multi-step graph (capture)
+        # grid-synchronised time loops (pkc_rnn_persist_form 2) that gave up waiting for a peer
+        # workgroup (every spin is bounded; the loop then ends and sets its timeout word): summed
+        # on the device after each such launch, raised at the next host sync (loss_values /
+        # chunk_totals) instead of passing on a half-computed layer
+        self.loop_fail = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._loop_forms = {}
 
     # ------------------------------------------------------------------ graph construction
     def _build_graph(self):
@@ -1841,6 +1847,7 @@ class Engine:
                             C.c_void_p(ra.U_h[g]), H * H, s)
             self._k("rnn_fwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_fwd", C.byref(ra), s)
+            self._loop_watch(ra, lb, False)
 
     def _forward_kernels(self, s, train, batch=None, defer_loss=False, pending=None):
         """pending: the previous step's deferred last launch (see _optim_kernels), run together
@@ -2112,6 +2119,7 @@ class Engine:
             ra.dy, ra.dy_nslab, ra.dy_slab_stride = dy_ptr, dy_ns, dy_stride
             self._k("rnn_bwd_loop T=%d H=%d" % (T, H), 2.0 * n.G * T * lb["B2"] * H * H,
                     4.0 * T * n.G * H * H, "pkc_rnn_bwd", C.byref(ra), ptr(lb["dpre"]), s)
+            self._loop_watch(ra, lb, True)
             _, (x_ptr, ldx) = self._rec_inputs(n, li)
             hsrc = lb["hq"] if sp["ibits"] else lb["hs"]
             # bf16 step mode: the weight gradients read bf16 operand copies (BF16IN: half the
@@ -2722,14 +2730,35 @@ class Engine:
         self.graph = g
         return True
 
+    def _loop_watch(self, ra, lb, bwd):
+        """After a layer's pkc_rnn_fwd / pkc_rnn_bwd: when it ran as a grid-synchronised loop,
+        add its timeout word (rwork[4 B2 H + 1], zeroed by the launch) to loop_fail."""
+        key = (id(lb), bwd, ra.T)
+        form = self._loop_forms.get(key)
+        if form is None:
+            form = self._loop_forms[key] = L.lib().pkc_rnn_persist_form(C.byref(ra), int(bwd))
+        if form == 2 and not (bwd and ra.T < 2):
+            o = 4 * lb["B2"] * lb["H"] + 1
+            self.loop_fail.add_(lb["rwork"][o:o + 1].view(torch.int32))
+
+    def _check_loops(self):
+        if int(self.loop_fail.item()) != 0:
+            raise L.PkcError("a grid-synchronised recurrent time loop gave up waiting for its peer "
+                             "workgroups (%d launch(es)): the GPU was shared with another persistent "
+                             "kernel or the grid was not co-resident; set PKC_RNN_LSTM_PERSIST=0 / "
+                             "PKC_RNN_LIGRU_GRID=0 to use the per-step launches"
+                             % int(self.loop_fail.item()))
+
     def loss_values(self):
         """(loss_final, err) of the last step (forces a sync)."""
         v = self.loss_out.cpu()
+        self._check_loops()
         return float(v[0]), float(v[1])
 
     def chunk_totals(self):
         """(loss_sum, err_sum) over the batches since bind_chunk (core.py:251-252)."""
         v = self.loss_acc.cpu()
+        self._check_loops()
         return float(v[0]), float(v[1])
 
     def head_output(self, out_name):
