@@ -1246,15 +1246,18 @@ static int fit_split(int rs, int base) {
 }
 
 // bf16 loops with more than 16 rows (C4: 2 x 16): the workgroups per unit block the rows are
-// split over (PKC_RNN_LSTM_RS = 1, 2 or 4; 1 keeps both 16-row chains in one workgroup)
-static int lstm_bf16_rows_split(const pkc_rnn_args* a) {
-  static const int rs = [] {
-    const char* v = getenv("PKC_RNN_LSTM_RS");
-    const int x = v ? atoi(v) : 2;
-    return x == 1 || x == 4 ? x : 2;
-  }();
+// split over (PKC_RNN_LSTM_RS = 1, 2 or 4; 1 keeps both 16-row chains in one workgroup;
+// PKC_RNN_LSTM_RS_BWD sets the BPTT loop's apart)
+static int lstm_bf16_rows_split(const pkc_rnn_args* a, bool bwd = false) {
+  auto knob = [](const char* name, int dflt) {
+    const char* v = getenv(name);
+    const int x = v ? atoi(v) : dflt;
+    return x == 1 || x == 2 || x == 4 ? x : dflt;
+  };
+  static const int rs = knob("PKC_RNN_LSTM_RS", 2);
+  static const int rsb = knob("PKC_RNN_LSTM_RS_BWD", rs);
   if ((a->bidir ? 2 * a->B : a->B) <= 16) return 1;
-  const int r = fit_split(rs, a->H / lstmp::UPW);
+  const int r = fit_split(bwd ? rsb : rs, a->H / lstmp::UPW);
   return r == 3 ? 2 : r;                        // (the bf16 loops take 1, 2 or 4)
 }
 
@@ -1431,7 +1434,7 @@ int rnn_lstm_persist_bwd(const pkc_rnn_args* a, hipStream_t s) {
     else hipLaunchKernelGGL(f32_bwd_loop<32>, gf, dim3(FNT), 0, s, *a);
   } else {
     const int co = lstm_bf16_coalesced();
-    const int rs = lstm_bf16_rows_split(a);
+    const int rs = lstm_bf16_rows_split(a, true);
     if (rs == 4) {
       const dim3 g4(grid.x, 4);
       if (kc == 2) hipLaunchKernelGGL((bf_bwd_loop<2, 4>), g4, dim3(FNT), 0, s, *a, co);
