@@ -111,29 +111,51 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// The step counter is sharded: NSH counters on 128-byte lines of their own after the launch's
+// [counter, timeout] words (ctr + SHW (1 + s)); workgroup b adds its arrivals to shard b % NSH
+// (blocks b and b + 8 share an XCD), so no line takes more than 1 / NSH of the grid's atomics
+// (one counter serialises them: ≈ 12 ns each, MI355X_MICROARCH.md fanin row), and the poller sums
+// every shard (the visibility table's first row: a poll of every shard of a sharded counter).
+constexpr int NSH = 8, SHW = 32;
+constexpr int CTR_FLOATS = (1 + NSH) * SHW;    // the launch's counter block in work (floats)
+
 // This workgroup's payload of the step is stored: every storing wave drains its stores, then one
-// lane (behind the workgroup barrier) adds the workgroup's arrival
+// lane (behind the workgroup barrier) adds the workgroup's arrival to its shard
 __device__ __forceinline__ void arrive(unsigned* ctr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    const unsigned b = blockIdx.x + gridDim.x * blockIdx.y;
+    __hip_atomic_fetch_add((gu32*)(ctr + SHW * (1 + b % NSH)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-// Wait until ctr >= target: thread 0 polls, the other waves wait at the barrier it then joins.
-// false on every thread of the workgroup when the wait timed out.
+// Wait until the shards sum to >= target: wave 0 polls (lane s < NSH loads shard s, the wave sums
+// them), the other waves wait at the barrier it then joins.  false on every thread of the
+// workgroup when the wait timed out (the timeout word ctr[1] is then set).
 __device__ __forceinline__ bool wait_ctr(unsigned* ctr, unsigned target, int* abort_lds) {
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
     unsigned spins = 0;
     int ab = 0;
-    while (__hip_atomic_load((gu32*)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    for (;;) {
+      unsigned v = l < NSH ? __hip_atomic_load((gu32*)(ctr + SHW * (1 + l)), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0u;
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      const unsigned tot = (unsigned)__builtin_amdgcn_readfirstlane((int)v);   // lanes 0-7's sum
+      if (tot >= target) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > SPIN_MAX) {
-        __hip_atomic_store((gu32*)(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0) __hip_atomic_store((gu32*)(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ab = 1;
         break;
       }
     }
-    *abort_lds = ab;
+    if (l == 0) *abort_lds = ab;
   }
   lds_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: loads stay below)
@@ -1193,6 +1215,7 @@ bool rnn_lstm_persist_ok(const pkc_rnn_args* a, bool bwd) {
   if (env && env[0] == '0') return false;
   if (a->cell != PKC_CELL_LSTM || a->ln_gamma || a->kmap_fwd || a->kmap_bwd || !a->work) return false;
   if (a->H / lstmp::UPW > device_cus()) return false;   // (every workgroup resident: one per CU)
+  if ((int64_t)4 * (a->bidir ? 2 * a->B : a->B) * a->H < lstmp::CTR_FLOATS) return false;
   const int64_t B2 = a->bidir ? 2 * a->B : a->B;
   // byte offsets of the 16-byte payload loads (dgates: G x T x B2 x H floats) below the
   // descriptors' 2^31 - 16 range
@@ -1282,6 +1305,7 @@ bool rnn_ligru_grid_ok(const pkc_rnn_args* a, bool bwd) {
     return false;
   if ((int64_t)a->T * B2 * a->H * 2 * 4 >= (1ll << 31) - 64) return false;
   if ((a->H + lstmp::LUPW - 1) / lstmp::LUPW > device_cus()) return false;   // (co-residency)
+  if (4 * B2 * a->H < lstmp::CTR_FLOATS) return false;   // (the sharded counters in work[4n, 8n))
   return bwd ? (a->dgates && a->ut) : true;
 }
 
@@ -1334,7 +1358,8 @@ static int ligru_grid_rows_split(const pkc_rnn_args* a) {
 
 static int lstm_ctr_reset(const pkc_rnn_args* a, hipStream_t s) {
   const int64_t B2 = a->bidir ? 2 * a->B : a->B;
-  PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * B2 * a->H, 0, 16, s), "pkc_rnn persistent LSTM counters");
+  PKC_HIP_CHECK(hipMemsetAsync(a->work + 4 * B2 * a->H, 0, sizeof(float) * lstmp::CTR_FLOATS, s),
+                "pkc_rnn persistent LSTM counters");
   return PKC_OK;
 }
 

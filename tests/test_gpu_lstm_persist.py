@@ -83,10 +83,18 @@ def _run(H, T, B, seed, persist, load=False, bf16=False, bidir=False, f32=False)
             for k in ("hs", "cs", "gates", "hq", "dgates", "hs_h", "dgates_h"):
                 if lb.get(k) is not None:
                     out["%d.%s" % (li, k)] = lb[k].cpu()
-            out["%d.timeout" % li] = lb["rwork"][4 * n:4 * n + 2].view(torch.int32).cpu()
+            out["%d.timeout" % li] = _ctr_words(lb["rwork"], n)
         return out, forms
     finally:
         os.environ.pop("PKC_RNN_LSTM_PERSIST", None)
+
+
+def _ctr_words(rwork, n):
+    """[arrivals, timeout word] of a layer's last grid-synchronised launch: the step counter is
+    8 shards on 128-byte lines after the [counter, timeout] words at work[4 B2 H]
+    (pkc_rnn_lstm_persist.hip NSH / SHW)."""
+    w = rwork[4 * n:4 * n + 9 * 32].view(torch.int32).cpu()
+    return torch.stack([w[32::32][:8].sum(), w[1]])
 
 
 BWD_KEYS = ("dgates", "dx0", "grad")      # what the BPTT products feed
@@ -249,7 +257,7 @@ def _run_ligru(H, T, B, seed, grid, hcgs, load=False):
             out["%d.hs" % li] = lb["hs"][:(T + 1) * n].cpu()
             for k in ("gates", "dgates"):
                 out["%d.%s" % (li, k)] = lb[k][:2 * T * n].cpu()
-            out["%d.timeout" % li] = lb["rwork"][4 * n:4 * n + 2].view(torch.int32).cpu()
+            out["%d.timeout" % li] = _ctr_words(lb["rwork"], n)
         return out, eng.rec_forms()
     finally:
         os.environ.pop("PKC_RNN_LIGRU_GRID", None)
