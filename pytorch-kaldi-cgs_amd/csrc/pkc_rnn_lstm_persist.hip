@@ -1269,8 +1269,8 @@ static int fit_split(int rs, int base) {
 }
 
 // bf16 loops with more than 16 rows (C4: 2 x 16): the workgroups per unit block the rows are
-// split over (PKC_RNN_LSTM_RS = 1, 2 or 4; 1 keeps both 16-row chains in one workgroup;
-// PKC_RNN_LSTM_RS_BWD sets the BPTT loop's apart)
+// split over (PKC_RNN_LSTM_RS = 1, 2 or 4 for the forward loop, default 2; 1 keeps both 16-row
+// chains in one workgroup; PKC_RNN_LSTM_RS_BWD for the BPTT loop, default 4)
 static int lstm_bf16_rows_split(const pkc_rnn_args* a, bool bwd = false) {
   auto knob = [](const char* name, int dflt) {
     const char* v = getenv(name);
@@ -1278,7 +1278,9 @@ static int lstm_bf16_rows_split(const pkc_rnn_args* a, bool bwd = false) {
     return x == 1 || x == 2 || x == 4 ? x : dflt;
   };
   static const int rs = knob("PKC_RNN_LSTM_RS", 2);
-  static const int rsb = knob("PKC_RNN_LSTM_RS_BWD", rs);
+  // (the BPTT's default is 4 row blocks: with the sharded step counter the 256-workgroup BPTT
+  // measured 13.56 vs 14.83-14.89 us per step-layer at C4, profiles/r06_c4_bf16_bwd_rows_split_ab.txt)
+  static const int rsb = knob("PKC_RNN_LSTM_RS_BWD", 4);
   if ((a->bidir ? 2 * a->B : a->B) <= 16) return 1;
   const int r = fit_split(bwd ? rsb : rs, a->H / lstmp::UPW);
   return r == 3 ? 2 : r;                        // (the bf16 loops take 1, 2 or 4)

@@ -166,7 +166,7 @@ def test_lstm_persist_bf16_bit_identical_to_steps(H, T, B, bidir, seed, load, mo
     print("bf16 H %d T %d B %d bidir %s forms %s" % (H, T, B, bidir, forms))
     bad = []
     n = (2 * B if bidir else B) * H
-    nwg = (H // 16) * (2 if (2 * B if bidir else B) > 16 else 1)   # > 16 rows: two row halves
+    nwg = (H // 16) * (4 if (2 * B if bidir else B) > 16 else 1)   # > 16 rows: 4 BPTT row blocks
     for k in ref:
         if k.endswith(".timeout"):
             assert int(got[k][0]) == nwg * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
