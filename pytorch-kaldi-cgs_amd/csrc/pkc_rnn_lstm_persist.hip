@@ -1287,12 +1287,13 @@ static int lstm_bf16_rows_split(const pkc_rnn_args* a, bool bwd = false) {
 }
 
 // QX BPTT loop: workgroups per column block the B rows are split over (PKC_RNN_LSTM_QX_RS, default
-// 2 when B > 8; 1: all rows in one workgroup)
+// 4 when B > 8 — with the sharded counter 13.61-13.66 against 14.00 us per step-layer for 2 at C5,
+// profiles/r06_c5_qx_bwd_rows_split_sharded_ab.txt; 1: all rows in one workgroup)
 static int lstm_qx_bwd_rows_split(const pkc_rnn_args* a) {
   static const int rs = [] {
     const char* v = getenv("PKC_RNN_LSTM_QX_RS");
-    const int x = v ? atoi(v) : 2;
-    return x >= 1 && x <= 4 ? x : 2;
+    const int x = v ? atoi(v) : 4;
+    return x >= 1 && x <= 4 ? x : 4;
   }();
   return a->B > 8 ? fit_split(rs, a->H / lstmp::UPW) : 1;
 }

@@ -124,10 +124,10 @@ def test_lstm_persist_bit_identical_to_steps(H, T, B, seed, load, x3, monkeypatc
     for k in ref:
         if k.endswith(".timeout"):
             # [step counter, timeout word] of the last persistent launch, the BPTT's (32 x (T - 2)
-            # arrivals; B > 8 rows: two row blocks per column block, 64 x (T - 2)); with per-step
+            # arrivals; B > 8 rows: four row blocks per column block, 128 x (T - 2)); with per-step
             # BPTT launches (H != 512) their gate slabs hold these words
             if H == 512:
-                nwg = 32 * (2 if B > 8 else 1)
+                nwg = 32 * (4 if B > 8 else 1)
                 assert int(got[k][0]) == nwg * (T - 2), "%s: arrivals %d" % (k, int(got[k][0]))
                 assert int(got[k][1]) == 0, "%s: a persistent loop timed out" % k
             continue
